@@ -1,0 +1,438 @@
+// MFMA GEMM core for libmoegan_hip (gfx950).
+//
+// C[m, n] = sum_k A[m, k] * B[k, n], tiles staged through LDS with both
+// operands stored k-contiguous ([rows][BK+pad]) so every lane reads its MFMA
+// fragment with one 16-byte ds_read.  The K loop prefetches tile k+1 into
+// registers while the MFMAs consume tile k.  256 threads = 4 waves in a 2x2
+// arrangement; each wave owns a (BM/2)x(BN/2) sub-tile of 16x16 fragments.
+//
+//   T = bf16_t : v_mfma_f32_16x16x32_bf16 (fp32 accumulate)
+//   T = float  : v_mfma_f32_16x16x4_f32   (exact fp32, the parity mode)
+//
+// Operand access is delegated to loader structs so one kernel body serves
+// plain / transposed operands, implicit NHWC convolutions (with the
+// modulated-conv style scale fused into the load), row gathers for expert
+// dispatch and GELU-on-load for expert hidden activations.
+//
+//   KC loader (reduction index contiguous in memory):
+//      RowState row(int r) const;  vec load(const RowState&, int k0, int kofs) const;
+//   MC loader (output index contiguous, reduction index strided):
+//      ColState col(int c0) const; vec load(const ColState&, int k) const;  (c0..c0+VEC-1)
+//
+// Grouping (expert batches) is resolved per block from device-side offset
+// tables, so no host synchronisation is needed to size the launch.
+#pragma once
+#include "mg_common.h"
+
+namespace mg {
+
+constexpr int BK = 32;
+constexpr int NTHREADS = 256;
+
+template <typename T> struct Frag;
+template <> struct Frag<bf16_t> { static constexpr int PAD = 8; };
+template <> struct Frag<float> { static constexpr int PAD = 4; };
+
+template <typename T> MG_DEV typename VecOf<T>::type vzero() { return typename VecOf<T>::type(0); }
+
+// scale a vector by per-element fp32 factors (modulation / gate), returning storage type
+MG_DEV f32x4_t vscale(f32x4_t v, const float* s) { return f32x4_t{v[0] * s[0], v[1] * s[1], v[2] * s[2], v[3] * s[3]}; }
+MG_DEV u16x8_t vscale(u16x8_t v, const float* s) {
+  u16x8_t r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(bf2f(v[j]) * s[j]);
+  return r;
+}
+MG_DEV f32x4_t vscale1(f32x4_t v, float s) { return v * s; }
+MG_DEV u16x8_t vscale1(u16x8_t v, float s) {
+  u16x8_t r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(bf2f(v[j]) * s);
+  return r;
+}
+MG_DEV f32x4_t vgelu(f32x4_t v) { return f32x4_t{gelu_erf(v[0]), gelu_erf(v[1]), gelu_erf(v[2]), gelu_erf(v[3])}; }
+MG_DEV u16x8_t vgelu(u16x8_t v) {
+  u16x8_t r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(gelu_erf(bf2f(v[j])));
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Loaders
+// ---------------------------------------------------------------------------
+// KC, plain rows with optional row gather / per-row scale / GELU-on-load.
+//   row r -> source row (idx ? idx[r] / idx_div : r); value *= rs[r] if rs
+template <typename T>
+struct LdKC {
+  const T* p; int64_t ld; int rows; int K;
+  const int* idx; int idx_div;   // gather: source row = idx[r] / idx_div
+  const float* rs;               // optional per-row scale (indexed by r)
+  int gelu;                      // apply GELU to loaded values
+  struct RowState { const T* base; float s; };
+  struct ColState {};
+  MG_DEV void set_group(int) {}
+  MG_DEV RowState row(int r) const {
+    RowState st{nullptr, 1.f};
+    if (r < rows) {
+      int src = idx ? idx[r] / idx_div : r;
+      st.base = p + (int64_t)src * ld;
+      if (rs) st.s = rs[r];
+    }
+    return st;
+  }
+  MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
+    int k = k0 + kofs;
+    if (!st.base || k >= K) return vzero<T>();
+    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(st.base + k);
+    if (gelu) v = vgelu(v);
+    if (rs) v = vscale1(v, st.s);
+    return v;
+  }
+};
+
+// KC, implicit NHWC convolution: row = output pixel (b, oh, ow), k = tap*Cin + ci.
+// Requires Cin % BK == 0 (tap uniform inside a K tile) and power-of-two OH/OW/Cin.
+template <typename T>
+struct LdKCConv {
+  const T* x; int H, W, Cin, lgCin, lgOW, lgOHW, M;
+  int KW, stride, pad, K;
+  const float* scale;  // optional [B, Cin] per-sample input-channel scale (modulation)
+  struct RowState { int b, oh, ow; };
+  struct ColState {};
+  MG_DEV void set_group(int) {}
+  MG_DEV RowState row(int r) const {
+    RowState st;
+    if (r >= M) { st.b = -1; st.oh = st.ow = 0; return st; }
+    st.b = r >> lgOHW;
+    int rem = r & ((1 << lgOHW) - 1);
+    st.oh = rem >> lgOW;
+    st.ow = rem & ((1 << lgOW) - 1);
+    return st;
+  }
+  MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
+    if (st.b < 0 || k0 >= K) return vzero<T>();
+    int tap = k0 >> lgCin;
+    int ci = (k0 & (Cin - 1)) + kofs;
+    int kh = tap / KW, kw = tap - (tap / KW) * KW;
+    int ih = st.oh * stride - pad + kh, iw = st.ow * stride - pad + kw;
+    if (ih < 0 || ih >= H || iw < 0 || iw >= W) return vzero<T>();
+    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(x + (((int64_t)st.b * H + ih) * W + iw) * Cin + ci);
+    if (scale) v = vscale(v, scale + (int64_t)st.b * Cin + ci);
+    return v;
+  }
+};
+
+// MC, plain: element (k, c) at p[k*ld + c]; optional row gather on k, per-k scale, GELU-on-load.
+template <typename T>
+struct LdMC {
+  const T* p; int64_t ld; int cols; int K;
+  const int* idx; int idx_div; const float* rs; int gelu;
+  int64_t group_stride;  // added per group (grouped-K mode: rows are absolute anyway)
+  struct ColState { int c0; };
+  struct RowState {};
+  MG_DEV void set_group(int) {}
+  MG_DEV ColState col(int c0) const { return ColState{c0}; }
+  MG_DEV typename VecOf<T>::type load(const ColState& st, int k) const {
+    if (st.c0 >= cols || k >= K) return vzero<T>();
+    int src = idx ? idx[k] / idx_div : k;
+    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(p + (int64_t)src * ld + st.c0);
+    if (gelu) v = vgelu(v);
+    if (rs) v = vscale1(v, rs[k]);
+    return v;
+  }
+};
+
+// MC, implicit conv columns for weight gradients: element (k = pixel, c = tap*Cin + ci).
+template <typename T>
+struct LdMCConv {
+  const T* x; int H, W, Cin, lgCin, lgOW, lgOHW, K;  // K = number of output pixels
+  int KW, stride, pad, cols;
+  const float* scale;
+  struct ColState { int kh, kw, ci; bool ok; };
+  struct RowState {};
+  MG_DEV void set_group(int) {}
+  MG_DEV ColState col(int c0) const {
+    ColState st;
+    st.ok = c0 < cols;
+    int tap = c0 >> lgCin;
+    st.ci = c0 & (Cin - 1);
+    st.kh = tap / KW;
+    st.kw = tap - st.kh * KW;
+    return st;
+  }
+  MG_DEV typename VecOf<T>::type load(const ColState& st, int k) const {
+    if (!st.ok || k >= K) return vzero<T>();
+    int b = k >> lgOHW;
+    int rem = k & ((1 << lgOHW) - 1);
+    int oh = rem >> lgOW, ow = rem & ((1 << lgOW) - 1);
+    int ih = oh * stride - pad + st.kh, iw = ow * stride - pad + st.kw;
+    if (ih < 0 || ih >= H || iw < 0 || iw >= W) return vzero<T>();
+    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(x + (((int64_t)b * H + ih) * W + iw) * Cin + st.ci);
+    if (scale) v = vscale(v, scale + (int64_t)b * Cin + st.ci);
+    return v;
+  }
+};
+
+// Grouped B operand: KC rows of a per-group weight (base + g*gstride).
+template <typename T>
+struct LdKCGroupW {
+  const T* p0; int64_t ld; int rows; int K; int64_t gstride;
+  const T* p;
+  struct RowState { const T* base; };
+  struct ColState {};
+  MG_DEV void set_group(int g) { p = p0 + (int64_t)g * gstride; }
+  MG_DEV RowState row(int r) const { return RowState{r < rows ? p + (int64_t)r * ld : nullptr}; }
+  MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
+    int k = k0 + kofs;
+    if (!st.base || k >= K) return vzero<T>();
+    return *reinterpret_cast<const typename VecOf<T>::type*>(st.base + k);
+  }
+};
+template <typename T>
+struct LdMCGroupW {
+  const T* p0; int64_t ld; int cols; int K; int64_t gstride;
+  const T* p;
+  struct ColState { int c0; };
+  struct RowState {};
+  MG_DEV void set_group(int g) { p = p0 + (int64_t)g * gstride; }
+  MG_DEV ColState col(int c0) const { return ColState{c0}; }
+  MG_DEV typename VecOf<T>::type load(const ColState& st, int k) const {
+    if (st.c0 >= cols || k >= K) return vzero<T>();
+    return *reinterpret_cast<const typename VecOf<T>::type*>(p + (int64_t)k * ld + st.c0);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Epilogue
+// ---------------------------------------------------------------------------
+enum { ACT_NONE = 0, ACT_LRELU = 1, ACT_GELU = 2, ACT_MUL_GELU_GRAD = 3, ACT_MUL_LRELU_GRAD = 4 };
+
+template <typename TO>
+struct Epi {
+  TO* C; int64_t ldc; int64_t gstride_c;  // per-group output offset
+  float alpha;
+  const float* bias; int64_t gstride_bias;  // bias[n] (+ g*gstride_bias)
+  const float* scale; int scale_shift; int64_t scale_ld;  // v *= scale[(m >> shift)*ld + n]
+  const float* rowscale;                      // v *= rowscale[m]
+  int act; const TO* aux; int64_t ld_aux;     // aux for *_GRAD acts
+  const TO* resid; int64_t ld_res;
+  int accumulate;  // C += v (non-atomic)
+  int atomic;      // fp32 atomic add (split-K / scatter)
+  int remap_lgcin, remap_taps;  // weight-grad layout remap when remap_taps > 0
+  int g;
+  MG_DEV void set_group(int gg) { g = gg; }
+  MG_DEV void operator()(int m, int n, float v) const {
+    v *= alpha;
+    if (scale) v *= scale[(int64_t)(m >> scale_shift) * scale_ld + n];
+    if (bias) v += bias[(int64_t)g * gstride_bias + n];
+    if (act == ACT_LRELU) v = lrelu(v);
+    else if (act == ACT_GELU) v = gelu_erf(v);
+    else if (act == ACT_MUL_GELU_GRAD) v *= gelu_erf_grad(ldf(aux, (int64_t)m * ld_aux + n));
+    else if (act == ACT_MUL_LRELU_GRAD) v *= lrelu_grad(ldf(aux, (int64_t)m * ld_aux + n));
+    if (rowscale) v *= rowscale[m];
+    if (resid) v += ldf(resid, (int64_t)m * ld_res + n);
+    int64_t nn = n;
+    if (remap_taps > 0) nn = (int64_t)(n & ((1 << remap_lgcin) - 1)) * remap_taps + (n >> remap_lgcin);
+    int64_t idx = (int64_t)g * gstride_c + (int64_t)m * ldc + nn;
+    if (atomic) {
+      atomicAdd(reinterpret_cast<float*>(C) + idx, v);
+    } else {
+      if (accumulate) v += ldf(C, idx);
+      stf(C, idx, v);
+    }
+  }
+};
+
+// grouping descriptor (device tables)
+struct Grouping {
+  int mode;              // 0 none, 1 grouped-M (rows), 2 grouped-K (reduction rows)
+  int ngroups;
+  const int* row_off;    // [ngroups+1] row (mode 1) / reduction (mode 2) offsets
+  const int* tile_off;   // mode 1: [ngroups+1] prefix of ceil(rows_g / BM)
+};
+
+// ---------------------------------------------------------------------------
+// Kernel
+// ---------------------------------------------------------------------------
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
+__global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M, int N, int K, int kchunk, Grouping grp) {
+  constexpr int VEC = VecOf<T>::N;
+  typedef typename VecOf<T>::type vec_t;
+  constexpr int LDK = BK + Frag<T>::PAD;
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  // per-thread vector counts
+  constexpr int A_VPT = BM * BK / VEC / NTHREADS;
+  constexpr int B_VPT = BN * BK / VEC / NTHREADS;
+  static_assert(A_VPT >= 1 && B_VPT >= 1, "tile too small for 256 threads");
+  __shared__ __attribute__((aligned(16))) T As[BM * LDK];
+  __shared__ __attribute__((aligned(16))) T Bs[BN * LDK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // ---- resolve tile / group ----
+  int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int mrow_base = 0;  // global row offset of this group (mode 1)
+  int Mloc = M;
+  int kbeg = blockIdx.z * kchunk, kend = min(K, kbeg + kchunk);
+  int g = 0;
+  if (grp.mode == 1) {
+    int t = blockIdx.x;
+    g = -1;
+    for (int i = 0; i < grp.ngroups; ++i)
+      if (t >= grp.tile_off[i] && t < grp.tile_off[i + 1]) { g = i; break; }
+    if (g < 0) return;
+    mrow_base = grp.row_off[g];
+    Mloc = grp.row_off[g + 1] - mrow_base;
+    m0 = (t - grp.tile_off[g]) * BM;
+  } else if (grp.mode == 2) {
+    int splits = gridDim.z / grp.ngroups;
+    g = blockIdx.z / splits;
+    int s = blockIdx.z - g * splits;
+    int r0 = grp.row_off[g], r1 = grp.row_off[g + 1];
+    int per = ((r1 - r0 + splits - 1) / splits + BK - 1) / BK * BK;
+    kbeg = r0 + s * per;
+    kend = min(r1, kbeg + per);
+    if (kbeg >= kend) return;
+  }
+  A.set_group(g);
+  B.set_group(g);
+  ep.set_group(g);
+  // in grouped-M mode the A loader / epilogue see absolute rows; clamp via Mloc
+  const int mlimit = mrow_base + Mloc;
+
+  // ---- per-thread load slots ----
+  vec_t ra[A_VPT], rb[B_VPT];
+  typename AL::RowState ast[A_KC ? A_VPT : 1];
+  typename AL::ColState acs[A_KC ? 1 : A_VPT];
+  typename BL::RowState bst[B_KC ? B_VPT : 1];
+  typename BL::ColState bcs[B_KC ? 1 : B_VPT];
+  int a_r[A_VPT], a_k[A_VPT], b_r[B_VPT], b_k[B_VPT];
+#pragma unroll
+  for (int i = 0; i < A_VPT; ++i) {
+    int v = tid + i * NTHREADS;
+    if constexpr (A_KC) {
+      a_r[i] = v / (BK / VEC); a_k[i] = (v % (BK / VEC)) * VEC;
+      int r = mrow_base + m0 + a_r[i];
+      ast[i] = A.row(r < mlimit ? r : 0x7fffffff);
+    } else {
+      a_k[i] = v / (BM / VEC); a_r[i] = (v % (BM / VEC)) * VEC;
+      int c = mrow_base + m0 + a_r[i];
+      acs[i] = A.col(c < mlimit ? c : 0x7fffffff);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < B_VPT; ++i) {
+    int v = tid + i * NTHREADS;
+    if constexpr (B_KC) {
+      b_r[i] = v / (BK / VEC); b_k[i] = (v % (BK / VEC)) * VEC;
+      bst[i] = B.row(n0 + b_r[i]);
+    } else {
+      b_k[i] = v / (BN / VEC); b_r[i] = (v % (BN / VEC)) * VEC;
+      bcs[i] = B.col(n0 + b_r[i]);
+    }
+  }
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_VPT; ++i) {
+      if constexpr (A_KC) ra[i] = (k0 + a_k[i] < kend) ? A.load(ast[i], k0, a_k[i]) : vzero<T>();
+      else ra[i] = (k0 + a_k[i] < kend) ? A.load(acs[i], k0 + a_k[i]) : vzero<T>();
+    }
+#pragma unroll
+    for (int i = 0; i < B_VPT; ++i) {
+      if constexpr (B_KC) rb[i] = (k0 + b_k[i] < kend) ? B.load(bst[i], k0, b_k[i]) : vzero<T>();
+      else rb[i] = (k0 + b_k[i] < kend) ? B.load(bcs[i], k0 + b_k[i]) : vzero<T>();
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_VPT; ++i) {
+      if constexpr (A_KC) *reinterpret_cast<vec_t*>(&As[a_r[i] * LDK + a_k[i]]) = ra[i];
+      else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) As[(a_r[i] + j) * LDK + a_k[i]] = ra[i][j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_VPT; ++i) {
+      if constexpr (B_KC) *reinterpret_cast<vec_t*>(&Bs[b_r[i] * LDK + b_k[i]]) = rb[i];
+      else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) Bs[(b_r[i] + j) * LDK + b_k[i]] = rb[i][j];
+      }
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (kbeg < kend) gload(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    sstore();
+    __syncthreads();
+    if (k0 + BK < kend) gload(k0 + BK);
+    const int fr = lane & 15, fq = lane >> 4;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8_t af[FM], bfv[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&As[(wm * WM + i * 16 + fr) * LDK + fq * 8]));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfv[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&Bs[(wn * WN + j * 16 + fr) * LDK + fq * 8]));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        float af[FM], bfv[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = As[(wm * WM + i * 16 + fr) * LDK + kk * 4 + fq];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfv[j] = Bs[(wn * WN + j * 16 + fr) * LDK + kk * 4 + fq];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue ----
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int m = m0 + wm * WM + i * 16 + fq * 4 + r;
+        int n = n0 + wn * WN + j * 16 + fr;
+        if (m < Mloc && n < N) ep(mrow_base + m, n, acc[i][j][r]);
+      }
+}
+
+// launch helper: picks the grid; grouped-M launches an upper bound of tiles.
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
+inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, int K, int splits, Grouping grp,
+                        int max_tiles_m, hipStream_t st) {
+  int kchunk = K;
+  if (grp.mode != 2 && splits > 1) kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  if (grp.mode != 2) splits = (K + kchunk - 1) / kchunk;
+  if (splits < 1) splits = 1;
+  int gx = grp.mode == 1 ? max_tiles_m : cdiv(M, BM);
+  int gz = grp.mode == 2 ? splits * grp.ngroups : splits;
+  dim3 grid(gx, cdiv(N, BN), gz);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP>), grid, dim3(NTHREADS), 0, st, A, B, ep, M, N,
+                     K, kchunk, grp);
+}
+
+}  // namespace mg

@@ -1,0 +1,291 @@
+// GEMM / implicit-conv entry points of libmoegan_hip.
+#include <string>
+
+#include "mg_gemm.h"
+
+using namespace mg;
+
+namespace {
+
+template <typename TO>
+Epi<TO> make_epi(void* C, int64_t ldc, const mg_epilogue* e) {
+  Epi<TO> ep;
+  ep.C = reinterpret_cast<TO*>(C);
+  ep.ldc = ldc;
+  ep.gstride_c = 0;
+  ep.alpha = e ? e->alpha : 1.f;
+  ep.bias = e ? e->bias : nullptr;
+  ep.gstride_bias = 0;
+  ep.scale = e ? e->scale : nullptr;
+  ep.scale_shift = e ? e->scale_shift : 0;
+  ep.scale_ld = e ? e->scale_ld : 0;
+  ep.rowscale = e ? e->rowscale : nullptr;
+  ep.act = e ? e->act : 0;
+  ep.aux = e ? reinterpret_cast<const TO*>(e->aux) : nullptr;
+  ep.ld_aux = e ? e->ld_aux : 0;
+  ep.resid = e ? reinterpret_cast<const TO*>(e->resid) : nullptr;
+  ep.ld_res = e ? e->ld_res : 0;
+  ep.accumulate = e ? e->accumulate : 0;
+  ep.atomic = e ? e->atomic : 0;
+  ep.remap_lgcin = e ? e->remap_lgcin : 0;
+  ep.remap_taps = e ? e->remap_taps : 0;
+  ep.g = 0;
+  return ep;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+inline int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+inline bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+constexpr Grouping kNoGroup{0, 1, nullptr, nullptr};
+
+template <typename T, typename TO, int BM, int BN, bool AK, bool BKc>
+void run_plain(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+               const mg_epilogue* e, int splits, hipStream_t st) {
+  auto ep = make_epi<TO>(C, ldc, e);
+  const int32_t* aidx = e ? e->a_idx : nullptr;
+  int adiv = (e && e->a_idx_div > 0) ? e->a_idx_div : 1;
+  const float* ars = e ? e->a_rowscale : nullptr;
+  int agelu = e ? e->a_gelu : 0;
+  if constexpr (AK) {
+    LdKC<T> la{reinterpret_cast<const T*>(A), lda, M, K, aidx, adiv, ars, agelu};
+    if constexpr (BKc) {
+      LdKC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
+      launch_gemm<T, BM, BN, true, true>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
+    } else {
+      LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0, 0};
+      launch_gemm<T, BM, BN, true, false>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
+    }
+  } else {
+    LdMC<T> la{reinterpret_cast<const T*>(A), lda, M, K, aidx, adiv, ars, agelu, 0};
+    if constexpr (BKc) {
+      LdKC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
+      launch_gemm<T, BM, BN, false, true>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
+    } else {
+      LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0, 0};
+      launch_gemm<T, BM, BN, false, false>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
+    }
+  }
+}
+
+template <typename T, typename TO, int BM, int BN>
+void run_plain_orient(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
+                      int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, int splits, hipStream_t st) {
+  if (a_kc && b_kc) run_plain<T, TO, BM, BN, true, true>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else if (a_kc) run_plain<T, TO, BM, BN, true, false>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else if (b_kc) run_plain<T, TO, BM, BN, false, true>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else run_plain<T, TO, BM, BN, false, false>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+}
+
+template <typename T, typename TO>
+void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
+                     int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, int splits, hipStream_t st) {
+  if ((int64_t)cdiv(M, 128) * cdiv(N, 128) * splits >= 160)
+    run_plain_orient<T, TO, 128, 128>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else
+    run_plain_orient<T, TO, 64, 64>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+}
+
+}  // namespace
+
+extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t lda, int a_kc, const void* B,
+                       int64_t ldb, int b_kc, void* C, int64_t ldc, int c_dtype, const mg_epilogue* ep, int splits,
+                       void* stream) {
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
+  MG_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
+  if (M == 0 || N == 0) return MG_OK;
+  const int vec = dtype == MG_F32 ? 4 : 8;
+  MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
+  MG_REQUIRE(lda % vec == 0 && ldb % vec == 0, "lda/ldb must be multiples of the 16-byte vector");
+  MG_REQUIRE(a_kc ? (K % vec == 0) : (M % vec == 0), "A vector dim must be a multiple of the 16-byte vector");
+  MG_REQUIRE(b_kc ? (K % vec == 0) : (N % vec == 0), "B vector dim must be a multiple of the 16-byte vector");
+  if (splits < 1) splits = 1;
+  MG_REQUIRE(splits == 1 || (ep && ep->atomic && c_dtype == MG_F32), "split-K requires an atomic fp32 epilogue");
+  MG_REQUIRE(!(ep && ep->atomic) || c_dtype == MG_F32, "atomic epilogue requires fp32 C");
+  if (K == 0) splits = 1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_F32) {
+    if (c_dtype == MG_F32) run_plain_tiles<float, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
+    else run_plain_tiles<float, bf16_t>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
+  } else {
+    if (c_dtype == MG_F32) run_plain_tiles<bf16_t, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
+    else run_plain_tiles<bf16_t, bf16_t>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
+  }
+  return mg_check_launch("mg_gemm");
+}
+
+// ---------------------------------------------------------------------------
+// implicit-GEMM convolution
+// ---------------------------------------------------------------------------
+namespace {
+template <typename T, typename TO, int BM, int BN>
+void run_conv(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW, int stride,
+              int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
+  int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  int M = B * OH * OW, K = KH * KW * Cin;
+  LdKCConv<T> la{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), M,
+                 KW, stride, pad, K, sc};
+  LdKC<T> lb{reinterpret_cast<const T*>(wpack), K, Cout, K, nullptr, 1, nullptr, 0};
+  auto ep = make_epi<TO>(y, ldy, e);
+  launch_gemm<T, BM, BN, true, true>(la, lb, ep, M, Cout, K, 1, kNoGroup, 0, st);
+}
+template <typename T, typename TO>
+void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW,
+                    int stride, int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e,
+                    hipStream_t st) {
+  int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  int64_t M = (int64_t)B * OH * OW;
+  if (cdiv(M, 128) * (int64_t)cdiv(Cout, 128) >= 160 && Cout > 64)
+    run_conv<T, TO, 128, 128>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+  else
+    run_conv<T, TO, 64, 64>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+}
+}  // namespace
+
+extern "C" int mg_conv2d_fwd(int dtype, const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout,
+                             int KH, int KW, int stride, int pad, const float* in_scale, void* y, int64_t ldy,
+                             int y_dtype, const mg_epilogue* ep, void* stream) {
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
+  MG_REQUIRE(Cin % BK == 0 && pow2(Cin), "Cin must be a power of two >= 32");
+  int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  MG_REQUIRE(pow2(H) && pow2(W) && pow2(OH) && pow2(OW), "spatial sizes must be powers of two");
+  MG_REQUIRE(aligned16(x) && aligned16(wpack), "x/wpack must be 16-byte aligned");
+  MG_REQUIRE(!(ep && ep->atomic) || y_dtype == MG_F32, "atomic epilogue requires fp32 output");
+  if (B == 0) return MG_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_F32) {
+    if (y_dtype == MG_F32) run_conv_tiles<float, float>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, in_scale, y, ldy, ep, st);
+    else run_conv_tiles<float, bf16_t>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, in_scale, y, ldy, ep, st);
+  } else {
+    if (y_dtype == MG_F32) run_conv_tiles<bf16_t, float>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, in_scale, y, ldy, ep, st);
+    else run_conv_tiles<bf16_t, bf16_t>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, in_scale, y, ldy, ep, st);
+  }
+  return mg_check_launch("mg_conv2d_fwd");
+}
+
+namespace {
+template <typename T, int BM, int BN>
+void run_wgrad(const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin, const float* sc, int Cout,
+               int KH, int KW, int stride, int pad, float* gw, int splits, hipStream_t st) {
+  int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  int P = B * OH * OW, N = KH * KW * Cin;
+  LdMC<T> la{reinterpret_cast<const T*>(gy), ldg, Cout, P, nullptr, 1, nullptr, 0, 0};
+  LdMCConv<T> lb{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), P,
+                 KW, stride, pad, N, sc};
+  mg_epilogue e{};
+  e.alpha = 1.f;
+  e.atomic = 1;
+  e.remap_lgcin = ilog2(Cin);
+  e.remap_taps = KH * KW;
+  auto ep = make_epi<float>(gw, N, &e);
+  launch_gemm<T, BM, BN, false, false>(la, lb, ep, Cout, N, P, splits, kNoGroup, 0, st);
+}
+}  // namespace
+
+extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin,
+                               const float* in_scale, int Cout, int KH, int KW, int stride, int pad, float* gw,
+                               int splits, void* stream) {
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
+  const int vec = dtype == MG_F32 ? 4 : 8;
+  int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  MG_REQUIRE(pow2(Cin) && Cin >= vec, "Cin must be a power of two >= vector width");
+  MG_REQUIRE(pow2(OH) && pow2(OW), "output spatial sizes must be powers of two");
+  MG_REQUIRE(Cout % vec == 0 && ldg % vec == 0, "Cout / ldg must be multiples of the vector width");
+  MG_REQUIRE(aligned16(gy) && aligned16(x), "gy/x must be 16-byte aligned");
+  if (B == 0) return MG_OK;
+  if (splits < 1) {  // auto: enough blocks to cover the chip
+    int64_t tiles = (int64_t)cdiv(Cout, 64) * cdiv(KH * KW * Cin, 64);
+    int64_t P = (int64_t)B * OH * OW;
+    splits = (int)std::max<int64_t>(1, std::min<int64_t>(512 / std::max<int64_t>(tiles, 1), P / 256));
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_F32) run_wgrad<float, 64, 64>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
+  else run_wgrad<bf16_t, 64, 64>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
+  return mg_check_launch("mg_conv2d_wgrad");
+}
+
+// ---------------------------------------------------------------------------
+// grouped (per-expert) GEMMs
+// ---------------------------------------------------------------------------
+namespace {
+template <typename T, typename TO, bool BKc>
+void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_off, const int32_t* tile_off,
+                 int max_tiles, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t b_gstride, void* C,
+                 int64_t ldc, const mg_epilogue* e, hipStream_t st) {
+  auto ep = make_epi<TO>(C, ldc, e);
+  ep.gstride_bias = N;
+  const int32_t* aidx = e ? e->a_idx : nullptr;
+  int adiv = (e && e->a_idx_div > 0) ? e->a_idx_div : 1;
+  LdKC<T> la{reinterpret_cast<const T*>(A), lda, total_rows, K, aidx, adiv, e ? e->a_rowscale : nullptr,
+             e ? e->a_gelu : 0};
+  Grouping grp{1, ngroups, row_off, tile_off};
+  if constexpr (BKc) {
+    LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
+    launch_gemm<T, 128, 128, true, true>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+  } else {
+    LdMCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
+    launch_gemm<T, 128, 128, true, false>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+  }
+}
+
+template <typename T>
+void run_grouped_wgrad(int M, int N, int ngroups, const int32_t* row_off, int total_rows, const void* A, int64_t lda,
+                       const void* B, int64_t ldb, const int32_t* b_idx, int b_idx_div, int b_gelu, float* C,
+                       int splits, const mg_epilogue* e, hipStream_t st) {
+  LdMC<T> la{reinterpret_cast<const T*>(A), lda, M, total_rows, e ? e->a_idx : nullptr,
+             (e && e->a_idx_div > 0) ? e->a_idx_div : 1, e ? e->a_rowscale : nullptr, e ? e->a_gelu : 0, 0};
+  LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, total_rows, b_idx, b_idx_div > 0 ? b_idx_div : 1, nullptr,
+             b_gelu, 0};
+  mg_epilogue ee{};
+  ee.alpha = e ? e->alpha : 1.f;
+  ee.atomic = 1;
+  auto ep = make_epi<float>(C, N, &ee);
+  ep.gstride_c = (int64_t)M * N;
+  Grouping grp{2, ngroups, row_off, nullptr};
+  launch_gemm<T, 64, 64, false, false>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
+}
+}  // namespace
+
+extern "C" int mg_gemm_grouped(int dtype, int total_rows, int N, int K, int ngroups, const int32_t* row_off,
+                               const int32_t* tile_off, int max_tiles, const void* A, int64_t lda, const void* B,
+                               int64_t ldb, int b_kc, int64_t b_gstride, void* C, int64_t ldc, int c_dtype,
+                               const mg_epilogue* ep, void* stream) {
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
+  const int vec = dtype == MG_F32 ? 4 : 8;
+  MG_REQUIRE(K % vec == 0 && lda % vec == 0 && ldb % vec == 0, "K/lda/ldb must be multiples of the vector width");
+  MG_REQUIRE(b_kc || N % vec == 0, "N must be a multiple of the vector width for b_kc=0");
+  MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
+  if (max_tiles <= 0 || N == 0) return MG_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define MG_GRP(T, TO)                                                                                           \
+  (b_kc ? run_grouped<T, TO, true>(total_rows, N, K, ngroups, row_off, tile_off, max_tiles, A, lda, B, ldb,     \
+                                   b_gstride, C, ldc, ep, st)                                                    \
+        : run_grouped<T, TO, false>(total_rows, N, K, ngroups, row_off, tile_off, max_tiles, A, lda, B, ldb,    \
+                                    b_gstride, C, ldc, ep, st))
+  if (dtype == MG_F32) {
+    if (c_dtype == MG_F32) MG_GRP(float, float); else MG_GRP(float, bf16_t);
+  } else {
+    if (c_dtype == MG_F32) MG_GRP(bf16_t, float); else MG_GRP(bf16_t, bf16_t);
+  }
+#undef MG_GRP
+  return mg_check_launch("mg_gemm_grouped");
+}
+
+extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const int32_t* row_off, int total_rows,
+                                     const void* A, int64_t lda, const void* B, int64_t ldb, const int32_t* b_idx,
+                                     int b_idx_div, int b_gelu, float* C, int splits, const mg_epilogue* ep,
+                                     void* stream) {
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
+  const int vec = dtype == MG_F32 ? 4 : 8;
+  MG_REQUIRE(M % vec == 0 && N % vec == 0 && lda % vec == 0 && ldb % vec == 0, "M/N/lda/ldb must be vector multiples");
+  MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
+  if (splits < 1) splits = std::max(1, std::min(64, 512 / std::max(1, cdiv(M, 64) * cdiv(N, 64) * ngroups)));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_F32) run_grouped_wgrad<float>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st);
+  else run_grouped_wgrad<bf16_t>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st);
+  return mg_check_launch("mg_gemm_grouped_wgrad");
+}

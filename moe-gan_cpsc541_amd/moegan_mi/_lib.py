@@ -1,0 +1,106 @@
+"""ctypes binding of libmoegan_hip.so (include/moegan_hip.h).
+
+The HIP library is the product: there is no CPU or PyTorch fallback behind
+these calls.  If the shared object is missing or fails to load, ``lib()``
+raises -- the hot path fails loudly instead of silently running elsewhere.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmoegan_hip.so")
+
+MG_F32, MG_BF16 = 0, 1
+ACT_NONE, ACT_LRELU, ACT_GELU, ACT_MUL_GELU_GRAD, ACT_MUL_LRELU_GRAD = 0, 1, 2, 3, 4
+
+_c_void_p, _i32, _i64, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+
+
+class Epilogue(ctypes.Structure):
+    """Mirror of ``mg_epilogue`` (include/moegan_hip.h)."""
+    _fields_ = [("alpha", _f32), ("bias", _c_void_p), ("scale", _c_void_p), ("scale_shift", _i32),
+                ("scale_ld", _i64), ("rowscale", _c_void_p), ("act", _i32), ("aux", _c_void_p),
+                ("ld_aux", _i64), ("resid", _c_void_p), ("ld_res", _i64), ("accumulate", _i32),
+                ("atomic", _i32), ("remap_lgcin", _i32), ("remap_taps", _i32), ("a_idx", _c_void_p),
+                ("a_idx_div", _i32), ("a_rowscale", _c_void_p), ("a_gelu", _i32)]
+
+
+# (name, argtypes) of every exported entry point; restype is int32 unless noted
+_SIGS = {}
+
+
+def _sig(name, *args):
+    _SIGS[name] = args
+
+
+P, I, L, F = _c_void_p, _i32, _i64, _f32
+EP = ctypes.POINTER(Epilogue)
+_sig("mg_version")
+_sig("mg_gemm", I, I, I, I, P, L, I, P, L, I, P, L, I, EP, I, P)
+_sig("mg_conv2d_fwd", I, P, I, I, I, I, P, I, I, I, I, I, P, P, L, I, EP, P)
+_sig("mg_conv2d_wgrad", I, P, L, P, I, I, I, I, P, I, I, I, I, I, P, I, P)
+_sig("mg_gemm_grouped", I, I, I, I, I, P, P, I, P, L, P, L, I, L, P, L, I, EP, P)
+_sig("mg_gemm_grouped_wgrad", I, I, I, I, P, I, P, L, P, L, P, I, I, P, I, EP, P)
+
+_lib = None
+
+
+class MGError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MGError(f"libmoegan_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        h = ctypes.CDLL(LIB_PATH)
+        h.mg_last_error.restype = ctypes.c_char_p
+        for name, args in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = list(args)
+            fn.restype = ctypes.c_int32
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return ["mg_last_error"] + list(_SIGS)
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise MGError(f"{name} failed ({rc}): {lib().mg_last_error().decode()}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dt(t):
+    if t.dtype == torch.float32:
+        return MG_F32
+    if t.dtype == torch.bfloat16:
+        return MG_BF16
+    raise MGError(f"unsupported dtype {t.dtype}")
+
+
+def epilogue(alpha=1.0, bias=None, scale=None, scale_shift=0, scale_ld=0, rowscale=None, act=0, aux=None,
+             ld_aux=0, resid=None, ld_res=0, accumulate=0, atomic=0, remap_lgcin=0, remap_taps=0, a_idx=None,
+             a_idx_div=1, a_rowscale=None, a_gelu=0):
+    e = Epilogue(alpha, ptr(bias), ptr(scale), scale_shift, scale_ld, ptr(rowscale), act, ptr(aux), ld_aux,
+                 ptr(resid), ld_res, accumulate, atomic, remap_lgcin, remap_taps, ptr(a_idx), a_idx_div,
+                 ptr(a_rowscale), a_gelu)
+    # keep the tensors alive until the launch has been enqueued
+    e._keep = (bias, scale, rowscale, aux, resid, a_idx, a_rowscale)
+    return e

@@ -1,0 +1,102 @@
+"""HIP MFMA GEMM / implicit-conv kernels vs plain PyTorch fp32 on the GPU."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from moegan_mi import _lib as L  # noqa: E402
+from moegan_mi import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("M,N,K", [(200, 72, 96), (512, 512, 520), (64, 8, 8), (1000, 136, 64)])
+def test_gemm_orientations(dtype, tol, a_kc, b_kc, M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(0)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    B = torch.randn(N, K, device=DEV, generator=g)
+    ref = A.double() @ B.double().T
+    As = A.to(dtype) if a_kc else A.T.contiguous().to(dtype)
+    Bs = B.to(dtype) if b_kc else B.T.contiguous().to(dtype)
+    if dtype == torch.bfloat16:
+        ref = As.double() @ Bs.double().T if (a_kc and b_kc) else A.to(dtype).double() @ B.to(dtype).double().T
+    C = ops.gemm(As, Bs, M, N, K, a_kc=a_kc, b_kc=b_kc, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert rel(C, ref) < tol
+
+
+def test_gemm_epilogue_bias_act_resid_splitk():
+    g = torch.Generator(device=DEV).manual_seed(1)
+    M, N, K = 300, 256, 1024
+    A = torch.randn(M, K, device=DEV, generator=g)
+    W = torch.randn(N, K, device=DEV, generator=g) / 32
+    b = torch.randn(N, device=DEV, generator=g)
+    R = torch.randn(M, N, device=DEV, generator=g)
+    y = ops.linear(A, W, bias=b, act=L.ACT_GELU, resid=R, ld_res=N)
+    ref = F.gelu(A @ W.T + b) + R
+    assert rel(y, ref) < 1e-5
+    y2 = torch.zeros(M, N, device=DEV)
+    ops.gemm(A, W, M, N, K, out=y2, ep=L.epilogue(atomic=1), splits=4)
+    assert rel(y2, A @ W.T) < 1e-5
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("B,H,Cin,Cout,k,stride,pad", [(3, 8, 64, 96, 3, 1, 1), (2, 16, 128, 32, 3, 1, 1),
+                                                       (2, 4, 512, 256, 1, 1, 0), (2, 16, 128, 256, 4, 2, 1)])
+def test_conv_fwd_wgrad(dtype, tol, B, H, Cin, Cout, k, stride, pad):
+    g = torch.Generator(device=DEV).manual_seed(2)
+    x = torch.randn(B, Cin, H, H, device=DEV, generator=g)
+    w = torch.randn(Cout, Cin, k, k, device=DEV, generator=g) / (Cin * k * k) ** 0.5
+    s = torch.rand(B, Cin, device=DEV, generator=g) + 0.5
+    xs = x * s[:, :, None, None]
+    ref = F.conv2d(xs, w, stride=stride, padding=pad)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(dtype)
+    wp = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().to(dtype)
+    y = ops.conv2d(xn, wp, Cout, k, k, stride, pad, in_scale=s, out_dtype=torch.float32)
+    assert rel(y.permute(0, 3, 1, 2), ref) < tol
+    # weight gradient
+    gy = torch.randn_like(ref)
+    xr = xs.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    (F.conv2d(xr, wr, stride=stride, padding=pad) * gy).sum().backward()
+    gw = torch.zeros_like(w)
+    ops.conv2d_wgrad(gy.permute(0, 2, 3, 1).contiguous().to(dtype), xn, Cout, k, k, stride, pad, gw, in_scale=s)
+    assert rel(gw, wr.grad) < tol * 2
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+def test_grouped_gemm_and_wgrad(dtype, tol):
+    g = torch.Generator(device=DEV).manual_seed(3)
+    E, C, H4 = 4, 64, 256
+    counts = [37, 0, 300, 129]
+    rows = sum(counts)
+    row_off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=DEV)
+    tiles = [(c + 127) // 128 for c in counts]
+    tile_off = torch.tensor([0] + list(torch.tensor(tiles).cumsum(0)), dtype=torch.int32, device=DEV)
+    tok = torch.randn(500, C, device=DEV, generator=g)
+    perm = torch.randint(0, 500 * 2, (rows,), device=DEV, generator=g, dtype=torch.int32)  # assignment ids (t*k+j)
+    W1 = torch.randn(E, H4, C, device=DEV, generator=g) / 8
+    b1 = torch.randn(E, H4, device=DEV, generator=g)
+    out = torch.empty(rows, H4, device=DEV, dtype=dtype)
+    ops.gemm_grouped(tok.to(dtype), W1.to(dtype), row_off, tile_off, sum(tiles) + 2, H4, C, b_gstride=H4 * C,
+                     out=out, ep=L.epilogue(bias=b1, act=L.ACT_GELU, a_idx=perm, a_idx_div=2))
+    ref = torch.empty(rows, H4, device=DEV)
+    src = tok[(perm // 2).long()]
+    for e in range(E):
+        r0, r1 = int(row_off[e]), int(row_off[e + 1])
+        ref[r0:r1] = F.gelu(src[r0:r1] @ W1[e].T + b1[e])
+    assert rel(out, ref) < tol
+    # grouped wgrad: gW[e] = sum_r gP[r]^T tok[perm[r]/2]
+    gP = torch.randn(rows, H4, device=DEV, generator=g)
+    gW = torch.zeros(E, H4, C, device=DEV)
+    ops.gemm_grouped_wgrad(gP.to(dtype), tok.to(dtype), row_off, rows, H4, C, gW, b_idx=perm, b_idx_div=2)
+    refw = torch.stack([gP[int(row_off[e]):int(row_off[e + 1])].T @ src[int(row_off[e]):int(row_off[e + 1])]
+                        for e in range(E)])
+    assert rel(gW, refw) < tol * 2
