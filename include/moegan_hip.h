@@ -36,6 +36,7 @@ extern "C" {
 #define MG_ACT_GELU 2           /* exact-erf GELU  (t2i_moe_gan.py:258) */
 #define MG_ACT_MUL_GELU_GRAD 3  /* v *= GELU'(aux[m,n]) */
 #define MG_ACT_MUL_LRELU_GRAD 4 /* v *= LReLU'(aux[m,n]) */
+#define MG_ACT_RSQRT_EPS 5      /* v = rsqrt(v + 1e-8)  (demodulation, t2i_moe_gan.py:165) */
 
 /* Fused GEMM epilogue / prologue options (all pointers optional = NULL).
  *   v = alpha * acc
@@ -66,6 +67,9 @@ typedef struct mg_epilogue {
   int32_t a_idx_div;
   const float* a_rowscale;
   int32_t a_gelu;
+  const float* addvec; /* v += addvec[(m >> add_shift) * add_ld + n] (per-image broadcast add) */
+  int32_t add_shift;
+  int64_t add_ld;
 } mg_epilogue;
 
 const char* mg_last_error(void);
@@ -98,6 +102,14 @@ int mg_conv2d_fwd(int dtype, const void* x, int B, int H, int W, int Cin, const 
 int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin,
                     const float* in_scale, int Cout, int KH, int KW, int stride, int pad, float* gw, int splits,
                     void* stream);
+
+/* Data gradient of a 4x4 / stride-2 / pad-1 convolution (the discriminator's
+ * conv_layers, t2i_moe_gan.py:876,880), as four output-parity implicit GEMMs:
+ *   out[b, ih, iw, ci] = epilogue( sum_{co,kh,kw} g[b, oh, ow, co] * W[co, ci, kh, kw] ),  ih = 2*oh - 1 + kh
+ * g: [B, OH, OW, Cg] NHWC; out: [B, 2*OH, 2*OW, ldo]; wcls = mg_pack_dgrad_s2() of W.
+ * Used for the ordinary D backward and for the R1 gradient / double-backward (:1282). */
+int mg_conv2d_dgrad_s2(int dtype, const void* g, int B, int OH, int OW, int Cg, const void* wcls, int Cin,
+                       void* out, int64_t ldo, int out_dtype, const mg_epilogue* ep, void* stream);
 
 /* Grouped (per-expert) GEMM, grouped over output rows:
  *   for each group g: rows [row_off[g], row_off[g+1]) of C =

@@ -1,0 +1,317 @@
+// LayerNorm and self-attention kernels of the AttentionBlock (t2i_moe_gan.py:493-576).
+//
+// Token layout: rows = B*L tokens (L = H*W per image), C channels.
+// Self-attention (nn.MultiheadAttention, 8 heads, batch_first) works on the
+// packed projection qkv [rows, 3C] (q | k | v, head h at columns h*d..h*d+d).
+// At this model's sizes (L <= 256, d = C/8 <= 64) one workgroup holds one
+// (image, head) pair entirely in LDS; each thread owns a query row (forward,
+// backward dQ) or a key row (backward dK/dV).  The cross-attention has a
+// single key, so its softmax is identically 1 and it is computed as a per-image
+// vector by plain GEMMs in the host engine (no kernel here).
+#include "mg_common.h"
+
+namespace {
+
+template <typename T, int NPL>  // NPL = C/64 elements per lane
+__global__ void k_ln_fwd(const T* __restrict__ x, int64_t ldx, int R, const float* __restrict__ gamma,
+                         const float* __restrict__ beta, float eps, T* __restrict__ y, int64_t ldy,
+                         float* __restrict__ mean, float* __restrict__ rstd, int act) {
+  int lane = threadIdx.x & 63;
+  int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  constexpr int C = NPL * 64;
+  float v[NPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    v[i] = ldf(x, (int64_t)r * ldx + lane + 64 * i);
+    s += v[i];
+  }
+  float mu = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    float t = v[i] - mu;
+    q += t * t;
+  }
+  float rs = rsqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) {
+    int c = lane + 64 * i;
+    float o = (v[i] - mu) * rs * gamma[c] + beta[c];
+    stf(y, (int64_t)r * ldy + c, act ? lrelu(o) : o);
+  }
+  if (lane == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
+template <typename T, typename TG, int NPL>
+__global__ void k_ln_bwd(const TG* __restrict__ gy, int64_t ldg, const T* __restrict__ x, int64_t ldx, int R,
+                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                         const float* __restrict__ gamma, T* __restrict__ gx, int64_t ldgx, int accumulate,
+                         float* __restrict__ ggamma, float* __restrict__ gbeta, int rows_per_wave) {
+  int lane = threadIdx.x & 63;
+  constexpr int C = NPL * 64;
+  float pg[NPL], pb[NPL];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) pg[i] = pb[i] = 0.f;
+  int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (int rr = 0; rr < rows_per_wave; ++rr) {
+    int r = wave * rows_per_wave + rr;
+    if (r >= R) break;
+    float mu = mean[r], rs = rstd[r];
+    float xh[NPL], gh[NPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      int c = lane + 64 * i;
+      float g = ldf(gy, (int64_t)r * ldg + c);
+      xh[i] = (ldf(x, (int64_t)r * ldx + c) - mu) * rs;
+      gh[i] = g * gamma[c];
+      pg[i] += g * xh[i];
+      pb[i] += g;
+      s1 += gh[i];
+      s2 += gh[i] * xh[i];
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+    if (gx) {
+#pragma unroll
+      for (int i = 0; i < NPL; ++i) {
+        int c = lane + 64 * i;
+        float v = rs * (gh[i] - s1 - xh[i] * s2);
+        if (accumulate) v += ldf(gx, (int64_t)r * ldgx + c);
+        stf(gx, (int64_t)r * ldgx + c, v);
+      }
+    }
+  }
+  if (ggamma) {
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      atomicAdd(ggamma + lane + 64 * i, pg[i]);
+      atomicAdd(gbeta + lane + 64 * i, pb[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// self-attention forward: block = (image b, head h); thread i = query row i
+// ---------------------------------------------------------------------------
+template <typename T, int D>
+__global__ void k_attn_fwd(const T* __restrict__ qkv, int L, int C, int heads, T* __restrict__ out,
+                           float* __restrict__ lse) {
+  extern __shared__ float sm[];
+  float* Ks = sm;
+  float* Vs = sm + L * D;
+  int b = blockIdx.x / heads, h = blockIdx.x - (blockIdx.x / heads) * heads;
+  const int64_t ld = 3LL * C;
+  const T* base = qkv + (int64_t)b * L * ld;
+  for (int e = threadIdx.x; e < L * D; e += blockDim.x) {
+    int j = e / D, c = e - j * D;
+    Ks[e] = ldf(base, (int64_t)j * ld + C + h * D + c);
+    Vs[e] = ldf(base, (int64_t)j * ld + 2 * C + h * D + c);
+  }
+  __syncthreads();
+  int i = threadIdx.x;
+  if (i >= L) return;
+  const float scale = rsqrtf((float)D);
+  float q[D], acc[D];
+#pragma unroll
+  for (int c = 0; c < D; ++c) {
+    q[c] = ldf(base, (int64_t)i * ld + h * D + c) * scale;
+    acc[c] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j < L; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) s += q[c] * Ks[j * D + c];
+    float mn = fmaxf(m, s);
+    float corr = __expf(m - mn);
+    float p = __expf(s - mn);
+    l = l * corr + p;
+#pragma unroll
+    for (int c = 0; c < D; ++c) acc[c] = acc[c] * corr + p * Vs[j * D + c];
+    m = mn;
+  }
+  float inv = 1.f / l;
+  int64_t orow = ((int64_t)b * L + i) * C + h * D;
+#pragma unroll
+  for (int c = 0; c < D; ++c) stf(out, orow + c, acc[c] * inv);
+  lse[((int64_t)b * heads + h) * L + i] = m + __logf(l);
+}
+
+// backward: pass A (thread = query row): dQ; pass B (thread = key row): dK, dV.
+// LDS holds K,V during pass A and Q,dO during pass B (2*L*D floats + 2*L).
+template <typename T, typename TG, int D>
+__global__ void k_attn_bwd(const T* __restrict__ qkv, const T* __restrict__ out, const TG* __restrict__ gout,
+                           const float* __restrict__ lse, int L, int C, int heads, T* __restrict__ gqkv) {
+  extern __shared__ float sm[];
+  float* S0 = sm;
+  float* S1 = S0 + L * D;
+  float* Ls = S1 + L * D;  // lse
+  float* Ds = Ls + L;      // delta_i = dO_i . O_i
+  int b = blockIdx.x / heads, h = blockIdx.x - (blockIdx.x / heads) * heads;
+  const int64_t ld = 3LL * C;
+  const T* base = qkv + (int64_t)b * L * ld;
+  const float scale = rsqrtf((float)D);
+  for (int e = threadIdx.x; e < L * D; e += blockDim.x) {
+    int j = e / D, c = e - j * D;
+    S0[e] = ldf(base, (int64_t)j * ld + C + h * D + c);      // K
+    S1[e] = ldf(base, (int64_t)j * ld + 2 * C + h * D + c);  // V
+  }
+  int t = threadIdx.x;
+  float q[D], g[D];
+  int64_t grow = ((int64_t)b * L + t) * C + h * D;
+  if (t < L) {
+    float dsum = 0.f;
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      q[c] = ldf(base, (int64_t)t * ld + h * D + c) * scale;
+      g[c] = ldf(gout, grow + c);
+      dsum += g[c] * ldf(out, grow + c);
+    }
+    Ds[t] = dsum;
+    Ls[t] = lse[((int64_t)b * heads + h) * L + t];
+  }
+  __syncthreads();
+  int64_t row = ((int64_t)b * L + t) * ld + h * D;
+  if (t < L) {
+    float dq[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) dq[c] = 0.f;
+    float li = Ls[t], di = Ds[t];
+    for (int j = 0; j < L; ++j) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        s += q[c] * S0[j * D + c];
+        dp += g[c] * S1[j * D + c];
+      }
+      float ds = __expf(s - li) * (dp - di);
+#pragma unroll
+      for (int c = 0; c < D; ++c) dq[c] += ds * S0[j * D + c];
+    }
+#pragma unroll
+    for (int c = 0; c < D; ++c) stf(gqkv, row + c, dq[c] * scale);
+  }
+  __syncthreads();
+  if (t < L) {
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      S0[t * D + c] = q[c];  // Q (scaled)
+      S1[t * D + c] = g[c];  // dO
+    }
+  }
+  __syncthreads();
+  if (t < L) {
+    float k[D], v[D], dk[D], dv[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      k[c] = ldf(base, (int64_t)t * ld + C + h * D + c);
+      v[c] = ldf(base, (int64_t)t * ld + 2 * C + h * D + c);
+      dk[c] = dv[c] = 0.f;
+    }
+    for (int i = 0; i < L; ++i) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        s += S0[i * D + c] * k[c];
+        dp += S1[i * D + c] * v[c];
+      }
+      float p = __expf(s - Ls[i]);
+      float ds = p * (dp - Ds[i]);
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        dv[c] += p * S1[i * D + c];
+        dk[c] += ds * S0[i * D + c];  // S0 carries the 1/sqrt(D) scale
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      stf(gqkv, row + C + c, dk[c]);
+      stf(gqkv, row + 2 * C + c, dv[c]);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int mg_layernorm_fwd(int dtype, const void* x, int64_t ldx, int R, int C, const float* gamma,
+                                const float* beta, float eps, void* y, int64_t ldy, float* mean, float* rstd, int act,
+                                void* stream) {
+  MG_REQUIRE(C == 128 || C == 256 || C == 512, "C must be 128, 256 or 512");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (R == 0) return MG_OK;
+  dim3 grid(cdiv(R, 4)), blk(256);
+#define L_(T, N) hipLaunchKernelGGL((k_ln_fwd<T, N>), grid, blk, 0, st, (const T*)x, ldx, R, gamma, beta, eps, (T*)y, ldy, mean, rstd, act)
+  if (dtype == MG_F32) {
+    if (C == 128) L_(float, 2); else if (C == 256) L_(float, 4); else L_(float, 8);
+  } else {
+    if (C == 128) L_(bf16_t, 2); else if (C == 256) L_(bf16_t, 4); else L_(bf16_t, 8);
+  }
+#undef L_
+  return mg_check_launch("mg_layernorm_fwd");
+}
+
+extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t ldg, const void* x, int64_t ldx,
+                                int R, int C, const float* mean, const float* rstd, const float* gamma, void* gx,
+                                int64_t ldgx, int accumulate, float* ggamma, float* gbeta, void* stream) {
+  MG_REQUIRE(C == 128 || C == 256 || C == 512, "C must be 128, 256 or 512");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (R == 0) return MG_OK;
+  int rpw = std::max(1, std::min(64, R / 1024));
+  dim3 grid(cdiv(cdiv(R, rpw), 4)), blk(256);
+#define L_(T, TG, N) hipLaunchKernelGGL((k_ln_bwd<T, TG, N>), grid, blk, 0, st, (const TG*)gy, ldg, (const T*)x, ldx, R, \
+                                        mean, rstd, gamma, (T*)gx, ldgx, accumulate, ggamma, gbeta, rpw)
+#define LC_(T, TG) if (C == 128) L_(T, TG, 2); else if (C == 256) L_(T, TG, 4); else L_(T, TG, 8)
+  if (dtype == MG_F32) {
+    if (gy_dtype == MG_F32) { LC_(float, float); } else { LC_(float, bf16_t); }
+  } else {
+    if (gy_dtype == MG_F32) { LC_(bf16_t, float); } else { LC_(bf16_t, bf16_t); }
+  }
+#undef LC_
+#undef L_
+  return mg_check_launch("mg_layernorm_bwd");
+}
+
+extern "C" int mg_attn_fwd(int dtype, const void* qkv, int B, int L, int C, int heads, void* out, float* lse,
+                           void* stream) {
+  int D = C / heads;
+  MG_REQUIRE(D == 16 || D == 32 || D == 64, "head dim must be 16, 32 or 64");
+  MG_REQUIRE(L <= 1024, "at most 1024 tokens per image");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int thr = std::max(64, ((L + 63) / 64) * 64);
+  size_t sm = 2 * (size_t)L * D * sizeof(float);
+#define L_(T, DD) hipLaunchKernelGGL((k_attn_fwd<T, DD>), dim3(B * heads), dim3(thr), sm, st, (const T*)qkv, L, C, heads, (T*)out, lse)
+  if (dtype == MG_F32) {
+    if (D == 16) L_(float, 16); else if (D == 32) L_(float, 32); else L_(float, 64);
+  } else {
+    if (D == 16) L_(bf16_t, 16); else if (D == 32) L_(bf16_t, 32); else L_(bf16_t, 64);
+  }
+#undef L_
+  return mg_check_launch("mg_attn_fwd");
+}
+
+extern "C" int mg_attn_bwd(int dtype, int gout_dtype, const void* qkv, const void* out, const void* gout,
+                           const float* lse, int B, int L, int C, int heads, void* gqkv, void* stream) {
+  int D = C / heads;
+  MG_REQUIRE(D == 16 || D == 32 || D == 64, "head dim must be 16, 32 or 64");
+  MG_REQUIRE(L <= 1024, "at most 1024 tokens per image");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int thr = std::max(64, ((L + 63) / 64) * 64);
+  size_t sm = (2 * (size_t)L * D + 2 * (size_t)L) * sizeof(float);
+#define L_(T, TG, DD) hipLaunchKernelGGL((k_attn_bwd<T, TG, DD>), dim3(B * heads), dim3(thr), sm, st, (const T*)qkv, \
+                                         (const T*)out, (const TG*)gout, lse, L, C, heads, (T*)gqkv)
+#define LD_(T, TG) if (D == 16) L_(T, TG, 16); else if (D == 32) L_(T, TG, 32); else L_(T, TG, 64)
+  if (dtype == MG_F32) {
+    if (gout_dtype == MG_F32) { LD_(float, float); } else { LD_(float, bf16_t); }
+  } else {
+    if (gout_dtype == MG_F32) { LD_(bf16_t, float); } else { LD_(bf16_t, bf16_t); }
+  }
+#undef LD_
+#undef L_
+  return mg_check_launch("mg_attn_bwd");
+}

@@ -1,0 +1,336 @@
+// Discriminator pieces not covered by the implicit-GEMM convs (t2i_moe_gan.py:858-907)
+// and the GAN / R1 loss reductions of the training step (t2i_moe_gan.py:1276-1312, :1379-1382).
+//
+//  * conv_layers.0 (3 -> 128, 4x4 / s2 / p1) has K = 48: an explicit im2col
+//    (K padded to the vector width) feeds the generic GEMM, forward and weight-grad.
+//  * output_layer (384 -> 1, 4x4 valid) has N = 1: a bandwidth-bound direct
+//    kernel.  Its 128 text channels are spatially constant, so their
+//    contribution is a per-image scalar tb[b] computed by a GEMV on the host
+//    side; the kernel below handles the 256 image channels.
+//  * R1 needs the gradient of sum(out) w.r.t. the image: the head's part of it
+//    is the same for every image (it only depends on W2), so it is built once
+//    with a broadcast "gradient of ones".
+#include "mg_common.h"
+
+namespace {
+
+// im2col for a 4x4 / stride-2 / pad-1 conv: row = output pixel, col = (kh*4+kw)*C + c, padded to Kp
+template <typename TI, typename TO>
+__global__ void k_im2col(const TI* __restrict__ x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H,
+                         int W, int C, int Kp, TO* __restrict__ out) {
+  int OH = H / 2, OW = W / 2;
+  int64_t n = (int64_t)B * OH * OW * Kp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int k = (int)(i % Kp);
+    int64_t r = i / Kp;
+    float v = 0.f;
+    if (k < 16 * C) {
+      int tap = k / C, c = k - (k / C) * C;
+      int kh = tap >> 2, kw = tap & 3;
+      int ow = (int)(r % OW), oh = (int)((r / OW) % OH), b = (int)(r / ((int64_t)OW * OH));
+      int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = ldf(x, b * sb + ih * sh + iw * sw + c * sc);
+    }
+    stf(out, i, v);
+  }
+}
+
+// head, image channels: out[b, o] = sum_{c<256, kh, kw} h1[b, oy+kh, ox+kw, c] * W2[c, kh, kw]
+// one wave per output pixel; lanes over channels
+template <typename T>
+__global__ void k_head_fwd(const T* __restrict__ h1, const float* __restrict__ W2, int B, int Hf, int Cf,
+                           float* __restrict__ out) {
+  int Ho = Hf - 3;
+  int64_t n = (int64_t)B * Ho * Ho;
+  int lane = threadIdx.x & 63;
+  int64_t o = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (o >= n) return;
+  int b = (int)(o / (Ho * Ho));
+  int rem = (int)(o - (int64_t)b * Ho * Ho);
+  int oy = rem / Ho, ox = rem - (rem / Ho) * Ho;
+  float s = 0.f;
+  for (int tap = 0; tap < 16; ++tap) {
+    int kh = tap >> 2, kw = tap & 3;
+    const T* row = h1 + (((int64_t)b * Hf + oy + kh) * Hf + ox + kw) * Cf;
+    for (int c = lane; c < Cf; c += 64) s += ldf(row, c) * W2[c * 16 + tap];
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[o] = s;
+}
+
+// head backward into the image features, fused with conv_layers.2's LeakyReLU:
+//   g_a1[b, y, x, c] = lrelu'(a1[b,y,x,c]) * sum_{oy,ox} g[b, oy, ox] * W2[c, y-oy, x-ox]
+// g_bstride = 0 broadcasts one gradient map to every image (R1: gradient of sum(out)).
+template <typename T, typename TO>
+__global__ void k_head_bwd_data(const float* __restrict__ g, int64_t g_bstride, const float* __restrict__ W2,
+                                const T* __restrict__ a1, int B, int Hf, int Cf, TO* __restrict__ ga1) {
+  int Ho = Hf - 3;
+  int64_t n = (int64_t)B * Hf * Hf * Cf;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % Cf);
+    int64_t pix = i / Cf;
+    int x = (int)(pix % Hf), y = (int)((pix / Hf) % Hf), b = (int)(pix / ((int64_t)Hf * Hf));
+    const float* gb = g + (int64_t)b * g_bstride;
+    float s = 0.f;
+    for (int kh = 0; kh < 4; ++kh) {
+      int oy = y - kh;
+      if (oy < 0 || oy >= Ho) continue;
+      for (int kw = 0; kw < 4; ++kw) {
+        int ox = x - kw;
+        if (ox < 0 || ox >= Ho) continue;
+        s += gb[oy * Ho + ox] * W2[c * 16 + kh * 4 + kw];
+      }
+    }
+    if (a1) s *= lrelu_grad(ldf(a1, i));
+    stf(ga1, i, s);
+  }
+}
+
+// dW2[c, tap] += sum_b sum_o g[b, o] * h1[b, o + tap, c]   (block per image, thread per channel)
+template <typename T>
+__global__ void k_head_bwd_w(const float* __restrict__ g, int64_t g_bstride, const T* __restrict__ h1, int Hf,
+                             int Cf, float* __restrict__ dW2) {
+  int b = blockIdx.x;
+  int c = threadIdx.x;
+  if (c >= Cf) return;
+  int Ho = Hf - 3;
+  const float* gb = g + (int64_t)b * g_bstride;
+  float acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = 0.f;
+  for (int oy = 0; oy < Ho; ++oy)
+    for (int ox = 0; ox < Ho; ++ox) {
+      float gv = gb[oy * Ho + ox];
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+        acc[t] += gv * ldf(h1, (((int64_t)b * Hf + oy + (t >> 2)) * Hf + ox + (t & 3)) * Cf + c);
+    }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) atomicAdd(&dW2[c * 16 + t], acc[t]);
+}
+
+// D loss (t2i_moe_gan.py:940-949, :1309).  img_real = image part of the 64x64 real logits
+// [B, No]; img_fake = image part of the 16x16 fake logits [B]; tb[b] = text part + bias of
+// image b's caption.  real = img_real + tb[b]; mism = img_real + tb[perm[b]]; fake = img_fake + tb[b].
+// out (zeroed by caller): [0] d_loss_gan, [1] mean softplus(-real), [2] mean softplus(fake), [3] mean softplus(mism)
+// g_img_real / g_img_fake: d loss / d image-part logits; g_tb (zeroed): d loss / d tb.
+__global__ void k_d_loss(const float* __restrict__ img, const float* __restrict__ img_fake,
+                         const float* __restrict__ tb, const int* __restrict__ perm, int B, int No,
+                         float* __restrict__ out, float* __restrict__ g_img, float* __restrict__ g_fake,
+                         float* __restrict__ g_tb, float* __restrict__ real_out, float* __restrict__ mism_out,
+                         float* __restrict__ fake_out) {
+  __shared__ float red[4][16];
+  int b = blockIdx.x;
+  float sr = 0.f, sm = 0.f, gr = 0.f, gm = 0.f;
+  float inv = 1.f / ((float)B * No);
+  if (b < B) {
+    float tr = tb[b], tm = tb[perm[b]];
+    for (int o = threadIdx.x; o < No; o += blockDim.x) {
+      float base = img[(int64_t)b * No + o];
+      float r = base + tr, m = base + tm;
+      if (real_out) real_out[(int64_t)b * No + o] = r;
+      if (mism_out) mism_out[(int64_t)b * No + o] = m;
+      float spr = (-r > 20.f) ? -r : log1pf(expf(-r));  // softplus, torch threshold 20
+      float spm = (m > 20.f) ? m : log1pf(expf(m));
+      sr += spr;
+      sm += spm;
+      float dr = -1.f / (1.f + expf(r)) * inv;  // d softplus(-r)/dr = -sigmoid(-r)
+      float dm = 1.f / (1.f + expf(-m)) * inv;
+      g_img[(int64_t)b * No + o] = dr + dm;
+      gr += dr;
+      gm += dm;
+    }
+    sr = wave_sum(sr); sm = wave_sum(sm); gr = wave_sum(gr); gm = wave_sum(gm);
+    int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = sr; red[1][w] = sm; red[2][w] = gr; red[3][w] = gm; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float a = 0, c = 0, d = 0, e = 0;
+      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { a += red[0][i]; c += red[1][i]; d += red[2][i]; e += red[3][i]; }
+      atomicAdd(&out[1], a * inv);
+      atomicAdd(&out[3], c * inv);
+      atomicAdd(&out[0], (a + c) * inv);
+      atomicAdd(&g_tb[b], d);
+      atomicAdd(&g_tb[perm[b]], e);
+    }
+  } else {
+    float sf = 0.f;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) {
+      float f = img_fake[i] + tb[i];
+      if (fake_out) fake_out[i] = f;
+      sf += (f > 20.f) ? f : log1pf(expf(f));
+      float gf = 1.f / (1.f + expf(-f)) / B;
+      g_fake[i] = gf;
+      atomicAdd(&g_tb[i], gf);
+    }
+    sf = wave_sum(sf);
+    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = sf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float a = 0;
+      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) a += red[0][i];
+      atomicAdd(&out[2], a / B);
+      atomicAdd(&out[0], a / B);
+    }
+  }
+}
+
+// G adversarial loss softplus(-f).mean() (t2i_moe_gan.py:919) and its gradient
+__global__ void k_g_loss(const float* __restrict__ fake, int B, float scale, float* __restrict__ out,
+                         float* __restrict__ g) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    float f = fake[i];
+    s += (-f > 20.f) ? -f : log1pf(expf(-f));
+    g[i] = -1.f / (1.f + expf(f)) / B * scale;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) a += red[i];
+    out[0] = a / B;
+  }
+}
+
+// R1 (t2i_moe_gan.py:1285-1286): r1 = gamma/2 * mean_b ||g_b||^2; u = gamma/B * g  (d r1 / d g)
+template <typename T, typename TU>
+__global__ void k_r1(const T* __restrict__ g, int64_t per, int B, float gamma, float* __restrict__ r1,
+                     TU* __restrict__ u) {
+  __shared__ float red[16];
+  int b = blockIdx.y;
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < per; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = ldf(g, (int64_t)b * per + i);
+    s += v * v;
+    if (u) stf(u, (int64_t)b * per + i, gamma / B * v);
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) a += red[i];
+    atomicAdd(r1, a * gamma * 0.5f / B);
+  }
+}
+
+// out = a * lrelu'(m)  (elementwise; m = pre- or post-activation, same sign)
+template <typename T, typename TM, typename TO>
+__global__ void k_mask_mul(const T* __restrict__ a, const TM* __restrict__ m, int64_t n, TO* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    stf(out, i, ldf(a, i) * lrelu_grad(ldf(m, i)));
+}
+
+// text branch of the head (t2i_moe_gan.py:895-902): tb[b] = sum_c t[b,c] * w2sum[c] (+ bias)
+//   g_tpre[b,c] = g_tb[b] * w2sum[c] * lrelu'(t[b,c]);  dW2[256+c, tap] += sum_b g_tb[b] * t[b,c]  (all 16 taps)
+__global__ void k_d_text_bwd(const float* __restrict__ g_tb, const float* __restrict__ t,
+                             const float* __restrict__ w2sum, int B, int Ct, int cofs, float* __restrict__ g_tpre,
+                             float* __restrict__ dW2) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= Ct) return;
+  float acc = 0.f;
+  for (int b = 0; b < B; ++b) {
+    float tv = t[(int64_t)b * Ct + c];
+    acc += g_tb[b] * tv;
+    g_tpre[(int64_t)b * Ct + c] = g_tb[b] * w2sum[c] * lrelu_grad(tv);
+  }
+  for (int tap = 0; tap < 16; ++tap) dW2[(int64_t)(cofs + c) * 16 + tap] += acc;
+}
+
+inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
+
+}  // namespace
+
+extern "C" int mg_d_text_bwd(const float* g_tb, const float* t, const float* w2sum, int B, int Ct, int cofs,
+                             float* g_tpre, float* dW2, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_d_text_bwd, dim3(cdiv(Ct, 128)), dim3(128), 0, st, g_tb, t, w2sum, B, Ct, cofs, g_tpre, dW2);
+  return mg_check_launch("mg_d_text_bwd");
+}
+
+extern "C" int mg_im2col_4x4s2(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B,
+                               int H, int W, int C, int Kp, int out_dtype, void* out, void* stream) {
+  MG_REQUIRE(Kp >= 16 * C, "Kp too small");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)B * (H / 2) * (W / 2) * Kp;
+#define L_(TI, TO) hipLaunchKernelGGL((k_im2col<TI, TO>), dim3(nblk(n)), dim3(256), 0, st, (const TI*)x, sb, sh, sw, sc, B, H, W, C, Kp, (TO*)out)
+  if (in_dtype == MG_F32) { if (out_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+  else { if (out_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+  return mg_check_launch("mg_im2col_4x4s2");
+}
+
+extern "C" int mg_disc_head_fwd(int dtype, const void* h1, const float* W2, int B, int Hf, int Cf, float* out,
+                                void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)B * (Hf - 3) * (Hf - 3);
+  dim3 grid((unsigned)((n + 3) / 4));
+  if (dtype == MG_F32) hipLaunchKernelGGL(k_head_fwd<float>, grid, dim3(256), 0, st, (const float*)h1, W2, B, Hf, Cf, out);
+  else hipLaunchKernelGGL(k_head_fwd<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)h1, W2, B, Hf, Cf, out);
+  return mg_check_launch("mg_disc_head_fwd");
+}
+
+extern "C" int mg_disc_head_bwd_data(int dtype, const float* g, int64_t g_bstride, const float* W2, const void* a1,
+                                     int B, int Hf, int Cf, int out_dtype, void* ga1, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)B * Hf * Hf * Cf;
+#define L_(T, TO) hipLaunchKernelGGL((k_head_bwd_data<T, TO>), dim3(nblk(n)), dim3(256), 0, st, g, g_bstride, W2, (const T*)a1, B, Hf, Cf, (TO*)ga1)
+  if (dtype == MG_F32) { if (out_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+  else { if (out_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+  return mg_check_launch("mg_disc_head_bwd_data");
+}
+
+extern "C" int mg_disc_head_bwd_w(int dtype, const float* g, int64_t g_bstride, const void* h1, int B, int Hf, int Cf,
+                                  float* dW2, void* stream) {
+  MG_REQUIRE(Cf <= 1024, "Cf <= 1024");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int thr = ((Cf + 63) / 64) * 64;
+  if (dtype == MG_F32) hipLaunchKernelGGL(k_head_bwd_w<float>, dim3(B), dim3(thr), 0, st, g, g_bstride, (const float*)h1, Hf, Cf, dW2);
+  else hipLaunchKernelGGL(k_head_bwd_w<bf16_t>, dim3(B), dim3(thr), 0, st, g, g_bstride, (const bf16_t*)h1, Hf, Cf, dW2);
+  return mg_check_launch("mg_disc_head_bwd_w");
+}
+
+extern "C" int mg_d_loss(const float* img_real, const float* img_fake, const float* tb, const int32_t* perm, int B,
+                         int No, float* out, float* g_img, float* g_fake, float* g_tb, float* real_out,
+                         float* mism_out, float* fake_out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_d_loss, dim3(B + 1), dim3(256), 0, st, img_real, img_fake, tb, perm, B, No, out, g_img, g_fake,
+                     g_tb, real_out, mism_out, fake_out);
+  return mg_check_launch("mg_d_loss");
+}
+
+extern "C" int mg_g_loss(const float* fake, int B, float scale, float* out, float* g, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_g_loss, dim3(1), dim3(256), 0, st, fake, B, scale, out, g);
+  return mg_check_launch("mg_g_loss");
+}
+
+extern "C" int mg_r1(int dtype, const void* g, int64_t per, int B, float gamma, float* r1, int u_dtype, void* u,
+                     void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)std::min<int64_t>((per + 255) / 256, 64), B);
+#define L_(T, TU) hipLaunchKernelGGL((k_r1<T, TU>), grid, dim3(256), 0, st, (const T*)g, per, B, gamma, r1, (TU*)u)
+  if (dtype == MG_F32) { if (u_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+  else { if (u_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+  return mg_check_launch("mg_r1");
+}
+
+extern "C" int mg_lrelu_mask_mul(int a_dtype, const void* a, int m_dtype, const void* m, int64_t n, int out_dtype,
+                                 void* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define L_(T, TM, TO) hipLaunchKernelGGL((k_mask_mul<T, TM, TO>), dim3(nblk(n)), dim3(256), 0, st, (const T*)a, (const TM*)m, n, (TO*)out)
+  if (a_dtype == MG_F32) {
+    if (m_dtype == MG_F32) { if (out_dtype == MG_F32) L_(float, float, float); else L_(float, float, bf16_t); }
+    else { if (out_dtype == MG_F32) L_(float, bf16_t, float); else L_(float, bf16_t, bf16_t); }
+  } else {
+    if (m_dtype == MG_F32) { if (out_dtype == MG_F32) L_(bf16_t, float, float); else L_(bf16_t, float, bf16_t); }
+    else { if (out_dtype == MG_F32) L_(bf16_t, bf16_t, float); else L_(bf16_t, bf16_t, bf16_t); }
+  }
+#undef L_
+  return mg_check_launch("mg_lrelu_mask_mul");
+}

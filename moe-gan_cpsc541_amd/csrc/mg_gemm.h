@@ -174,6 +174,40 @@ struct LdMCConv {
   }
 };
 
+// KC, data gradient of a 4x4 / stride-2 / pad-1 convolution ("transposed conv"),
+// split into the 4 output-parity classes (py, px).  Row r (class-major) =
+// (class, b, i, j) -> input-grid pixel (b, 2i+py, 2j+px); k = t*Cg + co with
+// t = ty*2 + tx the 2x2 taps of that class reading g[b, i+dy, j+dx, co].
+template <typename T>
+struct LdKCConvT {
+  const T* g; int OH, OW, Cg, lgCg, lgOW, lgOHW, Mc, K;
+  int cls;
+  struct RowState { int b, i, j; };
+  struct ColState {};
+  MG_DEV void set_group(int c) { cls = c; }
+  MG_DEV RowState row(int r) const {
+    RowState st;
+    if (r == 0x7fffffff) { st.b = -1; st.i = st.j = 0; return st; }
+    int rem = r - cls * Mc;
+    st.b = rem >> lgOHW;
+    st.i = (rem >> lgOW) & ((1 << (lgOHW - lgOW)) - 1);
+    st.j = rem & ((1 << lgOW) - 1);
+    return st;
+  }
+  MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
+    if (st.b < 0 || k0 >= K) return vzero<T>();
+    int t = k0 >> lgCg;
+    int co = (k0 & (Cg - 1)) + kofs;
+    int ty = t >> 1, tx = t & 1;
+    int py = cls >> 1, px = cls & 1;
+    int dy = py ? (ty ? 0 : 1) : (ty ? -1 : 0);
+    int dx = px ? (tx ? 0 : 1) : (tx ? -1 : 0);
+    int oh = st.i + dy, ow = st.j + dx;
+    if (oh < 0 || oh >= OH || ow < 0 || ow >= OW) return vzero<T>();
+    return *reinterpret_cast<const typename VecOf<T>::type*>(g + (((int64_t)st.b * OH + oh) * OW + ow) * Cg + co);
+  }
+};
+
 // Grouped B operand: KC rows of a per-group weight (base + g*gstride).
 template <typename T>
 struct LdKCGroupW {
@@ -206,7 +240,7 @@ struct LdMCGroupW {
 // ---------------------------------------------------------------------------
 // Epilogue
 // ---------------------------------------------------------------------------
-enum { ACT_NONE = 0, ACT_LRELU = 1, ACT_GELU = 2, ACT_MUL_GELU_GRAD = 3, ACT_MUL_LRELU_GRAD = 4 };
+enum { ACT_NONE = 0, ACT_LRELU = 1, ACT_GELU = 2, ACT_MUL_GELU_GRAD = 3, ACT_MUL_LRELU_GRAD = 4, ACT_RSQRT_EPS = 5 };
 
 template <typename TO>
 struct Epi {
@@ -220,6 +254,8 @@ struct Epi {
   int accumulate;  // C += v (non-atomic)
   int atomic;      // fp32 atomic add (split-K / scatter)
   int remap_lgcin, remap_taps;  // weight-grad layout remap when remap_taps > 0
+  const float* addvec; int add_shift; int64_t add_ld;  // v += addvec[(m >> add_shift)*add_ld + n]
+  int rm_mode, rm_Mc, rm_lgOW, rm_lgOHW;  // rm_mode 1: stride-2 transposed-conv class rows -> NHWC rows
   int g;
   MG_DEV void set_group(int gg) { g = gg; }
   MG_DEV void operator()(int m, int n, float v) const {
@@ -230,7 +266,15 @@ struct Epi {
     else if (act == ACT_GELU) v = gelu_erf(v);
     else if (act == ACT_MUL_GELU_GRAD) v *= gelu_erf_grad(ldf(aux, (int64_t)m * ld_aux + n));
     else if (act == ACT_MUL_LRELU_GRAD) v *= lrelu_grad(ldf(aux, (int64_t)m * ld_aux + n));
+    else if (act == ACT_RSQRT_EPS) v = rsqrtf(v + 1e-8f);
     if (rowscale) v *= rowscale[m];
+    if (addvec) v += addvec[(int64_t)(m >> add_shift) * add_ld + n];
+    if (rm_mode == 1) {  // class-major (py,px,b,i,j) -> NHWC row (b, 2i+py, 2j+px)
+      int cls = m / rm_Mc, rem = m - cls * rm_Mc;
+      int b = rem >> rm_lgOHW, i = (rem >> rm_lgOW) & ((1 << (rm_lgOHW - rm_lgOW)) - 1), j = rem & ((1 << rm_lgOW) - 1);
+      int OW2 = 2 << rm_lgOW, OH2 = 2 << (rm_lgOHW - rm_lgOW);
+      m = (b * OH2 + 2 * i + (cls >> 1)) * OW2 + 2 * j + (cls & 1);
+    }
     if (resid) v += ldf(resid, (int64_t)m * ld_res + n);
     int64_t nn = n;
     if (remap_taps > 0) nn = (int64_t)(n & ((1 << remap_lgcin) - 1)) * remap_taps + (n >> remap_lgcin);
@@ -250,6 +294,7 @@ struct Grouping {
   int ngroups;
   const int* row_off;    // [ngroups+1] row (mode 1) / reduction (mode 2) offsets
   const int* tile_off;   // mode 1: [ngroups+1] prefix of ceil(rows_g / BM)
+  int rows_per_group;    // mode 3: ngroups equal groups of this many rows (no tables)
 };
 
 // ---------------------------------------------------------------------------
@@ -286,6 +331,13 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
     mrow_base = grp.row_off[g];
     Mloc = grp.row_off[g + 1] - mrow_base;
     m0 = (t - grp.tile_off[g]) * BM;
+  } else if (grp.mode == 3) {
+    int tpg = (grp.rows_per_group + BM - 1) / BM;
+    g = blockIdx.x / tpg;
+    if (g >= grp.ngroups) return;
+    mrow_base = g * grp.rows_per_group;
+    Mloc = grp.rows_per_group;
+    m0 = (blockIdx.x - g * tpg) * BM;
   } else if (grp.mode == 2) {
     int splits = gridDim.z / grp.ngroups;
     g = blockIdx.z / splits;
@@ -428,7 +480,7 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   if (grp.mode != 2 && splits > 1) kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
   if (grp.mode != 2) splits = (K + kchunk - 1) / kchunk;
   if (splits < 1) splits = 1;
-  int gx = grp.mode == 1 ? max_tiles_m : cdiv(M, BM);
+  int gx = grp.mode == 1 ? max_tiles_m : grp.mode == 3 ? cdiv(grp.rows_per_group, BM) * grp.ngroups : cdiv(M, BM);
   int gz = grp.mode == 2 ? splits * grp.ngroups : splits;
   dim3 grid(gx, cdiv(N, BN), gz);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP>), grid, dim3(NTHREADS), 0, st, A, B, ep, M, N,

@@ -29,6 +29,12 @@ Epi<TO> make_epi(void* C, int64_t ldc, const mg_epilogue* e) {
   ep.atomic = e ? e->atomic : 0;
   ep.remap_lgcin = e ? e->remap_lgcin : 0;
   ep.remap_taps = e ? e->remap_taps : 0;
+  ep.addvec = e ? e->addvec : nullptr;
+  ep.add_shift = e ? e->add_shift : 0;
+  ep.add_ld = e ? e->add_ld : 0;
+  ep.rm_mode = 0;
+  ep.rm_Mc = 1;
+  ep.rm_lgOW = ep.rm_lgOHW = 0;
   ep.g = 0;
   return ep;
 }
@@ -41,7 +47,7 @@ inline int ilog2(int v) {
 }
 inline bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 
-constexpr Grouping kNoGroup{0, 1, nullptr, nullptr};
+constexpr Grouping kNoGroup{0, 1, nullptr, nullptr, 0};
 
 template <typename T, typename TO, int BM, int BN, bool AK, bool BKc>
 void run_plain(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
@@ -222,7 +228,7 @@ void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_o
   int adiv = (e && e->a_idx_div > 0) ? e->a_idx_div : 1;
   LdKC<T> la{reinterpret_cast<const T*>(A), lda, total_rows, K, aidx, adiv, e ? e->a_rowscale : nullptr,
              e ? e->a_gelu : 0};
-  Grouping grp{1, ngroups, row_off, tile_off};
+  Grouping grp{1, ngroups, row_off, tile_off, 0};
   if constexpr (BKc) {
     LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
     launch_gemm<T, 128, 128, true, true>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
@@ -245,7 +251,7 @@ void run_grouped_wgrad(int M, int N, int ngroups, const int32_t* row_off, int to
   ee.atomic = 1;
   auto ep = make_epi<float>(C, N, &ee);
   ep.gstride_c = (int64_t)M * N;
-  Grouping grp{2, ngroups, row_off, nullptr};
+  Grouping grp{2, ngroups, row_off, nullptr, 0};
   launch_gemm<T, 64, 64, false, false>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
 }
 }  // namespace
@@ -288,4 +294,46 @@ extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const
   if (dtype == MG_F32) run_grouped_wgrad<float>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st);
   else run_grouped_wgrad<bf16_t>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st);
   return mg_check_launch("mg_gemm_grouped_wgrad");
+}
+
+// ---------------------------------------------------------------------------
+// data gradient of a 4x4 / stride-2 / pad-1 conv (discriminator convs, R1 path)
+// ---------------------------------------------------------------------------
+namespace {
+template <typename T, typename TO>
+void run_dgrad_s2(const void* g, int B, int OH, int OW, int Cg, const void* wcls, int Cin, void* out, int64_t ldo,
+                  const mg_epilogue* e, hipStream_t st) {
+  int Mc = B * OH * OW;
+  LdKCConvT<T> la{reinterpret_cast<const T*>(g), OH, OW, Cg, ilog2(Cg), ilog2(OW), ilog2(OH * OW), Mc, 4 * Cg, 0};
+  LdKCGroupW<T> lb{reinterpret_cast<const T*>(wcls), 4 * Cg, Cin, 4 * Cg, (int64_t)Cin * 4 * Cg, nullptr};
+  auto ep = make_epi<TO>(out, ldo, e);
+  ep.rm_mode = 1;
+  ep.rm_Mc = Mc;
+  ep.rm_lgOW = ilog2(OW);
+  ep.rm_lgOHW = ilog2(OH * OW);
+  Grouping grp{3, 4, nullptr, nullptr, Mc};
+  if (Cin >= 128)
+    launch_gemm<T, 128, 128, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);
+  else
+    launch_gemm<T, 64, 64, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);
+}
+}  // namespace
+
+extern "C" int mg_conv2d_dgrad_s2(int dtype, const void* g, int B, int OH, int OW, int Cg, const void* wcls, int Cin,
+                                  void* out, int64_t ldo, int out_dtype, const mg_epilogue* ep, void* stream) {
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
+  MG_REQUIRE(pow2(Cg) && Cg >= BK, "Cg must be a power of two >= 32");
+  MG_REQUIRE(pow2(OH) && pow2(OW), "OH, OW must be powers of two");
+  MG_REQUIRE(aligned16(g) && aligned16(wcls), "g/wcls must be 16-byte aligned");
+  MG_REQUIRE(!(ep && ep->atomic) || out_dtype == MG_F32, "atomic epilogue requires fp32 output");
+  if (B == 0) return MG_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_F32) {
+    if (out_dtype == MG_F32) run_dgrad_s2<float, float>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st);
+    else run_dgrad_s2<float, bf16_t>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st);
+  } else {
+    if (out_dtype == MG_F32) run_dgrad_s2<bf16_t, float>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st);
+    else run_dgrad_s2<bf16_t, bf16_t>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st);
+  }
+  return mg_check_launch("mg_conv2d_dgrad_s2");
 }

@@ -1,0 +1,699 @@
+// Bayesian router + mixture-of-experts dispatch/combine (t2i_moe_gan.py:265-491).
+//
+// The router's weight-uncertainty projections are sampled once per forward
+// (explicit epsilon, :302-333), then re-associated:
+//     logits_raw = [x @ Wf | w @ Wt] @ Wc = x @ (Wf @ Wc[:128]) + (w @ Wt) @ Wc[128:]
+// so the per-token work is a C x E product (E experts) instead of C x 128 + 256 x E,
+// and the text half is a per-image [B, E] vector (the text rows repeat per image, :456).
+// Per token: temperature scale + clamp (:375-381), softmax, clamp, renormalise
+// (:384-389), then top-k selection with lowest-index tie-break (:393 / :473).
+// k == E reproduces the reference's dense soft training combine (:465-470);
+// k == 1 with eval weights reproduces the hard top-1 eval dispatch (:471-483).
+// Dispatch builds per-expert position lists deterministically (token order),
+// consumed by the grouped expert GEMMs (mg_gemm_grouped) without host syncs.
+#include "mg_common.h"
+
+namespace {
+
+MG_DEV float softplusf(float x) { return log1pf(expf(x)); }
+MG_DEV float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ void k_reparam(const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
+                          int64_t n, float* __restrict__ W) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float m = fminf(fmaxf(mu[i], -10.f), 10.f);
+    float r = fminf(fmaxf(rho[i], -8.f), 4.f);
+    float sg = fminf(fmaxf(softplusf(r), 1e-6f), 10.f);
+    float e = fminf(fmaxf(eps[i], -2.f), 2.f);
+    W[i] = m + sg * e;
+  }
+}
+
+MG_DEV float teff_of(const float* temp, float anneal) { return fminf(fmaxf(temp[0] * anneal, 0.5f), 5.f); }
+
+// TEAM lanes per token; block = 256 threads = 256/TEAM tokens
+template <typename T, int E>
+__global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int C, const float* __restrict__ Wfc,
+                             const float* __restrict__ Lt, int lgHW, const float* __restrict__ temp, float anneal,
+                             int k, int eval_mode, float* __restrict__ probs, float* __restrict__ zlog,
+                             int* __restrict__ topi, float* __restrict__ gate) {
+  constexpr int TEAM = 8;
+  constexpr int VEC = VecOf<T>::N;
+  extern __shared__ float wsm[];  // Wfc [C][E]
+  for (int i = threadIdx.x; i < C * E; i += blockDim.x) wsm[i] = Wfc[i];
+  __syncthreads();
+  int team = threadIdx.x / TEAM, tl = threadIdx.x % TEAM;
+  int t = blockIdx.x * (blockDim.x / TEAM) + team;
+  bool ok = t < Tn;
+  float acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = 0.f;
+  if (ok) {
+    for (int c0 = tl * VEC; c0 < C; c0 += TEAM * VEC) {
+      auto v = *reinterpret_cast<const typename VecOf<T>::type*>(tok + (int64_t)t * ld + c0);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        float x;
+        if constexpr (sizeof(T) == 4) x = v[j]; else x = bf2f(v[j]);
+        const float* wr = wsm + (c0 + j) * E;
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += x * wr[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    acc[e] += __shfl_xor(acc[e], 1, 64);
+    acc[e] += __shfl_xor(acc[e], 2, 64);
+    acc[e] += __shfl_xor(acc[e], 4, 64);
+  }
+  if (!ok || tl != 0) return;
+  int b = t >> lgHW;
+  float te = teff_of(temp, anneal);
+  float z[E], p[E];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    z[e] = (acc[e] + Lt[(int64_t)b * E + e]) / te;
+    float l = fminf(fmaxf(z[e], -20.f), 20.f);
+    p[e] = l;
+    mx = fmaxf(mx, l);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    p[e] = expf(p[e] - mx);
+    s += p[e];
+  }
+  float s2 = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    p[e] = fminf(fmaxf(p[e] / s, 1e-6f), 1.f);
+    s2 += p[e];
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    p[e] = p[e] / s2;
+    zlog[(int64_t)t * E + e] = z[e];
+  }
+  // top-k, lowest index first among equals
+  unsigned long long used = 0ull;
+  float gsum = 0.f;
+  float gv[E];
+  int gi[E];
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    float bv = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (!((used >> e) & 1ull) && (best < 0 || p[e] > bv)) {
+        best = e;
+        bv = p[e];
+      }
+    used |= 1ull << best;
+    gi[j] = best;
+    gv[j] = bv;
+    gsum += bv;
+  }
+  for (int j = 0; j < k; ++j) {
+    topi[(int64_t)t * k + j] = gi[j];
+    float g = eval_mode ? 1.f : (k == E ? gv[j] : gv[j] / gsum);
+    gate[(int64_t)t * k + j] = g;
+  }
+  if (eval_mode) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) probs[(int64_t)t * E + e] = (e == gi[0]) ? 1.f : 0.f;
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) probs[(int64_t)t * E + e] = p[e];
+  }
+}
+
+// ---- dispatch: deterministic per-expert position lists ----
+constexpr int DCH = 4096;  // assignments per block
+__global__ void k_disp_count(const int* __restrict__ topi, int n, int E, int* __restrict__ blk_counts) {
+  extern __shared__ int cnt[];
+  for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  int a0 = blockIdx.x * DCH, a1 = min(n, a0 + DCH);
+  for (int a = a0 + threadIdx.x; a < a1; a += blockDim.x) atomicAdd(&cnt[topi[a]], 1);
+  __syncthreads();
+  for (int e = threadIdx.x; e < E; e += blockDim.x) blk_counts[blockIdx.x * E + e] = cnt[e];
+}
+
+__global__ void k_disp_scan(int* __restrict__ blk_counts, int nblk, int E, int bm, int* __restrict__ row_off,
+                            int* __restrict__ tile_off) {
+  // single block; thread e scans expert e over blocks (in place -> block bases relative to expert start)
+  __shared__ int tot[1024];
+  int e = threadIdx.x;
+  if (e < E) {
+    int s = 0;
+    for (int b = 0; b < nblk; ++b) {
+      int c = blk_counts[b * E + e];
+      blk_counts[b * E + e] = s;
+      s += c;
+    }
+    tot[e] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int r = 0, tl = 0;
+    for (int i = 0; i < E; ++i) {
+      row_off[i] = r;
+      tile_off[i] = tl;
+      r += tot[i];
+      tl += (tot[i] + bm - 1) / bm;
+    }
+    row_off[E] = r;
+    tile_off[E] = tl;
+  }
+}
+
+// each thread owns DCH/256 = 16 consecutive assignments of the block's chunk
+template <int E>
+__global__ void k_disp_scatter(const int* __restrict__ topi, const float* __restrict__ gate, int n,
+                               const int* __restrict__ blk_base, const int* __restrict__ row_off,
+                               int* __restrict__ perm, int* __restrict__ pos_of, float* __restrict__ gate_pos) {
+  constexpr int PER = DCH / 256;
+  __shared__ int pre[256 * E];
+  int a0 = blockIdx.x * DCH + threadIdx.x * PER;
+  int loc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) loc[e] = 0;
+  for (int i = 0; i < PER; ++i) {
+    int a = a0 + i;
+    if (a < n) {
+      int ex = topi[a];
+#pragma unroll
+      for (int e = 0; e < E; ++e) loc[e] += (ex == e);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) pre[e * 256 + threadIdx.x] = loc[e];
+  __syncthreads();
+  if (threadIdx.x < E) {  // exclusive scan per expert across threads
+    int e = threadIdx.x, s = 0;
+    for (int i = 0; i < 256; ++i) {
+      int c = pre[e * 256 + i];
+      pre[e * 256 + i] = s;
+      s += c;
+    }
+  }
+  __syncthreads();
+  int off[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) off[e] = row_off[e] + blk_base[blockIdx.x * E + e] + pre[e * 256 + threadIdx.x];
+  for (int i = 0; i < PER; ++i) {
+    int a = a0 + i;
+    if (a < n) {
+      int ex = topi[a];
+      int pos = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (ex == e) pos = off[e]++;
+      perm[pos] = a;
+      pos_of[a] = pos;
+      gate_pos[pos] = gate[a];
+    }
+  }
+}
+
+// out[t] = resid[t] + sum_j gate[t,j] * Y[pos_of[t*k+j]]
+template <typename T>
+__global__ void k_combine(const T* __restrict__ Y, int64_t ldy, const int* __restrict__ pos_of,
+                          const float* __restrict__ gate, int Tn, int k, int C, const T* __restrict__ resid,
+                          int64_t ldr, T* __restrict__ out, int64_t ldo) {
+  int64_t n = (int64_t)Tn * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int t = (int)(i / C), c = (int)(i - (int64_t)t * C);
+    float s = 0.f;
+    for (int j = 0; j < k; ++j) {
+      int a = t * k + j;
+      s += gate[a] * ldf(Y, (int64_t)pos_of[a] * ldy + c);
+    }
+    if (resid) s = ldf(resid, (int64_t)t * ldr + c) + s;
+    stf(out, (int64_t)t * ldo + c, s);
+  }
+}
+
+// g_gate[a] = <gout[t], Y[pos_of[a]]>, one wave per assignment
+template <typename T, typename TG>
+__global__ void k_gate_grad(const TG* __restrict__ gout, int64_t ldg, const T* __restrict__ Y, int64_t ldy,
+                            const int* __restrict__ pos_of, int n, int k, int C, float* __restrict__ g_gate) {
+  int a = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (a >= n) return;
+  int t = a / k;
+  int64_t pr = (int64_t)pos_of[a] * ldy;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += ldf(gout, (int64_t)t * ldg + c) * ldf(Y, pr + c);
+  s = wave_sum(s);
+  if (lane == 0) g_gate[a] = s;
+}
+
+// per-token router backward: (g_gate, balance coefficients) -> g_raw [T, E]
+template <int E>
+__global__ void k_router_bwd(const float* __restrict__ probs, const float* __restrict__ zlog,
+                             const int* __restrict__ topi, const float* __restrict__ gate,
+                             const float* __restrict__ g_gate, const float* __restrict__ g_probs,
+                             const float* __restrict__ coef, int Tn, int k, int lgHW, const float* __restrict__ temp,
+                             float anneal, float* __restrict__ g_raw, float* __restrict__ gsum,
+                             float* __restrict__ g_temp) {
+  __shared__ float red[18 * E];
+  __shared__ float tred[4];
+  int t0 = blockIdx.x * blockDim.x;
+  int b0 = t0 >> lgHW;
+  for (int i = threadIdx.x; i < 18 * E; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  int t = t0 + threadIdx.x;
+  float te = teff_of(temp, anneal);
+  float gt_part = 0.f;
+  if (t < Tn) {
+    float p[E], gp[E], z[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      p[e] = probs[(int64_t)t * E + e];
+      z[e] = zlog[(int64_t)t * E + e];
+      gp[e] = (coef ? coef[e] : 0.f) + (g_probs ? g_probs[(int64_t)t * E + e] : 0.f);
+    }
+    if (g_gate) {
+      if (k == E) {
+        for (int j = 0; j < k; ++j) {
+          int ex = topi[(int64_t)t * k + j];
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+            if (e == ex) gp[e] += g_gate[(int64_t)t * k + j];
+        }
+      } else {
+        float S = 0.f, dot = 0.f;
+        for (int j = 0; j < k; ++j) {
+          int ex = topi[(int64_t)t * k + j];
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+            if (e == ex) S += p[e];
+          dot += g_gate[(int64_t)t * k + j] * gate[(int64_t)t * k + j];
+        }
+        for (int j = 0; j < k; ++j) {
+          int ex = topi[(int64_t)t * k + j];
+          float v = (g_gate[(int64_t)t * k + j] - dot) / S;
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+            if (e == ex) gp[e] += v;
+        }
+      }
+    }
+    // recompute softmax s and clamped q
+    float l[E], s[E], q[E];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      l[e] = fminf(fmaxf(z[e], -20.f), 20.f);
+      mx = fmaxf(mx, l[e]);
+    }
+    float den = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      s[e] = expf(l[e] - mx);
+      den += s[e];
+    }
+    float Sq = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      s[e] /= den;
+      q[e] = fminf(fmaxf(s[e], 1e-6f), 1.f);
+      Sq += q[e];
+    }
+    // p = q / Sq
+    float d1 = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) d1 += gp[e] * (q[e] / Sq);
+    float gs_[E];
+    float d2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float gq = (gp[e] - d1) / Sq;
+      gs_[e] = (s[e] >= 1e-6f && s[e] <= 1.f) ? gq : 0.f;
+      d2 += gs_[e] * s[e];
+    }
+    int bl = (t >> lgHW) - b0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float gl = s[e] * (gs_[e] - d2);
+      gl = (z[e] >= -20.f && z[e] <= 20.f) ? gl : 0.f;
+      gt_part += -gl * z[e] / te;
+      float gr = gl / te;
+      g_raw[(int64_t)t * E + e] = gr;
+      atomicAdd(&red[bl * E + e], gr);
+    }
+  }
+  gt_part = wave_sum(gt_part);
+  if ((threadIdx.x & 63) == 0) tred[threadIdx.x >> 6] = gt_part;
+  __syncthreads();
+  int tl = min(Tn, t0 + (int)blockDim.x) - 1;
+  int nimg = (tl >> lgHW) - b0 + 1;
+  for (int i = threadIdx.x; i < nimg * E; i += blockDim.x) atomicAdd(&gsum[(int64_t)b0 * E + i], red[i]);
+  if (threadIdx.x == 0 && g_temp) {
+    float tt = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tt += tred[i];
+    float raw = temp[0] * anneal;
+    if (raw >= 0.5f && raw <= 5.f) atomicAdd(g_temp, tt * anneal);
+  }
+}
+
+// g_tok[t, c] = sum_j gX[pos_of[t*k+j], c] + sum_e g_raw[t, e] * Wfc[c, e]
+template <typename T, typename TO>
+__global__ void k_token_grad(const T* __restrict__ gX, int64_t ldx, const int* __restrict__ pos_of, int Tn, int k,
+                             int C, const float* __restrict__ g_raw, const float* __restrict__ Wfc, int E,
+                             TO* __restrict__ out, int64_t ldo) {
+  int64_t n = (int64_t)Tn * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int t = (int)(i / C), c = (int)(i - (int64_t)t * C);
+    float s = 0.f;
+    if (gX)
+      for (int j = 0; j < k; ++j) s += ldf(gX, (int64_t)pos_of[t * k + j] * ldx + c);
+    for (int e = 0; e < E; ++e) s += g_raw[(int64_t)t * E + e] * Wfc[(int64_t)c * E + e];
+    stf(out, (int64_t)t * ldo + c, s);
+  }
+}
+
+// G1[c, e] += sum_t tok[t, c] * g_raw[t, e]
+template <typename T, int E>
+__global__ void k_router_feat_grad(const T* __restrict__ tok, int64_t ld, int Tn, int C,
+                                   const float* __restrict__ g_raw, int chunk, float* __restrict__ G1) {
+  __shared__ float gr[64 * E];
+  int c = threadIdx.x;
+  int t0 = blockIdx.x * chunk, t1 = min(Tn, t0 + chunk);
+  float acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = 0.f;
+  for (int tb = t0; tb < t1; tb += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * E; i += blockDim.x) {
+      int tt = tb + i / E;
+      gr[i] = tt < t1 ? g_raw[(int64_t)tb * E + i] : 0.f;
+    }
+    __syncthreads();
+    if (c < C) {
+      int te = min(64, t1 - tb);
+      for (int j = 0; j < te; ++j) {
+        float x = ldf(tok, (int64_t)(tb + j) * ld + c);
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += x * gr[j * E + e];
+      }
+    }
+  }
+  if (c < C) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) atomicAdd(&G1[(int64_t)c * E + e], acc[e]);
+  }
+}
+
+// out[g][n] += sum_{r in group g} X[src(r)][n] * rs[r]  (grouped bias gradients)
+template <typename T>
+__global__ void k_grouped_colsum(const T* __restrict__ X, int64_t ld, const int* __restrict__ idx, int idx_div,
+                                 const float* __restrict__ rs, const int* __restrict__ row_off, int G, int N,
+                                 int rows_per_block, float* __restrict__ out) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  int total = row_off[G];
+  int r0 = blockIdx.y * rows_per_block, r1 = min(total, r0 + rows_per_block);
+  if (r0 >= r1) return;
+  int g = 0;
+  while (g < G && row_off[g + 1] <= r0) ++g;
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    while (r >= row_off[g + 1]) {
+      atomicAdd(&out[(int64_t)g * N + n], s);
+      s = 0.f;
+      ++g;
+    }
+    int src = idx ? idx[r] / idx_div : r;
+    float v = ldf(X, (int64_t)src * ld + n);
+    s += rs ? v * rs[r] : v;
+  }
+  atomicAdd(&out[(int64_t)g * N + n], s);
+}
+
+// KL of one router (t2i_moe_gan.py:405-423): out[0] = clamp(nan_to_num(sum), 0, 120), out[1] = grad-pass flag
+__global__ void k_router_kl(const float* __restrict__ mf, const float* __restrict__ rf, int nf,
+                            const float* __restrict__ mt, const float* __restrict__ rt, int nt,
+                            const float* __restrict__ mc, const float* __restrict__ rc, int nc,
+                            float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int part = 0; part < 3; ++part) {
+    const float* m = part == 0 ? mf : part == 1 ? mt : mc;
+    const float* r = part == 0 ? rf : part == 1 ? rt : rc;
+    int n = part == 0 ? nf : part == 1 ? nt : nc;
+    float ps = 0.f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      float sg = softplusf(r[i]);
+      float lv = 2.f * logf(sg);
+      ps += expf(lv) + m[i] * m[i] - 1.f - lv;
+    }
+    ps = wave_sum(ps);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ps;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float tt = 0.f;
+      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tt += red[i];
+      s += 0.5f * tt;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float v = s;
+    float pass = 1.f;
+    if (isnan(v)) { v = 0.f; pass = 0.f; }
+    else if (isinf(v)) { v = v > 0 ? 200.f : 0.f; pass = 0.f; }
+    if (v > 120.f) { v = 120.f; pass = 0.f; }
+    if (v < 0.f) { v = 0.f; pass = 0.f; }
+    out[0] = v;
+    out[1] = pass;
+  }
+}
+
+// gmu += gW*[|mu|<=10] + c*mu ; grho += gW*clamp(eps)*dsigma/drho + c*sig(rho)*(sigma - 1/sigma)
+__global__ void k_router_param_bwd(const float* __restrict__ mu, const float* __restrict__ rho,
+                                   const float* __restrict__ eps, const float* __restrict__ gW, int64_t n,
+                                   const float* __restrict__ klc, float* __restrict__ gmu, float* __restrict__ grho) {
+  float c = klc ? klc[0] : 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float m = mu[i], r = rho[i];
+    float gm = c * m, gr = 0.f;
+    float sp = softplusf(r);
+    float sgm = sigmoidf_(r);
+    gr += c * sgm * (sp - 1.f / sp);
+    if (gW) {
+      float g = gW[i];
+      if (m >= -10.f && m <= 10.f) gm += g;
+      float rcl = fminf(fmaxf(r, -8.f), 4.f);
+      float spc = softplusf(rcl);
+      if (r >= -8.f && r <= 4.f && spc >= 1e-6f && spc <= 10.f) gr += g * fminf(fmaxf(eps[i], -2.f), 2.f) * sigmoidf_(rcl);
+    }
+    gmu[i] += gm;
+    grho[i] += gr;
+  }
+}
+
+// balance loss (t2i_moe_gan.py:951-1000) from the global per-expert prob sums:
+// out[0] = loss; coef[e] = d loss / d probs[t, e] (* grad_scale)
+__global__ void k_balance(const float* __restrict__ load, int E, float T, float weight, float grad_scale,
+                          float* __restrict__ out, float* __restrict__ coef) {
+  if (threadIdx.x != 0) return;
+  float frac[64];
+  float mean = 0.f;
+  for (int e = 0; e < E; ++e) {
+    frac[e] = (load[e] + 1e-6f) / T;
+    mean += frac[e];
+  }
+  mean /= E;
+  float var = 0.f;
+  for (int e = 0; e < E; ++e) var += (frac[e] - mean) * (frac[e] - mean);
+  float sd = sqrtf(var / (E - 1));
+  float den = mean + 1e-6f;
+  float cv = sd / den;
+  float raw = E * cv;
+  float L = isnan(raw) ? 0.f : fminf(fmaxf(raw, 0.f), 10.f);
+  out[0] = weight * L;
+  bool pass = !isnan(raw) && raw >= 0.f && raw <= 10.f;
+  for (int e = 0; e < E; ++e) {
+    float dcv = 0.f;
+    if (pass && sd > 0.f) {
+      float dsd = (frac[e] - mean) / ((E - 1) * sd);
+      dcv = (dsd * den - sd / E) / (den * den);
+    }
+    coef[e] = pass ? weight * E * dcv / T * grad_scale : 0.f;
+  }
+}
+
+// generator KL (t2i_moe_gan.py:846, :1367-1376, :1402-1404): total = sum of the routers' clamped KLs;
+// the step clamps total at 50 (zero gradient above).  coef[r] = eff_w * [total <= 50] * pass_r
+__global__ void k_kl_coefs(const float* __restrict__ kl2, int R, float eff_w, float* __restrict__ coef,
+                           float* __restrict__ total) {
+  if (threadIdx.x != 0) return;
+  float t = 0.f;
+  for (int r = 0; r < R; ++r) t += kl2[2 * r];
+  bool live = !(t > 50.f);
+  for (int r = 0; r < R; ++r) coef[r] = live ? eff_w * kl2[2 * r + 1] : 0.f;
+  total[0] = live ? t : 50.f;
+}
+
+inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
+
+}  // namespace
+
+extern "C" int mg_kl_coefs(const float* kl2, int R, float eff_w, float* coef, float* total, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_kl_coefs, dim3(1), dim3(64), 0, st, kl2, R, eff_w, coef, total);
+  return mg_check_launch("mg_kl_coefs");
+}
+
+extern "C" int mg_router_reparam(const float* mu, const float* rho, const float* eps, int64_t n, float* W,
+                                 void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_reparam, dim3(nblk(n)), dim3(256), 0, st, mu, rho, eps, n, W);
+  return mg_check_launch("mg_router_reparam");
+}
+
+extern "C" int mg_router_fwd(int dtype, const void* tok, int64_t ld, int T, int C, const float* Wfc, const float* Lt,
+                             int E, int k, int HW, const float* temperature, float anneal, int eval_mode,
+                             float* probs, float* zlog, int32_t* topi, float* gate, void* stream) {
+  MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
+  MG_REQUIRE(k >= 1 && k <= E, "bad k");
+  MG_REQUIRE((HW & (HW - 1)) == 0, "HW must be a power of two");
+  const int vec = dtype == MG_F32 ? 4 : 8;
+  MG_REQUIRE(C % (vec * 8) == 0 && ld % vec == 0, "C must be a multiple of 8 vectors");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int lg = 0;
+  while ((1 << lg) < HW) ++lg;
+  dim3 grid(cdiv(T, 32));
+  size_t sm = (size_t)C * E * sizeof(float);
+#define L_(TT, EE) hipLaunchKernelGGL((k_router_fwd<TT, EE>), grid, dim3(256), sm, st, (const TT*)tok, ld, T, C, Wfc, Lt, lg, \
+                                      temperature, anneal, k, eval_mode, probs, zlog, topi, gate)
+#define LE_(TT) if (E == 4) L_(TT, 4); else if (E == 8) L_(TT, 8); else if (E == 16) L_(TT, 16); else L_(TT, 32)
+  if (dtype == MG_F32) { LE_(float); } else { LE_(bf16_t); }
+#undef LE_
+#undef L_
+  return mg_check_launch("mg_router_fwd");
+}
+
+extern "C" int mg_moe_dispatch(const int32_t* topi, const float* gate, int T, int k, int E, int bm, int32_t* ws,
+                               int32_t* row_off, int32_t* tile_off, int32_t* perm, int32_t* pos_of, float* gate_pos,
+                               void* stream) {
+  MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int n = T * k;
+  int nb = cdiv(n, DCH);
+  MG_REQUIRE(nb <= 65535, "too many assignments");
+  hipLaunchKernelGGL(k_disp_count, dim3(nb), dim3(256), E * sizeof(int), st, topi, n, E, ws);
+  hipLaunchKernelGGL(k_disp_scan, dim3(1), dim3(64), 0, st, ws, nb, E, bm, row_off, tile_off);
+#define L_(EE) hipLaunchKernelGGL((k_disp_scatter<EE>), dim3(nb), dim3(256), 0, st, topi, gate, n, ws, row_off, perm, pos_of, gate_pos)
+  if (E == 4) L_(4); else if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
+#undef L_
+  return mg_check_launch("mg_moe_dispatch");
+}
+
+extern "C" int mg_moe_combine(int dtype, const void* Y, int64_t ldy, const int32_t* pos_of, const float* gate, int T,
+                              int k, int C, const void* resid, int64_t ldr, void* out, int64_t ldo, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)T * C;
+  if (dtype == MG_F32)
+    hipLaunchKernelGGL(k_combine<float>, dim3(nblk(n)), dim3(256), 0, st, (const float*)Y, ldy, pos_of, gate, T, k, C,
+                       (const float*)resid, ldr, (float*)out, ldo);
+  else
+    hipLaunchKernelGGL(k_combine<bf16_t>, dim3(nblk(n)), dim3(256), 0, st, (const bf16_t*)Y, ldy, pos_of, gate, T, k,
+                       C, (const bf16_t*)resid, ldr, (bf16_t*)out, ldo);
+  return mg_check_launch("mg_moe_combine");
+}
+
+extern "C" int mg_moe_gate_grad(int dtype, int gout_dtype, const void* gout, int64_t ldg, const void* Y, int64_t ldy,
+                                const int32_t* pos_of, int T, int k, int C, float* g_gate, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int n = T * k;
+  dim3 grid(cdiv(n, 4));
+#define L_(TT, TG) hipLaunchKernelGGL((k_gate_grad<TT, TG>), grid, dim3(256), 0, st, (const TG*)gout, ldg, (const TT*)Y, ldy, pos_of, n, k, C, g_gate)
+  if (dtype == MG_F32) { if (gout_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+  else { if (gout_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+  return mg_check_launch("mg_moe_gate_grad");
+}
+
+extern "C" int mg_router_bwd(const float* probs, const float* zlog, const int32_t* topi, const float* gate,
+                             const float* g_gate, const float* g_probs, const float* coef, int T, int E, int k, int HW,
+                             const float* temperature, float anneal, float* g_raw, float* gsum, float* g_temp,
+                             void* stream) {
+  MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
+  MG_REQUIRE(HW >= 16 && (HW & (HW - 1)) == 0, "HW must be a power of two >= 16");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int lg = 0;
+  while ((1 << lg) < HW) ++lg;
+  dim3 grid(cdiv(T, 256));
+#define L_(EE) hipLaunchKernelGGL((k_router_bwd<EE>), grid, dim3(256), 0, st, probs, zlog, topi, gate, g_gate, g_probs, coef, T, k, lg, \
+                                  temperature, anneal, g_raw, gsum, g_temp)
+  if (E == 4) L_(4); else if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
+#undef L_
+  return mg_check_launch("mg_router_bwd");
+}
+
+extern "C" int mg_moe_token_grad(int dtype, const void* gX, int64_t ldx, const int32_t* pos_of, int T, int k, int C,
+                                 const float* g_raw, const float* Wfc, int E, int out_dtype, void* out, int64_t ldo,
+                                 void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)T * C;
+#define L_(TT, TO) hipLaunchKernelGGL((k_token_grad<TT, TO>), dim3(nblk(n)), dim3(256), 0, st, (const TT*)gX, ldx, pos_of, T, k, C, g_raw, Wfc, E, (TO*)out, ldo)
+  if (dtype == MG_F32) { if (out_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+  else { if (out_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+  return mg_check_launch("mg_moe_token_grad");
+}
+
+extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T, int C, const float* g_raw, int E,
+                                   float* G1, void* stream) {
+  MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
+  MG_REQUIRE(C <= 512, "C <= 512");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int chunk = std::max(256, ((T / 128) + 63) / 64 * 64);
+  dim3 grid(cdiv(T, chunk));
+  int thr = ((C + 63) / 64) * 64;
+#define L_(TT, EE) hipLaunchKernelGGL((k_router_feat_grad<TT, EE>), grid, dim3(thr), 0, st, (const TT*)tok, ld, T, C, g_raw, chunk, G1)
+#define LE_(TT) if (E == 4) L_(TT, 4); else if (E == 8) L_(TT, 8); else if (E == 16) L_(TT, 16); else L_(TT, 32)
+  if (dtype == MG_F32) { LE_(float); } else { LE_(bf16_t); }
+#undef LE_
+#undef L_
+  return mg_check_launch("mg_router_feat_grad");
+}
+
+extern "C" int mg_grouped_colsum(int dtype, const void* X, int64_t ld, const int32_t* idx, int idx_div, const float* rs,
+                                 const int32_t* row_off, int G, int N, int max_rows, float* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int rpb = std::max(64, max_rows / 512);
+  dim3 grid(cdiv(N, 256), cdiv(max_rows, rpb));
+  if (dtype == MG_F32)
+    hipLaunchKernelGGL(k_grouped_colsum<float>, grid, dim3(256), 0, st, (const float*)X, ld, idx, idx_div > 0 ? idx_div : 1, rs, row_off, G, N, rpb, out);
+  else
+    hipLaunchKernelGGL(k_grouped_colsum<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)X, ld, idx, idx_div > 0 ? idx_div : 1, rs, row_off, G, N, rpb, out);
+  return mg_check_launch("mg_grouped_colsum");
+}
+
+extern "C" int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const float* mu_t, const float* rho_t,
+                            int nt, const float* mu_c, const float* rho_c, int nc, float* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_router_kl, dim3(1), dim3(1024), 0, st, mu_f, rho_f, nf, mu_t, rho_t, nt, mu_c, rho_c, nc, out);
+  return mg_check_launch("mg_router_kl");
+}
+
+extern "C" int mg_router_param_bwd(const float* mu, const float* rho, const float* eps, const float* gW, int64_t n,
+                                   const float* kl_coef, float* gmu, float* grho, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_router_param_bwd, dim3(nblk(n)), dim3(256), 0, st, mu, rho, eps, gW, n, kl_coef, gmu, grho);
+  return mg_check_launch("mg_router_param_bwd");
+}
+
+extern "C" int mg_balance(const float* load, int E, float T, float weight, float grad_scale, float* out, float* coef,
+                          void* stream) {
+  MG_REQUIRE(E >= 2 && E <= 64, "E out of range");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_balance, dim3(1), dim3(64), 0, st, load, E, T, weight, grad_scale, out, coef);
+  return mg_check_launch("mg_balance");
+}

@@ -1,0 +1,317 @@
+// Modulated Transformation Module warp (t2i_moe_gan.py:218-239) and the
+// bilinear x2 upsample of GenerativeBlock (t2i_moe_gan.py:633, 657-658).  NHWC.
+//
+// Warp forward, one wave per output pixel:
+//   off = conv3x3(o1, w2) + b2         (offset_net's second conv, 32 -> 2, fused)
+//   grid = linspace grid + 0.05 * off, clamp(-1, 1)
+//   out = grid_sample(x, grid, bilinear, zeros, align_corners=False)
+// The sample coordinates and clamp masks are saved for the backward, which
+// scatters dL/dx with fp32 atomics (256-B contiguous per wave instruction) and
+// reduces dL/dgrid across the wave.
+#include "mg_common.h"
+
+namespace {
+
+// torch.linspace(-1, 1, n)[i] (symmetric evaluation, as ATen does)
+MG_DEV float linspace_pm1(int i, int n) {
+  if (n == 1) return -1.f;
+  float step = 2.f / (float)(n - 1);
+  return (i < n / 2) ? (-1.f + step * (float)i) : (1.f - step * (float)(n - 1 - i));
+}
+
+template <typename T>
+__global__ void k_warp_fwd(const T* __restrict__ x, const T* __restrict__ o1, const float* __restrict__ w2,
+                           const float* __restrict__ b2, int B, int H, int W, int C, T* __restrict__ out,
+                           float* __restrict__ samp) {
+  int lane = threadIdx.x & 63;
+  int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (p >= (int64_t)B * H * W) return;
+  int b = (int)(p / (H * W));
+  int rem = (int)(p - (int64_t)b * H * W);
+  int h = rem / W, w = rem - (rem / W) * W;
+  // offset conv 32 -> 2 (3x3, pad 1): lanes split the 288 (tap, channel) products
+  float s0 = 0.f, s1 = 0.f;
+  for (int i = lane; i < 288; i += 64) {
+    int tap = i >> 5, c = i & 31;
+    int kh = tap / 3, kw = tap - kh * 3;
+    int yy = h + kh - 1, xx = w + kw - 1;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      float v = ldf(o1, (((int64_t)b * H + yy) * W + xx) * 32 + c);
+      s0 += v * w2[(0 * 32 + c) * 9 + tap];
+      s1 += v * w2[(1 * 32 + c) * 9 + tap];
+    }
+  }
+  s0 = wave_sum(s0) + b2[0];
+  s1 = wave_sum(s1) + b2[1];
+  float gx = linspace_pm1(w, W) + s0 * 0.05f;
+  float gy = linspace_pm1(h, H) + s1 * 0.05f;
+  float mx = (gx >= -1.f && gx <= 1.f) ? 1.f : 0.f;
+  float my = (gy >= -1.f && gy <= 1.f) ? 1.f : 0.f;
+  gx = fminf(fmaxf(gx, -1.f), 1.f);
+  gy = fminf(fmaxf(gy, -1.f), 1.f);
+  float ix = ((gx + 1.f) * W - 1.f) * 0.5f;
+  float iy = ((gy + 1.f) * H - 1.f) * 0.5f;
+  if (lane == 0) {
+    samp[p * 4 + 0] = ix;
+    samp[p * 4 + 1] = iy;
+    samp[p * 4 + 2] = mx;
+    samp[p * 4 + 3] = my;
+  }
+  int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+  int x1 = x0 + 1, y1 = y0 + 1;
+  float wnw = ((float)x1 - ix) * ((float)y1 - iy);
+  float wne = (ix - (float)x0) * ((float)y1 - iy);
+  float wsw = ((float)x1 - ix) * (iy - (float)y0);
+  float wse = (ix - (float)x0) * (iy - (float)y0);
+  bool vx0 = x0 >= 0 && x0 < W, vx1 = x1 >= 0 && x1 < W, vy0 = y0 >= 0 && y0 < H, vy1 = y1 >= 0 && y1 < H;
+  const T* xb = x + (int64_t)b * H * W * C;
+  for (int c = lane; c < C; c += 64) {
+    float v = 0.f;
+    if (vy0 && vx0) v += wnw * ldf(xb, ((int64_t)y0 * W + x0) * C + c);
+    if (vy0 && vx1) v += wne * ldf(xb, ((int64_t)y0 * W + x1) * C + c);
+    if (vy1 && vx0) v += wsw * ldf(xb, ((int64_t)y1 * W + x0) * C + c);
+    if (vy1 && vx1) v += wse * ldf(xb, ((int64_t)y1 * W + x1) * C + c);
+    stf(out, p * C + c, v);
+  }
+}
+
+template <typename T, typename TG>
+__global__ void k_warp_bwd(const TG* __restrict__ gout, const T* __restrict__ x, const float* __restrict__ samp,
+                           int B, int H, int W, int C, float* __restrict__ gx, float* __restrict__ goff) {
+  int lane = threadIdx.x & 63;
+  int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (p >= (int64_t)B * H * W) return;
+  int b = (int)(p / (H * W));
+  float ix = samp[p * 4 + 0], iy = samp[p * 4 + 1], mx = samp[p * 4 + 2], my = samp[p * 4 + 3];
+  int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+  int x1 = x0 + 1, y1 = y0 + 1;
+  float ax1 = (float)x1 - ix, ax0 = ix - (float)x0, ay1 = (float)y1 - iy, ay0 = iy - (float)y0;
+  float wnw = ax1 * ay1, wne = ax0 * ay1, wsw = ax1 * ay0, wse = ax0 * ay0;
+  bool vx0 = x0 >= 0 && x0 < W, vx1 = x1 >= 0 && x1 < W, vy0 = y0 >= 0 && y0 < H, vy1 = y1 >= 0 && y1 < H;
+  const T* xb = x + (int64_t)b * H * W * C;
+  float* gb = gx + (int64_t)b * H * W * C;
+  float gix = 0.f, giy = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    float g = ldf(gout, p * C + c);
+    if (vy0 && vx0) {
+      int64_t o = ((int64_t)y0 * W + x0) * C + c;
+      float v = ldf(xb, o);
+      gix -= v * ay1 * g;
+      giy -= v * ax1 * g;
+      atomicAdd(gb + o, wnw * g);
+    }
+    if (vy0 && vx1) {
+      int64_t o = ((int64_t)y0 * W + x1) * C + c;
+      float v = ldf(xb, o);
+      gix += v * ay1 * g;
+      giy -= v * ax0 * g;
+      atomicAdd(gb + o, wne * g);
+    }
+    if (vy1 && vx0) {
+      int64_t o = ((int64_t)y1 * W + x0) * C + c;
+      float v = ldf(xb, o);
+      gix -= v * ay0 * g;
+      giy += v * ax1 * g;
+      atomicAdd(gb + o, wsw * g);
+    }
+    if (vy1 && vx1) {
+      int64_t o = ((int64_t)y1 * W + x1) * C + c;
+      float v = ldf(xb, o);
+      gix += v * ay0 * g;
+      giy += v * ax0 * g;
+      atomicAdd(gb + o, wse * g);
+    }
+  }
+  gix = wave_sum(gix);
+  giy = wave_sum(giy);
+  if (lane == 0) {
+    goff[p * 2 + 0] = gix * (0.5f * W) * mx * 0.05f;
+    goff[p * 2 + 1] = giy * (0.5f * H) * my * 0.05f;
+  }
+}
+
+// offset_net second conv backward (32 -> 2, 3x3, pad 1) fused with the first conv's LeakyReLU:
+//   g_a1[q, c] = lrelu'(o1[q,c]) * sum_{j,kh,kw} goff[q - (kh-1, kw-1), j] * w2[j, c, kh, kw]
+//   gw2[j, c, kh, kw] += sum_q goff[q - (kh-1,kw-1), j] * o1[q, c];  gb2[j] += sum_p goff[p, j]
+template <typename T>
+__global__ void k_offset_head_bwd(const float* __restrict__ goff, const T* __restrict__ o1,
+                                  const float* __restrict__ w2, int B, int H, int W, int ppb, T* __restrict__ ga1,
+                                  float* __restrict__ gw2, float* __restrict__ gb2) {
+  __shared__ float sw[576];
+  __shared__ float red[576 + 2];
+  for (int i = threadIdx.x; i < 576; i += blockDim.x) {
+    sw[i] = w2[i];
+    red[i] = 0.f;
+  }
+  if (threadIdx.x < 2) red[576 + threadIdx.x] = 0.f;
+  __syncthreads();
+  int c = threadIdx.x & 31, pl = threadIdx.x >> 5;  // 8 pixel lanes
+  int64_t P = (int64_t)B * H * W;
+  float accw[18];
+#pragma unroll
+  for (int i = 0; i < 18; ++i) accw[i] = 0.f;
+  float accb0 = 0.f, accb1 = 0.f;
+  for (int it = pl; it < ppb; it += 8) {
+    int64_t q = (int64_t)blockIdx.x * ppb + it;
+    if (q >= P) break;
+    int b = (int)(q / (H * W));
+    int rem = (int)(q - (int64_t)b * H * W);
+    int h = rem / W, w = rem - (rem / W) * W;
+    float ov = ldf(o1, q * 32 + c);
+    float g = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      int kh = tap / 3, kw = tap % 3;
+      int yy = h - (kh - 1), xx = w - (kw - 1);  // output pixel p that reads q through this tap
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        int64_t pp = ((int64_t)b * H + yy) * W + xx;
+        float g0 = goff[pp * 2], g1 = goff[pp * 2 + 1];
+        g += g0 * sw[c * 9 + tap] + g1 * sw[(32 + c) * 9 + tap];
+        accw[tap] += g0 * ov;
+        accw[9 + tap] += g1 * ov;
+      }
+    }
+    stf(ga1, q * 32 + c, ov > 0.f ? g : 0.2f * g);
+    if (c == 0) {
+      accb0 += goff[q * 2];
+      accb1 += goff[q * 2 + 1];
+    }
+  }
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    atomicAdd(&red[c * 9 + tap], accw[tap]);
+    atomicAdd(&red[(32 + c) * 9 + tap], accw[9 + tap]);
+  }
+  if (c == 0) {
+    atomicAdd(&red[576], accb0);
+    atomicAdd(&red[577], accb1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 578; i += blockDim.x) {
+    if (i < 576) atomicAdd(&gw2[i], red[i]);
+    else atomicAdd(&gb2[i - 576], red[i]);
+  }
+}
+
+// bilinear x2 source index (align_corners=False, scale 0.5): clamped at 0
+MG_DEV void src_idx(int o, int in_size, int& i0, int& i1, float& l1) {
+  float s = fmaxf(((float)o + 0.5f) * 0.5f - 0.5f, 0.f);
+  i0 = (int)s;
+  i1 = min(i0 + 1, in_size - 1);
+  l1 = s - (float)i0;
+}
+
+template <typename T>
+__global__ void k_up2_fwd(const T* __restrict__ x, int B, int H, int W, int C, T* __restrict__ out) {
+  int OH = 2 * H, OW = 2 * W;
+  int64_t n = (int64_t)B * OH * OW * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t pix = i / C;
+    int ox = (int)(pix % OW);
+    int oy = (int)((pix / OW) % OH);
+    int b = (int)(pix / ((int64_t)OW * OH));
+    int y0, y1, x0, x1;
+    float ly, lx;
+    src_idx(oy, H, y0, y1, ly);
+    src_idx(ox, W, x0, x1, lx);
+    const T* xb = x + (int64_t)b * H * W * C + c;
+    float v = (1.f - ly) * ((1.f - lx) * ldf(xb, ((int64_t)y0 * W + x0) * C) + lx * ldf(xb, ((int64_t)y0 * W + x1) * C)) +
+              ly * ((1.f - lx) * ldf(xb, ((int64_t)y1 * W + x0) * C) + lx * ldf(xb, ((int64_t)y1 * W + x1) * C));
+    stf(out, i, v);
+  }
+}
+
+template <typename TG, typename T>
+__global__ void k_up2_bwd(const TG* __restrict__ gout, int B, int H, int W, int C, T* __restrict__ gx,
+                          int accumulate) {
+  int OH = 2 * H, OW = 2 * W;
+  int64_t n = (int64_t)B * H * W * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t pix = i / C;
+    int ix = (int)(pix % W);
+    int iy = (int)((pix / W) % H);
+    int b = (int)(pix / ((int64_t)W * H));
+    float s = 0.f;
+    for (int oy = max(0, 2 * iy - 2); oy <= min(OH - 1, 2 * iy + 2); ++oy) {
+      int y0, y1;
+      float ly;
+      src_idx(oy, H, y0, y1, ly);
+      float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
+      if (wy == 0.f) continue;
+      for (int ox = max(0, 2 * ix - 2); ox <= min(OW - 1, 2 * ix + 2); ++ox) {
+        int x0, x1;
+        float lx;
+        src_idx(ox, W, x0, x1, lx);
+        float wx = (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f);
+        if (wx == 0.f) continue;
+        s += wy * wx * ldf(gout, (((int64_t)b * OH + oy) * OW + ox) * C + c);
+      }
+    }
+    if (accumulate) s += ldf(gx, i);
+    stf(gx, i, s);
+  }
+}
+
+inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
+
+}  // namespace
+
+extern "C" int mg_warp_fwd(int dtype, const void* x, const void* o1, const float* w2, const float* b2, int B, int H,
+                           int W, int C, void* out, float* samp, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t P = (int64_t)B * H * W;
+  dim3 grid((unsigned)((P + 3) / 4));
+  if (dtype == MG_F32)
+    hipLaunchKernelGGL(k_warp_fwd<float>, grid, dim3(256), 0, st, (const float*)x, (const float*)o1, w2, b2, B, H, W, C, (float*)out, samp);
+  else
+    hipLaunchKernelGGL(k_warp_fwd<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)o1, w2, b2, B, H, W, C, (bf16_t*)out, samp);
+  return mg_check_launch("mg_warp_fwd");
+}
+
+extern "C" int mg_warp_bwd(int dtype, int gout_dtype, const void* gout, const void* x, const float* samp, int B, int H,
+                           int W, int C, float* gx, float* goff, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t P = (int64_t)B * H * W;
+  dim3 grid((unsigned)((P + 3) / 4));
+#define L_(T, TG) hipLaunchKernelGGL((k_warp_bwd<T, TG>), grid, dim3(256), 0, st, (const TG*)gout, (const T*)x, samp, B, H, W, C, gx, goff)
+  if (dtype == MG_F32) { if (gout_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+  else { if (gout_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+  return mg_check_launch("mg_warp_bwd");
+}
+
+extern "C" int mg_offset_head_bwd(int dtype, const float* goff, const void* o1, const float* w2, int B, int H, int W,
+                                  void* ga1, float* gw2, float* gb2, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t P = (int64_t)B * H * W;
+  int ppb = 64;
+  dim3 grid((unsigned)((P + ppb - 1) / ppb));
+  if (dtype == MG_F32)
+    hipLaunchKernelGGL(k_offset_head_bwd<float>, grid, dim3(256), 0, st, goff, (const float*)o1, w2, B, H, W, ppb, (float*)ga1, gw2, gb2);
+  else
+    hipLaunchKernelGGL(k_offset_head_bwd<bf16_t>, grid, dim3(256), 0, st, goff, (const bf16_t*)o1, w2, B, H, W, ppb, (bf16_t*)ga1, gw2, gb2);
+  return mg_check_launch("mg_offset_head_bwd");
+}
+
+extern "C" int mg_upsample2x_fwd(int dtype, const void* x, int B, int H, int W, int C, void* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = 4LL * B * H * W * C;
+  if (dtype == MG_F32)
+    hipLaunchKernelGGL(k_up2_fwd<float>, dim3(nblk(n)), dim3(256), 0, st, (const float*)x, B, H, W, C, (float*)out);
+  else
+    hipLaunchKernelGGL(k_up2_fwd<bf16_t>, dim3(nblk(n)), dim3(256), 0, st, (const bf16_t*)x, B, H, W, C, (bf16_t*)out);
+  return mg_check_launch("mg_upsample2x_fwd");
+}
+
+extern "C" int mg_upsample2x_bwd(int gout_dtype, const void* gout, int B, int H, int W, int C, int gx_dtype, void* gx,
+                                 int accumulate, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)B * H * W * C;
+#define L_(TG, T) hipLaunchKernelGGL((k_up2_bwd<TG, T>), dim3(nblk(n)), dim3(256), 0, st, (const TG*)gout, B, H, W, C, (T*)gx, accumulate)
+  if (gout_dtype == MG_F32) { if (gx_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+  else { if (gx_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+  return mg_check_launch("mg_upsample2x_bwd");
+}

@@ -1,0 +1,368 @@
+// Per-step weight preparation, casts, reductions and the flat AdamW of libmoegan_hip.
+#include "mg_common.h"
+
+namespace {
+
+// wpack[o][(kh*KW+kw)*Cin + ci] = W[o][ci][kh][kw]; rows o >= Cout zero (padding)
+template <typename T>
+__global__ void k_pack_conv(const float* __restrict__ W, int Cout, int Cin, int KH, int KW, int rows,
+                            T* __restrict__ out) {
+  int64_t K = (int64_t)KH * KW * Cin;
+  int64_t n = (int64_t)rows * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int o = (int)(i / K);
+    int r = (int)(i - (int64_t)o * K);
+    int tap = r / Cin, ci = r - tap * Cin;
+    int kh = tap / KW, kw = tap - kh * KW;
+    float v = o < Cout ? W[(((int64_t)o * Cin + ci) * KH + kh) * KW + kw] : 0.f;
+    stf(out, i, v);
+  }
+}
+
+// out[ci][(kh'*KW+kw')*Cout + o] = W[o][ci][KH-1-kh'][KW-1-kw']   (stride-1 data gradient)
+template <typename T>
+__global__ void k_pack_conv_flip(const float* __restrict__ W, int Cout, int Cin, int KH, int KW, int rows,
+                                 T* __restrict__ out) {
+  int64_t K = (int64_t)KH * KW * Cout;
+  int64_t n = (int64_t)rows * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int ci = (int)(i / K);
+    int r = (int)(i - (int64_t)ci * K);
+    int tap = r / Cout, o = r - tap * Cout;
+    int kh = KH - 1 - tap / KW, kw = KW - 1 - (tap % KW);
+    float v = ci < Cin ? W[(((int64_t)o * Cin + ci) * KH + kh) * KW + kw] : 0.f;
+    stf(out, i, v);
+  }
+}
+
+// out[cls][ci][t*Cg + co] = W[co][ci][kh(py,ty)][kw(px,tx)]   (4x4 / stride-2 / pad-1 data gradient)
+template <typename T>
+__global__ void k_pack_dgrad_s2(const float* __restrict__ W, int Cg, int Cin, int rows, T* __restrict__ out) {
+  int64_t K = 4LL * Cg;
+  int64_t n = 4LL * rows * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int cls = (int)(i / ((int64_t)rows * K));
+    int64_t r = i - (int64_t)cls * rows * K;
+    int ci = (int)(r / K);
+    int k = (int)(r - (int64_t)ci * K);
+    int t = k / Cg, co = k - t * Cg;
+    int ty = t >> 1, tx = t & 1, py = cls >> 1, px = cls & 1;
+    int kh = py ? (ty ? 2 : 0) : (ty ? 3 : 1);
+    int kw = px ? (tx ? 2 : 0) : (tx ? 3 : 1);
+    float v = ci < Cin ? W[(((int64_t)co * Cin + ci) * 4 + kh) * 4 + kw] : 0.f;
+    stf(out, i, v);
+  }
+}
+
+// wsq[o][ci] = sum_taps W[o][ci][tap]^2   (rows o >= Cout zero)
+__global__ void k_wsq(const float* __restrict__ W, int Cout, int Cin, int taps, int rows, float* __restrict__ out) {
+  int64_t n = (int64_t)rows * Cin;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int o = (int)(i / Cin);
+    float s = 0.f;
+    if (o < Cout)
+      for (int t = 0; t < taps; ++t) {
+        float w = W[i * taps + t];
+        s += w * w;
+      }
+    out[i] = s;
+  }
+}
+
+// gW[o][ci][t] += 2 * W[o][ci][t] * gwsq[o][ci]
+__global__ void k_wsq_bwd(const float* __restrict__ W, const float* __restrict__ gwsq, int Cout, int Cin, int taps,
+                          float* __restrict__ gW) {
+  int64_t n = (int64_t)Cout * Cin * taps;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    gW[i] += 2.f * W[i] * gwsq[i / taps];
+}
+
+template <typename TI, typename TO>
+__global__ void k_cast(const TI* __restrict__ in, TO* __restrict__ out, int64_t n, float alpha, int square) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = ldf(in, i) * alpha;
+    stf(out, i, square ? v * v : v);
+  }
+}
+
+// strided 2-D copy/cast: out[r*ldo + c] (+)= alpha * in[r*ldi + c]
+template <typename TI, typename TO>
+__global__ void k_copy2d(const TI* __restrict__ in, int64_t ldi, TO* __restrict__ out, int64_t ldo, int R, int C,
+                         float alpha, int accumulate) {
+  int64_t n = (int64_t)R * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
+    float v = alpha * ldf(in, (int64_t)r * ldi + c);
+    if (accumulate) v += ldf(out, (int64_t)r * ldo + c);
+    stf(out, (int64_t)r * ldo + c, v);
+  }
+}
+
+// out[c] (+)= sum_r X[r*ld + c]   (column sums; fp32 atomics across row splits)
+template <typename T>
+__global__ void k_colsum(const T* __restrict__ X, int64_t ld, int R, int C, int rows_per_block,
+                         float* __restrict__ out) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  int r0 = blockIdx.y * rows_per_block, r1 = min(R, r0 + rows_per_block);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += ldf(X, (int64_t)r * ld + c);
+  atomicAdd(out + c, s);
+}
+
+// weight norm: W[o] = g[o] * v[o] / ||v[o]||  (t2i_moe_gan.py:869-886, torch weight_norm dim=0)
+__global__ void k_wn_fwd(const float* __restrict__ v, const float* __restrict__ g, int O, int K,
+                         float* __restrict__ W, float* __restrict__ norm) {
+  int o = blockIdx.x;
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    float x = v[(int64_t)o * K + k];
+    s += x * x;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+    red[0] = sqrtf(t);
+  }
+  __syncthreads();
+  float n = red[0];
+  if (threadIdx.x == 0) norm[o] = n;
+  float sc = g[o] / n;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) W[(int64_t)o * K + k] = v[(int64_t)o * K + k] * sc;
+}
+
+// gg[o] += sum_k gW*v/n ; gv = (g/n) * (gW - (gg_o/n) * v)
+__global__ void k_wn_bwd(const float* __restrict__ v, const float* __restrict__ g, const float* __restrict__ norm,
+                         const float* __restrict__ gW, int O, int K, float* __restrict__ gv, float* __restrict__ gg) {
+  int o = blockIdx.x;
+  __shared__ float red[16];
+  float n = norm[o];
+  float s = 0.f;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) s += gW[(int64_t)o * K + k] * v[(int64_t)o * K + k];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+    red[0] = t / n;
+  }
+  __syncthreads();
+  float ggo = red[0];
+  if (threadIdx.x == 0) gg[o] += ggo;
+  float a = g[o] / n, b = ggo / n;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    int64_t i = (int64_t)o * K + k;
+    gv[i] += a * (gW[i] - b * v[i]);
+  }
+}
+
+// sum of squares of n floats, accumulated into out[0]
+__global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = x[i];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+    atomicAdd(out, t);
+  }
+}
+
+// torch.optim.AdamW (single-tensor semantics, t2i_moe_gan.py:1101-1102) fused with
+// clip_grad_norm_ (t2i_moe_gan.py:1333-1337 / :1417-1421): coef = min(1, max_norm / (||g|| + 1e-6)).
+__global__ void k_adamw(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                        float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                        float bc1, float bc2_sqrt, const float* __restrict__ sumsq, float max_norm) {
+  float coef = 1.f;
+  if (sumsq) {
+    float tn = sqrtf(sumsq[0]);
+    coef = fminf(max_norm / (tn + 1e-6f), 1.f);
+  }
+  float step_size = lr / bc1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * coef;
+    float pi = p[i] * (1.f - lr * wd);
+    float mi = m[i] + (gi - m[i]) * (1.f - b1);
+    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi - step_size * (mi / denom);
+  }
+}
+
+// generator constant [1, C, 4, 4] (NCHW) -> NHWC [B, 4, 4, C]
+template <typename T>
+__global__ void k_const_fwd(const float* __restrict__ cst, int C, int HW, int B, T* __restrict__ out) {
+  int64_t n = (int64_t)B * HW * C;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int p = (int)((i / C) % HW);
+    stf(out, i, cst[(int64_t)c * HW + p]);
+  }
+}
+// gconst[c][p] += sum_b g[b][p][c]
+template <typename T>
+__global__ void k_const_bwd(const T* __restrict__ g, int C, int HW, int B, float* __restrict__ gc) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * HW) return;
+  int p = i / C, c = i - p * C;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += ldf(g, ((int64_t)b * HW + p) * C + c);
+  gc[(int64_t)c * HW + p] += s;
+}
+
+inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
+
+}  // namespace
+
+#define DISPATCH_T(dtype, ...)                          \
+  do {                                                  \
+    if ((dtype) == MG_F32) {                            \
+      typedef float T;                                  \
+      __VA_ARGS__;                                      \
+    } else {                                            \
+      typedef bf16_t T;                                 \
+      __VA_ARGS__;                                      \
+    }                                                   \
+  } while (0)
+
+extern "C" int mg_pack_conv(int dtype, const float* W, int Cout, int Cin, int KH, int KW, int rows, void* out,
+                            void* stream) {
+  MG_REQUIRE(rows >= Cout, "rows < Cout");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)rows * KH * KW * Cin;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(k_pack_conv<T>, dim3(nblk(n)), dim3(256), 0, st, W, Cout, Cin, KH, KW, rows,
+                                       reinterpret_cast<T*>(out)));
+  return mg_check_launch("mg_pack_conv");
+}
+
+extern "C" int mg_pack_conv_flip(int dtype, const float* W, int Cout, int Cin, int KH, int KW, int rows, void* out,
+                                 void* stream) {
+  MG_REQUIRE(rows >= Cin, "rows < Cin");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)rows * KH * KW * Cout;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(k_pack_conv_flip<T>, dim3(nblk(n)), dim3(256), 0, st, W, Cout, Cin, KH, KW,
+                                       rows, reinterpret_cast<T*>(out)));
+  return mg_check_launch("mg_pack_conv_flip");
+}
+
+extern "C" int mg_pack_dgrad_s2(int dtype, const float* W, int Cg, int Cin, int rows, void* out, void* stream) {
+  MG_REQUIRE(rows >= Cin, "rows < Cin");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = 16LL * rows * Cg;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(k_pack_dgrad_s2<T>, dim3(nblk(n)), dim3(256), 0, st, W, Cg, Cin, rows,
+                                       reinterpret_cast<T*>(out)));
+  return mg_check_launch("mg_pack_dgrad_s2");
+}
+
+extern "C" int mg_wsq(const float* W, int Cout, int Cin, int taps, int rows, float* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_wsq, dim3(nblk((int64_t)rows * Cin)), dim3(256), 0, st, W, Cout, Cin, taps, rows, out);
+  return mg_check_launch("mg_wsq");
+}
+
+extern "C" int mg_wsq_bwd(const float* W, const float* gwsq, int Cout, int Cin, int taps, float* gW, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_wsq_bwd, dim3(nblk((int64_t)Cout * Cin * taps)), dim3(256), 0, st, W, gwsq, Cout, Cin, taps, gW);
+  return mg_check_launch("mg_wsq_bwd");
+}
+
+extern "C" int mg_cast(int in_dtype, const void* in, int out_dtype, void* out, int64_t n, float alpha, int square,
+                       void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) return MG_OK;
+  if (in_dtype == MG_F32 && out_dtype == MG_F32)
+    hipLaunchKernelGGL((k_cast<float, float>), dim3(nblk(n)), dim3(256), 0, st, (const float*)in, (float*)out, n, alpha, square);
+  else if (in_dtype == MG_F32)
+    hipLaunchKernelGGL((k_cast<float, bf16_t>), dim3(nblk(n)), dim3(256), 0, st, (const float*)in, (bf16_t*)out, n, alpha, square);
+  else if (out_dtype == MG_F32)
+    hipLaunchKernelGGL((k_cast<bf16_t, float>), dim3(nblk(n)), dim3(256), 0, st, (const bf16_t*)in, (float*)out, n, alpha, square);
+  else
+    hipLaunchKernelGGL((k_cast<bf16_t, bf16_t>), dim3(nblk(n)), dim3(256), 0, st, (const bf16_t*)in, (bf16_t*)out, n, alpha, square);
+  return mg_check_launch("mg_cast");
+}
+
+extern "C" int mg_copy2d(int in_dtype, const void* in, int64_t ldi, int out_dtype, void* out, int64_t ldo, int R,
+                         int C, float alpha, int accumulate, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)R * C;
+  if (n == 0) return MG_OK;
+  if (in_dtype == MG_F32 && out_dtype == MG_F32)
+    hipLaunchKernelGGL((k_copy2d<float, float>), dim3(nblk(n)), dim3(256), 0, st, (const float*)in, ldi, (float*)out, ldo, R, C, alpha, accumulate);
+  else if (in_dtype == MG_F32)
+    hipLaunchKernelGGL((k_copy2d<float, bf16_t>), dim3(nblk(n)), dim3(256), 0, st, (const float*)in, ldi, (bf16_t*)out, ldo, R, C, alpha, accumulate);
+  else if (out_dtype == MG_F32)
+    hipLaunchKernelGGL((k_copy2d<bf16_t, float>), dim3(nblk(n)), dim3(256), 0, st, (const bf16_t*)in, ldi, (float*)out, ldo, R, C, alpha, accumulate);
+  else
+    hipLaunchKernelGGL((k_copy2d<bf16_t, bf16_t>), dim3(nblk(n)), dim3(256), 0, st, (const bf16_t*)in, ldi, (bf16_t*)out, ldo, R, C, alpha, accumulate);
+  return mg_check_launch("mg_copy2d");
+}
+
+extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, float* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (R == 0 || C == 0) return MG_OK;
+  int rpb = std::max(16, R / 256);
+  dim3 grid(cdiv(C, 256), cdiv(R, rpb));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum<T>, grid, dim3(256), 0, st, reinterpret_cast<const T*>(X), ld, R, C,
+                                       rpb, out));
+  return mg_check_launch("mg_colsum");
+}
+
+extern "C" int mg_weight_norm_fwd(const float* v, const float* g, int O, int K, float* W, float* norm, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_wn_fwd, dim3(O), dim3(256), 0, st, v, g, O, K, W, norm);
+  return mg_check_launch("mg_weight_norm_fwd");
+}
+
+extern "C" int mg_weight_norm_bwd(const float* v, const float* g, const float* norm, const float* gW, int O, int K,
+                                  float* gv, float* gg, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_wn_bwd, dim3(O), dim3(256), 0, st, v, g, norm, gW, O, K, gv, gg);
+  return mg_check_launch("mg_weight_norm_bwd");
+}
+
+extern "C" int mg_sumsq(const float* x, int64_t n, float* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) return MG_OK;
+  hipLaunchKernelGGL(k_sumsq, dim3(std::min(nblk(n), 1024)), dim3(256), 0, st, x, n, out);
+  return mg_check_launch("mg_sumsq");
+}
+
+extern "C" int mg_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                        float eps, float weight_decay, int step, const float* sumsq, float max_norm, void* stream) {
+  MG_REQUIRE(step >= 1, "step must be >= 1");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) return MG_OK;
+  float bc1 = 1.f - powf(beta1, (float)step);
+  float bc2 = 1.f - powf(beta2, (float)step);
+  hipLaunchKernelGGL(k_adamw, dim3(std::min(nblk(n), 4096)), dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps,
+                     weight_decay, bc1, sqrtf(bc2), sumsq, max_norm);
+  return mg_check_launch("mg_adamw");
+}
+
+extern "C" int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, void* out, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)B * HW * C;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(k_const_fwd<T>, dim3(nblk(n)), dim3(256), 0, st, cst, C, HW, B,
+                                       reinterpret_cast<T*>(out)));
+  return mg_check_launch("mg_const_fwd");
+}
+
+extern "C" int mg_const_bwd(int dtype, const void* g, int C, int HW, int B, float* gc, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(k_const_bwd<T>, dim3(cdiv(C * HW, 256)), dim3(256), 0, st,
+                                       reinterpret_cast<const T*>(g), C, HW, B, gc));
+  return mg_check_launch("mg_const_bwd");
+}
