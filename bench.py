@@ -1,0 +1,183 @@
+"""Benchmark: images/sec of one full G+D training step (BASELINE.json metric) on N MI355X.
+
+Default workload = BASELINE.json configs[1] ("C2"): 64x64 real images, E=8 experts top-2,
+batch 256 per GPU, bf16 activations / MFMA operands (fp32 master weights + AdamW), R1 on.
+A step is the whole train_aurora_gan batch body (t2i_moe_gan.py:1262-1421): D phase with R1,
+G forward x2 (fresh router noise each), G phase, both AdamW steps, clip_grad_norm_ both.
+Synthetic data (no network): real ~U(-1,1), captions ~N(0,1) CLIP-like 512-d, z ~N(0,1),
+router epsilon drawn on device inside the step, random-init weights (reference init).
+
+Multi-GPU: one process per GPU (torchrun), RCCL all-reduce of the flat D/G gradients and the
+[E] expert-load vector; per-GPU batch fixed ("weak" scaling).  Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "moe-gan_cpsc541_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
+# G+D step FLOPs/image = 6.810 + 0.806 * k_active GFLOP
+def gflop_per_image(k_active):
+    return 6.810 + 0.806 * k_active
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--experts", type=int, default=8)
+    ap.add_argument("--topk", type=int, default=2)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--time-kernel", default="d_conv1",
+                    help="kernel whose launches are timed with HIP events for the roofline field")
+    return ap.parse_args()
+
+
+def make_eps(E, dev, gen):
+    dims = [(512, 512), (256, 512), (128, 512)]
+    return [(torch.randn(c, 128, device=dev, generator=gen), torch.randn(t, 128, device=dev, generator=gen),
+             torch.randn(256, E, device=dev, generator=gen)) for c, t in dims]
+
+
+def cpu_baseline(args, E, k):
+    """Oracle (CPU restatement of the reference step) on a bounded sample: B=8, same E/top-k."""
+    from oracle import aurora_cpu as O
+    from moegan_mi.layout import discriminator_shapes, generator_shapes
+    from moegan_mi.init import init_discriminator, init_generator  # noqa: F401
+    from oracle.recipe import fill_state
+    torch.set_num_threads(os.cpu_count() or 1)
+    B = 8
+    PG = {n: torch.from_numpy(v) for n, v in fill_state(generator_shapes(E), 0).items()}
+    PD = {n: torch.from_numpy(v).requires_grad_(True) for n, v in fill_state(discriminator_shapes(), 50).items()}
+    for n, v in PG.items():
+        if not n.split(".")[-1].startswith("epsilon_"):
+            v.requires_grad_(True)
+    optG = torch.optim.AdamW([v for v in PG.values() if v.requires_grad], lr=2e-4, betas=(0.5, 0.999),
+                             weight_decay=0.01)
+    optD = torch.optim.AdamW(list(PD.values()), lr=2e-4, betas=(0.5, 0.999), weight_decay=0.01)
+    g = torch.Generator().manual_seed(0)
+    real = torch.rand(B, 3, 64, 64, generator=g) * 2 - 1
+    text = torch.randn(B, 512, generator=g)
+    z = torch.randn(B, 512, generator=g)
+    dims = [(512, 512), (256, 512), (128, 512)]
+    mk = lambda: [tuple(torch.randn(s, generator=g) for s in ((c, 128), (t, 128), (256, E))) for c, t in dims]  # noqa
+    O.train_step(PG, PD, optG, optD, real, text, z, mk(), mk(), torch.randperm(B, generator=g), topk=k)  # warm
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        O.train_step(PG, PD, optG, optD, real, text, z, mk(), mk(), torch.randperm(B, generator=g), topk=k)
+    dt = time.perf_counter() - t0
+    return {"value": round(B * args.cpu_steps / dt, 3), "unit": "images/sec", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"oracle/aurora_cpu.train_step, B={B}, E={E} top-{k}, fp32, "
+                                      f"{args.cpu_steps} timed steps after 1 warm-up"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        pg = dist.group.WORLD
+
+    from moegan_mi import ops
+    from moegan_mi.init import init_discriminator, init_generator
+    from moegan_mi.step import StepConfig, TrainStep
+
+    E, k, B = args.experts, args.topk, args.batch
+    ts = TrainStep(StepConfig(E=E, topk=k, dtype=args.dtype), dev, process_group=pg)
+    init_generator(ts.gs, seed=0)
+    init_discriminator(ts.ds, seed=1)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    real = torch.rand(B, 3, 64, 64, device=dev, generator=gen) * 2 - 1
+    text = torch.randn(B, 512, device=dev, generator=gen)
+    z = torch.randn(B, 512, device=dev, generator=gen)
+    eps_gen = torch.Generator(device=dev).manual_seed(3)  # identical router noise on every rank
+
+    def one_step():
+        eps_d = make_eps(E, dev, eps_gen)
+        eps_g = make_eps(E, dev, eps_gen)
+        perm = torch.randperm(B, device=dev, generator=gen).int()
+        return ts.step(real, text, z, eps_d, eps_g, perm, anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+
+    # live timing of the roofline kernel: D conv_layers.2 forward on the 64x64 real batch
+    # (implicit GEMM M = B*16*16, N = 256, K = 4*4*128)
+    want_dims = (B * 256, 256, 2048)
+    ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "conv2d" and dims == want_dims)
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(args.steps):
+        out = one_step()
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    kt = ops.TIMER.results()
+    ops.TIMER = None
+    if pg is not None:
+        t = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t)
+    finite = bool(torch.isfinite(out["d_losses"]).all() and torch.isfinite(out["g_gan"]).all())
+
+    if rank == 0:
+        imgs = B * world * args.steps
+        value = imgs / elapsed
+        ms = elapsed / args.steps * 1e3
+        kms = [ms_ for _, _, ms_ in kt]
+        avg_ms = sum(kms) / max(len(kms), 1)
+        M, N, K = want_dims
+        flop = 2.0 * M * N * K
+        achieved = flop / (avg_ms * 1e-3) / 1e12 if kms else None
+        peak = MFMA_PEAK_TFLOPS[args.dtype]
+        roof = {"bound": "mfma", "kernel": "mg_conv2d_fwd D conv_layers.2 (64x64 real), implicit GEMM "
+                                          f"M={M} N={N} K={K}", "achieved": round(achieved, 2) if achieved else None,
+                "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
+                "traffic": None, "launches_timed": len(kms), "avg_launch_ms": round(avg_ms, 4)}
+        step_tflops = gflop_per_image(k) * B * world / (ms * 1e-3) / 1e3
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(args, E, k)
+            except Exception as e:  # the baseline is a report, never the measured value
+                cpu = {"error": repr(e)}
+        line = {"metric": "images/sec (G+D step, 64x64 MS-COCO layout)", "value": round(value, 2),
+                "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": args.dtype, "data": "synthetic (U(-1,1) images, N(0,1) 512-d captions, random init)",
+                "config": {"workload": f"C2: 64x64, {E} experts top-{k}, batch {B}/GPU, {args.dtype}, R1 on",
+                           "global_batch": B * world, "experts": E, "topk": k, "parallelism": f"dp{world}"},
+                "step_tflops_algorithmic": round(step_tflops, 2),
+                "step_mfma_frac": round(step_tflops / peak, 4), "finite": finite,
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if pg is not None:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

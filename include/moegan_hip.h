@@ -130,6 +130,152 @@ int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const int32_t* r
                           const void* A, int64_t lda, const void* B, int64_t ldb, const int32_t* b_idx,
                           int b_idx_div, int b_gelu, float* C, int splits, const mg_epilogue* ep, void* stream);
 
+/* ---- op-level entry points ---- */
+
+/* LayerNorm over C (128/256/512) per row (+ optional LeakyReLU), saving mean/rstd. t2i_moe_gan.py:505-507, :684. */
+int mg_layernorm_fwd(int dtype, const void* x, int64_t ldx, int R, int C, const float* gamma, const float* beta, float eps, void* y, int64_t ldy, float* mean, float* rstd, int act, void* stream);
+
+/* LayerNorm backward (gx (+)=, ggamma/gbeta += via atomics). */
+int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t ldg, const void* x, int64_t ldx, int R, int C, const float* mean, const float* rstd, const float* gamma, void* gx, int64_t ldgx, int accumulate, float* ggamma, float* gbeta, void* stream);
+
+/* Self-attention core for nn.MultiheadAttention (8 heads) on packed qkv [B*L, 3C]; saves logsumexp. t2i_moe_gan.py:513, :546. */
+int mg_attn_fwd(int dtype, const void* qkv, int B, int L, int C, int heads, void* out, float* lse, void* stream);
+
+/* Self-attention backward -> gqkv [B*L, 3C]. */
+int mg_attn_bwd(int dtype, int gout_dtype, const void* qkv, const void* out, const void* gout, const float* lse, int B, int L, int C, int heads, void* gqkv, void* stream);
+
+/* Head text-branch backward: g_tpre, dW2 text rows (all taps). */
+int mg_d_text_bwd(const float* g_tb, const float* t, const float* w2sum, int B, int Ct, int cofs, float* g_tpre, float* dW2, void* stream);
+
+/* im2col for the discriminator's first conv (3->128, 4x4/s2/p1), any input strides, K padded to Kp. */
+int mg_im2col_4x4s2(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H, int W, int C, int Kp, int out_dtype, void* out, void* stream);
+
+/* Discriminator output_layer, image channels: out[b,o] = sum h1[b,o+tap,c] W2[c,tap] (t2i_moe_gan.py:885-907). */
+int mg_disc_head_fwd(int dtype, const void* h1, const float* W2, int B, int Hf, int Cf, float* out, void* stream);
+
+/* Head backward into features, fused with LeakyReLU' of a1 (g_bstride = 0 broadcasts: R1). */
+int mg_disc_head_bwd_data(int dtype, const float* g, int64_t g_bstride, const float* W2, const void* a1, int B, int Hf, int Cf, int out_dtype, void* ga1, void* stream);
+
+/* Head weight gradient (image channels) dW2[c,tap] += sum_b,o g h1. */
+int mg_disc_head_bwd_w(int dtype, const float* g, int64_t g_bstride, const void* h1, int B, int Hf, int Cf, float* dW2, void* stream);
+
+/* Discriminator loss (t2i_moe_gan.py:940-949) for real (64x64 patch logits), fake and mismatched-text logits + gradients. */
+int mg_d_loss(const float* img_real, const float* img_fake, const float* tb, const int32_t* perm, int B, int No, float* out, float* g_img, float* g_fake, float* g_tb, float* real_out, float* mism_out, float* fake_out, void* stream);
+
+/* Generator adversarial loss softplus(-f).mean() and its gradient (t2i_moe_gan.py:917-924). */
+int mg_g_loss(const float* fake, int B, float scale, float* out, float* g, void* stream);
+
+/* R1 penalty (t2i_moe_gan.py:1285-1286): r1 += gamma/2 mean_b ||g_b||^2; u = gamma/B g. */
+int mg_r1(int dtype, const void* g, int64_t per, int B, float gamma, float* r1, int u_dtype, void* u, void* stream);
+
+/* out = a * LeakyReLU'(m). */
+int mg_lrelu_mask_mul(int a_dtype, const void* a, int m_dtype, const void* m, int64_t n, int out_dtype, void* out, void* stream);
+
+/* out[b,c] += sum_{p<HW} X[b*HW+p, c]  (per-image sums: cross-attention vector gradient). */
+int mg_segsum(int dtype, const void* X, int64_t ld, int B, int HW, int C, float* out, void* stream);
+
+/* ModulatedConv backward, output side: gyt = gy*d (gy = gz * lrelu'), gdd = -0.5 d^2 sum_pix gy*y; z may carry a fused residual (zsub). t2i_moe_gan.py:154-186. */
+int mg_modconv_bwd_out(int dtype, int gz_dtype, const void* gz, int64_t ld_gz, const void* z, int64_t ld_z, const void* zsub, int64_t ld_zsub, const float* d, int B, int HW, int Cout, int act, void* gyt, int64_t ld_gyt, float* gdd, void* stream);
+
+/* ModulatedConv backward, input side: gx (+)= gxt*s, gs[b,ci] += sum_pix gxt*x. */
+int mg_modconv_bwd_in(int gxt_dtype, const void* gxt, int64_t ld_gxt, int dtype, const void* x, int64_t ld_x, const float* s, int B, int HW, int Cin, int gx_dtype, void* gx, int64_t ld_gx, int accumulate, float* gs, void* stream);
+
+/* Generator KL total and per-router gradient coefficients (total clamped at 50, t2i_moe_gan.py:1369-1370). */
+int mg_kl_coefs(const float* kl2, int R, float eff_w, float* coef, float* total, void* stream);
+
+/* BayesianRouter.reparameterize with explicit epsilon (t2i_moe_gan.py:302-333). */
+int mg_router_reparam(const float* mu, const float* rho, const float* eps, int64_t n, float* W, void* stream);
+
+/* BayesianRouter.forward on tokens (t2i_moe_gan.py:335-402): logits = tok@Wfc + Lt[b], temperature/clamp/softmax/clamp/renorm, top-k (lowest index on ties), gate weights (renormalised for k<E, probs for k==E, 1 in eval). zlog = scaled pre-clamp logits. */
+int mg_router_fwd(int dtype, const void* tok, int64_t ld, int T, int C, const float* Wfc, const float* Lt, int E, int k, int HW, const float* temperature, float anneal, int eval_mode, float* probs, float* zlog, int32_t* topi, float* gate, void* stream);
+
+/* Deterministic per-expert position lists (token order): row_off/tile_off (BM=bm), perm[pos]=assignment, pos_of[assignment]=pos, gate_pos. ws: int32 [ceil(T*k/4096)*E]. */
+int mg_moe_dispatch(const int32_t* topi, const float* gate, int T, int k, int E, int bm, int32_t* ws, int32_t* row_off, int32_t* tile_off, int32_t* perm, int32_t* pos_of, float* gate_pos, void* stream);
+
+/* out[t] = resid[t] + sum_j gate[t,j] Y[pos_of[t*k+j]]  (SparseMoE combine + AttentionBlock residual, t2i_moe_gan.py:465-470, :571). */
+int mg_moe_combine(int dtype, const void* Y, int64_t ldy, const int32_t* pos_of, const float* gate, int T, int k, int C, const void* resid, int64_t ldr, void* out, int64_t ldo, void* stream);
+
+/* g_gate[t*k+j] = <gout[t], Y[pos_of[t*k+j]]>. */
+int mg_moe_gate_grad(int dtype, int gout_dtype, const void* gout, int64_t ldg, const void* Y, int64_t ldy, const int32_t* pos_of, int T, int k, int C, float* g_gate, void* stream);
+
+/* Router backward per token -> g_raw [T,E], per-image sums gsum [B,E] (+=), temperature grad (+=). */
+int mg_router_bwd(const float* probs, const float* zlog, const int32_t* topi, const float* gate, const float* g_gate, const float* g_probs, const float* coef, int T, int E, int k, int HW, const float* temperature, float anneal, float* g_raw, float* gsum, float* g_temp, void* stream);
+
+/* g_tok[t] = sum_j gX[pos_of[t*k+j]] + sum_e g_raw[t,e] Wfc[:,e]. */
+int mg_moe_token_grad(int dtype, const void* gX, int64_t ldx, const int32_t* pos_of, int T, int k, int C, const float* g_raw, const float* Wfc, int E, int out_dtype, void* out, int64_t ldo, void* stream);
+
+/* G1[c,e] += sum_t tok[t,c] g_raw[t,e]. */
+int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T, int C, const float* g_raw, int E, float* G1, void* stream);
+
+/* out[g][n] += sum_{r in group g} X[idx(r)][n] * rs[r]  (per-expert bias gradients). */
+int mg_grouped_colsum(int dtype, const void* X, int64_t ld, const int32_t* idx, int idx_div, const float* rs, const int32_t* row_off, int G, int N, int max_rows, float* out, void* stream);
+
+/* BayesianRouter.kl_divergence (t2i_moe_gan.py:405-423): out[0] = clamped KL, out[1] = gradient-pass flag. */
+int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const float* mu_t, const float* rho_t, int nt, const float* mu_c, const float* rho_c, int nc, float* out, void* stream);
+
+/* Router parameter gradients: reparameterisation chain + KL term (coefficient *kl_coef). */
+int mg_router_param_bwd(const float* mu, const float* rho, const float* eps, const float* gW, int64_t n, const float* kl_coef, float* gmu, float* grho, void* stream);
+
+/* moe_balance_loss from global per-expert prob sums (t2i_moe_gan.py:951-1000): out[0] = loss, coef[e] = d loss/d probs[t,e] * grad_scale. */
+int mg_balance(const float* load, int E, float T, float weight, float grad_scale, float* out, float* coef, void* stream);
+
+/* MTM offset head (conv 32->2) + linspace grid + clamp + bilinear grid_sample (zeros, align_corners=False), t2i_moe_gan.py:222-239. samp [P,4] saved. */
+int mg_warp_fwd(int dtype, const void* x, const void* o1, const float* w2, const float* b2, int B, int H, int W, int C, void* out, float* samp, void* stream);
+
+/* grid_sample backward: gx (fp32, +=, atomics) and goff [P,2] = d loss / d offsets. */
+int mg_warp_bwd(int dtype, int gout_dtype, const void* gout, const void* x, const float* samp, int B, int H, int W, int C, float* gx, float* goff, void* stream);
+
+/* offset_net second conv backward fused with the first conv's LeakyReLU: ga1, gw2 +=, gb2 +=. */
+int mg_offset_head_bwd(int dtype, const float* goff, const void* o1, const float* w2, int B, int H, int W, void* ga1, float* gw2, float* gb2, void* stream);
+
+/* nn.Upsample(scale_factor=2, bilinear, align_corners=False), NHWC (t2i_moe_gan.py:633). */
+int mg_upsample2x_fwd(int dtype, const void* x, int B, int H, int W, int C, void* out, void* stream);
+
+/* bilinear x2 backward (gather form, deterministic). */
+int mg_upsample2x_bwd(int gout_dtype, const void* gout, int B, int H, int W, int C, int gx_dtype, void* gx, int accumulate, void* stream);
+
+/* Per-step weight packing (fp32 master -> compute dtype): wpack[o][(kh*KW+kw)*Cin+ci] = W[o][ci][kh][kw]; rows >= Cout zero-padded. */
+int mg_pack_conv(int dtype, const float* W, int Cout, int Cin, int KH, int KW, int rows, void* out, void* stream);
+
+/* Flipped/transposed pack for the stride-1 data gradient: out[ci][(kh*KW+kw)*Cout+o] = W[o][ci][KH-1-kh][KW-1-kw]. */
+int mg_pack_conv_flip(int dtype, const float* W, int Cout, int Cin, int KH, int KW, int rows, void* out, void* stream);
+
+/* Per-parity-class pack for mg_conv2d_dgrad_s2: out[cls][ci][t*Cg+co]. */
+int mg_pack_dgrad_s2(int dtype, const float* W, int Cg, int Cin, int rows, void* out, void* stream);
+
+/* wsq[o][ci] = sum_taps W[o][ci][tap]^2 (demodulation, t2i_moe_gan.py:165). */
+int mg_wsq(const float* W, int Cout, int Cin, int taps, int rows, float* out, void* stream);
+
+/* gW[o][ci][t] += 2 W[o][ci][t] gwsq[o][ci]  (demodulation backward). */
+int mg_wsq_bwd(const float* W, const float* gwsq, int Cout, int Cin, int taps, float* gW, void* stream);
+
+/* out = (alpha*in)[^2 if square] with dtype conversion. */
+int mg_cast(int in_dtype, const void* in, int out_dtype, void* out, int64_t n, float alpha, int square, void* stream);
+
+/* strided 2-D copy/cast: out[r*ldo+c] (+)= alpha*in[r*ldi+c]. */
+int mg_copy2d(int in_dtype, const void* in, int64_t ldi, int out_dtype, void* out, int64_t ldo, int R, int C, float alpha, int accumulate, void* stream);
+
+/* out[c] += sum_r X[r*ld+c]  (bias gradients). */
+int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, float* out, void* stream);
+
+/* weight_norm (dim 0): W = g v / ||v||  (t2i_moe_gan.py:869-886). */
+int mg_weight_norm_fwd(const float* v, const float* g, int O, int K, float* W, float* norm, void* stream);
+
+/* weight_norm backward: gg += sum gW v/||v||, gv += (g/||v||)(gW - gg_o v/||v||). */
+int mg_weight_norm_bwd(const float* v, const float* g, const float* norm, const float* gW, int O, int K, float* gv, float* gg, void* stream);
+
+/* out[0] += sum x^2 (clip_grad_norm_ total norm, t2i_moe_gan.py:1336/1420). */
+int mg_sumsq(const float* x, int64_t n, float* out, void* stream);
+
+/* torch.optim.AdamW step over a flat fp32 range fused with clip_grad_norm_ (coef from *sumsq, max_norm); t2i_moe_gan.py:1101-1102. */
+int mg_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, int step, const float* sumsq, float max_norm, void* stream);
+
+/* generator constant [1,C,4,4] -> NHWC [B,4,4,C] (t2i_moe_gan.py:815). */
+int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, void* out, void* stream);
+
+/* gconst[c][p] += sum_b g[b][p][c]. */
+int mg_const_bwd(int dtype, const void* g, int C, int HW, int B, float* gc, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmoegan_hip.so")
 
 MG_F32, MG_BF16 = 0, 1
-ACT_NONE, ACT_LRELU, ACT_GELU, ACT_MUL_GELU_GRAD, ACT_MUL_LRELU_GRAD = 0, 1, 2, 3, 4
+ACT_NONE, ACT_LRELU, ACT_GELU, ACT_MUL_GELU_GRAD, ACT_MUL_LRELU_GRAD, ACT_RSQRT_EPS = 0, 1, 2, 3, 4, 5
 
 _c_void_p, _i32, _i64, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
 
@@ -24,25 +24,39 @@ class Epilogue(ctypes.Structure):
                 ("scale_ld", _i64), ("rowscale", _c_void_p), ("act", _i32), ("aux", _c_void_p),
                 ("ld_aux", _i64), ("resid", _c_void_p), ("ld_res", _i64), ("accumulate", _i32),
                 ("atomic", _i32), ("remap_lgcin", _i32), ("remap_taps", _i32), ("a_idx", _c_void_p),
-                ("a_idx_div", _i32), ("a_rowscale", _c_void_p), ("a_gelu", _i32)]
+                ("a_idx_div", _i32), ("a_rowscale", _c_void_p), ("a_gelu", _i32), ("addvec", _c_void_p),
+                ("add_shift", _i32), ("add_ld", _i64)]
 
 
-# (name, argtypes) of every exported entry point; restype is int32 unless noted
-_SIGS = {}
+# Argument types are derived from include/moegan_hip.h itself, so the binding
+# cannot drift from the C ABI (the header travels with the library).
+_HEADER = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "moegan_hip.h"))
+_CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "float": _f32, "void": _c_void_p,
+          "mg_epilogue": ctypes.POINTER(Epilogue)}
 
 
-def _sig(name, *args):
-    _SIGS[name] = args
+def _parse_header(path=_HEADER):
+    import re
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    sigs = {}
+    for name, args in re.findall(r"\b(?:int|const char\*)\s+(mg_\w+)\(([^)]*)\);", txt, flags=re.S):
+        types = []
+        for a in args.split(","):
+            a = " ".join(a.split())
+            if not a or a == "void":
+                continue
+            base = a.replace("const ", "").split()[0].rstrip("*")
+            if "*" in a:
+                types.append(_CTYPE["mg_epilogue"] if base == "mg_epilogue" else _c_void_p)
+            else:
+                types.append(_CTYPE[base])
+        sigs[name] = types
+    return sigs
 
 
-P, I, L, F = _c_void_p, _i32, _i64, _f32
+_SIGS = _parse_header()
 EP = ctypes.POINTER(Epilogue)
-_sig("mg_version")
-_sig("mg_gemm", I, I, I, I, P, L, I, P, L, I, P, L, I, EP, I, P)
-_sig("mg_conv2d_fwd", I, P, I, I, I, I, P, I, I, I, I, I, P, P, L, I, EP, P)
-_sig("mg_conv2d_wgrad", I, P, L, P, I, I, I, I, P, I, I, I, I, I, P, I, P)
-_sig("mg_gemm_grouped", I, I, I, I, I, P, P, I, P, L, P, L, I, L, P, L, I, EP, P)
-_sig("mg_gemm_grouped_wgrad", I, I, I, I, P, I, P, L, P, L, P, I, I, P, I, EP, P)
 
 _lib = None
 
@@ -57,17 +71,20 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise MGError(f"libmoegan_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
         h = ctypes.CDLL(LIB_PATH)
-        h.mg_last_error.restype = ctypes.c_char_p
         for name, args in _SIGS.items():
+            if name == "mg_last_error":
+                continue
             fn = getattr(h, name)
             fn.argtypes = list(args)
             fn.restype = ctypes.c_int32
+        h.mg_last_error.restype = ctypes.c_char_p
+        h.mg_last_error.argtypes = []
         _lib = h
     return _lib
 
 
 def exported_symbols():
-    return ["mg_last_error"] + list(_SIGS)
+    return list(_SIGS)
 
 
 def call(name, *args):
@@ -97,10 +114,10 @@ def dt(t):
 
 def epilogue(alpha=1.0, bias=None, scale=None, scale_shift=0, scale_ld=0, rowscale=None, act=0, aux=None,
              ld_aux=0, resid=None, ld_res=0, accumulate=0, atomic=0, remap_lgcin=0, remap_taps=0, a_idx=None,
-             a_idx_div=1, a_rowscale=None, a_gelu=0):
+             a_idx_div=1, a_rowscale=None, a_gelu=0, addvec=None, add_shift=0, add_ld=0):
     e = Epilogue(alpha, ptr(bias), ptr(scale), scale_shift, scale_ld, ptr(rowscale), act, ptr(aux), ld_aux,
                  ptr(resid), ld_res, accumulate, atomic, remap_lgcin, remap_taps, ptr(a_idx), a_idx_div,
-                 ptr(a_rowscale), a_gelu)
+                 ptr(a_rowscale), a_gelu, ptr(addvec), add_shift, add_ld)
     # keep the tensors alive until the launch has been enqueued
-    e._keep = (bias, scale, rowscale, aux, resid, a_idx, a_rowscale)
+    e._keep = (bias, scale, rowscale, aux, resid, a_idx, a_rowscale, addvec)
     return e

@@ -1,0 +1,199 @@
+"""Explicit discriminator forward/backward, GAN losses and the R1 double backward.
+
+AuroraDiscriminator (t2i_moe_gan.py:858-907) on the HIP kernels, NHWC:
+    a0 = conv0(img) [4x4/s2/p1, 3->128]   h0 = LReLU(a0)
+    a1 = conv1(h0)  [4x4/s2/p1, 128->256] h1 = LReLU(a1)
+    t  = LReLU(WN-Linear(text))           out = head([h1 | tile(t)])  (4x4 valid, 384->1)
+The head's 128 text channels are spatially constant, so their contribution is
+a per-image scalar tb[b] = sum_c t[b,c] * sum_taps W2[256+c] (+ bias); the
+mismatched-text pass therefore reuses the real pass's image features and only
+re-indexes tb (t2i_moe_gan.py:1303-1305: D(real.detach(), text[perm])).
+
+R1 (t2i_moe_gan.py:1282-1286) is computed in closed form.  With masks
+m0 = LReLU'(a0), m1 = LReLU'(a1) (piecewise constant, zero second derivative):
+    g_x   = C0^T m0 C1^T m1 Gh1           (Gh1 = head^T(ones), identical for every image)
+    r1    = gamma/2 * mean_b ||g_x_b||^2, u = gamma/B * g_x
+    dW0  += wgrad0(x=u, dy=m0 C1^T m1 Gh1)
+    v1    = m1 C1(m0 C0 u)
+    dW1  += wgrad1(x=m0 C0 u, dy=m1 Gh1);   dW2[:256] += head_wgrad(x=v1, dy=ones)
+All weights are weight-normed (g * v / ||v||); gradients flow back to g and v.
+"""
+import torch
+
+from . import _lib as L
+from . import ops
+
+E_ = ops.E
+MUL_LRELU_GRAD, LRELU = L.ACT_MUL_LRELU_GRAD, L.ACT_LRELU
+WN_LAYERS = ("conv_layers.0.", "conv_layers.2.", "output_layer.0.", "text_projection.0.")
+
+
+class DiscriminatorEngine:
+    def __init__(self, store, cdt=torch.float32):
+        self.st = store
+        self.cdt = cdt
+        self.dev = store.device
+        self.ones_cache = {}
+
+    def P(self, n):
+        return self.st.view(n)
+
+    def G(self, n):
+        return self.st.gview(n)
+
+    def _ones(self, n):
+        if n not in self.ones_cache:
+            self.ones_cache[n] = torch.ones(n, device=self.dev)
+        return self.ones_cache[n]
+
+    # ------------------------------------------------------------------
+    def prep(self):
+        """Weight-norm the four layers and pack them (call after every D optimizer step)."""
+        W, norm = {}, {}
+        for pre in WN_LAYERS:
+            W[pre], norm[pre] = ops.weight_norm_fwd(self.P(pre + "weight_v"), self.P(pre + "weight_g"))
+        self.W, self.norm = W, norm
+        cdt = self.cdt
+        self.W0p = ops.pack_conv(W["conv_layers.0."], cdt)  # [128, 48] (k = tap*3 + c)
+        self.W0cls = ops.pack_dgrad_s2(W["conv_layers.0."], cdt, rows=3)  # [4, 3, 4*128]
+        self.W1p = ops.pack_conv(W["conv_layers.2."], cdt)  # [256, 16*128]
+        self.W1cls = ops.pack_dgrad_s2(W["conv_layers.2."], cdt)  # [4, 128, 4*256]
+        W2 = W["output_layer.0."].view(384, 16)
+        self.W2img = W2[:256]
+        self.w2sum = ops.gemm(W2[256:], self._ones(16).view(1, 16), 128, 1, 16).view(128)
+        self.Wt = W["text_projection.0."]
+
+    # ------------------------------------------------------------------
+    def text_branch(self, text):
+        t = ops.linear(text, self.Wt, bias=self.P("text_projection.0.bias"), act=LRELU)  # [B,128]
+        tb = ops.gemm(t, self.w2sum.view(1, 128), t.shape[0], 1, 128, ep=E_(bias=self.P("output_layer.0.bias")))
+        return t, tb.view(-1)
+
+    def conv_stack(self, img, layout, B, H):
+        """img: NCHW fp32 (layout 'nchw') or NHWC padded [B,H,W,ld] (layout ('nhwc', ld))."""
+        if layout == "nchw":
+            strides = (3 * H * H, H, 1, H * H)
+        else:
+            ld = layout[1]
+            strides = (H * H * ld, H * ld, ld, 1)
+        cols = ops.im2col_4x4s2(img, strides, B, H, H, 3, 48, self.cdt)  # [B*(H/2)^2, 48]
+        h0 = ops.linear(cols, self.W0p, bias=self.P("conv_layers.0.bias"), act=LRELU).view(B, H // 2, H // 2, 128)
+        h1 = ops.conv2d(h0, self.W1p, 256, 4, 4, 2, 1, ep=E_(bias=self.P("conv_layers.2.bias"), act=LRELU))
+        return cols, h0, h1
+
+    def forward(self, img, layout, text, B, H):
+        cols, h0, h1 = self.conv_stack(img, layout, B, H)
+        img_part = ops.disc_head_fwd(h1, self.W2img)  # [B, (H/4-3)^2]
+        return dict(cols=cols, h0=h0, h1=h1, img_part=img_part, H=H, B=B)
+
+    # ------------------------------------------------------------------
+    def stack_backward(self, f, g_img_part, want_params=True, g_input=None):
+        """Backprop d loss / d image-part logits through the conv stack.
+        Accumulates dW (effective weights) into self.dW; optionally writes the image gradient."""
+        B, H = f["B"], f["H"]
+        Hf = H // 4
+        g_a1 = torch.empty(B, Hf, Hf, 256, device=self.dev, dtype=self.cdt)
+        ops.disc_head_bwd_data(g_img_part, g_img_part.shape[1], self.W2img, f["h1"], g_a1)
+        if want_params:
+            ops.disc_head_bwd_w(g_img_part, g_img_part.shape[1], f["h1"], self.dW["output_layer.0."])
+            ops.conv2d_wgrad(g_a1, f["h0"], 256, 4, 4, 2, 1, self.dW["conv_layers.2."])
+            ops.colsum(g_a1.view(-1, 256), self.G("conv_layers.2.bias"))
+        g_a0 = torch.empty(B, H // 2, H // 2, 128, device=self.dev, dtype=self.cdt)
+        ops.dgrad_s2(g_a1, self.W1cls, 128, g_a0, ep=E_(act=MUL_LRELU_GRAD, aux=f["h0"], ld_aux=128))
+        if want_params:
+            ops.gemm(g_a0.view(-1, 128), f["cols"], 128, 48, g_a0.numel() // 128, a_kc=False, b_kc=False,
+                     out=self.dW["conv_layers.0."].view(128, 48), ep=E_(accumulate=1))
+            ops.colsum(g_a0.view(-1, 128), self.G("conv_layers.0.bias"))
+        if g_input is not None:
+            ops.dgrad_s2(g_a0, self.W0cls, 3, g_input)
+        return g_a1, g_a0
+
+    def begin_grads(self):
+        self.dW = {pre: torch.zeros_like(self.W[pre]) for pre in WN_LAYERS}
+
+    def finish_grads(self):
+        # reference weight layout: conv_layers.0 packed as [o][tap*3+c] in the GEMM -> remap to [o][c][kh][kw]
+        for pre in WN_LAYERS:
+            ops.weight_norm_bwd(self.P(pre + "weight_v"), self.P(pre + "weight_g"), self.norm[pre], self.dW[pre],
+                                self.G(pre + "weight_v"), self.G(pre + "weight_g"))
+
+    # ------------------------------------------------------------------
+    def d_phase(self, real_nchw, text, fake_img, fake_layout, perm, r1_gamma):
+        """D loss + R1 and all D parameter gradients (t2i_moe_gan.py:1276-1326).
+        real_nchw [B,3,64,64] fp32; fake_img: generator output (NHWC padded [B,16,16,ld]).
+        Returns device scalars [d_loss_gan, sp_real, sp_fake, sp_mism] and r1, plus logits."""
+        B = real_nchw.shape[0]
+        Hr = real_nchw.shape[-1]
+        dev = self.dev
+        self.begin_grads()
+        t, tb = self.text_branch(text)
+        fr = self.forward(real_nchw, "nchw", text, B, Hr)
+        ff = self.forward(fake_img, fake_layout, text, B, fake_img.shape[1])
+        No = fr["img_part"].shape[1]
+        out = torch.zeros(4, device=dev)
+        g_img = torch.empty(B, No, device=dev)
+        g_fake = torch.empty(B, ff["img_part"].shape[1], device=dev)
+        g_tb = torch.zeros(B, device=dev)
+        real_pred = torch.empty(B, No, device=dev)
+        mism_pred = torch.empty(B, No, device=dev)
+        fake_pred = torch.empty(B, device=dev)
+        ops.d_loss(fr["img_part"], ff["img_part"].view(-1), tb, perm, out, g_img, g_fake.view(-1), g_tb,
+                   real_pred, mism_pred, fake_pred)
+        # ordinary first-order backward (real + mismatched share the image features)
+        self.stack_backward(fr, g_img)
+        self.stack_backward(ff, g_fake)
+        # text branch + head bias
+        g_tpre = torch.empty(B, 128, device=dev)
+        ops.d_text_bwd(g_tb, t, self.w2sum, 256, g_tpre, self.dW["output_layer.0."].view(384, 16))
+        ops.colsum(g_tb.view(B, 1), self.G("output_layer.0.bias"))
+        ops.linear_wgrad(g_tpre, text, self.dW["text_projection.0."])
+        ops.colsum(g_tpre, self.G("text_projection.0.bias"))
+        # ---- R1 ----
+        Hf = Hr // 4
+        Ho = Hf - 3
+        g1 = self._ones(Ho * Ho).view(1, -1)
+        gA1 = torch.empty(B, Hf, Hf, 256, device=dev, dtype=self.cdt)
+        ops.disc_head_bwd_data(g1, 0, self.W2img, fr["h1"], gA1)  # m1 * Gh1
+        gA0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
+        ops.dgrad_s2(gA1, self.W1cls, 128, gA0, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
+        gx = torch.zeros(B, Hr, Hr, 4, device=dev)
+        ops.dgrad_s2(gA0, self.W0cls, 3, gx)  # d sum(real_pred) / d real  (NHWC, channel-padded)
+        r1 = torch.zeros(1, device=dev)
+        u = torch.empty(B, Hr, Hr, 4, device=dev, dtype=self.cdt)
+        ops.r1(gx, B, r1_gamma, r1, u)
+        cols_u = ops.im2col_4x4s2(u, (Hr * Hr * 4, Hr * 4, 4, 1), B, Hr, Hr, 3, 48, self.cdt)
+        m0v0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
+        ops.gemm(cols_u, self.W0p, cols_u.shape[0], 128, 48, out=m0v0.view(-1, 128),
+                 ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
+        m1v1 = ops.conv2d(m0v0, self.W1p, 256, 4, 4, 2, 1, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h1"], ld_aux=256))
+        ops.gemm(gA0.view(-1, 128), cols_u, 128, 48, gA0.numel() // 128, a_kc=False, b_kc=False,
+                 out=self.dW["conv_layers.0."].view(128, 48), ep=E_(accumulate=1))
+        ops.conv2d_wgrad(gA1, m0v0, 256, 4, 4, 2, 1, self.dW["conv_layers.2."])
+        ops.disc_head_bwd_w(g1, 0, m1v1, self.dW["output_layer.0."])
+        self._remap_w0()
+        self.finish_grads()
+        return dict(losses=out, r1=r1, real_pred=real_pred, mism_pred=mism_pred, fake_pred=fake_pred, r1_grad=gx)
+
+    def _remap_w0(self):
+        """dW0 was accumulated in the GEMM layout [o][tap*3 + c]; convert to [o][c][kh][kw]."""
+        g = self.dW["conv_layers.0."].view(128, 16, 3)
+        self.dW["conv_layers.0."] = g.permute(0, 2, 1).contiguous().view(128, 3, 4, 4)
+
+    # ------------------------------------------------------------------
+    def g_phase(self, fake_img, fake_layout, text, scale=1.0):
+        """Adversarial loss of the generator step (t2i_moe_gan.py:1379-1382) and d loss / d fake image.
+        D parameter gradients are not formed: with gradient_accumulation_steps=1 the reference zeroes
+        them before they are ever used (t2i_moe_gan.py:1272 vs :1407)."""
+        B = fake_img.shape[0]
+        Hs = fake_img.shape[1]
+        t, tb = self.text_branch(text)
+        f = self.forward(fake_img, fake_layout, text, B, Hs)
+        fake_pred = torch.empty(B, device=self.dev)
+        ops.copy2d(f["img_part"], fake_pred.view(B, 1), B, 1)
+        ops.copy2d(tb.view(B, 1), fake_pred.view(B, 1), B, 1, accumulate=1)
+        loss = torch.zeros(1, device=self.dev)
+        g = torch.empty(B, 1, device=self.dev)
+        ops.g_loss(fake_pred, loss, g.view(-1), scale)
+        g_img = torch.zeros(fake_img.shape, device=self.dev, dtype=self.cdt)
+        self.stack_backward(f, g, want_params=False, g_input=g_img)
+        return loss, fake_pred, g_img

@@ -1,0 +1,484 @@
+"""Explicit forward/backward of the Aurora MoE generator on the HIP kernels.
+
+Mirrors AuroraGenerator (t2i_moe_gan.py:668-855) module by module, but as an
+explicit two-pass engine: ``forward`` records exactly the activations its
+``backward`` needs (no autograd graph, no tape), every contraction runs on the
+MFMA GEMM core, and all activations are NHWC token rows in HBM.
+
+Numerics: ``cdt`` is the activation / MFMA-operand dtype (fp32 = parity mode,
+bf16 = the C2 bench mode).  Styles, demodulation coefficients, router logits,
+LayerNorm statistics and every parameter gradient stay fp32.
+
+Randomness is explicit: router epsilon triples, z and the mismatch
+permutation are inputs (SURVEY.md §7 "Randomness parity").
+"""
+import torch
+
+from . import _lib as L
+from . import ops
+from .layout import GEN_BLOCKS
+
+E_ = ops.E
+LRELU, GELU, RSQRT = L.ACT_LRELU, L.ACT_GELU, L.ACT_RSQRT_EPS
+MUL_GELU_GRAD, MUL_LRELU_GRAD = L.ACT_MUL_GELU_GRAD, L.ACT_MUL_LRELU_GRAD
+
+
+def _modconv_prefixes(E=None):
+    out = []
+    for name, cin, cout, _, _ in GEN_BLOCKS:
+        cb = name + ".conv_block."
+        out += [(cb + "mtm1.modulated_conv.", 3), (cb + "mtm2.modulated_conv.", 3)]
+        if cin != cout:
+            out.append((cb + "skip_proj.", 1))
+        out += [(name + ".attn_block.proj_in.", 1), (name + ".attn_block.proj_out.", 1)]
+    out += [("to_rgb_8.", 1), ("to_rgb_16.", 1)]
+    return out
+
+
+class GeneratorEngine:
+    def __init__(self, store, E, topk=None, cdt=torch.float32):
+        self.st = store
+        self.E = E
+        self.k = topk or E
+        self.cdt = cdt
+        self.dev = store.device
+        self.packs = {}
+        self._ones = None
+
+    # parameter access
+    def P(self, n):
+        return self.st.view(n)
+
+    def Pc(self, n):
+        return self.st.cview(n)
+
+    def G(self, n):
+        return self.st.gview(n)
+
+    # ------------------------------------------------------------------
+    # per-step weight preparation (after every optimizer step)
+    # ------------------------------------------------------------------
+    def prep(self):
+        self.st.refresh_shadow()
+        pk = {}
+        for pre, k in _modconv_prefixes():
+            W = self.P(pre + "weight")
+            Cout = W.shape[0]
+            rows = max(Cout, 8)
+            ent = {"rows": rows, "wsq": ops.wsq(W, rows=rows)}
+            if k == 3:
+                ent["w"] = ops.pack_conv(W, self.cdt)
+                ent["wflip"] = ops.pack_conv(W, self.cdt, flip=True)
+            elif rows != Cout:
+                ent["w"] = ops.pack_conv(W, self.cdt, rows=rows)
+            else:
+                ent["w"] = self.Pc(pre + "weight").view(Cout, -1)
+            pk[pre] = ent
+        for name, _, _, _, _ in GEN_BLOCKS:
+            for m in ("mtm1", "mtm2"):
+                pre = f"{name}.conv_block.{m}.offset_net.0."
+                W = self.P(pre + "weight")
+                pk[pre] = {"w": ops.pack_conv(W, self.cdt), "wflip": ops.pack_conv(W, self.cdt, flip=True)}
+        self.packs = pk
+
+    # ------------------------------------------------------------------
+    # ModulatedConv  (t2i_moe_gan.py:154-186), fused form
+    # ------------------------------------------------------------------
+    def mc_fwd(self, pre, x, w, act=0, resid=None, save=True):
+        B, H, W, Cin = x.shape
+        HW = H * W
+        pk = self.packs[pre]
+        rows = pk["rows"]
+        Wt = self.P(pre + "weight")
+        k = Wt.shape[-1]
+        s = ops.linear(w, self.P(pre + "modulation.weight"), bias=self.P(pre + "modulation.bias"))  # :158
+        s2 = ops.cast(s, square=1)
+        d = ops.gemm(s2, pk["wsq"], B, rows, Cin, ep=E_(act=RSQRT))  # demod coefficients [B, rows] (:165)
+        ep = E_(scale=d, scale_shift=ops.ilog2(HW), scale_ld=rows, act=act, resid=resid,
+                ld_res=resid.shape[-1] if resid is not None else 0)
+        y = ops.conv2d(x, pk["w"], rows, k, k, 1, k // 2, in_scale=s, ep=ep, out_dtype=self.cdt)
+        sv = (x, w, s, s2, d, y, resid, act) if save else None
+        return y, sv
+
+    def mc_bwd(self, pre, sv, gz, gx, gw, accumulate=0):
+        """gz: grad of the conv output (post activation / residual). Writes/accumulates gx, accumulates gw."""
+        x, w, s, s2, d, z, zsub, act = sv
+        B, H, W, Cin = x.shape
+        HW = H * W
+        pk = self.packs[pre]
+        rows = pk["rows"]
+        Wt = self.P(pre + "weight")
+        Cout, k = Wt.shape[0], Wt.shape[-1]
+        P = B * HW
+        gyt = torch.empty(P, rows, device=self.dev, dtype=self.cdt)
+        gdd = torch.empty(B, rows, device=self.dev, dtype=torch.float32)
+        ops.modconv_bwd_out(gz.view(P, -1), z.view(P, -1), d, B, HW, rows, act, gyt, gdd,
+                            zsub=None if zsub is None else zsub.view(P, -1))
+        # data gradient of the shared-weight conv
+        if k == 3:
+            gxt = ops.conv2d(gyt.view(B, H, W, rows), pk["wflip"], Cin, 3, 3, 1, 1)
+        else:
+            gxt = ops.gemm(gyt, pk["w"], P, Cin, rows, b_kc=False)
+        gs = torch.zeros(B, Cin, device=self.dev, dtype=torch.float32)
+        ops.modconv_bwd_in(gxt.view(P, Cin), x.view(P, Cin), s, B, HW, Cin,
+                           None if gx is None else gx.view(P, -1), gs, accumulate)
+        # weight gradient (fp32, reference layout)
+        if rows == Cout:
+            ops.conv2d_wgrad(gyt, x, Cout, k, k, 1, k // 2, self.G(pre + "weight"), in_scale=s)
+        else:
+            tmp = torch.zeros(rows, Cin, k, k, device=self.dev)
+            ops.conv2d_wgrad(gyt, x, rows, k, k, 1, k // 2, tmp, in_scale=s)
+            self.G(pre + "weight").add_(tmp[:Cout])
+        # demodulation backward
+        gwsq = ops.gemm(gdd, s2, rows, Cin, B, a_kc=False, b_kc=False)  # [rows, Cin] = gdd^T s^2
+        ops.wsq_bwd(Wt, gwsq[:Cout], self.G(pre + "weight"))
+        ops.gemm(gdd, pk["wsq"], B, Cin, rows, b_kc=False, out=gs,
+                 ep=E_(alpha=2.0, scale=s, scale_ld=Cin, accumulate=1))  # gs += 2 s (gdd @ wsq)
+        # style = modulation(w)
+        ops.linear_wgrad(gs, w, self.G(pre + "modulation.weight"))
+        ops.colsum(gs, self.G(pre + "modulation.bias"))
+        ops.gemm(gs, self.P(pre + "modulation.weight"), B, w.shape[1], Cin, b_kc=False, out=gw,
+                 ep=E_(accumulate=1))
+
+    # ------------------------------------------------------------------
+    # Modulated Transformation Module  (t2i_moe_gan.py:218-247)
+    # ------------------------------------------------------------------
+    def mtm_fwd(self, pre, x, w, resid=None, save=True):
+        opk = self.packs[pre + "offset_net.0."]
+        o1 = ops.conv2d(x, opk["w"], 32, 3, 3, 1, 1, out_dtype=self.cdt,
+                        ep=E_(bias=self.P(pre + "offset_net.0.bias"), act=LRELU))
+        xw, samp = ops.warp_fwd(x, o1, self.P(pre + "offset_net.2.weight"), self.P(pre + "offset_net.2.bias"))
+        y, msv = self.mc_fwd(pre + "modulated_conv.", xw, w, act=1, resid=resid, save=save)
+        return y, ((x, o1, samp, xw, msv) if save else None)
+
+    def mtm_bwd(self, pre, sv, gz, gx, gw, accumulate=0):
+        x, o1, samp, xw, msv = sv
+        B, H, W, Cin = x.shape
+        P = B * H * W
+        g_xw = torch.empty(P, Cin, device=self.dev, dtype=self.cdt)
+        self.mc_bwd(pre + "modulated_conv.", msv, gz, g_xw, gw)
+        gx32 = torch.zeros(B, H, W, Cin, device=self.dev, dtype=torch.float32)
+        goff = torch.empty(P, 2, device=self.dev, dtype=torch.float32)
+        ops.warp_bwd(g_xw, x, samp, gx32, goff)
+        ga1 = torch.empty(B, H, W, 32, device=self.dev, dtype=self.cdt)
+        ops.offset_head_bwd(goff, o1, self.P(pre + "offset_net.2.weight"), ga1,
+                            self.G(pre + "offset_net.2.weight"), self.G(pre + "offset_net.2.bias"))
+        opk = self.packs[pre + "offset_net.0."]
+        ops.conv2d(ga1, opk["wflip"], Cin, 3, 3, 1, 1, out=gx32, ep=E_(accumulate=1))
+        ops.conv2d_wgrad(ga1, x, 32, 3, 3, 1, 1, self.G(pre + "offset_net.0.weight"))
+        ops.colsum(ga1.view(P, 32), self.G(pre + "offset_net.0.bias"))
+        ops.copy2d(gx32.view(P, Cin), gx.view(P, Cin), P, Cin, accumulate=accumulate)
+
+    # ------------------------------------------------------------------
+    # ConvolutionBlock  (t2i_moe_gan.py:579-621)
+    # ------------------------------------------------------------------
+    def cb_fwd(self, pre, x, w, save=True):
+        h1, sv1 = self.mtm_fwd(pre + "mtm1.", x, w, save=save)
+        svs = None
+        if (pre + "skip_proj.weight") in self.st.offsets:
+            sk, svs = self.mc_fwd(pre + "skip_proj.", x, w, save=save)
+        else:
+            sk = x
+        out, sv2 = self.mtm_fwd(pre + "mtm2.", h1, w, resid=sk, save=save)
+        return out, ((sv1, svs, sv2, h1) if save else None)
+
+    def cb_bwd(self, pre, sv, g_out, gx, gw):
+        sv1, svs, sv2, h1 = sv
+        g_h1 = torch.empty_like(h1)
+        self.mtm_bwd(pre + "mtm2.", sv2, g_out, g_h1, gw)
+        if svs is not None:
+            self.mc_bwd(pre + "skip_proj.", svs, g_out, gx, gw)
+        else:
+            ops.copy2d(g_out.view(-1, g_out.shape[-1]), gx.view(-1, gx.shape[-1]), g_out.numel() // g_out.shape[-1],
+                       g_out.shape[-1])
+        self.mtm_bwd(pre + "mtm1.", sv1, g_h1, gx, gw, accumulate=1)
+
+    # ------------------------------------------------------------------
+    # SparseMoE + BayesianRouter  (t2i_moe_gan.py:265-491)
+    # ------------------------------------------------------------------
+    def moe_fwd(self, pre, tok, resid, w, HW, eps, anneal, train=True, save=True):
+        r = pre + "router."
+        T, C = tok.shape
+        B = w.shape[0]
+        E, k = self.E, (self.k if train else 1)
+        if train:
+            Wf = ops.reparam(self.P(r + "feature_mu"), self.P(r + "feature_rho"), eps[0])
+            Wt = ops.reparam(self.P(r + "text_mu"), self.P(r + "text_rho"), eps[1])
+            Wc = ops.reparam(self.P(r + "combined_mu"), self.P(r + "combined_rho"), eps[2])
+        else:
+            Wf, Wt, Wc = self.P(r + "feature_mu"), self.P(r + "text_mu"), self.P(r + "combined_mu")
+        Wfc = ops.gemm(Wf, Wc[:128], C, E, 128, b_kc=False)  # [C, E]
+        u = ops.gemm(w, Wt, B, 128, w.shape[1], b_kc=False)  # [B, 128]
+        Lt = ops.gemm(u, Wc[128:], B, E, 128, b_kc=False)  # [B, E]
+        probs, zlog, topi, gate = ops.router_fwd(tok, Wfc, Lt, E, k, HW, self.P(r + "temperature"), anneal,
+                                                 eval_mode=0 if train else 1)
+        row_off, tile_off, perm, pos_of, gate_pos = ops.moe_dispatch(topi, gate, E)
+        n = T * k
+        max_tiles = (n + 127) // 128 + E
+        ex = pre + "experts."
+        W1 = self.st.group_view(ex + "0.net.0.weight", f"{ex}{E-1}.net.0.weight", self._cbuf())
+        b1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias")
+        W2 = self.st.group_view(ex + "0.net.2.weight", f"{ex}{E-1}.net.2.weight", self._cbuf())
+        b2 = self.st.group_view(ex + "0.net.2.bias", f"{ex}{E-1}.net.2.bias")
+        Hd = 4 * C
+        Pre = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+        ops.gemm_grouped(tok, W1, row_off, tile_off, max_tiles, Hd, C, b_gstride=Hd * C, out=Pre, ldb=C,
+                         ep=E_(bias=b1, a_idx=perm, a_idx_div=k))
+        Y = torch.empty(n, C, device=self.dev, dtype=self.cdt)
+        ops.gemm_grouped(Pre, W2, row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y, ldb=Hd,
+                         ep=E_(bias=b2, a_gelu=1))
+        out = torch.empty(T, C, device=self.dev, dtype=self.cdt)
+        ops.moe_combine(Y, pos_of, gate, resid, out)  # x_spatial + moe_out (:571)
+        kl2 = None
+        if train:
+            kl2 = torch.empty(2, device=self.dev, dtype=torch.float32)
+            ops.router_kl(self.P(r + "feature_mu"), self.P(r + "feature_rho"), self.P(r + "text_mu"),
+                          self.P(r + "text_rho"), self.P(r + "combined_mu"), self.P(r + "combined_rho"), kl2)
+        sv = None
+        if save:
+            sv = dict(tok=tok, w=w, HW=HW, eps=eps, anneal=anneal, Wf=Wf, Wt=Wt, Wc=Wc, Wfc=Wfc, u=u, probs=probs,
+                      zlog=zlog, topi=topi, gate=gate, row_off=row_off, tile_off=tile_off, perm=perm, pos_of=pos_of,
+                      gate_pos=gate_pos, Pre=Pre, Y=Y, W1=W1, W2=W2, max_tiles=max_tiles)
+        return out, probs, kl2, topi, sv
+
+    def _cbuf(self):
+        return self.st.shadow if self.st.shadow is not None else self.st.data
+
+    def moe_bwd(self, pre, sv, g_out, g_tok, gw, coef=None, kl_coef=None, g_probs=None):
+        """g_out: grad of (resid + moe) [T, C]; writes g_tok (grad of the LN3 tokens); accumulates gw."""
+        r = pre + "router."
+        tok, w, Y, Pre = sv["tok"], sv["w"], sv["Y"], sv["Pre"]
+        T, C = tok.shape
+        B = w.shape[0]
+        E, k = self.E, sv["topi"].shape[1]
+        n = T * k
+        Hd = 4 * C
+        row_off, tile_off, perm = sv["row_off"], sv["tile_off"], sv["perm"]
+        ex = pre + "experts."
+        g_gate = ops.moe_gate_grad(g_out, Y, sv["pos_of"], T, k)
+        # expert layer 2: dH = (gate * g_out[t]) @ W2_e, times GELU'(pre)
+        gP = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+        ops.gemm_grouped(g_out, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
+                         out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd, a_idx=perm, a_idx_div=k,
+                                       a_rowscale=sv["gate_pos"]))
+        gW2 = self.st.group_view(ex + "0.net.2.weight", f"{ex}{E-1}.net.2.weight", self.st.grad)
+        ops.gemm_grouped_wgrad(g_out, Pre, row_off, n, C, Hd, gW2, b_gelu=1,
+                               ep=E_(a_idx=perm, a_idx_div=k, a_rowscale=sv["gate_pos"]))
+        gb2 = self.st.group_view(ex + "0.net.2.bias", f"{ex}{E-1}.net.2.bias", self.st.grad)
+        ops.grouped_colsum(g_out, row_off, C, n, gb2, idx=perm, idx_div=k, rs=sv["gate_pos"])
+        # expert layer 1
+        gX = torch.empty(n, C, device=self.dev, dtype=self.cdt)
+        ops.gemm_grouped(gP, sv["W1"], row_off, tile_off, sv["max_tiles"], C, Hd, b_kc=False, b_gstride=Hd * C,
+                         out=gX, ldb=C)
+        gW1 = self.st.group_view(ex + "0.net.0.weight", f"{ex}{E-1}.net.0.weight", self.st.grad)
+        ops.gemm_grouped_wgrad(gP, tok, row_off, n, Hd, C, gW1, b_idx=perm, b_idx_div=k)
+        gb1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias", self.st.grad)
+        ops.grouped_colsum(gP, row_off, Hd, n, gb1)
+        # router
+        g_raw, gsum = ops.router_bwd(sv["probs"], sv["zlog"], sv["topi"], sv["gate"], g_gate, g_probs, coef,
+                                     sv["HW"], self.P(r + "temperature"), sv["anneal"], self.G(r + "temperature"), B)
+        ops.moe_token_grad(gX, sv["pos_of"], g_raw, sv["Wfc"], g_tok, k)
+        G1 = torch.zeros(C, E, device=self.dev, dtype=torch.float32)
+        ops.router_feat_grad(tok, g_raw, G1)
+        Wf, Wt, Wc, u = sv["Wf"], sv["Wt"], sv["Wc"], sv["u"]
+        gWf = ops.gemm(G1, Wc[:128], C, 128, E)  # G1 @ Wc1^T
+        gWc = torch.empty(256, E, device=self.dev, dtype=torch.float32)
+        ops.gemm(Wf, G1, 128, E, C, a_kc=False, b_kc=False, out=gWc[:128])  # Wf^T G1
+        g_u = ops.gemm(gsum, Wc[128:], B, 128, E)  # gsum @ Wc2^T
+        ops.gemm(u, gsum, 128, E, B, a_kc=False, b_kc=False, out=gWc[128:])  # u^T gsum
+        gWt = ops.gemm(w, g_u, w.shape[1], 128, B, a_kc=False, b_kc=False)  # w^T g_u
+        ops.gemm(g_u, Wt, B, w.shape[1], 128, out=gw, ep=E_(accumulate=1))  # gw += g_u Wt^T
+        for nm, gWx, epi in (("feature", gWf, 0), ("text", gWt, 1), ("combined", gWc, 2)):
+            ops.router_param_bwd(self.P(r + nm + "_mu"), self.P(r + nm + "_rho"), sv["eps"][epi], gWx, kl_coef,
+                                 self.G(r + nm + "_mu"), self.G(r + nm + "_rho"))
+
+    # ------------------------------------------------------------------
+    # AttentionBlock  (t2i_moe_gan.py:493-576)
+    # ------------------------------------------------------------------
+    def attn_fwd(self, pre, x, w, text_seq, eps, anneal, train=True, save=True):
+        B, H, W, C = x.shape
+        L_ = H * W
+        T = B * L_
+        xf0, sv_in = self.mc_fwd(pre + "proj_in.", x, w, save=save)
+        xf0 = xf0.view(T, C)
+        n1, mu1, rs1 = ops.layernorm_fwd(xf0, self.P(pre + "norm1.weight"), self.P(pre + "norm1.bias"))
+        qkv = ops.linear(n1, self.Pc(pre + "self_attn.in_proj_weight"), bias=self.P(pre + "self_attn.in_proj_bias"))
+        att, lse = ops.attn_fwd(qkv, B, L_, C)
+        # cross-attention against the single text token: softmax over one key == 1 (:553-555)
+        ca_W = self.P(pre + "cross_attn.in_proj_weight")
+        ca_b = self.P(pre + "cross_attn.in_proj_bias")
+        tp = ops.linear(text_seq, self.P(pre + "text_proj.weight"), bias=self.P(pre + "text_proj.bias"))
+        vv = ops.linear(tp, ca_W[2 * C:], bias=ca_b[2 * C:])
+        ca = ops.linear(vv, self.P(pre + "cross_attn.out_proj.weight"), bias=self.P(pre + "cross_attn.out_proj.bias"))
+        xf1 = ops.linear(att, self.Pc(pre + "self_attn.out_proj.weight"), bias=self.P(pre + "self_attn.out_proj.bias"),
+                         resid=xf0, ld_res=C, addvec=ca, add_shift=ops.ilog2(L_), add_ld=C)
+        n3, mu3, rs3 = ops.layernorm_fwd(xf1, self.P(pre + "norm3.weight"), self.P(pre + "norm3.bias"))
+        xpre, probs, kl2, topi, sv_moe = self.moe_fwd(pre + "moe.", n3, xf1, w, L_, eps, anneal, train, save)
+        out, sv_out = self.mc_fwd(pre + "proj_out.", xpre.view(B, H, W, C), w, save=save)
+        sv = None
+        if save:
+            sv = dict(sv_in=sv_in, xf0=xf0, n1=n1, mu1=mu1, rs1=rs1, qkv=qkv, att=att, lse=lse, tp=tp, vv=vv,
+                      xf1=xf1, n3=n3, mu3=mu3, rs3=rs3, sv_moe=sv_moe, sv_out=sv_out, text_seq=text_seq, B=B, L=L_)
+        return out, probs, kl2, topi, sv
+
+    def attn_bwd(self, pre, sv, g_out, gx, gw, g_text_seq, coef=None, kl_coef=None, g_probs=None):
+        B, L_ = sv["B"], sv["L"]
+        T, C = sv["xf0"].shape
+        g_xpre = torch.empty(T, C, device=self.dev, dtype=self.cdt)
+        self.mc_bwd(pre + "proj_out.", sv["sv_out"], g_out, g_xpre, gw)
+        # MoE branch -> LN3 -> residual
+        g_n3 = torch.empty(T, C, device=self.dev, dtype=self.cdt)
+        self.moe_bwd(pre + "moe.", sv["sv_moe"], g_xpre, g_n3, gw, coef=coef, kl_coef=kl_coef, g_probs=g_probs)
+        g_xf1 = g_xpre  # residual path, accumulate LN3 backward into it
+        ops.layernorm_bwd(g_n3, sv["xf1"], sv["mu3"], sv["rs3"], self.P(pre + "norm3.weight"), g_xf1,
+                          self.G(pre + "norm3.weight"), self.G(pre + "norm3.bias"), accumulate=1)
+        # cross-attention vector: sum over each image's tokens
+        g_ca = torch.zeros(B, C, device=self.dev, dtype=torch.float32)
+        ops.segsum(g_xf1, B, L_, C, g_ca)
+        ca_W = self.P(pre + "cross_attn.in_proj_weight")
+        gca_W = self.G(pre + "cross_attn.in_proj_weight")
+        ops.linear_wgrad(g_ca, sv["vv"], self.G(pre + "cross_attn.out_proj.weight"))
+        ops.colsum(g_ca, self.G(pre + "cross_attn.out_proj.bias"))
+        g_vv = ops.linear_dgrad(g_ca, self.P(pre + "cross_attn.out_proj.weight"))
+        ops.linear_wgrad(g_vv, sv["tp"], gca_W[2 * C:])
+        ops.colsum(g_vv, self.G(pre + "cross_attn.in_proj_bias")[2 * C:])
+        g_tp = ops.linear_dgrad(g_vv, ca_W[2 * C:])
+        ops.linear_wgrad(g_tp, sv["text_seq"], self.G(pre + "text_proj.weight"))
+        ops.colsum(g_tp, self.G(pre + "text_proj.bias"))
+        ops.linear_dgrad(g_tp, self.P(pre + "text_proj.weight"), out=g_text_seq, accumulate=1)
+        # self-attention
+        g_att = ops.linear_dgrad(g_xf1, self.Pc(pre + "self_attn.out_proj.weight"))
+        ops.linear_wgrad(g_xf1, sv["att"], self.G(pre + "self_attn.out_proj.weight"))
+        ops.colsum(g_xf1, self.G(pre + "self_attn.out_proj.bias"))
+        g_qkv = ops.attn_bwd(sv["qkv"], sv["att"], g_att, sv["lse"], B, L_, C)
+        g_n1 = ops.linear_dgrad(g_qkv, self.Pc(pre + "self_attn.in_proj_weight"))
+        ops.linear_wgrad(g_qkv, sv["n1"], self.G(pre + "self_attn.in_proj_weight"))
+        ops.colsum(g_qkv, self.G(pre + "self_attn.in_proj_bias"))
+        g_xf0 = g_xf1
+        ops.layernorm_bwd(g_n1, sv["xf0"], sv["mu1"], sv["rs1"], self.P(pre + "norm1.weight"), g_xf0,
+                          self.G(pre + "norm1.weight"), self.G(pre + "norm1.bias"), accumulate=1)
+        self.mc_bwd(pre + "proj_in.", sv["sv_in"], g_xf0, gx, gw)
+
+    # ------------------------------------------------------------------
+    # AuroraGenerator  (t2i_moe_gan.py:762-855)
+    # ------------------------------------------------------------------
+    def _mapping(self, zt, save):
+        hs = [zt]
+        h = zt
+        for i in (0, 2, 4):
+            h = ops.linear(h, self.P(f"mapping.{i}.weight"), bias=self.P(f"mapping.{i}.bias"), act=LRELU)
+            hs.append(h)
+        return h, hs
+
+    def forward(self, z, text, eps, anneal=1.0, psi=0.7, train=True, save=True, want_img8=False):
+        """Returns (img16 [B,16,16,8] padded NHWC, img8 or None, kl2 list, probs list, ctx)."""
+        B = z.shape[0]
+        dev = self.dev
+        if text.shape[0] != B and text.shape[0] == 1:
+            text = text.expand(B, -1).contiguous()
+        # text projection (:682-687, :790)
+        t0 = ops.linear(text, self.P("text_projection.0.weight"), bias=self.P("text_projection.0.bias"))
+        t1, tmu, trs = ops.layernorm_fwd(t0, self.P("text_projection.1.weight"), self.P("text_projection.1.bias"),
+                                         act=1)
+        text_seq = ops.linear(t1, self.P("text_projection.3.weight"), bias=self.P("text_projection.3.bias"))
+        # mapping + truncation (:793-808)
+        zt = torch.empty(B, z.shape[1] + text.shape[1], device=dev)
+        ops.copy2d(z, zt, B, z.shape[1], ldo=zt.shape[1])
+        ops.copy2d(text, zt[:, z.shape[1]:], B, text.shape[1], ldo=zt.shape[1])
+        h3, hs = self._mapping(zt, save)
+        if psi < 1.0:
+            zeros = torch.zeros(1, zt.shape[1], device=dev)
+            m3, _ = self._mapping(zeros, False)
+            mean = ops.linear(m3, self.P("mapping.6.weight"), bias=self.P("mapping.6.bias"))
+            beff = torch.empty(512, device=dev)
+            ops.copy2d(self.P("mapping.6.bias").view(1, -1), beff.view(1, -1), 1, 512, alpha=psi)
+            ops.copy2d(mean, beff.view(1, -1), 1, 512, alpha=1.0 - psi, accumulate=1)
+            w = ops.linear(h3, self.P("mapping.6.weight"), bias=beff, alpha=psi)
+        else:
+            w = ops.linear(h3, self.P("mapping.6.weight"), bias=self.P("mapping.6.bias"))
+        x = ops.const_fwd(self.P("constant"), B, self.cdt)
+        probs, kl2s, topis, blocks = [], [], [], []
+        img8, rgb8sv = None, None
+        for i, (name, cin, cout, res, up) in enumerate(GEN_BLOCKS):
+            if up:
+                x = ops.upsample2x(x)
+            x, cbsv = self.cb_fwd(name + ".conv_block.", x, w, save=save)
+            x, p, kl2, topi, asv = self.attn_fwd(name + ".attn_block.", x, w, text_seq,
+                                                 None if eps is None else eps[i], anneal, train, save)
+            probs.append(p)
+            kl2s.append(kl2)
+            topis.append(topi)
+            blocks.append((cbsv, asv, up))
+            if name == "gen_block_8" and want_img8:
+                img8, rgb8sv = self.mc_fwd("to_rgb_8.", x, w, save=save)
+        img16, rgbsv = self.mc_fwd("to_rgb_16.", x, w, save=save)
+        ctx = None
+        if save:
+            ctx = dict(B=B, text=text, z=z, t0=t0, t1=t1, tmu=tmu, trs=trs, text_seq=text_seq, hs=hs, h3=h3, w=w,
+                       psi=psi, blocks=blocks, rgbsv=rgbsv, rgb8sv=rgb8sv)
+        return img16, img8, kl2s, probs, topis, ctx
+
+    def backward(self, ctx, g_img16, coef=None, kl_coef=None, want_input_grads=False, g_probs=None, g_img8=None):
+        """Accumulate all generator parameter gradients for d loss / d img16 (+ balance coef on the last
+        router, + KL coefficients [3] per router).  Optional: per-router d loss / d probs [T, E] (g_probs list)
+        and d loss / d img8 (needs forward(..., want_img8=True, save=True)).  Returns (gz, gtext) if requested."""
+        B = ctx["B"]
+        dev = self.dev
+        gw = torch.zeros(B, 512, device=dev)
+        g_ts = torch.zeros(B, 512, device=dev)
+        sv = ctx["rgbsv"]
+        x_last = sv[0]
+        gx = torch.empty(x_last.shape, device=dev, dtype=self.cdt)
+        self.mc_bwd("to_rgb_16.", sv, g_img16, gx, gw)
+        nb = len(GEN_BLOCKS)
+        for i in reversed(range(nb)):
+            name, cin, cout, res, up = GEN_BLOCKS[i]
+            cbsv, asv, up = ctx["blocks"][i]
+            g_cb = torch.empty(gx.shape, device=dev, dtype=self.cdt)
+            kc = None if kl_coef is None else kl_coef[i:i + 1]
+            if name == "gen_block_8" and g_img8 is not None:
+                self.mc_bwd("to_rgb_8.", ctx["rgb8sv"], g_img8, gx, gw, accumulate=1)
+            self.attn_bwd(name + ".attn_block.", asv, gx, g_cb, gw, g_ts, coef=coef if i == nb - 1 else None,
+                          kl_coef=kc, g_probs=None if g_probs is None else g_probs[i])
+            x_in = cbsv[0][0]  # input of mtm1
+            g_in = torch.empty(x_in.shape, device=dev, dtype=self.cdt)
+            self.cb_bwd(name + ".conv_block.", cbsv, g_cb, g_in, gw)
+            if up:
+                Bq, H2, W2, Cq = g_in.shape
+                gprev = torch.empty(Bq, H2 // 2, W2 // 2, Cq, device=dev, dtype=self.cdt)
+                ops.upsample2x_bwd(g_in, gprev)
+                gx = gprev
+            else:
+                gx = g_in
+        ops.const_bwd(gx, self.G("constant"))
+        # truncation: w = mean + psi (w_full - mean), mean under no_grad
+        psi = ctx["psi"]
+        g6 = ops.cast(gw, alpha=psi if psi < 1.0 else 1.0)
+        hs = ctx["hs"]
+        ops.linear_wgrad(g6, hs[3], self.G("mapping.6.weight"))
+        ops.colsum(g6, self.G("mapping.6.bias"))
+        g = ops.linear_dgrad(g6, self.P("mapping.6.weight"))
+        for j, i in enumerate((4, 2, 0)):
+            ops.lrelu_mask_mul(g, hs[3 - j], g)
+            ops.linear_wgrad(g, hs[2 - j], self.G(f"mapping.{i}.weight"))
+            ops.colsum(g, self.G(f"mapping.{i}.bias"))
+            if i != 0 or want_input_grads:
+                g = ops.linear_dgrad(g, self.P(f"mapping.{i}.weight"))
+        g_zt = g if want_input_grads else None
+        # text projection backward
+        ops.linear_wgrad(g_ts, ctx["t1"], self.G("text_projection.3.weight"))
+        ops.colsum(g_ts, self.G("text_projection.3.bias"))
+        g_t1 = ops.linear_dgrad(g_ts, self.P("text_projection.3.weight"))
+        ops.lrelu_mask_mul(g_t1, ctx["t1"], g_t1)
+        g_t0 = torch.empty_like(g_t1)
+        ops.layernorm_bwd(g_t1, ctx["t0"], ctx["tmu"], ctx["trs"], self.P("text_projection.1.weight"), g_t0,
+                          self.G("text_projection.1.weight"), self.G("text_projection.1.bias"))
+        ops.linear_wgrad(g_t0, ctx["text"], self.G("text_projection.0.weight"))
+        ops.colsum(g_t0, self.G("text_projection.0.bias"))
+        if not want_input_grads:
+            return None, None
+        gtext = ops.linear_dgrad(g_t0, self.P("text_projection.0.weight"))
+        zd = ctx["z"].shape[1]
+        gz = g_zt[:, :zd].contiguous()
+        gtext = gtext + g_zt[:, zd:]
+        return gz, gtext

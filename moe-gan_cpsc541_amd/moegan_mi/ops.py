@@ -1,71 +1,468 @@
-"""Thin Python wrappers over the C ABI (tensor plumbing only; all math is in HIP)."""
+"""Thin Python wrappers over the C ABI (tensor plumbing only; all math is in HIP).
+
+Every function enqueues on torch's current stream and returns its output
+tensor(s).  Shapes follow include/moegan_hip.h: activations are NHWC/token
+rows, weights are in the reference layout unless a ``pack`` says otherwise.
+"""
 import math
 
 import torch
 
 from . import _lib as L
 
+call, ptr, dt, S = L.call, L.ptr, L.dt, L.stream
+E = L.epilogue
+
 
 def _ld(t):
     return t.stride(0) if t.dim() > 1 else t.shape[0]
 
 
+# Optional live kernel timer (bench.py): when set, launches whose (kind, dims) satisfy
+# TIMER.want(kind, dims) are bracketed by HIP events on the current stream.
+TIMER = None
+
+
+class KernelTimer:
+    def __init__(self, want):
+        self.want = want
+        self.events = []  # (kind, dims, start, end)
+
+    def wrap(self, kind, dims, fn):
+        if not self.want(kind, dims):
+            return fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = fn()
+        e.record()
+        self.events.append((kind, dims, s, e))
+        return r
+
+    def results(self):
+        torch.cuda.synchronize()
+        return [(k, d, s.elapsed_time(e)) for k, d, s, e in self.events]
+
+
+def _timed(kind, dims, fn):
+    if TIMER is None:
+        return fn()
+    return TIMER.wrap(kind, dims, fn)
+
+
+def ilog2(v):
+    r = int(math.log2(v))
+    assert 1 << r == v, v
+    return r
+
+
+# ---------------------------------------------------------------------------
+# GEMM family
+# ---------------------------------------------------------------------------
 def gemm(A, B, M, N, K, *, a_kc=True, b_kc=True, out=None, out_dtype=None, lda=None, ldb=None, ldc=None,
          ep=None, splits=1):
-    """C[M,N] = epilogue(op(A) @ op(B)).  See mg_gemm in include/moegan_hip.h."""
+    """C[M,N] = epilogue(op(A) @ op(B)) (mg_gemm)."""
     if out is None:
         out = torch.empty(M, N, device=A.device, dtype=out_dtype or A.dtype)
-    L.call("mg_gemm", L.dt(A), M, N, K, L.ptr(A), lda if lda is not None else _ld(A), int(a_kc), L.ptr(B),
-           ldb if ldb is not None else _ld(B), int(b_kc), L.ptr(out), ldc if ldc is not None else _ld(out),
-           L.dt(out), ep, splits, L.stream())
+    call("mg_gemm", dt(A), M, N, K, ptr(A), lda if lda is not None else _ld(A), int(a_kc), ptr(B),
+         ldb if ldb is not None else _ld(B), int(b_kc), ptr(out), ldc if ldc is not None else _ld(out),
+         dt(out), ep, splits, S())
     return out
 
 
-def linear(x, W, bias=None, act=0, out=None, **epk):
-    """y = act(x @ W^T + bias) for x [M,K], W [N,K] (nn.Linear semantics)."""
+def linear(x, W, bias=None, act=0, out=None, out_dtype=None, **epk):
+    """y = act(x @ W^T + bias), x [M,K], W [N,K]."""
     M, K = x.shape
     N = W.shape[0]
-    ep = L.epilogue(bias=bias, act=act, **epk)
-    return gemm(x, W, M, N, K, out=out, ep=ep)
+    return gemm(x, W, M, N, K, out=out, out_dtype=out_dtype, ep=E(bias=bias, act=act, **epk))
+
+
+def linear_dgrad(g, W, out=None, accumulate=0, out_dtype=None):
+    """gx = g @ W for g [M,N], W [N,K] -> [M,K]."""
+    M, N = g.shape
+    K = W.shape[1]
+    return gemm(g, W, M, K, N, b_kc=False, out=out, out_dtype=out_dtype, ep=E(accumulate=accumulate))
+
+
+def linear_wgrad(g, x, gW, alpha=1.0):
+    """gW [N,K] (fp32) += g^T x for g [M,N], x [M,K]."""
+    M, N = g.shape
+    K = x.shape[1]
+    return gemm(g, x, N, K, M, a_kc=False, b_kc=False, out=gW, ldc=gW.stride(0),
+                ep=E(alpha=alpha, accumulate=1))
 
 
 def conv2d(x, wpack, Cout, KH, KW, stride=1, pad=0, in_scale=None, out=None, out_dtype=None, ep=None, ldy=None):
-    """NHWC implicit-GEMM conv: x [B,H,W,Cin] -> y [B,OH,OW,Cout] (see mg_conv2d_fwd)."""
+    """NHWC implicit-GEMM conv (mg_conv2d_fwd): x [B,H,W,Cin] -> [B,OH,OW,Cout]."""
     B, H, W, Cin = x.shape
     OH = (H + 2 * pad - KH) // stride + 1
     OW = (W + 2 * pad - KW) // stride + 1
     if out is None:
         out = torch.empty(B, OH, OW, ldy or Cout, device=x.device, dtype=out_dtype or x.dtype)
-    L.call("mg_conv2d_fwd", L.dt(x), L.ptr(x), B, H, W, Cin, L.ptr(wpack), Cout, KH, KW, stride, pad,
-           L.ptr(in_scale), L.ptr(out), ldy or out.shape[-1], L.dt(out), ep, L.stream())
+    _timed("conv2d", (B * OH * OW, Cout, KH * KW * Cin),
+           lambda: call("mg_conv2d_fwd", dt(x), ptr(x), B, H, W, Cin, ptr(wpack), Cout, KH, KW, stride, pad,
+                        ptr(in_scale), ptr(out), ldy or out.shape[-1], dt(out), ep, S()))
     return out
 
 
 def conv2d_wgrad(gy, x, Cout, KH, KW, stride, pad, gw, in_scale=None, ldg=None, splits=0):
-    """gw [Cout,Cin,KH,KW] (fp32) += weight gradient (see mg_conv2d_wgrad)."""
+    """gw [Cout,Cin,KH,KW] fp32 += weight gradient (mg_conv2d_wgrad)."""
     B, H, W, Cin = x.shape
-    L.call("mg_conv2d_wgrad", L.dt(x), L.ptr(gy), ldg or gy.shape[-1], L.ptr(x), B, H, W, Cin, L.ptr(in_scale),
-           Cout, KH, KW, stride, pad, L.ptr(gw), splits, L.stream())
+    call("mg_conv2d_wgrad", dt(x), ptr(gy), ldg or gy.shape[-1], ptr(x), B, H, W, Cin, ptr(in_scale), Cout, KH, KW,
+         stride, pad, ptr(gw), splits, S())
     return gw
+
+
+def dgrad_s2(g, wcls, Cin, out, ep=None):
+    """4x4/s2/p1 conv data gradient: g [B,OH,OW,Cg] -> out [B,2OH,2OW,ldo]."""
+    B, OH, OW, Cg = g.shape
+    call("mg_conv2d_dgrad_s2", dt(g), ptr(g), B, OH, OW, Cg, ptr(wcls), Cin, ptr(out), out.shape[-1], dt(out), ep,
+         S())
+    return out
 
 
 def gemm_grouped(A, B, row_off, tile_off, max_tiles, N, K, *, b_kc=True, b_gstride, out, ep=None, lda=None,
                  ldb=None, ldc=None):
-    total_rows = out.shape[0]
-    L.call("mg_gemm_grouped", L.dt(A), total_rows, N, K, row_off.shape[0] - 1, L.ptr(row_off), L.ptr(tile_off),
-           max_tiles, L.ptr(A), lda or _ld(A), L.ptr(B), ldb or B.shape[-1], int(b_kc), b_gstride, L.ptr(out),
-           ldc or _ld(out), L.dt(out), ep, L.stream())
+    _timed("gemm_grouped", (out.shape[0], N, K),
+           lambda: call("mg_gemm_grouped", dt(A), out.shape[0], N, K, row_off.shape[0] - 1, ptr(row_off),
+                        ptr(tile_off), max_tiles, ptr(A), lda or _ld(A), ptr(B), ldb or B.shape[-1], int(b_kc),
+                        b_gstride, ptr(out), ldc or _ld(out), dt(out), ep, S()))
     return out
 
 
 def gemm_grouped_wgrad(A, B, row_off, total_rows, M, N, out, *, b_idx=None, b_idx_div=1, b_gelu=0, ep=None,
                        lda=None, ldb=None, splits=0):
-    """out[g] (fp32 [G,M,N]) += sum over rows of group g of A[r,:]^T B[r,:] (see mg_gemm_grouped_wgrad)."""
-    L.call("mg_gemm_grouped_wgrad", L.dt(A), M, N, row_off.shape[0] - 1, L.ptr(row_off), total_rows, L.ptr(A),
-           lda or _ld(A), L.ptr(B), ldb or _ld(B), L.ptr(b_idx), b_idx_div, b_gelu, L.ptr(out), splits, ep,
-           L.stream())
+    """out[g] (fp32 [G,M,N]) += sum over rows of group g of A[r,:]^T B[r,:]."""
+    call("mg_gemm_grouped_wgrad", dt(A), M, N, row_off.shape[0] - 1, ptr(row_off), total_rows, ptr(A),
+         lda or _ld(A), ptr(B), ldb or _ld(B), ptr(b_idx), b_idx_div, b_gelu, ptr(out), splits, ep, S())
     return out
 
 
-def ilog2(v):
-    return int(math.log2(v))
+# ---------------------------------------------------------------------------
+# prep / elementwise / reductions
+# ---------------------------------------------------------------------------
+def pack_conv(W, dtype, rows=None, flip=False):
+    Cout, Cin, KH, KW = W.shape
+    if flip:
+        rows = rows or Cin
+        out = torch.empty(rows, KH * KW * Cout, device=W.device, dtype=dtype)
+        call("mg_pack_conv_flip", dt(out), ptr(W), Cout, Cin, KH, KW, rows, ptr(out), S())
+    else:
+        rows = rows or Cout
+        out = torch.empty(rows, KH * KW * Cin, device=W.device, dtype=dtype)
+        call("mg_pack_conv", dt(out), ptr(W), Cout, Cin, KH, KW, rows, ptr(out), S())
+    return out
+
+
+def pack_dgrad_s2(W, dtype, rows=None):
+    Cg, Cin = W.shape[:2]
+    rows = rows or Cin
+    out = torch.empty(4, rows, 4 * Cg, device=W.device, dtype=dtype)
+    call("mg_pack_dgrad_s2", dt(out), ptr(W), Cg, Cin, rows, ptr(out), S())
+    return out
+
+
+def wsq(W, rows=None):
+    Cout, Cin = W.shape[:2]
+    taps = W[0, 0].numel()
+    rows = rows or Cout
+    out = torch.empty(rows, Cin, device=W.device, dtype=torch.float32)
+    call("mg_wsq", ptr(W), Cout, Cin, taps, rows, ptr(out), S())
+    return out
+
+
+def wsq_bwd(W, gwsq, gW):
+    Cout, Cin = W.shape[:2]
+    call("mg_wsq_bwd", ptr(W), ptr(gwsq), Cout, Cin, W[0, 0].numel(), ptr(gW), S())
+
+
+def cast(x, dtype=None, out=None, alpha=1.0, square=0):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=dtype or x.dtype)
+    call("mg_cast", dt(x), ptr(x), dt(out), ptr(out), x.numel(), alpha, square, S())
+    return out
+
+
+def copy2d(x, out, R, C, alpha=1.0, accumulate=0, ldi=None, ldo=None):
+    call("mg_copy2d", dt(x), ptr(x), ldi or _ld(x), dt(out), ptr(out), ldo or _ld(out), R, C, alpha, accumulate, S())
+    return out
+
+
+def colsum(X, out, R=None, C=None, ld=None):
+    R = R if R is not None else X.shape[0]
+    C = C if C is not None else X.shape[-1]
+    call("mg_colsum", dt(X), ptr(X), ld or X.shape[-1], R, C, ptr(out), S())
+    return out
+
+
+def segsum(X, B, HW, C, out, ld=None):
+    call("mg_segsum", dt(X), ptr(X), ld or C, B, HW, C, ptr(out), S())
+    return out
+
+
+def weight_norm_fwd(v, g):
+    O = v.shape[0]
+    K = v[0].numel()
+    W = torch.empty_like(v)
+    norm = torch.empty(O, device=v.device, dtype=torch.float32)
+    call("mg_weight_norm_fwd", ptr(v), ptr(g), O, K, ptr(W), ptr(norm), S())
+    return W, norm
+
+
+def weight_norm_bwd(v, g, norm, gW, gv, gg):
+    O = v.shape[0]
+    call("mg_weight_norm_bwd", ptr(v), ptr(g), ptr(norm), ptr(gW), O, v[0].numel(), ptr(gv), ptr(gg), S())
+
+
+def sumsq(x, out):
+    call("mg_sumsq", ptr(x), x.numel(), ptr(out), S())
+    return out
+
+
+def adamw(p, g, m, v, lr, beta1, beta2, eps, wd, step, sumsq_buf=None, max_norm=0.0):
+    call("mg_adamw", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps, wd, step, ptr(sumsq_buf),
+         max_norm, S())
+
+
+def const_fwd(cst, B, dtype):
+    C, HW = cst.shape[1], cst.shape[2] * cst.shape[3]
+    out = torch.empty(B, cst.shape[2], cst.shape[3], C, device=cst.device, dtype=dtype)
+    call("mg_const_fwd", dt(out), ptr(cst), C, HW, B, ptr(out), S())
+    return out
+
+
+def const_bwd(g, gcst):
+    B, H, W, C = g.shape
+    call("mg_const_bwd", dt(g), ptr(g), C, H * W, B, ptr(gcst), S())
+
+
+# ---------------------------------------------------------------------------
+# modulated conv helpers
+# ---------------------------------------------------------------------------
+def modconv_bwd_out(gz, z, d, B, HW, Cout, act, gyt, gdd, zsub=None, ld_gz=None, ld_z=None, ld_gyt=None):
+    call("mg_modconv_bwd_out", dt(z), dt(gz), ptr(gz), ld_gz or gz.shape[-1], ptr(z), ld_z or z.shape[-1],
+         ptr(zsub), zsub.shape[-1] if zsub is not None else 0, ptr(d), B, HW, Cout, act, ptr(gyt),
+         ld_gyt or gyt.shape[-1], ptr(gdd), S())
+
+
+def modconv_bwd_in(gxt, x, s, B, HW, Cin, gx, gs, accumulate=0):
+    call("mg_modconv_bwd_in", dt(gxt), ptr(gxt), gxt.shape[-1], dt(x), ptr(x), x.shape[-1], ptr(s), B, HW, Cin,
+         dt(gx) if gx is not None else 0, ptr(gx), gx.shape[-1] if gx is not None else 0, accumulate, ptr(gs), S())
+
+
+# ---------------------------------------------------------------------------
+# norm / attention
+# ---------------------------------------------------------------------------
+def layernorm_fwd(x, gamma, beta, eps=1e-5, act=0, out=None):
+    R, C = x.shape[0], x.shape[-1]
+    out = torch.empty_like(x) if out is None else out
+    mean = torch.empty(R, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(R, device=x.device, dtype=torch.float32)
+    call("mg_layernorm_fwd", dt(x), ptr(x), x.shape[-1], R, C, ptr(gamma), ptr(beta), eps, ptr(out), out.shape[-1],
+         ptr(mean), ptr(rstd), act, S())
+    return out, mean, rstd
+
+
+def layernorm_bwd(gy, x, mean, rstd, gamma, gx, ggamma, gbeta, accumulate=0):
+    R, C = x.shape[0], x.shape[-1]
+    call("mg_layernorm_bwd", dt(x), dt(gy), ptr(gy), gy.shape[-1], ptr(x), x.shape[-1], R, C, ptr(mean), ptr(rstd),
+         ptr(gamma), ptr(gx), gx.shape[-1] if gx is not None else 0, accumulate, ptr(ggamma), ptr(gbeta), S())
+
+
+def attn_fwd(qkv, B, L, C, heads=8):
+    out = torch.empty(B * L, C, device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty(B, heads, L, device=qkv.device, dtype=torch.float32)
+    call("mg_attn_fwd", dt(qkv), ptr(qkv), B, L, C, heads, ptr(out), ptr(lse), S())
+    return out, lse
+
+
+def attn_bwd(qkv, out, gout, lse, B, L, C, heads=8):
+    gqkv = torch.empty_like(qkv)
+    call("mg_attn_bwd", dt(qkv), dt(gout), ptr(qkv), ptr(out), ptr(gout), ptr(lse), B, L, C, heads, ptr(gqkv), S())
+    return gqkv
+
+
+# ---------------------------------------------------------------------------
+# router / MoE
+# ---------------------------------------------------------------------------
+def reparam(mu, rho, eps):
+    W = torch.empty_like(mu)
+    call("mg_router_reparam", ptr(mu), ptr(rho), ptr(eps), mu.numel(), ptr(W), S())
+    return W
+
+
+def router_fwd(tok, Wfc, Lt, E_, k, HW, temperature, anneal, eval_mode=0):
+    T, C = tok.shape
+    dev = tok.device
+    probs = torch.empty(T, E_, device=dev, dtype=torch.float32)
+    zlog = torch.empty(T, E_, device=dev, dtype=torch.float32)
+    topi = torch.empty(T, k, device=dev, dtype=torch.int32)
+    gate = torch.empty(T, k, device=dev, dtype=torch.float32)
+    call("mg_router_fwd", dt(tok), ptr(tok), tok.shape[-1], T, C, ptr(Wfc), ptr(Lt), E_, k, HW, ptr(temperature),
+         anneal, eval_mode, ptr(probs), ptr(zlog), ptr(topi), ptr(gate), S())
+    return probs, zlog, topi, gate
+
+
+def moe_dispatch(topi, gate, E_, bm=128):
+    T, k = topi.shape
+    dev = topi.device
+    n = T * k
+    ws = torch.empty(((n + 4095) // 4096) * E_, device=dev, dtype=torch.int32)
+    row_off = torch.empty(E_ + 1, device=dev, dtype=torch.int32)
+    tile_off = torch.empty(E_ + 1, device=dev, dtype=torch.int32)
+    perm = torch.empty(n, device=dev, dtype=torch.int32)
+    pos_of = torch.empty(n, device=dev, dtype=torch.int32)
+    gate_pos = torch.empty(n, device=dev, dtype=torch.float32)
+    call("mg_moe_dispatch", ptr(topi), ptr(gate), T, k, E_, bm, ptr(ws), ptr(row_off), ptr(tile_off), ptr(perm),
+         ptr(pos_of), ptr(gate_pos), S())
+    return row_off, tile_off, perm, pos_of, gate_pos
+
+
+def moe_combine(Y, pos_of, gate, resid, out):
+    T, k = gate.shape
+    C = out.shape[-1]
+    call("mg_moe_combine", dt(Y), ptr(Y), Y.shape[-1], ptr(pos_of), ptr(gate), T, k, C, ptr(resid),
+         resid.shape[-1] if resid is not None else 0, ptr(out), out.shape[-1], S())
+    return out
+
+
+def moe_gate_grad(gout, Y, pos_of, T, k):
+    g = torch.empty(T, k, device=Y.device, dtype=torch.float32)
+    call("mg_moe_gate_grad", dt(Y), dt(gout), ptr(gout), gout.shape[-1], ptr(Y), Y.shape[-1], ptr(pos_of), T, k,
+         Y.shape[-1], ptr(g), S())
+    return g
+
+
+def router_bwd(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, anneal, g_temp, B):
+    T, E_ = probs.shape
+    k = topi.shape[1]
+    g_raw = torch.empty(T, E_, device=probs.device, dtype=torch.float32)
+    gsum = torch.zeros(B, E_, device=probs.device, dtype=torch.float32)
+    call("mg_router_bwd", ptr(probs), ptr(zlog), ptr(topi), ptr(gate), ptr(g_gate), ptr(g_probs), ptr(coef), T, E_,
+         k, HW, ptr(temperature), anneal, ptr(g_raw), ptr(gsum), ptr(g_temp), S())
+    return g_raw, gsum
+
+
+def moe_token_grad(gX, pos_of, g_raw, Wfc, out, k):
+    T, C = out.shape
+    E_ = g_raw.shape[1]
+    call("mg_moe_token_grad", dt(gX) if gX is not None else dt(out), ptr(gX), gX.shape[-1] if gX is not None else 0,
+         ptr(pos_of), T, k, C, ptr(g_raw), ptr(Wfc), E_, dt(out), ptr(out), out.shape[-1], S())
+    return out
+
+
+def router_feat_grad(tok, g_raw, G1):
+    T, C = tok.shape
+    call("mg_router_feat_grad", dt(tok), ptr(tok), tok.shape[-1], T, C, ptr(g_raw), g_raw.shape[1], ptr(G1), S())
+    return G1
+
+
+def grouped_colsum(X, row_off, N, max_rows, out, idx=None, idx_div=1, rs=None):
+    call("mg_grouped_colsum", dt(X), ptr(X), X.shape[-1], ptr(idx), idx_div, ptr(rs), ptr(row_off),
+         row_off.shape[0] - 1, N, max_rows, ptr(out), S())
+    return out
+
+
+def router_kl(mf, rf, mt, rt, mc, rc, out):
+    call("mg_router_kl", ptr(mf), ptr(rf), mf.numel(), ptr(mt), ptr(rt), mt.numel(), ptr(mc), ptr(rc), mc.numel(),
+         ptr(out), S())
+    return out
+
+
+def kl_coefs(kl2, R, eff_w, coef, total):
+    call("mg_kl_coefs", ptr(kl2), R, eff_w, ptr(coef), ptr(total), S())
+
+
+def router_param_bwd(mu, rho, eps, gW, kl_coef, gmu, grho):
+    call("mg_router_param_bwd", ptr(mu), ptr(rho), ptr(eps), ptr(gW), mu.numel(), ptr(kl_coef), ptr(gmu),
+         ptr(grho), S())
+
+
+def balance(load, E_, T, weight, grad_scale, out, coef):
+    call("mg_balance", ptr(load), E_, float(T), weight, grad_scale, ptr(out), ptr(coef), S())
+
+
+# ---------------------------------------------------------------------------
+# MTM warp / upsample
+# ---------------------------------------------------------------------------
+def warp_fwd(x, o1, w2, b2):
+    B, H, W, C = x.shape
+    out = torch.empty_like(x)
+    samp = torch.empty(B * H * W, 4, device=x.device, dtype=torch.float32)
+    call("mg_warp_fwd", dt(x), ptr(x), ptr(o1), ptr(w2), ptr(b2), B, H, W, C, ptr(out), ptr(samp), S())
+    return out, samp
+
+
+def warp_bwd(gout, x, samp, gx32, goff):
+    B, H, W, C = x.shape
+    call("mg_warp_bwd", dt(x), dt(gout), ptr(gout), ptr(x), ptr(samp), B, H, W, C, ptr(gx32), ptr(goff), S())
+
+
+def offset_head_bwd(goff, o1, w2, ga1, gw2, gb2):
+    B, H, W, _ = o1.shape
+    call("mg_offset_head_bwd", dt(o1), ptr(goff), ptr(o1), ptr(w2), B, H, W, ptr(ga1), ptr(gw2), ptr(gb2), S())
+
+
+def upsample2x(x):
+    B, H, W, C = x.shape
+    out = torch.empty(B, 2 * H, 2 * W, C, device=x.device, dtype=x.dtype)
+    call("mg_upsample2x_fwd", dt(x), ptr(x), B, H, W, C, ptr(out), S())
+    return out
+
+
+def upsample2x_bwd(gout, gx, accumulate=0):
+    B, H, W, C = gx.shape
+    call("mg_upsample2x_bwd", dt(gout), ptr(gout), B, H, W, C, dt(gx), ptr(gx), accumulate, S())
+    return gx
+
+
+# ---------------------------------------------------------------------------
+# discriminator / losses
+# ---------------------------------------------------------------------------
+def im2col_4x4s2(x, strides, B, H, W, C, Kp, dtype):
+    out = torch.empty(B * (H // 2) * (W // 2), Kp, device=x.device, dtype=dtype)
+    sb, sh, sw, sc = strides
+    call("mg_im2col_4x4s2", dt(x), ptr(x), sb, sh, sw, sc, B, H, W, C, Kp, dt(out), ptr(out), S())
+    return out
+
+
+def disc_head_fwd(h1, W2img):
+    B, Hf, _, Cf = h1.shape
+    out = torch.empty(B, (Hf - 3) * (Hf - 3), device=h1.device, dtype=torch.float32)
+    call("mg_disc_head_fwd", dt(h1), ptr(h1), ptr(W2img), B, Hf, Cf, ptr(out), S())
+    return out
+
+
+def disc_head_bwd_data(g, g_bstride, W2img, a1, out):
+    B, Hf, _, Cf = out.shape
+    call("mg_disc_head_bwd_data", dt(a1), ptr(g), g_bstride, ptr(W2img), ptr(a1), B, Hf, Cf, dt(out), ptr(out), S())
+    return out
+
+
+def disc_head_bwd_w(g, g_bstride, h1, dW2):
+    B, Hf, _, Cf = h1.shape
+    call("mg_disc_head_bwd_w", dt(h1), ptr(g), g_bstride, ptr(h1), B, Hf, Cf, ptr(dW2), S())
+
+
+def d_text_bwd(g_tb, t, w2sum, cofs, g_tpre, dW2):
+    B, Ct = t.shape
+    call("mg_d_text_bwd", ptr(g_tb), ptr(t), ptr(w2sum), B, Ct, cofs, ptr(g_tpre), ptr(dW2), S())
+
+
+def d_loss(img_real, img_fake, tb, perm, out, g_img, g_fake, g_tb, real_out=None, mism_out=None, fake_out=None):
+    B, No = img_real.shape
+    call("mg_d_loss", ptr(img_real), ptr(img_fake), ptr(tb), ptr(perm), B, No, ptr(out), ptr(g_img), ptr(g_fake),
+         ptr(g_tb), ptr(real_out), ptr(mism_out), ptr(fake_out), S())
+
+
+def g_loss(fake, out, g, scale=1.0):
+    call("mg_g_loss", ptr(fake), fake.shape[0], scale, ptr(out), ptr(g), S())
+
+
+def r1(g, B, gamma, r1_out, u):
+    per = g.numel() // B
+    call("mg_r1", dt(g), ptr(g), per, B, gamma, ptr(r1_out), dt(u) if u is not None else 0, ptr(u), S())
+
+
+def lrelu_mask_mul(a, m, out):
+    call("mg_lrelu_mask_mul", dt(a), ptr(a), dt(m), ptr(m), a.numel(), dt(out), ptr(out), S())
+    return out

@@ -1,0 +1,136 @@
+"""Flat, HBM-resident parameter storage in the reference state_dict naming.
+
+Each model's parameters live in ONE fp32 buffer (plus one fp32 gradient
+buffer and the two AdamW moment buffers), so the optimizer, gradient norm,
+bf16 shadow cast and the data-parallel gradient all-reduce are each a single
+launch / collective over a contiguous range.  Views expose every tensor under
+its reference key and shape (t2i_moe_gan.py state_dict), which keeps
+checkpoints drop-in (sagemaker_train.py:297-301, inference.py:34-49).
+
+The flat ORDER is chosen for the kernels, not the reference: the E experts of
+an attention block are stored back to back ([E, 4C, C] / [E, C, 4C]) so the
+grouped expert GEMMs read them in place, and parameters the reference never
+updates are placed in a frozen tail outside the optimizer range.
+"""
+import re
+from collections import OrderedDict
+
+import torch
+
+from . import ops
+from .layout import is_buffer
+
+_EXPERT = re.compile(r"^(.*\.moe\.)experts\.(\d+)\.net\.(\d)\.(weight|bias)$")
+ALIGN = 8  # elements: keeps every view 16-byte aligned for fp32 and bf16 vector loads
+
+
+def flat_order(shapes, frozen_prefixes=()):
+    """Reference names reordered: experts grouped per (block, layer, kind); frozen names last."""
+    names = [n for n in shapes if not is_buffer(n)]
+    groups = OrderedDict()
+    order, frozen = [], []
+    for n in names:
+        m = _EXPERT.match(n)
+        if any(n.startswith(p) for p in frozen_prefixes):
+            frozen.append(n)
+        elif m:
+            key = (m.group(1), m.group(3), m.group(4))
+            if key not in groups:
+                groups[key] = []
+                order.append(key)
+            groups[key].append((int(m.group(2)), n))
+        else:
+            order.append(n)
+    out = []
+    for o in order:
+        if isinstance(o, tuple):
+            out.extend(n for _, n in sorted(groups[o]))
+        else:
+            out.append(o)
+    return out, frozen
+
+
+class ParamStore:
+    def __init__(self, shapes, device, frozen_prefixes=(), shadow_dtype=None):
+        self.shapes = OrderedDict((k, tuple(v)) for k, v in shapes.items())
+        self.device = torch.device(device)
+        order, frozen = flat_order(self.shapes, frozen_prefixes)
+        self.offsets = OrderedDict()
+        off = 0
+        for n in order + frozen:
+            numel = 1
+            for s in self.shapes[n]:
+                numel *= s
+            if n in frozen and not any(k in frozen for k in self.offsets):
+                self.n_opt = off
+            self.offsets[n] = (off, numel)
+            off += numel
+            if not _EXPERT.match(n):
+                off = (off + ALIGN - 1) // ALIGN * ALIGN
+            else:
+                off = off  # experts stay packed (each expert tensor is a multiple of 8 elements)
+        if not frozen:
+            self.n_opt = off
+        self.total = (off + ALIGN - 1) // ALIGN * ALIGN
+        self.data = torch.zeros(self.total, device=self.device, dtype=torch.float32)
+        self.grad = torch.zeros(self.total, device=self.device, dtype=torch.float32)
+        self.m = torch.zeros(self.total, device=self.device, dtype=torch.float32)
+        self.v = torch.zeros(self.total, device=self.device, dtype=torch.float32)
+        self.step_count = 0
+        self.buffers = OrderedDict((n, torch.zeros(s, device=self.device)) for n, s in self.shapes.items()
+                                   if is_buffer(n))
+        self.shadow_dtype = shadow_dtype
+        self.shadow = None
+        if shadow_dtype is not None and shadow_dtype != torch.float32:
+            self.shadow = torch.zeros(self.total, device=self.device, dtype=shadow_dtype)
+
+    # ---- views ----
+    def _v(self, buf, name):
+        off, n = self.offsets[name]
+        return buf[off:off + n].view(self.shapes[name])
+
+    def view(self, name):
+        return self._v(self.data, name)
+
+    def gview(self, name):
+        return self._v(self.grad, name)
+
+    def cview(self, name):
+        """Compute-dtype view (bf16 shadow if enabled, else the fp32 master)."""
+        return self._v(self.shadow if self.shadow is not None else self.data, name)
+
+    def group_view(self, first, last, buf=None):
+        """Contiguous range from the start of ``first`` to the end of ``last`` (expert groups)."""
+        buf = self.data if buf is None else buf
+        a, _ = self.offsets[first]
+        b, n = self.offsets[last]
+        return buf[a:b + n]
+
+    # ---- per-step ----
+    def refresh_shadow(self):
+        if self.shadow is not None:
+            ops.cast(self.data, out=self.shadow)
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    # ---- state dict (reference layout) ----
+    def state_dict(self, cpu=True):
+        sd = OrderedDict()
+        for n in self.shapes:
+            t = self.buffers[n] if is_buffer(n) else self.view(n)
+            sd[n] = t.detach().clone().cpu() if cpu else t.detach().clone()
+        return sd
+
+    def load_state_dict(self, sd, strict=True):
+        missing = [n for n in self.shapes if n not in sd]
+        unexpected = [n for n in sd if n not in self.shapes]
+        if strict and (missing or unexpected):
+            raise KeyError(f"state_dict mismatch: missing={missing[:5]} unexpected={unexpected[:5]}")
+        with torch.no_grad():
+            for n, t in sd.items():
+                if n not in self.shapes:
+                    continue
+                dst = self.buffers[n] if is_buffer(n) else self.view(n)
+                dst.copy_(torch.as_tensor(t).reshape(dst.shape).to(dst.device, torch.float32))
+        self.refresh_shadow()
