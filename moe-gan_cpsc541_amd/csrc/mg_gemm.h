@@ -259,6 +259,12 @@ struct Epi {
   int g;
   MG_DEV void set_group(int gg) { g = gg; }
   MG_DEV void operator()(int m, int n, float v) const {
+    if (rm_mode == 1) {  // class-major (py,px,b,i,j) -> NHWC row (b, 2i+py, 2j+px); all row lookups use it
+      int cls = m / rm_Mc, rem = m - cls * rm_Mc;
+      int b = rem >> rm_lgOHW, i = (rem >> rm_lgOW) & ((1 << (rm_lgOHW - rm_lgOW)) - 1), j = rem & ((1 << rm_lgOW) - 1);
+      int OW2 = 2 << rm_lgOW, OH2 = 2 << (rm_lgOHW - rm_lgOW);
+      m = (b * OH2 + 2 * i + (cls >> 1)) * OW2 + 2 * j + (cls & 1);
+    }
     v *= alpha;
     if (scale) v *= scale[(int64_t)(m >> scale_shift) * scale_ld + n];
     if (bias) v += bias[(int64_t)g * gstride_bias + n];
@@ -269,12 +275,6 @@ struct Epi {
     else if (act == ACT_RSQRT_EPS) v = rsqrtf(v + 1e-8f);
     if (rowscale) v *= rowscale[m];
     if (addvec) v += addvec[(int64_t)(m >> add_shift) * add_ld + n];
-    if (rm_mode == 1) {  // class-major (py,px,b,i,j) -> NHWC row (b, 2i+py, 2j+px)
-      int cls = m / rm_Mc, rem = m - cls * rm_Mc;
-      int b = rem >> rm_lgOHW, i = (rem >> rm_lgOW) & ((1 << (rm_lgOHW - rm_lgOW)) - 1), j = rem & ((1 << rm_lgOW) - 1);
-      int OW2 = 2 << rm_lgOW, OH2 = 2 << (rm_lgOHW - rm_lgOW);
-      m = (b * OH2 + 2 * i + (cls >> 1)) * OW2 + 2 * j + (cls & 1);
-    }
     if (resid) v += ldf(resid, (int64_t)m * ld_res + n);
     int64_t nn = n;
     if (remap_taps > 0) nn = (int64_t)(n & ((1 << remap_lgcin) - 1)) * remap_taps + (n >> remap_lgcin);
