@@ -57,7 +57,7 @@ def cpu_baseline(args, E, k):
     from moegan_mi.layout import discriminator_shapes, generator_shapes
     from moegan_mi.init import init_discriminator, init_generator  # noqa: F401
     from oracle.recipe import fill_state
-    torch.set_num_threads(os.cpu_count() or 1)
+    torch.set_num_threads(max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
     B = 8
     PG = {n: torch.from_numpy(v) for n, v in fill_state(generator_shapes(E), 0).items()}
     PD = {n: torch.from_numpy(v).requires_grad_(True) for n, v in fill_state(discriminator_shapes(), 50).items()}
@@ -75,12 +75,15 @@ def cpu_baseline(args, E, k):
     mk = lambda: [tuple(torch.randn(s, generator=g) for s in ((c, 128), (t, 128), (256, E))) for c, t in dims]  # noqa
     O.train_step(PG, PD, optG, optD, real, text, z, mk(), mk(), torch.randperm(B, generator=g), topk=k)  # warm
     t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
+    n = 0
+    while n < args.cpu_steps and (n == 0 or time.perf_counter() - t0 < 20.0):
         O.train_step(PG, PD, optG, optD, real, text, z, mk(), mk(), torch.randperm(B, generator=g), topk=k)
+        n += 1
+        print(f"[bench] cpu baseline step {n}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     dt = time.perf_counter() - t0
-    return {"value": round(B * args.cpu_steps / dt, 3), "unit": "images/sec", "cores": torch.get_num_threads(),
+    return {"value": round(B * n / dt, 3), "unit": "images/sec", "cores": torch.get_num_threads(),
             "kind": "port", "sample": f"oracle/aurora_cpu.train_step, B={B}, E={E} top-{k}, fp32, "
-                                      f"{args.cpu_steps} timed steps after 1 warm-up"}
+                                      f"{n} timed steps after 1 warm-up"}
 
 
 def main():
@@ -117,9 +120,12 @@ def main():
         perm = torch.randperm(B, device=dev, generator=gen).int()
         return ts.step(real, text, z, eps_d, eps_g, perm, anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8)
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        t_w = time.perf_counter()
         one_step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup step {i}: {(time.perf_counter() - t_w) * 1e3:.1f} ms", file=sys.stderr, flush=True)
 
     # live timing of the roofline kernel: D conv_layers.2 forward on the 64x64 real batch
     # (implicit GEMM M = B*16*16, N = 256, K = 4*4*128)
@@ -130,8 +136,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     out = None
-    for _ in range(args.steps):
+    for i in range(args.steps):
         out = one_step()
+        if rank == 0 and (i + 1) % max(1, args.steps // 4) == 0:
+            print(f"[bench] enqueued {i + 1}/{args.steps} steps", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if pg is not None:
         torch.distributed.barrier()

@@ -310,8 +310,11 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   constexpr int A_VPT = BM * BK / VEC / NTHREADS;
   constexpr int B_VPT = BN * BK / VEC / NTHREADS;
   static_assert(A_VPT >= 1 && B_VPT >= 1, "tile too small for 256 threads");
-  __shared__ __attribute__((aligned(16))) T As[BM * LDK];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * LDK];
+  // one LDS array: A tile, B tile; reused by the epilogue to stage accumulators
+  __shared__ __attribute__((aligned(16))) T smem[(BM + BN) * LDK];
+  T* As = smem;
+  T* Bs = smem + BM * LDK;
+  static_assert(4 * 16 * (WN + 1) * 4 <= (int)sizeof(T) * (BM + BN) * LDK, "epilogue staging does not fit");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -458,18 +461,27 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
     }
   }
 
-  // ---- epilogue ----
+  // ---- epilogue: stage one 16-row band of each wave's accumulators through LDS, then a plain
+  // (non-unrolled) loop applies the fused epilogue with consecutive lanes on consecutive columns.
+  // Static indexing keeps acc in registers; the loop keeps the inlined epilogue code small.
   const int fr = lane & 15, fq = lane >> 4;
+  float* cs = reinterpret_cast<float*>(smem) + wid * 16 * (WN + 1);
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int i = 0; i < FM; ++i) {
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int m = m0 + wm * WM + i * 16 + fq * 4 + r;
-        int n = n0 + wn * WN + j * 16 + fr;
-        if (m < Mloc && n < N) ep(mrow_base + m, n, acc[i][j][r]);
-      }
+      for (int r = 0; r < 4; ++r) cs[(fq * 4 + r) * (WN + 1) + j * 16 + fr] = acc[i][j][r];
+    __syncthreads();
+    const int mb = m0 + wm * WM + i * 16, nb = n0 + wn * WN;
+#pragma unroll 1
+    for (int e = lane; e < 16 * WN; e += 64) {
+      int rr = e / WN, cc = e - (e / WN) * WN;
+      int m = mb + rr, n = nb + cc;
+      if (m < Mloc && n < N) ep(mrow_base + m, n, cs[rr * (WN + 1) + cc]);
+    }
+  }
 }
 
 // launch helper: picks the grid; grouped-M launches an upper bound of tiles.

@@ -109,7 +109,15 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
   MG_REQUIRE(lda % vec == 0 && ldb % vec == 0, "lda/ldb must be multiples of the 16-byte vector");
   MG_REQUIRE(a_kc ? (K % vec == 0) : (M % vec == 0), "A vector dim must be a multiple of the 16-byte vector");
   MG_REQUIRE(b_kc ? (K % vec == 0) : (N % vec == 0), "B vector dim must be a multiple of the 16-byte vector");
-  if (splits < 1) splits = 1;
+  if (splits < 1) {  // auto split-K (atomic fp32 epilogues only): ~512 blocks, >= 256 of K per split
+    if (ep && ep->atomic) {
+      int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
+      int64_t want = std::max<int64_t>(1, 512 / std::max<int64_t>(tiles, 1));
+      splits = (int)std::max<int64_t>(1, std::min<int64_t>(want, K / 256));
+    } else {
+      splits = 1;
+    }
+  }
   MG_REQUIRE(splits == 1 || (ep && ep->atomic && c_dtype == MG_F32), "split-K requires an atomic fp32 epilogue");
   MG_REQUIRE(!(ep && ep->atomic) || c_dtype == MG_F32, "atomic epilogue requires fp32 C");
   if (K == 0) splits = 1;

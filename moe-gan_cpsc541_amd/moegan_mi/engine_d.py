@@ -102,7 +102,7 @@ class DiscriminatorEngine:
         ops.dgrad_s2(g_a1, self.W1cls, 128, g_a0, ep=E_(act=MUL_LRELU_GRAD, aux=f["h0"], ld_aux=128))
         if want_params:
             ops.gemm(g_a0.view(-1, 128), f["cols"], 128, 48, g_a0.numel() // 128, a_kc=False, b_kc=False,
-                     out=self.dW["conv_layers.0."].view(128, 48), ep=E_(accumulate=1))
+                     out=self.dW["conv_layers.0."].view(128, 48), ep=E_(atomic=1), splits=0)
             ops.colsum(g_a0.view(-1, 128), self.G("conv_layers.0.bias"))
         if g_input is not None:
             ops.dgrad_s2(g_a0, self.W0cls, 3, g_input)
@@ -167,7 +167,7 @@ class DiscriminatorEngine:
                  ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
         m1v1 = ops.conv2d(m0v0, self.W1p, 256, 4, 4, 2, 1, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h1"], ld_aux=256))
         ops.gemm(gA0.view(-1, 128), cols_u, 128, 48, gA0.numel() // 128, a_kc=False, b_kc=False,
-                 out=self.dW["conv_layers.0."].view(128, 48), ep=E_(accumulate=1))
+                 out=self.dW["conv_layers.0."].view(128, 48), ep=E_(atomic=1), splits=0)
         ops.conv2d_wgrad(gA1, m0v0, 256, 4, 4, 2, 1, self.dW["conv_layers.2."])
         ops.disc_head_bwd_w(g1, 0, m1v1, self.dW["output_layer.0."])
         self._remap_w0()

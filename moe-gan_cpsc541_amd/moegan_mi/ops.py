@@ -88,7 +88,7 @@ def linear_wgrad(g, x, gW, alpha=1.0):
     M, N = g.shape
     K = x.shape[1]
     return gemm(g, x, N, K, M, a_kc=False, b_kc=False, out=gW, ldc=gW.stride(0),
-                ep=E(alpha=alpha, accumulate=1))
+                ep=E(alpha=alpha, atomic=1), splits=0)
 
 
 def conv2d(x, wpack, Cout, KH, KW, stride=1, pad=0, in_scale=None, out=None, out_dtype=None, ep=None, ldy=None):
