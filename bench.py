@@ -162,10 +162,17 @@ def main():
         flop = 2.0 * M * N * K
         achieved = flop / (avg_ms * 1e-3) / 1e12 if kms else None
         peak = MFMA_PEAK_TFLOPS[args.dtype]
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_roofline_kernel.json")
+        if os.path.exists(pmc):  # HBM bytes per launch from the committed rocprofv3 --pmc passes
+            rec = json.load(open(pmc))
+            if rec.get("batch") == B and args.dtype == "bf16":
+                traffic = rec["traffic_bytes_per_launch"]
         roof = {"bound": "mfma", "kernel": "mg_conv2d_fwd D conv_layers.2 (64x64 real), implicit GEMM "
                                           f"M={M} N={N} K={K}", "achieved": round(achieved, 2) if achieved else None,
                 "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-                "traffic": None, "launches_timed": len(kms), "avg_launch_ms": round(avg_ms, 4)}
+                "traffic": traffic, "traffic_unit": "bytes per launch (HBM, PMC)",
+                "algorithmic_flop_per_launch": flop, "launches_timed": len(kms), "avg_launch_ms": round(avg_ms, 4)}
         step_tflops = gflop_per_image(k) * B * world / (ms * 1e-3) / 1e3
         cpu = None
         if not args.no_cpu_baseline and world == 1:
