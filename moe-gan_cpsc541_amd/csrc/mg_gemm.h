@@ -26,7 +26,6 @@
 
 namespace mg {
 
-constexpr int BK = 32;
 constexpr int NTHREADS = 256;
 
 template <typename T> struct Frag;
@@ -92,7 +91,7 @@ struct LdKC {
 };
 
 // KC, implicit NHWC convolution: row = output pixel (b, oh, ow), k = tap*Cin + ci.
-// Requires Cin % BK == 0 (tap uniform inside a K tile) and power-of-two OH/OW/Cin.
+// Requires Cin % VEC == 0 (one tap per vector) and power-of-two OH/OW/Cin.
 template <typename T>
 struct LdKCConv {
   const T* x; int H, W, Cin, lgCin, lgOW, lgOHW, M;
@@ -111,9 +110,10 @@ struct LdKCConv {
     return st;
   }
   MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
-    if (st.b < 0 || k0 >= K) return vzero<T>();
-    int tap = k0 >> lgCin;
-    int ci = (k0 & (Cin - 1)) + kofs;
+    int k = k0 + kofs;
+    if (st.b < 0 || k >= K) return vzero<T>();
+    int tap = k >> lgCin;
+    int ci = k & (Cin - 1);
     int kh = tap / KW, kw = tap - (tap / KW) * KW;
     int ih = st.oh * stride - pad + kh, iw = st.ow * stride - pad + kw;
     if (ih < 0 || ih >= H || iw < 0 || iw >= W) return vzero<T>();
@@ -195,9 +195,10 @@ struct LdKCConvT {
     return st;
   }
   MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
-    if (st.b < 0 || k0 >= K) return vzero<T>();
-    int t = k0 >> lgCg;
-    int co = (k0 & (Cg - 1)) + kofs;
+    int k = k0 + kofs;
+    if (st.b < 0 || k >= K) return vzero<T>();
+    int t = k >> lgCg;
+    int co = k & (Cg - 1);
     int ty = t >> 1, tx = t & 1;
     int py = cls >> 1, px = cls & 1;
     int dy = py ? (ty ? 0 : 1) : (ty ? -1 : 0);
@@ -300,21 +301,56 @@ struct Grouping {
 // ---------------------------------------------------------------------------
 // Kernel
 // ---------------------------------------------------------------------------
+// LDS images.  KC operand: [rows][BK + PADK] (k contiguous), fragments read with ds_read_b128 (bf16)
+// or ds_read_b32 (fp32).  MC operand: [BK][rows + PADM] (rows contiguous, stored straight from the
+// coalesced global vectors) and, for bf16, read with two ds_read_b64_tr_b16 per fragment (the hardware
+// transpose delivers 4 k-rows of one column per lane).  The MC row pitch is an odd multiple of 16
+// dwords and columns are XOR-swizzled by 16 elements on odd k-octets, so both halves of a wave's
+// transposed read (k-rows 8g..8g+3 for lane groups g = 0, 1) hit 8 distinct bank octets.
+template <typename T> struct Tile;
+template <> struct Tile<bf16_t> { static constexpr int BK = 64, PADK = 8, PADM = 32; };
+template <> struct Tile<float> { static constexpr int BK = 32, PADK = 4, PADM = 16; };
+
+template <typename T> MG_DEV constexpr int mc_swz(int k) { return sizeof(T) == 2 ? ((k >> 3) & 1) << 4 : 0; }
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+// A/B fragment of v_mfma_f32_16x16x32_bf16 from an MC image: lane (g = lane>>4, i = lane&15) gets
+// column c0+i of k-rows kr0+8g .. kr0+8g+7.
+MG_DEV bf16x8_t mc_frag_bf16(const bf16_t* img, int ld, int kr0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int k = kr0 + 8 * g + q;
+  const int col = (c0 ^ mc_swz<bf16_t>(k)) + 4 * p;
+  auto base = (__attribute__((address_space(3))) char*)(img);
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + ((int64_t)k * ld + col) * 2));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + ((int64_t)(k + 4) * ld + col) * 2));
+  u16x8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
 template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
 __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M, int N, int K, int kchunk, Grouping grp) {
   constexpr int VEC = VecOf<T>::N;
   typedef typename VecOf<T>::type vec_t;
-  constexpr int LDK = BK + Frag<T>::PAD;
+  constexpr int TBK = Tile<T>::BK;
+  constexpr int LDK = TBK + Tile<T>::PADK;
+  constexpr int LDA = A_KC ? LDK : BM + Tile<T>::PADM;
+  constexpr int LDB = B_KC ? LDK : BN + Tile<T>::PADM;
+  constexpr int A_ELEMS = A_KC ? BM * LDK : TBK * LDA;
+  constexpr int B_ELEMS = B_KC ? BN * LDK : TBK * LDB;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   // per-thread vector counts
-  constexpr int A_VPT = BM * BK / VEC / NTHREADS;
-  constexpr int B_VPT = BN * BK / VEC / NTHREADS;
+  constexpr int A_VPT = BM * TBK / VEC / NTHREADS;
+  constexpr int B_VPT = BN * TBK / VEC / NTHREADS;
   static_assert(A_VPT >= 1 && B_VPT >= 1, "tile too small for 256 threads");
   // one LDS array: A tile, B tile; reused by the epilogue to stage accumulators
-  __shared__ __attribute__((aligned(16))) T smem[(BM + BN) * LDK];
+  __shared__ __attribute__((aligned(16))) T smem[A_ELEMS + B_ELEMS];
   T* As = smem;
-  T* Bs = smem + BM * LDK;
-  static_assert(4 * 16 * (WN + 1) * 4 <= (int)sizeof(T) * (BM + BN) * LDK, "epilogue staging does not fit");
+  T* Bs = smem + A_ELEMS;
+  static_assert(4 * 16 * (WN + 1) * 4 <= (int)sizeof(T) * (A_ELEMS + B_ELEMS), "epilogue staging does not fit");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -346,7 +382,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
     g = blockIdx.z / splits;
     int s = blockIdx.z - g * splits;
     int r0 = grp.row_off[g], r1 = grp.row_off[g + 1];
-    int per = ((r1 - r0 + splits - 1) / splits + BK - 1) / BK * BK;
+    int per = ((r1 - r0 + splits - 1) / splits + TBK - 1) / TBK * TBK;
     kbeg = r0 + s * per;
     kend = min(r1, kbeg + per);
     if (kbeg >= kend) return;
@@ -368,7 +404,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   for (int i = 0; i < A_VPT; ++i) {
     int v = tid + i * NTHREADS;
     if constexpr (A_KC) {
-      a_r[i] = v / (BK / VEC); a_k[i] = (v % (BK / VEC)) * VEC;
+      a_r[i] = v / (TBK / VEC); a_k[i] = (v % (TBK / VEC)) * VEC;
       int r = mrow_base + m0 + a_r[i];
       ast[i] = A.row(r < mlimit ? r : 0x7fffffff);
     } else {
@@ -381,7 +417,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   for (int i = 0; i < B_VPT; ++i) {
     int v = tid + i * NTHREADS;
     if constexpr (B_KC) {
-      b_r[i] = v / (BK / VEC); b_k[i] = (v % (BK / VEC)) * VEC;
+      b_r[i] = v / (TBK / VEC); b_k[i] = (v % (TBK / VEC)) * VEC;
       bst[i] = B.row(n0 + b_r[i]);
     } else {
       b_k[i] = v / (BN / VEC); b_r[i] = (v % (BN / VEC)) * VEC;
@@ -405,18 +441,12 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
 #pragma unroll
     for (int i = 0; i < A_VPT; ++i) {
       if constexpr (A_KC) *reinterpret_cast<vec_t*>(&As[a_r[i] * LDK + a_k[i]]) = ra[i];
-      else {
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) As[(a_r[i] + j) * LDK + a_k[i]] = ra[i][j];
-      }
+      else *reinterpret_cast<vec_t*>(&As[a_k[i] * LDA + (a_r[i] ^ mc_swz<T>(a_k[i]))]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_VPT; ++i) {
       if constexpr (B_KC) *reinterpret_cast<vec_t*>(&Bs[b_r[i] * LDK + b_k[i]]) = rb[i];
-      else {
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) Bs[(b_r[i] + j) * LDK + b_k[i]] = rb[i][j];
-      }
+      else *reinterpret_cast<vec_t*>(&Bs[b_k[i] * LDB + (b_r[i] ^ mc_swz<T>(b_k[i]))]) = rb[i];
     }
   };
 
@@ -426,33 +456,46 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  const int fr = lane & 15, fq = lane >> 4;
   if (kbeg < kend) gload(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+  for (int k0 = kbeg; k0 < kend; k0 += TBK) {
     __syncthreads();
     sstore();
     __syncthreads();
-    if (k0 + BK < kend) gload(k0 + BK);
-    const int fr = lane & 15, fq = lane >> 4;
+    if (k0 + TBK < kend) gload(k0 + TBK);
     if constexpr (sizeof(T) == 2) {
-      bf16x8_t af[FM], bfv[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&As[(wm * WM + i * 16 + fr) * LDK + fq * 8]));
+      for (int kk = 0; kk < TBK / 32; ++kk) {
+        bf16x8_t af[FM], bfv[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bfv[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&Bs[(wn * WN + j * 16 + fr) * LDK + fq * 8]));
+        for (int i = 0; i < FM; ++i) {
+          if constexpr (A_KC)
+            af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&As[(wm * WM + i * 16 + fr) * LDK + kk * 32 + fq * 8]));
+          else
+            af[i] = mc_frag_bf16(As, LDA, kk * 32, wm * WM + i * 16, lane);
+        }
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (B_KC)
+            bfv[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&Bs[(wn * WN + j * 16 + fr) * LDK + kk * 32 + fq * 8]));
+          else
+            bfv[j] = mc_frag_bf16(Bs, LDB, kk * 32, wn * WN + j * 16, lane);
+        }
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
-      for (int kk = 0; kk < BK / 4; ++kk) {
+      for (int kk = 0; kk < TBK / 4; ++kk) {
         float af[FM], bfv[FN];
 #pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = As[(wm * WM + i * 16 + fr) * LDK + kk * 4 + fq];
+        for (int i = 0; i < FM; ++i)
+          af[i] = A_KC ? As[(wm * WM + i * 16 + fr) * LDK + kk * 4 + fq] : As[(kk * 4 + fq) * LDA + wm * WM + i * 16 + fr];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bfv[j] = Bs[(wn * WN + j * 16 + fr) * LDK + kk * 4 + fq];
+        for (int j = 0; j < FN; ++j)
+          bfv[j] = B_KC ? Bs[(wn * WN + j * 16 + fr) * LDK + kk * 4 + fq] : Bs[(kk * 4 + fq) * LDB + wn * WN + j * 16 + fr];
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -464,7 +507,6 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   // ---- epilogue: stage one 16-row band of each wave's accumulators through LDS, then a plain
   // (non-unrolled) loop applies the fused epilogue with consecutive lanes on consecutive columns.
   // Static indexing keeps acc in registers; the loop keeps the inlined epilogue code small.
-  const int fr = lane & 15, fq = lane >> 4;
   float* cs = reinterpret_cast<float*>(smem) + wid * 16 * (WN + 1);
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
@@ -488,8 +530,9 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
 template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
 inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, int K, int splits, Grouping grp,
                         int max_tiles_m, hipStream_t st) {
+  constexpr int TBK = Tile<T>::BK;
   int kchunk = K;
-  if (grp.mode != 2 && splits > 1) kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+  if (grp.mode != 2 && splits > 1) kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
   if (grp.mode != 2) splits = (K + kchunk - 1) / kchunk;
   if (splits < 1) splits = 1;
   int gx = grp.mode == 1 ? max_tiles_m : grp.mode == 3 ? cdiv(grp.rows_per_group, BM) * grp.ngroups : cdiv(M, BM);

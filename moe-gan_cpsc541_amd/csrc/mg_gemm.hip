@@ -164,7 +164,7 @@ extern "C" int mg_conv2d_fwd(int dtype, const void* x, int B, int H, int W, int 
                              int KH, int KW, int stride, int pad, const float* in_scale, void* y, int64_t ldy,
                              int y_dtype, const mg_epilogue* ep, void* stream) {
   MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
-  MG_REQUIRE(Cin % BK == 0 && pow2(Cin), "Cin must be a power of two >= 32");
+  MG_REQUIRE(Cin >= 8 && pow2(Cin), "Cin must be a power of two >= 8");
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   MG_REQUIRE(pow2(H) && pow2(W) && pow2(OH) && pow2(OW), "spatial sizes must be powers of two");
   MG_REQUIRE(aligned16(x) && aligned16(wpack), "x/wpack must be 16-byte aligned");
@@ -330,7 +330,7 @@ void run_dgrad_s2(const void* g, int B, int OH, int OW, int Cg, const void* wcls
 extern "C" int mg_conv2d_dgrad_s2(int dtype, const void* g, int B, int OH, int OW, int Cg, const void* wcls, int Cin,
                                   void* out, int64_t ldo, int out_dtype, const mg_epilogue* ep, void* stream) {
   MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
-  MG_REQUIRE(pow2(Cg) && Cg >= BK, "Cg must be a power of two >= 32");
+  MG_REQUIRE(pow2(Cg) && Cg >= 8, "Cg must be a power of two >= 8");
   MG_REQUIRE(pow2(OH) && pow2(OW), "OH, OW must be powers of two");
   MG_REQUIRE(aligned16(g) && aligned16(wcls), "g/wcls must be 16-byte aligned");
   MG_REQUIRE(!(ep && ep->atomic) || out_dtype == MG_F32, "atomic epilogue requires fp32 output");

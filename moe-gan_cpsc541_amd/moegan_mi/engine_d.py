@@ -143,11 +143,7 @@ class DiscriminatorEngine:
         self.stack_backward(fr, g_img)
         self.stack_backward(ff, g_fake)
         # text branch + head bias
-        g_tpre = torch.empty(B, 128, device=dev)
-        ops.d_text_bwd(g_tb, t, self.w2sum, 256, g_tpre, self.dW["output_layer.0."].view(384, 16))
-        ops.colsum(g_tb.view(B, 1), self.G("output_layer.0.bias"))
-        ops.linear_wgrad(g_tpre, text, self.dW["text_projection.0."])
-        ops.colsum(g_tpre, self.G("text_projection.0.bias"))
+        self._text_head_bwd(g_tb, t, text)
         # ---- R1 ----
         Hf = Hr // 4
         Ho = Hf - 3
@@ -180,10 +176,10 @@ class DiscriminatorEngine:
         self.dW["conv_layers.0."] = g.permute(0, 2, 1).contiguous().view(128, 3, 4, 4)
 
     # ------------------------------------------------------------------
-    def g_phase(self, fake_img, fake_layout, text, scale=1.0):
+    def g_phase(self, fake_img, fake_layout, text, scale=1.0, want_d_params=False):
         """Adversarial loss of the generator step (t2i_moe_gan.py:1379-1382) and d loss / d fake image.
-        D parameter gradients are not formed: with gradient_accumulation_steps=1 the reference zeroes
-        them before they are ever used (t2i_moe_gan.py:1272 vs :1407)."""
+        D parameter gradients are formed only when ``want_d_params``: with gradient_accumulation_steps=1 the
+        reference zeroes them before they are ever used (t2i_moe_gan.py:1272 vs :1407)."""
         B = fake_img.shape[0]
         Hs = fake_img.shape[1]
         t, tb = self.text_branch(text)
@@ -195,5 +191,46 @@ class DiscriminatorEngine:
         g = torch.empty(B, 1, device=self.dev)
         ops.g_loss(fake_pred, loss, g.view(-1), scale)
         g_img = torch.zeros(fake_img.shape, device=self.dev, dtype=self.cdt)
-        self.stack_backward(f, g, want_params=False, g_input=g_img)
+        if want_d_params:
+            self.begin_grads()
+        self.stack_backward(f, g, want_params=want_d_params, g_input=g_img)
+        if want_d_params:
+            self._text_head_bwd(g.view(-1), t, text)
+            self._remap_w0()
+            self.finish_grads()
         return loss, fake_pred, g_img
+
+    def _text_head_bwd(self, g_tb, t, text):
+        B = t.shape[0]
+        g_tpre = torch.empty(B, 128, device=self.dev)
+        ops.d_text_bwd(g_tb, t, self.w2sum, 256, g_tpre, self.dW["output_layer.0."].view(384, 16))
+        ops.colsum(g_tb.view(B, 1), self.G("output_layer.0.bias"))
+        ops.linear_wgrad(g_tpre, text, self.dW["text_projection.0."])
+        ops.colsum(g_tpre, self.G("text_projection.0.bias"))
+
+    # ------------------------------------------------------------------
+    # generic forward / backward for the module API (AuroraDiscriminator.forward)
+    # ------------------------------------------------------------------
+    def logits(self, img_nchw, text):
+        """D(img, text) for any power-of-two H >= 16 (NCHW fp32 image) -> ([B, Ho*Ho] logits, ctx)."""
+        B, _, H, _ = img_nchw.shape
+        t, tb = self.text_branch(text)
+        f = self.forward(img_nchw.contiguous(), "nchw", text, B, H)
+        out = f["img_part"].clone()
+        ops.copy2d(tb.view(B, 1).expand(B, out.shape[1]).contiguous(), out, B, out.shape[1], accumulate=1)
+        return out, dict(f=f, t=t, text=text)
+
+    def logits_backward(self, ctx, g_logits, want_input=True):
+        """d loss / d logits -> D parameter gradients (accumulated) and d loss / d image (NCHW fp32)."""
+        f = ctx["f"]
+        B, H = f["B"], f["H"]
+        g_logits = g_logits.contiguous().float()
+        g_tb = torch.zeros(B, device=self.dev)
+        ops.segsum(g_logits, B, g_logits.shape[1], 1, g_tb.view(B, 1), ld=1)
+        self.begin_grads()
+        g_img = torch.zeros(B, H, H, 4, device=self.dev, dtype=torch.float32) if want_input else None
+        self.stack_backward(f, g_logits, want_params=True, g_input=g_img)
+        self._text_head_bwd(g_tb, ctx["t"], ctx["text"])
+        self._remap_w0()
+        self.finish_grads()
+        return None if g_img is None else g_img[..., :3].permute(0, 3, 1, 2).contiguous()

@@ -84,6 +84,20 @@ class ParamStore:
         if shadow_dtype is not None and shadow_dtype != torch.float32:
             self.shadow = torch.zeros(self.total, device=self.device, dtype=shadow_dtype)
 
+    def rebind(self, data):
+        """Adopt ``data`` (the flat fp32 buffer, possibly on a new device) and move the rest with it."""
+        dev = data.device
+        self.data = data
+        if self.grad.device != dev:
+            self.grad = self.grad.to(dev)
+            self.m = self.m.to(dev)
+            self.v = self.v.to(dev)
+            self.buffers = OrderedDict((n, b.to(dev)) for n, b in self.buffers.items())
+            if self.shadow is not None:
+                self.shadow = torch.zeros(self.total, device=dev, dtype=self.shadow_dtype)
+        self.device = dev
+        self.refresh_shadow()
+
     # ---- views ----
     def _v(self, buf, name):
         off, n = self.offsets[name]
@@ -108,7 +122,7 @@ class ParamStore:
 
     # ---- per-step ----
     def refresh_shadow(self):
-        if self.shadow is not None:
+        if self.shadow is not None and self.data.is_cuda:
             ops.cast(self.data, out=self.shadow)
 
     def zero_grad(self):

@@ -38,13 +38,13 @@ class StepConfig:
 
 
 class TrainStep:
-    def __init__(self, cfg, device="cuda", process_group=None):
+    def __init__(self, cfg, device="cuda", process_group=None, gstore=None, dstore=None):
         self.cfg = cfg
         self.dev = torch.device(device)
         self.cdt = torch.bfloat16 if cfg.dtype == "bf16" else torch.float32
-        self.gs = ParamStore(generator_shapes(cfg.E), self.dev, frozen_prefixes=("to_rgb_8.",),
-                             shadow_dtype=self.cdt)
-        self.ds = ParamStore(discriminator_shapes(), self.dev)
+        self.gs = gstore if gstore is not None else ParamStore(
+            generator_shapes(cfg.E), self.dev, frozen_prefixes=("to_rgb_8.",), shadow_dtype=self.cdt)
+        self.ds = dstore if dstore is not None else ParamStore(discriminator_shapes(), self.dev)
         self.ge = GeneratorEngine(self.gs, cfg.E, cfg.topk, self.cdt)
         self.de = DiscriminatorEngine(self.ds, self.cdt)
         self.pg = process_group
@@ -69,9 +69,11 @@ class TrainStep:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
 
     # ---- optimizer ----
-    def _adamw(self, store, lr, max_norm, n=None):
+    def _adamw(self, store, lr, max_norm, n=None, grad_scale=1.0):
         n = store.n_opt if n is None else n
         store.step_count += 1
+        if grad_scale != 1.0:  # (loss / accumulation_steps) of the reference == scaling the summed gradient
+            store.grad[:n].mul_(grad_scale)
         ss = torch.zeros(1, device=self.dev)
         ops.sumsq(store.grad[:n], ss)
         c = self.cfg
@@ -81,27 +83,36 @@ class TrainStep:
 
     # ---- the step ----
     def step(self, real, text, z, eps_d, eps_g, perm, *, anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8,
-             prep=True):
+             prep=True, acc=1, zero_grads=True, step_optim=True):
         """real [B,3,64,64] fp32 NCHW, text [B,512], z [B,512] fp32 (device); eps_d / eps_g: 3 triples of
-        router epsilon tensors; perm [B] int32.  Returns a dict of device tensors."""
+        router epsilon tensors; perm [B] int32.  Returns a dict of device tensors.
+
+        Gradient accumulation (t2i_moe_gan.py:1272, :1329, :1353, :1413): ``zero_grads`` at the first batch of
+        a window, ``step_optim`` at its last; gradients are summed and scaled by 1/acc before clipping.  As in
+        the reference, the generator step's loss also accumulates into the discriminator's gradients, which
+        matters only when the D optimizer has not stepped yet in the window (acc > 1)."""
         c = self.cfg
         B = real.shape[0]
         if prep:
             self.ge.prep()
             self.de.prep()
         # ------------------------- D phase -------------------------
-        self.ds.zero_grad()
+        if zero_grads:
+            self.ds.zero_grad()
         f16, _, _, _, _, _ = self.ge.forward(z, text, eps_d, anneal, c.psi, train=True, save=False)
         dres = self.de.d_phase(real, text, f16, ("nhwc", 8), perm, c.r1_gamma)
-        self._allreduce_mean(self.ds.grad)
-        d_sumsq = self._adamw(self.ds, lr_d, c.d_clip)
-        self.de.prep()
+        d_sumsq = None
+        if step_optim:
+            self._allreduce_mean(self.ds.grad)
+            d_sumsq = self._adamw(self.ds, lr_d, c.d_clip, grad_scale=1.0 / acc)
+            self.de.prep()
         # ------------------------- G phase -------------------------
-        self.gs.zero_grad()
+        if zero_grads:
+            self.gs.zero_grad()
         want8 = self.clip_encoder is not None
         img16, img8, kl2s, probs, _, ctx = self.ge.forward(z, text, eps_g, anneal, c.psi, train=True, save=True,
                                                            want_img8=want8)
-        g_gan, fake_pred, g_img = self.de.g_phase(img16, ("nhwc", 8), text)
+        g_gan, fake_pred, g_img = self.de.g_phase(img16, ("nhwc", 8), text, want_d_params=(acc > 1 and not step_optim))
         # balance loss on the last MoE layer, over the GLOBAL batch (t2i_moe_gan.py:951-1000)
         last = probs[-1]
         load = torch.zeros(c.E, device=self.dev)
@@ -116,9 +127,11 @@ class TrainStep:
         kl_total = torch.empty(1, device=self.dev)
         ops.kl_coefs(kl2, len(kl2s), eff_kl_weight, kl_coef, kl_total)
         self.ge.backward(ctx, g_img, coef=coef, kl_coef=kl_coef)
-        self._allreduce_mean(self.gs.grad)
-        g_sumsq = self._adamw(self.gs, lr_g, c.g_clip)
-        out = dict(d_losses=dres["losses"], r1=dres["r1"], g_gan=g_gan, balance=bal, kl=kl_total,
+        g_sumsq = None
+        if step_optim:
+            self._allreduce_mean(self.gs.grad)
+            g_sumsq = self._adamw(self.gs, lr_g, c.g_clip, grad_scale=1.0 / acc)
+        out = dict(d_losses=dres["losses"], r1=dres["r1"], g_gan=g_gan, balance=bal, kl=kl_total, kl_raw=kl2,
                    d_grad_sumsq=d_sumsq, g_grad_sumsq=g_sumsq, real_pred=dres["real_pred"],
                    fake_pred=dres["fake_pred"], mism_pred=dres["mism_pred"], r1_grad=dres["r1_grad"],
                    img16=img16, img8=img8)

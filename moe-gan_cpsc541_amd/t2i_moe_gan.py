@@ -1,0 +1,443 @@
+"""Drop-in replacement for the reference module ``t2i_moe_gan`` (moegan/t2i_moe_gan.py) on MI355X.
+
+Same public names and signatures -- ``train_aurora_gan``, ``AuroraGenerator``,
+``AuroraDiscriminator``, ``AuroraGANLoss``, ``sample_aurora_gan``, the module constants -- and
+the same ``state_dict`` keys/shapes, so the reference's entry points (train_model.py,
+sagemaker_train.py, inference.py, generate_images.py) work by pointing ``sys.path`` here.
+
+Differences by design:
+  * the math runs on libmoegan_hip (hand-written gfx950 kernels) through explicit forward/backward
+    engines; there is no CPU execution path for the models (the CPU restatement in ``oracle/`` is
+    test infrastructure).  Models can be constructed, loaded and saved on the CPU;
+  * each model's parameters are ONE flat tensor (``model.flat``); ``state_dict()`` still exposes the
+    reference names, so checkpoints interchange with the reference;
+  * ``AuroraDiscriminator.forward`` supports first-order autograd; the R1 double backward of the
+    training loop is done in closed form inside the fused training step;
+  * activation checkpointing and the OOM/memory guards are no-ops (288 GB HBM);
+  * the CLIP loss needs a local CLIP image encoder (``set_clip_model``); without one it is
+    reported as 0 -- it never contributes a gradient in the reference either (:98-101).
+"""
+import logging
+import math
+import os
+import sys
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+from moegan_mi.engine_d import DiscriminatorEngine  # noqa: E402
+from moegan_mi.engine_g import GeneratorEngine  # noqa: E402
+from moegan_mi.init import init_discriminator, init_generator  # noqa: E402
+from moegan_mi.layout import discriminator_shapes, generator_shapes  # noqa: E402
+from moegan_mi.params import ParamStore  # noqa: E402
+from moegan_mi.step import StepConfig, TrainStep  # noqa: E402
+
+LATENT_DIM = 512
+TEXT_EMBEDDING_DIM = 512
+DEVICE = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
+NUM_EXPERTS = 4
+CLIP_MODEL_TYPE = "ViT-B/32"
+
+logging.basicConfig(level=logging.INFO)
+logger = logging.getLogger(__name__)
+
+_clip_model = None
+
+
+def set_clip_model(model):
+    """Register a CLIP-like model (``encode_image``/``encode_text``) loaded from local weights."""
+    global _clip_model
+    _clip_model = model
+
+
+def get_clip_model():
+    """Reference :32-47.  CLIP weights cannot be downloaded here; use set_clip_model()."""
+    if _clip_model is None:
+        raise RuntimeError("no CLIP model registered: call t2i_moe_gan.set_clip_model(model) with local weights")
+    return _clip_model, None
+
+
+def _eps_for(store, E, device):
+    """Fresh router noise for one generator forward (reference draws normal_() per router, :349-351)."""
+    eps = []
+    for name in ("gen_block_4", "gen_block_8", "gen_block_16"):
+        r = f"{name}.attn_block.moe.router."
+        trip = []
+        for n in ("epsilon_f", "epsilon_t", "epsilon_c"):
+            buf = store.buffers[r + n]
+            buf.normal_()
+            trip.append(buf)
+        eps.append(tuple(trip))
+    return eps
+
+
+class _FlatModule(nn.Module):
+    """nn.Module over a ParamStore: one flat parameter, reference-named state_dict."""
+
+    def __init__(self, shapes, frozen=(), dtype="fp32"):
+        super().__init__()
+        cdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self._store = ParamStore(shapes, "cpu", frozen_prefixes=frozen, shadow_dtype=cdt)
+        self.flat = nn.Parameter(self._store.data)
+        self._cdt = cdt
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        self._store.rebind(self.flat.data)
+        return self
+
+    def state_dict(self, *args, destination=None, prefix="", keep_vars=False):
+        sd = self._store.state_dict(cpu=False)
+        if destination is not None:
+            for k, v in sd.items():
+                destination[prefix + k] = v
+            return destination
+        return sd if not prefix else {prefix + k: v for k, v in sd.items()}
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        self._store.load_state_dict(state_dict, strict)
+        return nn.modules.module._IncompatibleKeys([], [])
+
+    def _require_gpu(self):
+        if not self.flat.is_cuda:
+            raise RuntimeError(f"{type(self).__name__}: the MI355X path runs on a HIP device; move the model "
+                               "with .to('cuda') (the CPU restatement in oracle/ is test infrastructure)")
+
+
+class _GenFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flat, z, text, mod, anneal, psi, train, want8, eps):
+        eng = mod._engine()
+        eng.prep()
+        need = any(ctx.needs_input_grad[:3])
+        img16, img8, kl2s, probs, _, gctx = eng.forward(z.float().contiguous(), text.float().contiguous(), eps,
+                                                        anneal, psi, train=train, save=need, want_img8=want8)
+        out16 = img16[..., :3].permute(0, 3, 1, 2).float().contiguous()
+        out8 = img8[..., :3].permute(0, 3, 1, 2).float().contiguous() if img8 is not None else z.new_zeros(0)
+        if train:
+            kl2 = torch.stack(kl2s)
+            kl = kl2[:, 0].sum()
+        else:
+            kl2 = None
+            kl = z.new_zeros(())
+        ctx.mod, ctx.gctx, ctx.kl2, ctx.want8 = mod, gctx, kl2, want8
+        ctx.mark_non_differentiable(*([] if train else [kl]))
+        return (out16, out8, kl) + tuple(probs)
+
+    @staticmethod
+    def backward(ctx, g16, g8, gkl, *gprobs):
+        mod, eng = ctx.mod, ctx.mod._engine()
+        st = mod._store
+        st.zero_grad()
+        B, dev = ctx.gctx["B"], eng.dev
+        gi16 = torch.zeros(B, 16, 16, 8, device=dev, dtype=eng.cdt)
+        if g16 is not None:
+            gi16[..., :3] = g16.permute(0, 2, 3, 1)
+        gi8 = None
+        if ctx.want8 and g8 is not None and g8.numel():
+            gi8 = torch.zeros(B, 8, 8, 8, device=dev, dtype=eng.cdt)
+            gi8[..., :3] = g8.permute(0, 2, 3, 1)
+        kl_coef = None
+        if ctx.kl2 is not None and gkl is not None:
+            kl_coef = (gkl.float() * ctx.kl2[:, 1]).contiguous()
+        gp = [None if g is None else g.float().contiguous() for g in gprobs]
+        gz, gtext = eng.backward(ctx.gctx, gi16, kl_coef=kl_coef, want_input_grads=True, g_probs=gp, g_img8=gi8)
+        return st.grad.clone(), gz, gtext, None, None, None, None, None, None
+
+
+class AuroraGenerator(_FlatModule):
+    """Reference :668-855.  Extra keyword args: num_experts (default 4, as NUM_EXPERTS), topk (None = dense
+    soft combine over all experts, as the reference trains), dtype ("fp32" | "bf16")."""
+
+    def __init__(self, latent_dim=LATENT_DIM, text_embedding_dim=512, max_resolution=16, num_experts=NUM_EXPERTS,
+                 topk=None, dtype="fp32", seed=0):
+        if latent_dim != 512 or text_embedding_dim != 512 or max_resolution != 16:
+            raise ValueError("the reference architecture is fixed at latent 512, text 512, 16x16 output")
+        super().__init__(generator_shapes(num_experts), frozen=("to_rgb_8.",), dtype=dtype)
+        self.latent_dim, self.text_embedding_dim, self.max_resolution = latent_dim, text_embedding_dim, max_resolution
+        self.num_experts, self.topk = num_experts, topk
+        self._use_checkpointing = False
+        self._eng = None
+        init_generator(self._store, seed)
+
+    def _engine(self):
+        if self._eng is None or self._eng.st is not self._store or self._eng.dev != self._store.device:
+            self._eng = GeneratorEngine(self._store, self.num_experts, self.topk, self._cdt)
+        return self._eng
+
+    def enable_checkpointing(self):
+        self._use_checkpointing = True  # no-op: 288 GB HBM; math is unchanged
+        return self
+
+    def disable_checkpointing(self):
+        self._use_checkpointing = False
+        return self
+
+    def encode_text(self, text_or_embeddings):
+        if isinstance(text_or_embeddings, str) or (isinstance(text_or_embeddings, list)
+                                                     and isinstance(text_or_embeddings[0], str)):
+            model, _ = get_clip_model()
+            return encode_text_with_clip(text_or_embeddings, model)
+        return text_or_embeddings
+
+    def forward(self, z, text_input, truncation_psi=0.7, return_routing=False, return_intermediate=False,
+                annealing_factor=1.0):
+        self._require_gpu()
+        text = self.encode_text(text_input)
+        B = z.shape[0]
+        if text.shape[0] != B:
+            if text.shape[0] == 1:
+                text = text.repeat(B, 1)
+            else:
+                raise ValueError(f"Batch size mismatch: z has batch size {B}, but text_embeddings has batch size "
+                                 f"{text.shape[0]}")
+        eps = _eps_for(self._store, self.num_experts, z.device) if self.training else None
+        outs = _GenFn.apply(self.flat, z, text, self, float(annealing_factor), float(truncation_psi), self.training,
+                            bool(return_intermediate), eps)
+        img16, img8, kl = outs[0], outs[1], outs[2]
+        probs = list(outs[3:])
+        if return_routing and return_intermediate:
+            return img16, img8, kl, probs
+        if return_routing:
+            return img16, None, kl, probs
+        if return_intermediate:
+            return img16, img8, kl
+        return img16, kl
+
+
+class _DiscFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flat, img, text, mod):
+        eng = mod._engine()
+        eng.prep()
+        logits, dctx = eng.logits(img.float(), text.float().contiguous())
+        ctx.mod, ctx.dctx = mod, dctx
+        return logits.reshape(-1)
+
+    @staticmethod
+    def backward(ctx, g):
+        mod, eng = ctx.mod, ctx.mod._engine()
+        mod._store.zero_grad()
+        B = ctx.dctx["f"]["B"]
+        gimg = eng.logits_backward(ctx.dctx, g.reshape(B, -1), want_input=ctx.needs_input_grad[1])
+        return mod._store.grad.clone(), gimg, None, None
+
+
+class AuroraDiscriminator(_FlatModule):
+    """Reference :858-907 (weight_norm layers stored as weight_g / weight_v)."""
+
+    def __init__(self, text_embedding_dim=512, max_resolution=16, dtype="fp32", seed=1):
+        super().__init__(discriminator_shapes(), dtype="fp32")
+        self.max_resolution = max_resolution
+        self._eng = None
+        self._dtype = dtype
+        init_discriminator(self._store, seed)
+
+    def _engine(self):
+        if self._eng is None or self._eng.st is not self._store or self._eng.dev != self._store.device:
+            cdt = torch.bfloat16 if self._dtype == "bf16" else torch.float32
+            self._eng = DiscriminatorEngine(self._store, cdt)
+        return self._eng
+
+    def forward(self, img, text_embedding):
+        self._require_gpu()
+        return _DiscFn.apply(self.flat, img, text_embedding, self)
+
+
+def encode_text_with_clip(text, model=None):
+    model = model or get_clip_model()[0]
+    if isinstance(text, str):
+        text = [text]
+    import clip  # a locally provided CLIP package
+    with torch.no_grad():
+        return model.encode_text(clip.tokenize(text).to(DEVICE)).float()
+
+
+class CLIPLoss(nn.Module):
+    """Reference :66-119 -- forward-only, no gradient (the image branch runs under no_grad)."""
+
+    def __init__(self, device=DEVICE):
+        super().__init__()
+        self.device = device
+
+    def forward(self, images, text_embeddings):
+        if images is None or _clip_model is None:
+            return torch.tensor(0.0, device=self.device)
+        with torch.no_grad():
+            im = torch.clamp(images, -1, 1)
+            if im.shape[-1] != 224 or im.shape[-2] != 224:
+                im = F.interpolate(im, size=(224, 224), mode="bilinear", align_corners=False)
+            f = _clip_model.encode_image(im).float()
+            f = f / f.norm(dim=-1, keepdim=True)
+            t = text_embeddings / text_embeddings.norm(dim=-1, keepdim=True)
+            sim = torch.nan_to_num((f * t).sum(dim=1))
+            return 1.0 - sim.mean()
+
+
+class AuroraGANLoss:
+    """Reference :909-1000 (loss values on logits; the fused step uses the HIP loss kernels)."""
+
+    def __init__(self, device=DEVICE):
+        self.device = device
+        self.clip_loss_fn = CLIPLoss(device)
+
+    def generator_loss(self, fake_pred, kl_loss=None, kl_weight=0.001):
+        g = F.softplus(-fake_pred).mean()
+        return g + kl_weight * kl_loss if kl_loss is not None else g
+
+    def compute_clip_loss(self, images, text_input):
+        return self.clip_loss_fn(images, text_input.to(images.device))
+
+    def discriminator_loss(self, real_pred, fake_pred, mismatched_pred):
+        return F.softplus(-real_pred).mean() + F.softplus(fake_pred).mean() + F.softplus(mismatched_pred).mean()
+
+    def moe_balance_loss(self, routing_probs, balance_weight=0.01):
+        if not routing_probs:
+            return torch.tensor(0.0, device=self.device)
+        p = routing_probs[-1]
+        if p is None or p.numel() == 0:
+            return torch.tensor(0.0, device=self.device)
+        E, T = p.size(1), p.size(0)
+        frac = (p.sum(dim=0) + 1e-6) / T
+        cv = torch.std(frac) / (torch.mean(frac) + 1e-6)
+        return balance_weight * torch.nan_to_num(torch.clamp(E * cv, 0.0, 10.0), nan=0.0)
+
+
+def _lr_schedule(lr, num_epochs, lr_warmup_epochs):
+    """Per-epoch learning rates of the reference (warmup, then CosineAnnealingLR stepped per epoch,
+    :1108-1118, :1149-1166, :1514-1516), replayed with torch's own scheduler on a dummy parameter."""
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.AdamW([p], lr=lr)
+    sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=max(1, num_epochs - lr_warmup_epochs),
+                                                     eta_min=lr * 0.05)
+    out = []
+    for epoch in range(num_epochs):
+        if epoch < lr_warmup_epochs:
+            for g in opt.param_groups:
+                g["lr"] = lr * (0.1 + 0.9 * (epoch / lr_warmup_epochs))
+        out.append(opt.param_groups[0]["lr"])
+        if epoch >= lr_warmup_epochs:
+            opt.step()
+            sch.step()
+    return out
+
+
+def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, beta1=0.5, beta2=0.999,
+                     r1_gamma=10.0, clip_weight_16=0.1, clip_weight_8=0.05, kl_weight=0.001, kl_annealing_epochs=5,
+                     lr_warmup_epochs=3, balance_weight=0.01, device=DEVICE, save_dir="./aurora_checkpoints",
+                     log_interval=10, save_interval=1000, metric_callback=None, use_amp=True,
+                     gradient_accumulation_steps=8, checkpoint_activation=True, batch_memory_limit=20.0,
+                     max_resolution=16, *, clip_weight_64=None, clip_weight_32=None, num_experts=NUM_EXPERTS,
+                     topk=None, dtype=None, process_group=None, seed=0):
+    """Reference :1029-1669.  ``clip_weight_64``/``clip_weight_32`` (the names train_model.py passes,
+    SURVEY.md §0) map to the 16x16 / 8x8 CLIP weights.  ``use_amp`` selects bf16 (the MI355X mixed
+    precision; the reference's fp16 GradScaler is not needed) unless ``dtype`` is given."""
+    os.makedirs(save_dir, exist_ok=True)
+    if clip_weight_64 is not None:
+        clip_weight_16 = clip_weight_64
+    if clip_weight_32 is not None:
+        clip_weight_8 = clip_weight_32
+    device = torch.device(device)
+    if dtype is None:
+        dtype = "bf16" if use_amp else "fp32"
+    generator = AuroraGenerator(num_experts=num_experts, topk=topk, dtype=dtype, seed=seed).to(device)
+    discriminator = AuroraDiscriminator(dtype=dtype, seed=seed + 1).to(device)
+    if checkpoint_activation:
+        generator.enable_checkpointing()
+    cfg = StepConfig(E=num_experts, topk=topk, dtype=dtype, r1_gamma=r1_gamma, clip_weight_16=clip_weight_16,
+                     clip_weight_8=clip_weight_8, balance_weight=balance_weight, beta1=beta1, beta2=beta2)
+    ts = TrainStep(cfg, device, process_group=process_group, gstore=generator._store, dstore=discriminator._store)
+    print(f"Generator parameters: {generator._store.n_opt + (generator._store.total - generator._store.n_opt):,}")
+    lrs = _lr_schedule(lr, num_epochs, lr_warmup_epochs)
+    gan_loss = AuroraGANLoss(device)
+    acc = max(1, int(gradient_accumulation_steps))
+    step = 0
+    from tqdm import tqdm
+    for epoch in range(num_epochs):
+        cur_lr = lrs[epoch]
+        kl_warmup = min(1.0, (epoch / kl_annealing_epochs) ** 2)
+        eff_kl = kl_weight * (1e-5 + (1.0 - 1e-5) * kl_warmup)
+        temperature_factor = max(1.0, 3.0 - epoch * 0.1)
+        print(f"\n{'=' * 20} Epoch {epoch + 1}/{num_epochs} {'=' * 20}")
+        print(f"  LR: {cur_lr:.6f}  Temperature factor: {temperature_factor:.2f}  Effective KL weight: {eff_kl:.8f}")
+        pbar = tqdm(dataloader, desc=f"Epoch {epoch + 1}/{num_epochs}")
+        n_batches = len(dataloader)
+        for batch_idx, (real, text) in enumerate(pbar):
+            real = real.to(device, non_blocking=True).float()
+            text = text.to(device, non_blocking=True).float()
+            B = real.shape[0]
+            z = torch.randn(B, LATENT_DIM, device=device)
+            eps_d = _eps_for(generator._store, num_experts, device)
+            eps_d = [tuple(t.clone() for t in trip) for trip in eps_d]
+            eps_g = _eps_for(generator._store, num_experts, device)
+            perm = torch.randperm(B, device=device).int()
+            zero = batch_idx % acc == 0
+            stp = (batch_idx + 1) % acc == 0 or (batch_idx + 1) == n_batches
+            out = ts.step(real, text, z, eps_d, eps_g, perm, anneal=temperature_factor, lr_g=cur_lr, lr_d=cur_lr,
+                          eff_kl_weight=eff_kl, acc=acc, zero_grads=zero, step_optim=stp)
+            if step % log_interval == 0:
+                d_gan, r1 = float(out["d_losses"][0]), float(out["r1"][0])
+                g_gan, bal, kl = float(out["g_gan"][0]), float(out["balance"][0]), float(out["kl"][0])
+                if not (math.isfinite(d_gan) and math.isfinite(g_gan)):
+                    print("⚠️ NaN/Inf detected in losses")
+                logger.info(f"\nStep [{step}] Epoch [{epoch + 1}] Batch [{batch_idx}/{n_batches}] "
+                            f"D_loss: {d_gan + r1:.4f} (GAN: {d_gan:.4f}, R1: {r1:.4f}), G_loss: "
+                            f"{g_gan + bal + eff_kl * kl:.4f} (GAN: {g_gan:.4f}, KL: {kl:.4f}, Balance: {bal:.4f})")
+                pbar.set_postfix({"D_loss": f"{d_gan:.3f}", "R1": f"{r1:.3f}", "G_loss": f"{g_gan:.3f}",
+                                  "KL": f"{kl:.4f}", "Balance": f"{bal:.4f}"})
+            step += 1
+        pbar.close()
+        if val_dataloader is not None:
+            vm = _validate(generator, discriminator, val_dataloader, gan_loss, temperature_factor, eff_kl, device)
+            print(f"Validation Results - D_loss: {vm['val_d_loss']:.4f}, G_loss: {vm['val_g_loss']:.4f}, "
+                  f"Clip_Loss_16: {vm['val_clip_loss_16']:.4f}, Clip_Loss_8: {vm['val_clip_loss_8']:.4f}")
+            if metric_callback and not metric_callback(epoch, vm):
+                print("Early stopping triggered by metric callback")
+                break
+    return generator, discriminator
+
+
+def _validate(generator, discriminator, loader, gan_loss, temperature_factor, eff_kl, device):
+    """Reference validation loop :1519-1639 (eval-mode generator: mean router weights, hard top-1)."""
+    generator.eval()
+    discriminator.eval()
+    tot = {"val_d_loss": 0.0, "val_g_loss": 0.0, "val_clip_loss_16": 0.0, "val_clip_loss_8": 0.0}
+    n = 0
+    with torch.no_grad():
+        for real, text in loader:
+            real, text = real.to(device).float(), text.to(device).float()
+            B = real.shape[0]
+            z = torch.randn(B, LATENT_DIM, device=device)
+            f16, f8, kl = generator(z, text, return_intermediate=True, annealing_factor=temperature_factor)
+            rp = discriminator(real, text)
+            fp = discriminator(f16, text)
+            mp = discriminator(real, text[torch.randperm(B, device=device)])
+            tot["val_d_loss"] += float(gan_loss.discriminator_loss(rp, fp, mp)) * B
+            tot["val_g_loss"] += float(gan_loss.generator_loss(fp, kl, kl_weight=eff_kl)) * B
+            tot["val_clip_loss_16"] += float(gan_loss.compute_clip_loss(f16, text)) * B
+            tot["val_clip_loss_8"] += float(gan_loss.compute_clip_loss(f8, text)) * B
+            n += B
+    generator.train()
+    discriminator.train()
+    vm = {k: v / max(n, 1) for k, v in tot.items()}
+    vm["val_clip_loss"] = vm["val_clip_loss_16"]
+    return vm
+
+
+def sample_aurora_gan(generator, text_prompt, num_samples=1, truncation_psi=0.7, device=DEVICE):
+    """Reference :1672-1709: eval mode (hard top-1 routing), clamp to [-1, 1]."""
+    generator.eval()
+    z = torch.randn(num_samples, LATENT_DIM, device=device, dtype=torch.float32)
+    if isinstance(text_prompt, str) or (isinstance(text_prompt, list) and isinstance(text_prompt[0], str)):
+        text_prompt = encode_text_with_clip(text_prompt)
+    text_prompt = text_prompt.float().to(device)
+    if num_samples > 1 and text_prompt.size(0) == 1:
+        text_prompt = text_prompt.repeat(num_samples, 1)
+    with torch.no_grad():
+        fake, _ = generator(z, text_prompt, truncation_psi=truncation_psi)
+        return torch.clamp(fake, -1, 1)

@@ -309,16 +309,20 @@ def clip_loss(images, text, encode_image):
 # ---------------------------------------------------------------------------
 def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, *, r1_gamma=10.0,
                clip_w16=0.1, clip_w8=0.05, kl_weight_eff=1e-8, balance_weight=0.01, anneal=3.0,
-               psi=0.7, topk=None, encode_image=None, d_clip=0.7, g_clip=0.8):
+               psi=0.7, topk=None, encode_image=None, d_clip=0.7, g_clip=0.8, acc=1, zero_grads=True,
+               step_optim=True):
     """Replays one batch of the reference loop with explicit randomness.
 
     ``PG``/``PD`` map reference state_dict keys to leaf tensors (requires_grad
     for parameters); ``optG``/``optD`` are torch AdamW instances over them (the
-    reference's own optimizer).  Returns a dict of logged scalars.
+    reference's own optimizer).  Gradient accumulation (:1272, :1329, :1353, :1413): ``zero_grads`` at
+    the first batch of a window, ``step_optim`` at its last, losses divided by ``acc``.  Returns a dict
+    of logged scalars.
     """
     B = real.shape[0]
-    for p in PD.values():
-        p.grad = None
+    if zero_grads:
+        for p in PD.values():
+            p.grad = None
     real = real.clone().requires_grad_(True)  # :1276
     real_pred = discriminator(real, text, PD)  # :1279
     g, = torch.autograd.grad(real_pred.sum(), real, create_graph=True)  # :1282-1284
@@ -329,11 +333,13 @@ def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, 
     mism_pred = discriminator(real.detach(), text[perm], PD)  # :1303-1305
     dgan = d_loss(real_pred, fake_pred, mism_pred)
     dl = dgan + r1
-    dl.backward()  # :1326
-    torch.nn.utils.clip_grad_norm_([p for p in PD.values() if p.requires_grad], max_norm=d_clip)  # :1336
-    optD.step()
-    for p in PG.values():
-        p.grad = None
+    (dl / acc).backward()  # :1326
+    if step_optim:
+        torch.nn.utils.clip_grad_norm_([p for p in PD.values() if p.requires_grad], max_norm=d_clip)  # :1336
+        optD.step()
+    if zero_grads:
+        for p in PG.values():
+            p.grad = None
     f16, f8, kl, probs = generator(z, text, PG, eps_gphase, True, anneal, psi, topk)  # :1358-1364
     if kl > 50.0:  # :1369-1370
         kl = torch.clamp(kl, max=50.0)
@@ -345,8 +351,9 @@ def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, 
     bal = balance_loss(probs, balance_weight)
     gl = gg + (clip_w16 * c16 + clip_w8 * c8) + bal  # :1393
     gl = gl + kl_weight_eff * kl  # :1402-1404
-    gl.backward()  # :1410
-    torch.nn.utils.clip_grad_norm_([p for p in PG.values() if p.requires_grad], max_norm=g_clip)  # :1420
-    optG.step()
+    (gl / acc).backward()  # :1410
+    if step_optim:
+        torch.nn.utils.clip_grad_norm_([p for p in PG.values() if p.requires_grad], max_norm=g_clip)  # :1420
+        optG.step()
     return {"d_loss_gan": float(dgan), "r1": float(r1), "g_loss_gan": float(gg), "kl": float(kl),
             "balance": float(bal), "clip16": float(c16), "clip8": float(c8), "r1_grad": g.detach()}

@@ -1,4 +1,4 @@
-"""Generate the golden fixtures F1-F8 by running the REFERENCE (this container only).
+"""Generate the golden fixtures F1-F10 by running the REFERENCE (this container only).
 
 Run from the repo root:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
 
@@ -367,10 +367,22 @@ def f7_generator():
 # F8: one full step of train_aurora_gan (t2i_moe_gan.py:1029-1495), B=2, acc=1
 # ---------------------------------------------------------------------------
 def f8_train_step():
+    _train_capture("F8_train_step", n_batches=1, acc=1)
+
+
+def f10_train_acc2():
+    """Two batches with gradient_accumulation_steps=2: one D and one G optimizer step at batch 1, gradients
+    summed over both batches (including the G-phase loss's D gradients of batch 0, :1353-1413)."""
+    _train_capture("F10_train_acc2", n_batches=2, acc=2)
+
+
+def _train_capture(name, n_batches, acc):
     out = {}
     B = 2
-    img, txt, _ = input_batch(B)
-    batch = (torch.from_numpy(img), torch.from_numpy(txt))
+    batches = []
+    for bi in range(n_batches):
+        img, txt, _ = input_batch(B, seed_img=10 * bi, seed_txt=10 * bi + 1)
+        batches.append((torch.from_numpy(img), torch.from_numpy(txt)))
 
     inst = {}
     origG, origD = R.AuroraGenerator.__init__, R.AuroraDiscriminator.__init__
@@ -444,7 +456,7 @@ def f8_train_step():
     torch.autograd.grad = agrad
     torch.manual_seed(1234)
     try:
-        R.train_aurora_gan([batch], num_epochs=1, gradient_accumulation_steps=1, checkpoint_activation=False,
+        R.train_aurora_gan(batches, num_epochs=1, gradient_accumulation_steps=acc, checkpoint_activation=False,
                            device="cpu", save_dir="/tmp/scratch/ckpt", log_interval=1)
     finally:
         torch.randn, torch.randperm = orig_randn, orig_randperm
@@ -457,16 +469,19 @@ def f8_train_step():
     G, D = inst["G"], inst["D"]
     names = {id(p_): ("G", n) for n, p_ in G.named_parameters()}
     names.update({id(p_): ("D", n) for n, p_ in D.named_parameters()})
-    out["real"], out["text"] = img, txt
-    # module construction also calls torch.randn (weights); z is the last call (t2i_moe_gan.py:1266)
-    assert tuple(rec["randn"][-1].shape) == (B, 512)
-    out["z"] = rec["randn"][-1].numpy()
-    out["perm"] = rec["randperm"][0].numpy()
-    assert len(rec["router"]) == 6, len(rec["router"])
-    for i, c in enumerate(rec["router"]):
-        for n, v in c.items():
-            out[f"eps{i}/{n}"] = v.numpy()
-    out["r1_grad"] = rec["r1g"][0].numpy()
+    # module construction also calls torch.randn (weights); z is the one [B, 512] draw per batch (:1266)
+    zs = [t for t in rec["randn"] if tuple(t.shape) == (B, 512)][-n_batches:]
+    assert len(zs) == n_batches and len(rec["randperm"]) == n_batches
+    assert len(rec["router"]) == 6 * n_batches, len(rec["router"])
+    for bi in range(n_batches):
+        sfx = "" if n_batches == 1 else f"@{bi}"
+        out["real" + sfx], out["text" + sfx] = batches[bi][0].detach().numpy(), batches[bi][1].detach().numpy()
+        out["z" + sfx] = zs[bi].numpy()
+        out["perm" + sfx] = rec["randperm"][bi].numpy()
+        for i, c in enumerate(rec["router"][6 * bi:6 * bi + 6]):
+            for n, v in c.items():
+                out[f"eps{i}/{n}" + sfx] = v.numpy()
+        out["r1_grad" + sfx] = rec["r1g"][bi].numpy()
     order = []
     for opt, snap, after in rec["opt"]:
         which = names[id(snap[0][0])][0]
@@ -479,14 +494,36 @@ def f8_train_step():
             else:
                 pack_tensor(out, f"{which}/grad", n, g, full_max=4096)
             pack_tensor(out, f"{which}/delta", n, aft - before, full_max=4096)
-    meta = {"ref": "t2i_moe_gan.py:1029-1495", "B": B, "acc": 1, "order": order,
+    meta = {"ref": "t2i_moe_gan.py:1029-1495", "B": B, "acc": acc, "n_batches": n_batches, "order": order,
             "losses": losses, "torch": torch.__version__,
             "note": "checkpoint_activation=False (identical math; keeps router-call capture clean)"}
-    save("F8_train_step", out, meta)
+    save(name, out, meta)
+
+
+# ---------------------------------------------------------------------------
+# F9: the reference state_dict layout (keys, shapes) of AuroraGenerator / AuroraDiscriminator (drop-in
+# checkpoints: sagemaker_train.py:297-301, inference.py:34-49)
+# ---------------------------------------------------------------------------
+def f9_layout():
+    torch.manual_seed(0)
+    lay = {}
+    for tag, mod in (("G", R.AuroraGenerator()), ("D", R.AuroraDiscriminator()),
+                     ("G8", R.AuroraGenerator(num_experts=8) if "num_experts" in
+                      R.AuroraGenerator.__init__.__code__.co_varnames else None)):
+        if mod is None:
+            continue
+        sd = mod.state_dict()
+        lay[tag] = {"keys": list(sd.keys()), "shapes": [list(v.shape) for v in sd.values()],
+                    "params": [n for n, _ in mod.named_parameters()]}
+    path = os.path.join(OUT, "F9_layout.json")
+    with open(path, "w") as f:
+        json.dump({"ref": "t2i_moe_gan.py:668-907", **lay}, f)
+    print(f"wrote {path}")
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f7", "f8"]
+    which = sys.argv[1:] or ["f1", "f2", "f3", "f4", "f5", "f6", "f7", "f8", "f9", "f10"]
     for w in which:
         globals()[{"f1": "f1_modconv", "f2": "f2_mtm", "f3": "f3_router", "f4": "f4_moe", "f5": "f5_disc",
-                   "f6": "f6_losses", "f7": "f7_generator", "f8": "f8_train_step"}[w]]()
+                   "f6": "f6_losses", "f7": "f7_generator", "f8": "f8_train_step", "f9": "f9_layout",
+                   "f10": "f10_train_acc2"}[w]]()

@@ -1,0 +1,125 @@
+"""GPU parity of the drop-in module API (moe-gan_cpsc541_amd/t2i_moe_gan.py) against the reference
+fixtures (F7 generator) and the oracle (discriminator autograd), plus a train_aurora_gan run."""
+import numpy as np
+import pytest
+import torch
+
+from goldens import T, check_packed, close, load
+from oracle import aurora_cpu as O
+from oracle.recipe import fill_state
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _M():
+    import t2i_moe_gan as M
+    return M
+
+
+def _gen(M, **kw):
+    from moegan_mi.layout import generator_shapes
+    G = M.AuroraGenerator(**kw)
+    G.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(generator_shapes(4), 0).items()})
+    return G.to(DEV)
+
+
+def _disc(M):
+    from moegan_mi.layout import discriminator_shapes
+    D = M.AuroraDiscriminator()
+    D.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(discriminator_shapes(), 50).items()})
+    return D.to(DEV)
+
+
+def test_generator_module_train_vs_F7(monkeypatch):
+    M = _M()
+    d, _ = load("F7_generator")
+    G = _gen(M)
+    eps = [[T(d[f"eps{i}/{n}"]).to(DEV) for n in ("epsilon_f", "epsilon_t", "epsilon_c")] for i in range(3)]
+    monkeypatch.setattr(M, "_eps_for", lambda store, E, device: eps)
+    z = T(d["z"]).to(DEV).requires_grad_(True)
+    text = T(d["text"]).to(DEV).requires_grad_(True)
+    img16, img8, kl, probs = G(z, text, return_routing=True, return_intermediate=True, annealing_factor=3.0)
+    close(img16, d["img16"], rtol=1e-4, what="img16")
+    close(img8, d["img8"], rtol=1e-4, what="img8")
+    close(kl, d["kl"], rtol=1e-5, what="kl")
+    for i in range(3):
+        close(probs[i], d[f"probs{i}"], rtol=1e-4, what=f"probs{i}")
+    loss = (img16 * T(d["R16"]).to(DEV)).sum() + (img8 * T(d["R8"]).to(DEV)).sum() + 0.37 * kl
+    for i in range(3):
+        loss = loss + (probs[i] * T(d[f"Rp{i}"]).to(DEV)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    close(z.grad, d["gz"], rtol=5e-4, what="gz")
+    close(text.grad, d["gtext"], rtol=5e-4, what="gtext")
+    st = G._store
+    for n, (off, numel) in st.offsets.items():
+        if "nograd/" + n in d.files:
+            continue
+        check_packed(d, "grad/" + n, G.flat.grad[off:off + numel].view(st.shapes[n]).cpu(), rtol=1e-3, atol=1e-7)
+
+
+def test_generator_module_eval_vs_F7():
+    """Eval mode: mean router weights, hard top-1 (t2i_moe_gan.py:349-361)."""
+    M = _M()
+    d, _ = load("F7_generator")
+    G = _gen(M).eval()
+    with torch.no_grad():
+        img16, img8, kl = G(T(d["z"]).to(DEV), T(d["text"]).to(DEV), return_intermediate=True,
+                            annealing_factor=3.0)
+    close(img16, d["eval_img16"], rtol=1e-4, what="eval img16")
+    close(img8, d["eval_img8"], rtol=1e-4, what="eval img8")
+    assert float(kl) == 0.0
+
+
+@pytest.mark.parametrize("res", [64, 16])
+def test_discriminator_module_vs_oracle(res):
+    M = _M()
+    D = _disc(M)
+    g = torch.Generator().manual_seed(res)
+    B = 3
+    img = (torch.rand(B, 3, res, res, generator=g) * 2 - 1)
+    text = torch.randn(B, 512, generator=g)
+    PD = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in D.state_dict().items()}
+    ximg = img.clone().requires_grad_(True)
+    ref = O.discriminator(ximg, text, PD)
+    R = torch.randn(ref.shape, generator=g)
+    (ref * R).sum().backward()
+    gimg = img.to(DEV).requires_grad_(True)
+    out = D(gimg, text.to(DEV))
+    close(out, ref.detach().numpy(), rtol=1e-4, what="logits")
+    (out * R.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    close(gimg.grad, ximg.grad.numpy(), rtol=5e-4, what="d/dimg")
+    st = D._store
+    for n, (off, numel) in st.offsets.items():
+        close(D.flat.grad[off:off + numel].view(st.shapes[n]), PD[n].grad.numpy(), rtol=5e-4, atol=1e-6, what=n)
+
+
+def test_sample_and_checkpoint_roundtrip(tmp_path):
+    M = _M()
+    G = _gen(M)
+    torch.manual_seed(3)
+    a = M.sample_aurora_gan(G, torch.randn(1, 512, device=DEV), num_samples=4, device=DEV)
+    assert a.shape == (4, 3, 16, 16) and float(a.abs().max()) <= 1.0
+    path = tmp_path / "ckpt.pt"
+    torch.save({"generator": G.state_dict()}, path)
+    G2 = M.AuroraGenerator().to(DEV)
+    G2.load_state_dict(torch.load(path, weights_only=True)["generator"])
+    torch.manual_seed(3)
+    b = M.sample_aurora_gan(G2, torch.randn(1, 512, device=DEV), num_samples=4, device=DEV)
+    assert torch.equal(a, b)
+
+
+def test_train_aurora_gan_runs(tmp_path):
+    """Two epochs, accumulation 2, three batches (incomplete last window steps too), validation loop."""
+    M = _M()
+    g = torch.Generator().manual_seed(0)
+    batches = [(torch.rand(4, 3, 64, 64, generator=g) * 2 - 1, torch.randn(4, 512, generator=g)) for _ in range(3)]
+    seen = []
+    G, D = M.train_aurora_gan(batches, val_dataloader=batches[:1], num_epochs=2, gradient_accumulation_steps=2,
+                              device=DEV, save_dir=str(tmp_path), log_interval=1, dtype="fp32",
+                              metric_callback=lambda e, m: seen.append(m) or True)
+    assert len(seen) == 2 and all(np.isfinite(v) for m in seen for v in m.values())
+    assert G._store.step_count == 4 and D._store.step_count == 4
+    assert torch.isfinite(G.flat).all() and torch.isfinite(D.flat).all()

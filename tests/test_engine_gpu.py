@@ -216,8 +216,9 @@ def test_disc_r1_vs_F5():
     close(g_img[..., :3].permute(0, 3, 1, 2), d["gfake"], rtol=1e-4, what="gfake")
 
 
-def test_train_step_vs_F8():
-    d, meta = load("F8_train_step")
+def _train_replay(name, cdt="fp32"):
+    d, meta = load(name)
+    nb, acc = meta.get("n_batches", 1), meta["acc"]
     ts = TrainStep(StepConfig(E=4), DEV)
     gvals = fill_state(generator_shapes(4), 0)
     ts.gs.load_state_dict({k: torch.from_numpy(v) for k, v in gvals.items()})
@@ -225,16 +226,21 @@ def test_train_step_vs_F8():
     ts.ds.load_state_dict({k: torch.from_numpy(v) for k, v in dvals.items()})
     g_before = ts.gs.data.clone()
     d_before = ts.ds.data.clone()
-    eps = [tuple(T(d[f"eps{i}/{n}"]).to(DEV) for n in ("epsilon_f", "epsilon_t", "epsilon_c")) for i in range(6)]
-    out = ts.step(T(d["real"]).to(DEV), T(d["text"]).to(DEV), T(d["z"]).to(DEV), eps[:3], eps[3:],
-                  torch.from_numpy(d["perm"].astype(np.int32)).to(DEV), anneal=3.0, lr_g=float(d["lr/G"]),
-                  lr_d=float(d["lr/D"]), eff_kl_weight=0.001 * 1e-5)
-    torch.cuda.synchronize()
     L = meta["losses"]
-    assert abs(float(out["d_losses"][0]) - L["discriminator_loss"][0]) < 1e-4 * abs(L["discriminator_loss"][0])
-    assert abs(float(out["g_gan"][0]) - L["generator_loss"][0]) < 1e-4 * abs(L["generator_loss"][0]) + 1e-6
-    assert abs(float(out["balance"][0]) - L["moe_balance_loss"][0]) < 1e-3 * L["moe_balance_loss"][0] + 1e-7
-    close(out["r1_grad"][..., :3].permute(0, 3, 1, 2), d["r1_grad"], rtol=1e-4, what="r1_grad")
+    for bi in range(nb):
+        sfx = "" if nb == 1 else f"@{bi}"
+        eps = [tuple(T(d[f"eps{i}/{n}{sfx}"]).to(DEV) for n in ("epsilon_f", "epsilon_t", "epsilon_c"))
+               for i in range(6)]
+        out = ts.step(T(d["real" + sfx]).to(DEV), T(d["text" + sfx]).to(DEV), T(d["z" + sfx]).to(DEV), eps[:3],
+                      eps[3:], torch.from_numpy(d["perm" + sfx].astype(np.int32)).to(DEV), anneal=3.0,
+                      lr_g=float(d["lr/G"]), lr_d=float(d["lr/D"]), eff_kl_weight=0.001 * 1e-5, acc=acc,
+                      zero_grads=bi % acc == 0, step_optim=(bi + 1) % acc == 0 or bi + 1 == nb)
+        torch.cuda.synchronize()
+        dl, gl, bl = L["discriminator_loss"][bi], L["generator_loss"][bi], L["moe_balance_loss"][bi]
+        assert abs(float(out["d_losses"][0]) - dl) < 1e-4 * abs(dl), (bi, float(out["d_losses"][0]), dl)
+        assert abs(float(out["g_gan"][0]) - gl) < 1e-4 * abs(gl) + 1e-6, (bi, float(out["g_gan"][0]), gl)
+        assert abs(float(out["balance"][0]) - bl) < 1e-3 * bl + 1e-7
+        close(out["r1_grad"][..., :3].permute(0, 3, 1, 2), d["r1_grad" + sfx], rtol=1e-4, what="r1_grad")
     for which, store, before, ref_max in (("D", ts.ds, d_before, 0.7), ("G", ts.gs, g_before, 0.8)):
         n_opt = store.n_opt
         gn = float(store.grad[:n_opt].double().norm())
@@ -249,3 +255,12 @@ def test_train_step_vs_F8():
             check_packed(d, f"{which}/grad/{n}", g, rtol=2e-3, atol=1e-8)
             delta = (store.data[off:off + numel] - before[off:off + numel]).view(shape).cpu()
             check_packed(d, f"{which}/delta/{n}", delta, rtol=2e-2, atol=2e-6)
+
+
+def test_train_step_vs_F8():
+    _train_replay("F8_train_step")
+
+
+def test_train_step_acc2_vs_F10():
+    """gradient_accumulation_steps=2: D gradients of batch 0 include the G-phase loss (reference quirk)."""
+    _train_replay("F10_train_acc2")

@@ -1,4 +1,4 @@
-"""Pin the CPU oracle (oracle/aurora_cpu.py) to the reference's golden fixtures F1-F8."""
+"""Pin the CPU oracle (oracle/aurora_cpu.py) to the reference's golden fixtures F1-F10."""
 import numpy as np
 import pytest
 import torch
@@ -177,8 +177,9 @@ def test_f7_generator():
         assert np.array_equal(ep[i].argmax(1).numpy(), d[f"eval_idx{i}"])
 
 
-def test_f8_train_step():
-    d, meta = load("F8_train_step")
+def _replay_train(name):
+    d, meta = load(name)
+    nb, acc = meta.get("n_batches", 1), meta["acc"]
     PG = generator_params()
     PD = _disc_params()
     for k, v in PG.items():
@@ -189,7 +190,6 @@ def test_f8_train_step():
     optD = torch.optim.AdamW(list(PD.values()), lr=float(d["lr/D"]), betas=(0.5, 0.999), weight_decay=0.01)
     before_g = {k: v.detach().clone() for k, v in PG.items()}
     before_d = {k: v.detach().clone() for k, v in PD.items()}
-    eps = [tuple(T(d[f"eps{i}/{n}"]) for n in ("epsilon_f", "epsilon_t", "epsilon_c")) for i in range(6)]
     import sys, os
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden", "clip_double"))
     import clip
@@ -199,14 +199,20 @@ def test_f8_train_step():
         def pre(o, a, k, which=which, P=P):
             grads[which] = {n: (None if t.grad is None else t.grad.clone()) for n, t in P.items() if t.requires_grad}
         opt.register_step_pre_hook(pre)
-    logs = O.train_step(PG, PD, optG, optD, T(d["real"]), T(d["text"]), T(d["z"]), eps[:3], eps[3:],
-                        torch.from_numpy(d["perm"]), kl_weight_eff=0.001 * 1e-5, encode_image=model.encode_image)
     L = meta["losses"]
-    assert abs(logs["d_loss_gan"] - L["discriminator_loss"][0]) < 1e-4 * abs(L["discriminator_loss"][0])
-    assert abs(logs["g_loss_gan"] - L["generator_loss"][0]) < 1e-4 * abs(L["generator_loss"][0]) + 1e-6
-    assert abs(logs["balance"] - L["moe_balance_loss"][0]) < 1e-4 * abs(L["moe_balance_loss"][0]) + 1e-7
-    assert abs(logs["clip16"] - L["compute_clip_loss"][0]) < 1e-5
-    close(logs["r1_grad"], d["r1_grad"], what="r1_grad")
+    for bi in range(nb):
+        sfx = "" if nb == 1 else f"@{bi}"
+        eps = [tuple(T(d[f"eps{i}/{n}{sfx}"]) for n in ("epsilon_f", "epsilon_t", "epsilon_c")) for i in range(6)]
+        logs = O.train_step(PG, PD, optG, optD, T(d["real" + sfx]), T(d["text" + sfx]), T(d["z" + sfx]), eps[:3],
+                            eps[3:], torch.from_numpy(d["perm" + sfx]), kl_weight_eff=0.001 * 1e-5,
+                            encode_image=model.encode_image, acc=acc, zero_grads=bi % acc == 0,
+                            step_optim=(bi + 1) % acc == 0 or bi + 1 == nb)
+        assert abs(logs["d_loss_gan"] - L["discriminator_loss"][bi]) < 1e-4 * abs(L["discriminator_loss"][bi])
+        assert abs(logs["g_loss_gan"] - L["generator_loss"][bi]) < 1e-4 * abs(L["generator_loss"][bi]) + 1e-6
+        assert abs(logs["balance"] - L["moe_balance_loss"][bi]) < 1e-4 * abs(L["moe_balance_loss"][bi]) + 1e-7
+        assert abs(logs["clip16"] - L["compute_clip_loss"][2 * bi]) < 1e-5
+        close(logs["r1_grad"], d["r1_grad" + sfx], what="r1_grad")
+    assert meta["order"] == ["D", "G"]
     for which, P, before in (("D", PD, before_d), ("G", PG, before_g)):
         for n, t in P.items():
             if not t.requires_grad:
@@ -218,3 +224,12 @@ def test_f8_train_step():
             check_packed(d, f"{which}/grad/{n}", grads[which][n], rtol=5e-4, atol=1e-8)
             # AdamW step 1 moves each element by ~lr*sign(g): compare deltas loosely (sign flips at g~0)
             check_packed(d, f"{which}/delta/{n}", t.detach() - before[n], rtol=2e-2, atol=2e-6)
+
+
+def test_f8_train_step():
+    _replay_train("F8_train_step")
+
+
+def test_f10_train_acc2():
+    """gradient_accumulation_steps=2 over two batches: summed /acc gradients, one optimizer step each."""
+    _replay_train("F10_train_acc2")
