@@ -70,10 +70,15 @@ typedef struct mg_epilogue {
   const float* addvec; /* v += addvec[(m >> add_shift) * add_ld + n] (per-image broadcast add) */
   int32_t add_shift;
   int64_t add_ld;
+  void* out_pre;       /* optional second output: the value before the activation (same dtype as C) */
+  int64_t ld_pre;
 } mg_epilogue;
 
 const char* mg_last_error(void);
 int mg_version(void);
+/* Tuning override for measurements (key: 0 conv-wgrad tile, 1 grouped-wgrad tile, 2 conv tile,
+   3 gemm tile [64 | 128], 4 conv-wgrad splits, 5 disable split-K slabs; value 0 = automatic). */
+int mg_set_tuning(int key, int value);
 
 /* Generic MFMA GEMM: C[M,N] = epilogue(op(A)[M,K] @ op(B)[K,N]).
  *   a_kc = 1 : A[m*lda + k]     a_kc = 0 : A[k*lda + m]
@@ -176,6 +181,14 @@ int mg_segsum(int dtype, const void* X, int64_t ld, int B, int HW, int C, float*
 
 /* ModulatedConv backward, output side: gyt = gy*d (gy = gz * lrelu'), gdd = -0.5 d^2 sum_pix gy*y; z may carry a fused residual (zsub). t2i_moe_gan.py:154-186. */
 int mg_modconv_bwd_out(int dtype, int gz_dtype, const void* gz, int64_t ld_gz, const void* z, int64_t ld_z, const void* zsub, int64_t ld_zsub, const float* d, int B, int HW, int Cout, int act, void* gyt, int64_t ld_gyt, float* gdd, void* stream);
+
+/* Row gather: out[r, :C] = src[idx[r] / idx_div, :C] * (rowscale ? rowscale[r] : 1)  (MoE dispatch
+   order, t2i_moe_gan.py:430-445: tokens routed to expert e, k copies per token).  C % 8 == 0. */
+int mg_gather_rows(int dtype, const void* src, int64_t lds, const int32_t* idx, int idx_div, const float* rowscale, int n, int C, void* out, int64_t ldo, void* stream);
+
+/* Modulated-conv input xs[b,p,c] = x[b,p,c] * s[b,c] (x rows [B*HW, ldx], C % 8 == 0); replaces the
+   per-tap operand scaling of the fused modulated conv (t2i_moe_gan.py:167-171, x * style). */
+int mg_scale_bc(int dtype, const void* x, int64_t ldx, const float* s, int B, int HW, int C, void* out, int64_t ldo, void* stream);
 
 /* ModulatedConv backward, input side: gx (+)= gxt*s, gs[b,ci] += sum_pix gxt*x. */
 int mg_modconv_bwd_in(int gxt_dtype, const void* gxt, int64_t ld_gxt, int dtype, const void* x, int64_t ld_x, const float* s, int B, int HW, int Cin, int gx_dtype, void* gx, int64_t ld_gx, int accumulate, float* gs, void* stream);

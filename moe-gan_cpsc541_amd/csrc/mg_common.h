@@ -15,12 +15,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 #define MG_DEV __device__ __forceinline__
 
 MG_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
-MG_DEV bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);  // keep NaN a NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+MG_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }  // v_cvt_pk_bf16_f32 (RNE)
 
 // Element load/store as float regardless of storage type.
 MG_DEV float ldf(const float* p, int64_t i) { return p[i]; }
@@ -31,6 +26,29 @@ MG_DEV void stf(bf16_t* p, int64_t i, float v) { p[i] = f2bf(v); }
 template <typename T> struct VecOf;  // 16-byte vectors
 template <> struct VecOf<float> { static constexpr int N = 4; typedef f32x4_t type; };
 template <> struct VecOf<bf16_t> { static constexpr int N = 8; typedef u16x8_t type; };
+
+// 8 consecutive elements <-> float[8] (16-B aligned bf16, or 2 x 16-B fp32)
+MG_DEV void ld8(const float* p, float* t) {
+  f32x4_t a = *reinterpret_cast<const f32x4_t*>(p), b = *reinterpret_cast<const f32x4_t*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { t[j] = a[j]; t[j + 4] = b[j]; }
+}
+MG_DEV void ld8(const bf16_t* p, float* t) {
+  u16x8_t a = *reinterpret_cast<const u16x8_t*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = bf2f(a[j]);
+}
+MG_DEV void st8(float* p, const float* v) {
+  *reinterpret_cast<f32x4_t*>(p) = f32x4_t{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4_t*>(p + 4) = f32x4_t{v[4], v[5], v[6], v[7]};
+}
+MG_DEV void st8(bf16_t* p, const float* v) {
+  u16x8_t r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(v[j]);
+  *reinterpret_cast<u16x8_t*>(p) = r;
+}
+inline bool mg_al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 MG_DEV float lrelu(float x) { return x > 0.f ? x : 0.2f * x; }
 MG_DEV float lrelu_grad(float y) { return y > 0.f ? 1.f : 0.2f; }
@@ -55,6 +73,12 @@ MG_DEV float wave_max(float v) {
 // ---- error plumbing (C-ABI returns 0 / negative, message via mg_last_error) ----
 void mg_set_error(const std::string& msg);
 int mg_check_launch(const char* what);
+// Tuning overrides (0 = automatic), set through mg_set_tuning for A/B measurements.
+enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, MG_TUNE_GEMM_TILE = 3,
+       MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_COUNT = 16 };
+extern int g_mg_tune[MG_TUNE_COUNT];
+// Library-owned device scratch (grown on demand, never shrunk; stream-ordered reuse on one stream).
+void* mg_workspace(size_t bytes);
 
 #define MG_REQUIRE(cond, msg)                       \
   do {                                              \

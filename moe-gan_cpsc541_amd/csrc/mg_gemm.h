@@ -97,16 +97,20 @@ struct LdKCConv {
   const T* x; int H, W, Cin, lgCin, lgOW, lgOHW, M;
   int KW, stride, pad, K;
   const float* scale;  // optional [B, Cin] per-sample input-channel scale (modulation)
-  struct RowState { int b, oh, ow; };
+  int kwinv;           // (tap * kwinv) >> 16 == tap / KW for every tap of the kernel
+  struct RowState { const T* base; int ih0, iw0, b; };
   struct ColState {};
   MG_DEV void set_group(int) {}
   MG_DEV RowState row(int r) const {
     RowState st;
-    if (r >= M) { st.b = -1; st.oh = st.ow = 0; return st; }
+    if (r >= M) { st.b = -1; st.base = x; st.ih0 = st.iw0 = 0; return st; }
     st.b = r >> lgOHW;
     int rem = r & ((1 << lgOHW) - 1);
-    st.oh = rem >> lgOW;
-    st.ow = rem & ((1 << lgOW) - 1);
+    int oh = rem >> lgOW, ow = rem & ((1 << lgOW) - 1);
+    st.ih0 = oh * stride - pad;
+    st.iw0 = ow * stride - pad;
+    // pointer of tap (0, 0), channel 0 (may point outside the image; only dereferenced in bounds)
+    st.base = x + ((((int64_t)st.b * H + st.ih0) * W + st.iw0) << lgCin);
     return st;
   }
   MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
@@ -114,10 +118,9 @@ struct LdKCConv {
     if (st.b < 0 || k >= K) return vzero<T>();
     int tap = k >> lgCin;
     int ci = k & (Cin - 1);
-    int kh = tap / KW, kw = tap - (tap / KW) * KW;
-    int ih = st.oh * stride - pad + kh, iw = st.ow * stride - pad + kw;
-    if (ih < 0 || ih >= H || iw < 0 || iw >= W) return vzero<T>();
-    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(x + (((int64_t)st.b * H + ih) * W + iw) * Cin + ci);
+    int kh = (tap * kwinv) >> 16, kw = tap - kh * KW;
+    if ((unsigned)(st.ih0 + kh) >= (unsigned)H || (unsigned)(st.iw0 + kw) >= (unsigned)W) return vzero<T>();
+    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(st.base + (((int64_t)(kh * W + kw)) << lgCin) + ci);
     if (scale) v = vscale(v, scale + (int64_t)st.b * Cin + ci);
     return v;
   }
@@ -257,18 +260,94 @@ struct Epi {
   int remap_lgcin, remap_taps;  // weight-grad layout remap when remap_taps > 0
   const float* addvec; int add_shift; int64_t add_ld;  // v += addvec[(m >> add_shift)*add_ld + n]
   int rm_mode, rm_Mc, rm_lgOW, rm_lgOHW;  // rm_mode 1: stride-2 transposed-conv class rows -> NHWC rows
+  TO* Cpre; int64_t ldc_pre;  // optional: store the pre-activation value too (row m, column n)
+  int64_t zstride;  // split-K partial slabs: output offset blockIdx.z * zstride (raw partial epilogue)
+  int vec_ok;       // host-checked: 8-column vector path legal (alignment / pitches, no remap, no atomics)
   int g;
   MG_DEV void set_group(int gg) { g = gg; }
-  MG_DEV void operator()(int m, int n, float v) const {
-    if (rm_mode == 1) {  // class-major (py,px,b,i,j) -> NHWC row (b, 2i+py, 2j+px); all row lookups use it
-      int cls = m / rm_Mc, rem = m - cls * rm_Mc;
-      int b = rem >> rm_lgOHW, i = (rem >> rm_lgOW) & ((1 << (rm_lgOHW - rm_lgOW)) - 1), j = rem & ((1 << rm_lgOW) - 1);
-      int OW2 = 2 << rm_lgOW, OH2 = 2 << (rm_lgOHW - rm_lgOW);
-      m = (b * OH2 + 2 * i + (cls >> 1)) * OW2 + 2 * j + (cls & 1);
+  MG_DEV int remap_row(int m) const {  // class-major (py,px,b,i,j) -> NHWC row (b, 2i+py, 2j+px)
+    int cls = m / rm_Mc, rem = m - cls * rm_Mc;
+    int b = rem >> rm_lgOHW, i = (rem >> rm_lgOW) & ((1 << (rm_lgOHW - rm_lgOW)) - 1), j = rem & ((1 << rm_lgOW) - 1);
+    int OW2 = 2 << rm_lgOW, OH2 = 2 << (rm_lgOHW - rm_lgOW);
+    return (b * OH2 + 2 * i + (cls >> 1)) * OW2 + 2 * j + (cls & 1);
+  }
+  // host side: decide whether the 8-column vector epilogue may be used
+  bool host_vec_ok() const {
+    auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    if (atomic || remap_taps > 0) return false;
+    if (!al(C) || ldc % 8 || gstride_c % 8 || zstride % 8) return false;
+    if (bias && (!al(bias) || gstride_bias % 4)) return false;
+    if (scale && (!al(scale) || scale_ld % 4)) return false;
+    if (aux && (act == ACT_MUL_GELU_GRAD || act == ACT_MUL_LRELU_GRAD) && (!al(aux) || ld_aux % 8)) return false;
+    if (resid && (!al(resid) || ld_res % 8)) return false;
+    if (Cpre && (!al(Cpre) || ldc_pre % 8)) return false;
+    if (addvec && (!al(addvec) || add_ld % 4)) return false;
+    return true;
+  }
+  // 8 consecutive columns n..n+7 (all < N), only when vec_ok
+  MG_DEV void vec8(int m, int n, float* v) const {
+    if (rm_mode == 1) m = remap_row(m);
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= alpha;
+    if (scale) {
+      ld8(scale + (int64_t)(m >> scale_shift) * scale_ld + n, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= t[j];
     }
+    if (bias) {
+      ld8(bias + (int64_t)g * gstride_bias + n, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += t[j];
+    }
+    if (Cpre) st8(Cpre + (int64_t)m * ldc_pre + n, v);
+    if (act == ACT_LRELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = lrelu(v[j]);
+    } else if (act == ACT_GELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+    } else if (act == ACT_MUL_GELU_GRAD) {
+      ld8(aux + (int64_t)m * ld_aux + n, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= gelu_erf_grad(t[j]);
+    } else if (act == ACT_MUL_LRELU_GRAD) {
+      ld8(aux + (int64_t)m * ld_aux + n, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= lrelu_grad(t[j]);
+    } else if (act == ACT_RSQRT_EPS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = rsqrtf(v[j] + 1e-8f);
+    }
+    if (rowscale) {
+      float r = rowscale[m];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= r;
+    }
+    if (addvec) {
+      ld8(addvec + (int64_t)(m >> add_shift) * add_ld + n, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += t[j];
+    }
+    if (resid) {
+      ld8(resid + (int64_t)m * ld_res + n, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += t[j];
+    }
+    TO* c = C + (int64_t)g * gstride_c + (int64_t)m * ldc + n + (int64_t)blockIdx.z * zstride;
+    if (accumulate) {
+      ld8(c, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += t[j];
+    }
+    st8(c, v);
+  }
+  MG_DEV void operator()(int m, int n, float v) const {
+    if (rm_mode == 1) m = remap_row(m);  // all row lookups use the NHWC row
     v *= alpha;
     if (scale) v *= scale[(int64_t)(m >> scale_shift) * scale_ld + n];
     if (bias) v += bias[(int64_t)g * gstride_bias + n];
+    if (Cpre) stf(Cpre, (int64_t)m * ldc_pre + n, v);
     if (act == ACT_LRELU) v = lrelu(v);
     else if (act == ACT_GELU) v = gelu_erf(v);
     else if (act == ACT_MUL_GELU_GRAD) v *= gelu_erf_grad(ldf(aux, (int64_t)m * ld_aux + n));
@@ -279,7 +358,7 @@ struct Epi {
     if (resid) v += ldf(resid, (int64_t)m * ld_res + n);
     int64_t nn = n;
     if (remap_taps > 0) nn = (int64_t)(n & ((1 << remap_lgcin) - 1)) * remap_taps + (n >> remap_lgcin);
-    int64_t idx = (int64_t)g * gstride_c + (int64_t)m * ldc + nn;
+    int64_t idx = (int64_t)g * gstride_c + (int64_t)m * ldc + nn + (int64_t)blockIdx.z * zstride;
     if (atomic) {
       atomicAdd(reinterpret_cast<float*>(C) + idx, v);
     } else {
@@ -308,10 +387,15 @@ struct Grouping {
 // dwords and columns are XOR-swizzled by 16 elements on odd k-octets, so both halves of a wave's
 // transposed read (k-rows 8g..8g+3 for lane groups g = 0, 1) hit 8 distinct bank octets.
 template <typename T> struct Tile;
-template <> struct Tile<bf16_t> { static constexpr int BK = 64, PADK = 8, PADM = 32; };
+template <> struct Tile<bf16_t> { static constexpr int BK = 64, PADK = 0, PADM = 32; };
 template <> struct Tile<float> { static constexpr int BK = 32, PADK = 4, PADM = 16; };
 
 template <typename T> MG_DEV constexpr int mc_swz(int k) { return sizeof(T) == 2 ? ((k >> 3) & 1) << 4 : 0; }
+// KC image element offset of (row r, k) for bf16: 16-B chunk (k / 8) stored at chunk (k / 8) ^ (r & 7)
+// of an unpadded 128-B row -- conflict-free ds_read_b128 fragment reads and ds_write_b128 stores.
+template <typename T> MG_DEV constexpr int kc_off(int r, int k, int ldk) {
+  return sizeof(T) == 2 ? r * ldk + ((((k >> 3) ^ (r & 7))) << 3) + (k & 7) : r * ldk + k;
+}
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
@@ -350,7 +434,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   __shared__ __attribute__((aligned(16))) T smem[A_ELEMS + B_ELEMS];
   T* As = smem;
   T* Bs = smem + A_ELEMS;
-  static_assert(4 * 16 * (WN + 1) * 4 <= (int)sizeof(T) * (A_ELEMS + B_ELEMS), "epilogue staging does not fit");
+  static_assert(4 * 16 * (WN + 4) * 4 <= (int)sizeof(T) * (A_ELEMS + B_ELEMS), "epilogue staging does not fit");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -440,12 +524,12 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   auto sstore = [&]() {
 #pragma unroll
     for (int i = 0; i < A_VPT; ++i) {
-      if constexpr (A_KC) *reinterpret_cast<vec_t*>(&As[a_r[i] * LDK + a_k[i]]) = ra[i];
+      if constexpr (A_KC) *reinterpret_cast<vec_t*>(&As[kc_off<T>(a_r[i], a_k[i], LDK)]) = ra[i];
       else *reinterpret_cast<vec_t*>(&As[a_k[i] * LDA + (a_r[i] ^ mc_swz<T>(a_k[i]))]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_VPT; ++i) {
-      if constexpr (B_KC) *reinterpret_cast<vec_t*>(&Bs[b_r[i] * LDK + b_k[i]]) = rb[i];
+      if constexpr (B_KC) *reinterpret_cast<vec_t*>(&Bs[kc_off<T>(b_r[i], b_k[i], LDK)]) = rb[i];
       else *reinterpret_cast<vec_t*>(&Bs[b_k[i] * LDB + (b_r[i] ^ mc_swz<T>(b_k[i]))]) = rb[i];
     }
   };
@@ -470,14 +554,14 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           if constexpr (A_KC)
-            af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&As[(wm * WM + i * 16 + fr) * LDK + kk * 32 + fq * 8]));
+            af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&As[kc_off<T>(wm * WM + i * 16 + fr, kk * 32 + fq * 8, LDK)]));
           else
             af[i] = mc_frag_bf16(As, LDA, kk * 32, wm * WM + i * 16, lane);
         }
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           if constexpr (B_KC)
-            bfv[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&Bs[(wn * WN + j * 16 + fr) * LDK + kk * 32 + fq * 8]));
+            bfv[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&Bs[kc_off<T>(wn * WN + j * 16 + fr, kk * 32 + fq * 8, LDK)]));
           else
             bfv[j] = mc_frag_bf16(Bs, LDB, kk * 32, wn * WN + j * 16, lane);
         }
@@ -507,21 +591,42 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   // ---- epilogue: stage one 16-row band of each wave's accumulators through LDS, then a plain
   // (non-unrolled) loop applies the fused epilogue with consecutive lanes on consecutive columns.
   // Static indexing keeps acc in registers; the loop keeps the inlined epilogue code small.
-  float* cs = reinterpret_cast<float*>(smem) + wid * 16 * (WN + 1);
+  constexpr int CSP = WN + 4;  // staging pitch in floats (16-B aligned rows)
+  float* cs = reinterpret_cast<float*>(smem) + wid * 16 * CSP;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cs[(fq * 4 + r) * (WN + 1) + j * 16 + fr] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) cs[(fq * 4 + r) * CSP + j * 16 + fr] = acc[i][j][r];
     __syncthreads();
     const int mb = m0 + wm * WM + i * 16, nb = n0 + wn * WN;
+    if (ep.vec_ok) {
+      // 8 consecutive columns per lane: vector loads of the epilogue operands, one 16-B store (bf16)
 #pragma unroll 1
-    for (int e = lane; e < 16 * WN; e += 64) {
-      int rr = e / WN, cc = e - (e / WN) * WN;
-      int m = mb + rr, n = nb + cc;
-      if (m < Mloc && n < N) ep(mrow_base + m, n, cs[rr * (WN + 1) + cc]);
+      for (int e = lane; e < 2 * WN; e += 64) {
+        int rr = e / (WN / 8), cc = (e - (e / (WN / 8)) * (WN / 8)) * 8;
+        int m = mb + rr, n = nb + cc;
+        if (m >= Mloc) continue;
+        const float* src = cs + rr * CSP + cc;
+        if (n + 8 <= N) {
+          float v[8];
+          f32x4_t a = *reinterpret_cast<const f32x4_t*>(src), b = *reinterpret_cast<const f32x4_t*>(src + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+          ep.vec8(mrow_base + m, n, v);
+        } else {
+          for (int j = 0; j < 8 && n + j < N; ++j) ep(mrow_base + m, n + j, src[j]);
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int e = lane; e < 16 * WN; e += 64) {
+        int rr = e / WN, cc = e - (e / WN) * WN;
+        int m = mb + rr, n = nb + cc;
+        if (m < Mloc && n < N) ep(mrow_base + m, n, cs[rr * CSP + cc]);
+      }
     }
   }
 }
@@ -538,8 +643,23 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   int gx = grp.mode == 1 ? max_tiles_m : grp.mode == 3 ? cdiv(grp.rows_per_group, BM) * grp.ngroups : cdiv(M, BM);
   int gz = grp.mode == 2 ? splits * grp.ngroups : splits;
   dim3 grid(gx, cdiv(N, BN), gz);
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP>), grid, dim3(NTHREADS), 0, st, A, B, ep, M, N,
+  EP e2 = ep;
+  e2.vec_ok = e2.host_vec_ok() ? 1 : 0;
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
                      K, kchunk, grp);
+}
+
+// split-K slab reduction: C = epilogue(sum_s ws[s]) for a [M, N] tile set (ws row pitch N).
+template <class EP>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                            EP ep) {
+  const int64_t MN = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += ws[s * MN + i];
+    int m = (int)(i / N), n = (int)(i - (int64_t)(i / N) * N);
+    ep(m, n, v);
+  }
 }
 
 }  // namespace mg

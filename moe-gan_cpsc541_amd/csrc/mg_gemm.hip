@@ -1,5 +1,7 @@
 // GEMM / implicit-conv entry points of libmoegan_hip.
+#include <algorithm>
 #include <string>
+#include <type_traits>
 
 #include "mg_gemm.h"
 
@@ -35,6 +37,10 @@ Epi<TO> make_epi(void* C, int64_t ldc, const mg_epilogue* e) {
   ep.rm_mode = 0;
   ep.rm_Mc = 1;
   ep.rm_lgOW = ep.rm_lgOHW = 0;
+  ep.Cpre = e ? reinterpret_cast<TO*>(e->out_pre) : nullptr;
+  ep.ldc_pre = e ? e->ld_pre : 0;
+  ep.zstride = 0;
+  ep.vec_ok = 0;
   ep.g = 0;
   return ep;
 }
@@ -46,6 +52,7 @@ inline int ilog2(int v) {
   return l;
 }
 inline bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+inline int kwinv(int KW) { return 65536 / KW + 1; }  // exact tap / KW for tap < 64
 
 constexpr Grouping kNoGroup{0, 1, nullptr, nullptr, 0};
 
@@ -90,10 +97,61 @@ void run_plain_orient(int a_kc, int b_kc, int M, int N, int K, const void* A, in
 template <typename T, typename TO>
 void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
                      int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, int splits, hipStream_t st) {
-  if ((int64_t)cdiv(M, 128) * cdiv(N, 128) * splits >= 160)
+  const int tile = g_mg_tune[MG_TUNE_GEMM_TILE];
+  if (tile == 128 || (tile == 0 && (int64_t)cdiv(M, 128) * cdiv(N, 128) * splits >= 480))
     run_plain_orient<T, TO, 128, 128>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
   else
     run_plain_orient<T, TO, 64, 64>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+}
+
+// Few-tile GEMMs (styles, mapping, router/attention projections at small M) are latency-bound: a
+// 64x64 grid of ~32 blocks walks K serially.  Split K over ~256 blocks into fp32 slabs and apply
+// the real epilogue in a reduction pass.  Returns false when the shape does not qualify.
+template <typename T, typename TO>
+bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
+                      int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, hipStream_t st) {
+  constexpr int TBK = Tile<T>::BK;
+  int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
+  if (tiles >= 96 || K < 4 * TBK) return false;
+  int splits = (int)std::min<int64_t>(256 / tiles, K / (2 * TBK));
+  if (splits < 2) return false;
+  int kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
+  splits = (K + kchunk - 1) / kchunk;
+  const int64_t MN = (int64_t)M * N;
+  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float)));
+  if (!ws) return false;
+  mg_epilogue raw{};
+  raw.alpha = 1.f;
+  Epi<float> slab = make_epi<float>(ws, N, &raw);
+  slab.zstride = MN;
+  slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
+  const int32_t* aidx = e ? e->a_idx : nullptr;
+  int adiv = (e && e->a_idx_div > 0) ? e->a_idx_div : 1;
+  const float* ars = e ? e->a_rowscale : nullptr;
+  int agelu = e ? e->a_gelu : 0;
+  auto go = [&](auto la, auto lb, auto akc, auto bkc) {
+    dim3 grid(cdiv(M, 64), cdiv(N, 64), splits);
+    hipLaunchKernelGGL((gemm_kernel<T, 64, 64, decltype(akc)::value, decltype(bkc)::value, decltype(la),
+                                    decltype(lb), Epi<float>>),
+                       grid, dim3(NTHREADS), 0, st, la, lb, slab, M, N, K, kchunk, kNoGroup);
+  };
+  const T* Ap = reinterpret_cast<const T*>(A);
+  const T* Bp = reinterpret_cast<const T*>(B);
+  using TT = std::true_type;
+  using FF = std::false_type;
+  if (a_kc) {
+    LdKC<T> la{Ap, lda, M, K, aidx, adiv, ars, agelu};
+    if (b_kc) go(la, LdKC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, TT{}, TT{});
+    else go(la, LdMC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0, 0}, TT{}, FF{});
+  } else {
+    LdMC<T> la{Ap, lda, M, K, aidx, adiv, ars, agelu, 0};
+    if (b_kc) go(la, LdKC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, FF{}, TT{});
+    else go(la, LdMC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0, 0}, FF{}, FF{});
+  }
+  auto ep = make_epi<TO>(C, ldc, e);
+  int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
+  hipLaunchKernelGGL((splitk_reduce_kernel<Epi<TO>>), dim3(blocks), dim3(256), 0, st, ws, splits, M, N, ep);
+  return true;
 }
 
 }  // namespace
@@ -122,6 +180,16 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
   MG_REQUIRE(!(ep && ep->atomic) || c_dtype == MG_F32, "atomic epilogue requires fp32 C");
   if (K == 0) splits = 1;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (splits == 1 && !(ep && ep->atomic) && !g_mg_tune[MG_TUNE_NO_SLABS]) {
+    bool done;
+    if (dtype == MG_F32)
+      done = c_dtype == MG_F32 ? run_splitk_slabs<float, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st)
+                               : run_splitk_slabs<float, bf16_t>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st);
+    else
+      done = c_dtype == MG_F32 ? run_splitk_slabs<bf16_t, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st)
+                               : run_splitk_slabs<bf16_t, bf16_t>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st);
+    if (done) return mg_check_launch("mg_gemm (split-K slabs)");
+  }
   if (dtype == MG_F32) {
     if (c_dtype == MG_F32) run_plain_tiles<float, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
     else run_plain_tiles<float, bf16_t>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
@@ -142,18 +210,54 @@ void run_conv(const void* x, int B, int H, int W, int Cin, const void* wpack, in
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int M = B * OH * OW, K = KH * KW * Cin;
   LdKCConv<T> la{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), M,
-                 KW, stride, pad, K, sc};
+                 KW, stride, pad, K, sc, kwinv(KW)};
   LdKC<T> lb{reinterpret_cast<const T*>(wpack), K, Cout, K, nullptr, 1, nullptr, 0};
   auto ep = make_epi<TO>(y, ldy, e);
   launch_gemm<T, BM, BN, true, true>(la, lb, ep, M, Cout, K, 1, kNoGroup, 0, st);
 }
+// Implicit conv with few output tiles (offset heads: Cout = 32 at 4x4 / 8x8) walks K = 9*Cin serially in
+// ~100 blocks; split K into fp32 slabs over ~512 blocks and apply the epilogue in the reduction.
+template <typename T, typename TO>
+bool conv_slabs(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW, int stride,
+                int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
+  constexpr int TBK = Tile<T>::BK;
+  int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  int M = B * OH * OW, K = KH * KW * Cin;
+  int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(Cout, 64);
+  if (tiles >= 256 || K < 8 * TBK || (e && e->atomic) || g_mg_tune[MG_TUNE_NO_SLABS]) return false;
+  int splits = (int)std::min<int64_t>(cdiv(512, tiles), K / (4 * TBK));
+  if (splits < 2) return false;
+  int kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
+  splits = (K + kchunk - 1) / kchunk;
+  const int64_t MN = (int64_t)M * Cout;
+  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float)));
+  if (!ws) return false;
+  mg_epilogue raw{};
+  raw.alpha = 1.f;
+  Epi<float> slab = make_epi<float>(ws, Cout, &raw);
+  slab.zstride = MN;
+  slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
+  LdKCConv<T> la{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), M,
+                 KW, stride, pad, K, sc, kwinv(KW)};
+  LdKC<T> lb{reinterpret_cast<const T*>(wpack), K, Cout, K, nullptr, 1, nullptr, 0};
+  dim3 grid(cdiv(M, 64), cdiv(Cout, 64), splits);
+  hipLaunchKernelGGL((gemm_kernel<T, 64, 64, true, true, LdKCConv<T>, LdKC<T>, Epi<float>>), grid, dim3(NTHREADS), 0,
+                     st, la, lb, slab, M, Cout, K, kchunk, kNoGroup);
+  auto ep = make_epi<TO>(y, ldy, e);
+  int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
+  hipLaunchKernelGGL((splitk_reduce_kernel<Epi<TO>>), dim3(blocks), dim3(256), 0, st, ws, splits, M, Cout, ep);
+  return true;
+}
+
 template <typename T, typename TO>
 void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW,
                     int stride, int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e,
                     hipStream_t st) {
+  if (conv_slabs<T, TO>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st)) return;
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int64_t M = (int64_t)B * OH * OW;
-  if (cdiv(M, 128) * (int64_t)cdiv(Cout, 128) >= 160 && Cout > 64)
+  const int tile = g_mg_tune[MG_TUNE_CONV_TILE];
+  if (tile == 128 || (tile == 0 && cdiv(M, 128) * (int64_t)cdiv(Cout, 128) >= 480 && Cout > 64))
     run_conv<T, TO, 128, 128>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
   else
     run_conv<T, TO, 64, 64>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
@@ -211,13 +315,22 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
   MG_REQUIRE(Cout % vec == 0 && ldg % vec == 0, "Cout / ldg must be multiples of the vector width");
   MG_REQUIRE(aligned16(gy) && aligned16(x), "gy/x must be 16-byte aligned");
   if (B == 0) return MG_OK;
-  if (splits < 1) {  // auto: enough blocks to cover the chip
-    int64_t tiles = (int64_t)cdiv(Cout, 64) * cdiv(KH * KW * Cin, 64);
-    int64_t P = (int64_t)B * OH * OW;
-    splits = (int)std::max<int64_t>(1, std::min<int64_t>(512 / std::max<int64_t>(tiles, 1), P / 256));
+  const int64_t P = (int64_t)B * OH * OW;
+  const int N = KH * KW * Cin;
+  // 128^2 tiles (half the operand traffic per flop) when both output dims fill them; split K so the grid
+  // covers the chip about twice (occupancy-2 kernels) without cutting a split below 1024 pixels
+  const int tile = g_mg_tune[MG_TUNE_WGRAD_TILE];
+  const bool big = dtype == MG_BF16 && Cout >= 128 && N >= 128 && tile == 128;
+  const int64_t tiles = big ? (int64_t)cdiv(Cout, 128) * cdiv(N, 128) : (int64_t)cdiv(Cout, 64) * cdiv(N, 64);
+  if (splits < 1 && g_mg_tune[MG_TUNE_WGRAD_SPLITS] > 0) splits = g_mg_tune[MG_TUNE_WGRAD_SPLITS];
+  if (splits < 1) {  // measured sweet spot: ~576 blocks, >= 2048 pixels per split
+    const int64_t want = big ? 288 : 576;
+    int64_t t = std::max<int64_t>(tiles, 1);
+    splits = (int)std::max<int64_t>(1, std::min<int64_t>((want + t / 2) / t, P / 2048));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == MG_F32) run_wgrad<float, 64, 64>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
+  else if (big) run_wgrad<bf16_t, 128, 128>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
   else run_wgrad<bf16_t, 64, 64>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
   return mg_check_launch("mg_conv2d_wgrad");
 }
@@ -260,7 +373,10 @@ void run_grouped_wgrad(int M, int N, int ngroups, const int32_t* row_off, int to
   auto ep = make_epi<float>(C, N, &ee);
   ep.gstride_c = (int64_t)M * N;
   Grouping grp{2, ngroups, row_off, nullptr, 0};
-  launch_gemm<T, 64, 64, false, false>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
+  if (sizeof(T) == 2 && M >= 128 && N >= 128 && g_mg_tune[MG_TUNE_GWGRAD_TILE] != 64)
+    launch_gemm<T, 128, 128, false, false>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
+  else
+    launch_gemm<T, 64, 64, false, false>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
 }
 }  // namespace
 
@@ -297,7 +413,12 @@ extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const
   const int vec = dtype == MG_F32 ? 4 : 8;
   MG_REQUIRE(M % vec == 0 && N % vec == 0 && lda % vec == 0 && ldb % vec == 0, "M/N/lda/ldb must be vector multiples");
   MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
-  if (splits < 1) splits = std::max(1, std::min(64, 512 / std::max(1, cdiv(M, 64) * cdiv(N, 64) * ngroups)));
+  if (splits < 1) {
+    const bool big = dtype == MG_BF16 && M >= 128 && N >= 128 && g_mg_tune[MG_TUNE_GWGRAD_TILE] != 64;
+    int tiles = big ? cdiv(M, 128) * cdiv(N, 128) * ngroups : cdiv(M, 64) * cdiv(N, 64) * ngroups;
+    int rows_per_group = std::max(1, total_rows / std::max(1, ngroups));
+    splits = std::max(1, std::min({64, cdiv(big ? 512 : 1024, std::max(1, tiles)), std::max(1, rows_per_group / 1024)}));
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == MG_F32) run_grouped_wgrad<float>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st);
   else run_grouped_wgrad<bf16_t>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st);

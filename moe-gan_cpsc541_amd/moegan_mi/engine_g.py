@@ -96,13 +96,14 @@ class GeneratorEngine:
         d = ops.gemm(s2, pk["wsq"], B, rows, Cin, ep=E_(act=RSQRT))  # demod coefficients [B, rows] (:165)
         ep = E_(scale=d, scale_shift=ops.ilog2(HW), scale_ld=rows, act=act, resid=resid,
                 ld_res=resid.shape[-1] if resid is not None else 0)
-        y = ops.conv2d(x, pk["w"], rows, k, k, 1, k // 2, in_scale=s, ep=ep, out_dtype=self.cdt)
-        sv = (x, w, s, s2, d, y, resid, act) if save else None
+        xs = ops.scale_bc(x, s)  # x * style, shared by the conv and its weight gradient
+        y = ops.conv2d(xs, pk["w"], rows, k, k, 1, k // 2, ep=ep, out_dtype=self.cdt)
+        sv = (x, xs, w, s, s2, d, y, resid, act) if save else None
         return y, sv
 
     def mc_bwd(self, pre, sv, gz, gx, gw, accumulate=0):
         """gz: grad of the conv output (post activation / residual). Writes/accumulates gx, accumulates gw."""
-        x, w, s, s2, d, z, zsub, act = sv
+        x, xs, w, s, s2, d, z, zsub, act = sv
         B, H, W, Cin = x.shape
         HW = H * W
         pk = self.packs[pre]
@@ -124,10 +125,10 @@ class GeneratorEngine:
                            None if gx is None else gx.view(P, -1), gs, accumulate)
         # weight gradient (fp32, reference layout)
         if rows == Cout:
-            ops.conv2d_wgrad(gyt, x, Cout, k, k, 1, k // 2, self.G(pre + "weight"), in_scale=s)
+            ops.conv2d_wgrad(gyt, xs, Cout, k, k, 1, k // 2, self.G(pre + "weight"))
         else:
             tmp = torch.zeros(rows, Cin, k, k, device=self.dev)
-            ops.conv2d_wgrad(gyt, x, rows, k, k, 1, k // 2, tmp, in_scale=s)
+            ops.conv2d_wgrad(gyt, xs, rows, k, k, 1, k // 2, tmp)
             self.G(pre + "weight").add_(tmp[:Cout])
         # demodulation backward
         gwsq = ops.gemm(gdd, s2, rows, Cin, B, a_kc=False, b_kc=False)  # [rows, Cin] = gdd^T s^2
@@ -221,12 +222,15 @@ class GeneratorEngine:
         W2 = self.st.group_view(ex + "0.net.2.weight", f"{ex}{E-1}.net.2.weight", self._cbuf())
         b2 = self.st.group_view(ex + "0.net.2.bias", f"{ex}{E-1}.net.2.bias")
         Hd = 4 * C
+        # tokens in dispatch order (k copies per token), shared by the expert GEMM and its weight gradient
+        Xg = ops.gather_rows(tok, perm, k)
         Pre = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
-        ops.gemm_grouped(tok, W1, row_off, tile_off, max_tiles, Hd, C, b_gstride=Hd * C, out=Pre, ldb=C,
-                         ep=E_(bias=b1, a_idx=perm, a_idx_div=k))
+        Hid = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+        ops.gemm_grouped(Xg, W1, row_off, tile_off, max_tiles, Hd, C, b_gstride=Hd * C, out=Hid, ldb=C,
+                         ep=E_(bias=b1, act=GELU, out_pre=Pre, ld_pre=Hd))
         Y = torch.empty(n, C, device=self.dev, dtype=self.cdt)
-        ops.gemm_grouped(Pre, W2, row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y, ldb=Hd,
-                         ep=E_(bias=b2, a_gelu=1))
+        ops.gemm_grouped(Hid, W2, row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y, ldb=Hd,
+                         ep=E_(bias=b2))
         out = torch.empty(T, C, device=self.dev, dtype=self.cdt)
         ops.moe_combine(Y, pos_of, gate, resid, out)  # x_spatial + moe_out (:571)
         kl2 = None
@@ -238,7 +242,7 @@ class GeneratorEngine:
         if save:
             sv = dict(tok=tok, w=w, HW=HW, eps=eps, anneal=anneal, Wf=Wf, Wt=Wt, Wc=Wc, Wfc=Wfc, u=u, probs=probs,
                       zlog=zlog, topi=topi, gate=gate, row_off=row_off, tile_off=tile_off, perm=perm, pos_of=pos_of,
-                      gate_pos=gate_pos, Pre=Pre, Y=Y, W1=W1, W2=W2, max_tiles=max_tiles)
+                      gate_pos=gate_pos, Pre=Pre, Hid=Hid, Xg=Xg, Y=Y, W1=W1, W2=W2, max_tiles=max_tiles)
         return out, probs, kl2, topi, sv
 
     def _cbuf(self):
@@ -256,22 +260,22 @@ class GeneratorEngine:
         row_off, tile_off, perm = sv["row_off"], sv["tile_off"], sv["perm"]
         ex = pre + "experts."
         g_gate = ops.moe_gate_grad(g_out, Y, sv["pos_of"], T, k)
-        # expert layer 2: dH = (gate * g_out[t]) @ W2_e, times GELU'(pre)
+        # gate-weighted output gradient in dispatch order: gG[r] = gate[r] * g_out[token(r)]
+        gG = ops.gather_rows(g_out, perm, k, rowscale=sv["gate_pos"])
+        # expert layer 2: dH = gG @ W2_e, times GELU'(pre)
         gP = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
-        ops.gemm_grouped(g_out, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
-                         out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd, a_idx=perm, a_idx_div=k,
-                                       a_rowscale=sv["gate_pos"]))
+        ops.gemm_grouped(gG, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
+                         out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd))
         gW2 = self.st.group_view(ex + "0.net.2.weight", f"{ex}{E-1}.net.2.weight", self.st.grad)
-        ops.gemm_grouped_wgrad(g_out, Pre, row_off, n, C, Hd, gW2, b_gelu=1,
-                               ep=E_(a_idx=perm, a_idx_div=k, a_rowscale=sv["gate_pos"]))
+        ops.gemm_grouped_wgrad(gG, sv["Hid"], row_off, n, C, Hd, gW2)
         gb2 = self.st.group_view(ex + "0.net.2.bias", f"{ex}{E-1}.net.2.bias", self.st.grad)
-        ops.grouped_colsum(g_out, row_off, C, n, gb2, idx=perm, idx_div=k, rs=sv["gate_pos"])
+        ops.grouped_colsum(gG, row_off, C, n, gb2)
         # expert layer 1
         gX = torch.empty(n, C, device=self.dev, dtype=self.cdt)
         ops.gemm_grouped(gP, sv["W1"], row_off, tile_off, sv["max_tiles"], C, Hd, b_kc=False, b_gstride=Hd * C,
                          out=gX, ldb=C)
         gW1 = self.st.group_view(ex + "0.net.0.weight", f"{ex}{E-1}.net.0.weight", self.st.grad)
-        ops.gemm_grouped_wgrad(gP, tok, row_off, n, Hd, C, gW1, b_idx=perm, b_idx_div=k)
+        ops.gemm_grouped_wgrad(gP, sv["Xg"], row_off, n, Hd, C, gW1)
         gb1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias", self.st.grad)
         ops.grouped_colsum(gP, row_off, Hd, n, gb1)
         # router

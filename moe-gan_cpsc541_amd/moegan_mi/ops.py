@@ -244,6 +244,25 @@ def modconv_bwd_out(gz, z, d, B, HW, Cout, act, gyt, gdd, zsub=None, ld_gz=None,
          ld_gyt or gyt.shape[-1], ptr(gdd), S())
 
 
+def gather_rows(src, idx, idx_div=1, rowscale=None, out=None):
+    """out[r] = src[idx[r] // idx_div] * rowscale[r] (mg_gather_rows)."""
+    n, C = idx.shape[0], src.shape[-1]
+    if out is None:
+        out = torch.empty(n, C, device=src.device, dtype=src.dtype)
+    call("mg_gather_rows", dt(src), ptr(src), _ld(src), ptr(idx), idx_div, ptr(rowscale), n, C, ptr(out), _ld(out), S())
+    return out
+
+
+def scale_bc(x, s, out=None):
+    """xs[b, ..., c] = x[b, ..., c] * s[b, c] for NHWC x [B, H, W, C] (mg_scale_bc)."""
+    B, C = x.shape[0], x.shape[-1]
+    HW = x.numel() // (B * C)
+    if out is None:
+        out = torch.empty_like(x)
+    call("mg_scale_bc", dt(x), ptr(x), C, ptr(s), B, HW, C, ptr(out), C, S())
+    return out
+
+
 def modconv_bwd_in(gxt, x, s, B, HW, Cin, gx, gs, accumulate=0):
     call("mg_modconv_bwd_in", dt(gxt), ptr(gxt), gxt.shape[-1], dt(x), ptr(x), x.shape[-1], ptr(s), B, HW, Cin,
          dt(gx) if gx is not None else 0, ptr(gx), gx.shape[-1] if gx is not None else 0, accumulate, ptr(gs), S())

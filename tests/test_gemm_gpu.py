@@ -47,6 +47,21 @@ def test_gemm_epilogue_bias_act_resid_splitk():
     assert rel(y2, A @ W.T) < 1e-5
 
 
+def test_gemm_slab_splitk_accumulate_and_bf16_out():
+    """Few-tile GEMMs take the split-K slab path: the epilogue runs once on the reduced sum."""
+    g = torch.Generator(device=DEV).manual_seed(2)
+    M, N, K = 256, 512, 512
+    A = torch.randn(M, K, device=DEV, generator=g)
+    W = torch.randn(N, K, device=DEV, generator=g) / 16
+    R = torch.randn(M, N, device=DEV, generator=g)
+    C = R.clone()
+    ops.gemm(A, W, M, N, K, out=C, ep=L.epilogue(alpha=0.5, accumulate=1))
+    assert rel(C, R + 0.5 * (A @ W.T)) < 1e-5
+    y = ops.linear(A.bfloat16(), W.bfloat16(), act=L.ACT_LRELU)
+    ref = F.leaky_relu(A.bfloat16().float() @ W.bfloat16().float().T, 0.2)
+    assert y.dtype == torch.bfloat16 and rel(y, ref) < 1e-2
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
 @pytest.mark.parametrize("B,H,Cin,Cout,k,stride,pad", [(3, 8, 64, 96, 3, 1, 1), (2, 16, 128, 32, 3, 1, 1),
                                                        (2, 4, 512, 256, 1, 1, 0), (2, 16, 128, 256, 4, 2, 1)])

@@ -1,0 +1,131 @@
+"""Time the GEMM-core launches that dominate the C2 training step, in one process.
+
+  python tools/gemm_probe.py [--iters 20] [--only NAME,...]
+
+Shapes are the bench workload's (B=256, bf16, E=8 top-2); each line prints the median launch
+time and the algorithmic TFLOP/s.  Used to A/B GEMM-core changes with a single GPU call.
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "moe-gan_cpsc541_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--variants", default="", help="';'-separated tuning sets, e.g. '0=64;0=128'")
+    a = ap.parse_args()
+    from moegan_mi import _lib as L
+    from moegan_mi import ops
+    dev = "cuda"
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def rn(*s, dt=torch.float32, sc=1.0):
+        return (torch.randn(*s, device=dev, generator=g) * sc).to(dt)
+
+    B = 256
+    cases = []
+    # D conv_layers.2 forward (roofline kernel)
+    h0 = rn(B, 32, 32, 128, dt=bf)
+    w1 = ops.pack_conv(rn(256, 128, 4, 4, sc=0.02), bf)
+    cases.append(("d_conv1_fwd", 2.0 * B * 256 * 256 * 2048,
+                  lambda: ops.conv2d(h0, w1, 256, 4, 4, 2, 1, ep=ops.E(act=L.ACT_LRELU))))
+    # modulated 3x3 convs (gen_block_16 / gen_block_8 MTM)
+    x16 = rn(B, 16, 16, 128, dt=bf)
+    s16 = rn(B, 128) + 1
+    w16 = ops.pack_conv(rn(128, 128, 3, 3, sc=0.03), bf)
+    cases.append(("modconv16_fwd", 2.0 * B * 256 * 128 * 1152,
+                  lambda: ops.conv2d(x16, w16, 128, 3, 3, 1, 1, in_scale=s16)))
+    x8 = rn(B, 8, 8, 256, dt=bf)
+    s8 = rn(B, 256) + 1
+    w8 = ops.pack_conv(rn(256, 256, 3, 3, sc=0.02), bf)
+    cases.append(("modconv8_fwd", 2.0 * B * 64 * 256 * 2304, lambda: ops.conv2d(x8, w8, 256, 3, 3, 1, 1, in_scale=s8)))
+    # weight gradients
+    gy16 = rn(B * 256, 128, dt=bf)
+    gw16 = torch.zeros(128, 128, 3, 3, device=dev)
+    cases.append(("modconv16_wgrad", 2.0 * B * 256 * 128 * 1152,
+                  lambda: ops.conv2d_wgrad(gy16, x16, 128, 3, 3, 1, 1, gw16)))
+    gy8 = rn(B * 64, 256, dt=bf)
+    x8b = rn(B, 8, 8, 512, dt=bf)
+    gw8 = torch.zeros(256, 512, 3, 3, device=dev)
+    cases.append(("modconv8_wgrad", 2.0 * B * 64 * 256 * 4608,
+                  lambda: ops.conv2d_wgrad(gy8, x8b, 256, 3, 3, 1, 1, gw8)))
+    gy1 = rn(B, 16, 16, 256, dt=bf)
+    gw1 = torch.zeros(256, 128, 4, 4, device=dev)
+    cases.append(("d_conv1_wgrad", 2.0 * B * 256 * 256 * 2048,
+                  lambda: ops.conv2d_wgrad(gy1, h0, 256, 4, 4, 2, 1, gw1)))
+    gl = rn(B * 256, 512, dt=bf)
+    xl = rn(B * 256, 128, dt=bf)
+    gwl = torch.zeros(512, 128, device=dev)
+    cases.append(("linear_wgrad_bf16", 2.0 * B * 256 * 512 * 128, lambda: ops.linear_wgrad(gl, xl, gwl)))
+    # grouped expert GEMM (8 experts x 16384 rows, 128 -> 512, GELU)
+    E_, rows = 8, 16384
+    Ae = rn(E_ * rows, 128, dt=bf)
+    We = rn(E_ * 512, 128, dt=bf, sc=0.05)
+    row_off = torch.arange(0, E_ + 1, device=dev, dtype=torch.int32) * rows
+    tile_off = torch.arange(0, E_ + 1, device=dev, dtype=torch.int32) * (rows // 128)
+    oute = torch.empty(E_ * rows, 512, device=dev, dtype=bf)
+    be = rn(E_, 512)
+    cases.append(("expert_fc1", 2.0 * E_ * rows * 512 * 128,
+                  lambda: ops.gemm_grouped(Ae, We, row_off, tile_off, E_ * rows // 128, 512, 128, b_gstride=512 * 128,
+                                           out=oute, ep=ops.E(act=L.ACT_GELU))))
+    # expert weight gradient (grouped over rows, plain operands)
+    gG = rn(E_ * rows, 128, dt=bf)
+    Hid = rn(E_ * rows, 512, dt=bf)
+    gWe = torch.zeros(E_, 128, 512, device=dev)
+    cases.append(("expert_wgrad", 2.0 * E_ * rows * 512 * 128,
+                  lambda: ops.gemm_grouped_wgrad(gG, Hid, row_off, E_ * rows, 128, 512, gWe)))
+    # calibration: square bf16 GEMM
+    Ab = rn(4096, 4096, dt=bf)
+    Bb = rn(4096, 4096, dt=bf)
+    cases.append(("gemm4096_bf16", 2.0 * 4096 ** 3, lambda: ops.gemm(Ab, Bb, 4096, 4096, 4096)))
+    # plain bf16 linear (attention proj / qkv shape)
+    xq = rn(B * 256, 128, dt=bf)
+    wq = rn(384, 128, dt=bf, sc=0.05)
+    cases.append(("qkv_linear_bf16", 2.0 * B * 256 * 384 * 128, lambda: ops.linear(xq, wq)))
+    # small fp32 GEMMs (styles, mapping)
+    w = rn(B, 512)
+    Wm = rn(512, 512, sc=0.04)
+    bm = rn(512)
+    cases.append(("style_fp32", 2.0 * B * 512 * 512, lambda: ops.linear(w, Wm, bias=bm)))
+    gs = rn(B, 512)
+    gwm = torch.zeros(512, 512, device=dev)
+    cases.append(("style_wgrad_fp32", 2.0 * B * 512 * 512, lambda: ops.linear_wgrad(gs, w, gwm)))
+    cases.append(("style_dgrad_fp32", 2.0 * B * 512 * 512, lambda: ops.linear_dgrad(gs, Wm)))
+
+    only = set(a.only.split(",")) if a.only else None
+    variants = [("", {})]
+    if a.variants:
+        variants = []
+        for v in a.variants.split(";"):
+            kv = dict(tuple(int(t) for t in x.split("=")) for x in v.split(",") if x)
+            variants.append((v, kv))
+    todo = [(n + (f"[{vn}]" if vn else ""), f, fn, kv) for n, f, fn in cases for vn, kv in variants
+            if not only or n in only]
+    for name, flop, fn, kv in todo:
+        for k in range(16):
+            L.call("mg_set_tuning", k, 0)
+        for k, v in kv.items():
+            L.call("mg_set_tuning", k, v)
+        for _ in range(3):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
+        for s, e in ev:
+            s.record()
+            fn()
+            e.record()
+        torch.cuda.synchronize()
+        ms = sorted(s.elapsed_time(e) for s, e in ev)
+        med = ms[len(ms) // 2]
+        print(f"{name:20s} {med * 1e3:9.1f} us  {flop / med / 1e9:8.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
