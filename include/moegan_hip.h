@@ -188,10 +188,11 @@ int mg_gather_rows(int dtype, const void* src, int64_t lds, const int32_t* idx, 
 
 /* Modulated-conv input xs[b,p,c] = x[b,p,c] * s[b,c] (x rows [B*HW, ldx], C % 8 == 0); replaces the
    per-tap operand scaling of the fused modulated conv (t2i_moe_gan.py:167-171, x * style). */
-int mg_scale_bc(int dtype, const void* x, int64_t ldx, const float* s, int B, int HW, int C, void* out, int64_t ldo, void* stream);
+int mg_scale_bc(int dtype, const void* x, int64_t ldx, const float* s, int64_t lds, int B, int HW, int C, void* out, int64_t ldo, void* stream);
 
-/* ModulatedConv backward, input side: gx (+)= gxt*s, gs[b,ci] += sum_pix gxt*x. */
-int mg_modconv_bwd_in(int gxt_dtype, const void* gxt, int64_t ld_gxt, int dtype, const void* x, int64_t ld_x, const float* s, int B, int HW, int Cin, int gx_dtype, void* gx, int64_t ld_gx, int accumulate, float* gs, void* stream);
+/* ModulatedConv backward, input side: gx (+)= gxt*s, gs[b,ci] += sum_pix gxt*x (s and gs rows of pitch ld_s:
+   column slices of the batched style matrix). */
+int mg_modconv_bwd_in(int gxt_dtype, const void* gxt, int64_t ld_gxt, int dtype, const void* x, int64_t ld_x, const float* s, int64_t ld_s, int B, int HW, int Cin, int gx_dtype, void* gx, int64_t ld_gx, int accumulate, float* gs, void* stream);
 
 /* Generator KL total and per-router gradient coefficients (total clamped at 50, t2i_moe_gan.py:1369-1370). */
 int mg_kl_coefs(const float* kl2, int R, float eff_w, float* coef, float* total, void* stream);

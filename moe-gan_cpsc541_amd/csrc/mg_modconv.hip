@@ -46,12 +46,12 @@ __global__ void k_bwd_out(const TG* __restrict__ gz, int64_t ld_gz, const T* __r
 
 template <typename TG, typename T, typename TO>
 __global__ void k_bwd_in(const TG* __restrict__ gxt, int64_t ld_gxt, const T* __restrict__ x, int64_t ld_x,
-                         const float* __restrict__ s, int HW, int Cin, TO* __restrict__ gx, int64_t ld_gx,
-                         int accumulate, float* __restrict__ gs) {
+                         const float* __restrict__ s, int64_t ld_s, int HW, int Cin, TO* __restrict__ gx,
+                         int64_t ld_gx, int accumulate, float* __restrict__ gs) {
   int b = blockIdx.x;
   int c = blockIdx.y * blockDim.x + threadIdx.x;
   if (c >= Cin) return;
-  float sc = s[(int64_t)b * Cin + c];
+  float sc = s[(int64_t)b * ld_s + c];
   float acc = 0.f;
   for (int p = 0; p < HW; ++p) {
     int64_t row = (int64_t)b * HW + p;
@@ -63,7 +63,7 @@ __global__ void k_bwd_in(const TG* __restrict__ gxt, int64_t ld_gxt, const T* __
       stf(gx, row * ld_gx + c, v);
     }
   }
-  gs[(int64_t)b * Cin + c] += acc;
+  gs[(int64_t)b * ld_s + c] += acc;
 }
 
 // out[b, c] (+)= sum_{p < HW} X[b*HW + p, c]   (per-image column sums)
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void k_bwd_out_v(const TG* __restrict__ gz, in
 
 template <typename TG, typename T, typename TO>
 __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, int64_t ld_gxt, const T* __restrict__ x,
-                                                  int64_t ld_x, const float* __restrict__ s, int HW, int Cin,
+                                                  int64_t ld_x, const float* __restrict__ s, int64_t ld_s, int HW, int Cin,
                                                   TO* __restrict__ gx, int64_t ld_gx, int accumulate,
                                                   float* __restrict__ gs) {
   __shared__ float red[256 * 8];
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, in
   float sc[8], acc[8], g[8], xx[8], t[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  if (live) ld8(s + (int64_t)b * Cin + c, sc);
+  if (live) ld8(s + (int64_t)b * ld_s + c, sc);
   for (int p = ty; live && p < HW; p += TY) {
     int64_t row = (int64_t)b * HW + p;
     ld8(gxt + row * ld_gxt + c, g);
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, in
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += red[(y * TX + tx) * 8 + j];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gs[(int64_t)b * Cin + c + j] += acc[j];
+    for (int j = 0; j < 8; ++j) gs[(int64_t)b * ld_s + c + j] += acc[j];
   }
 }
 
@@ -197,7 +197,8 @@ __global__ __launch_bounds__(256) void k_segsum_v(const T* __restrict__ X, int64
 // the forward conv and the weight gradient (instead of re-scaling every tap's operand in the GEMM loaders).
 template <typename T>
 __global__ __launch_bounds__(256) void k_scale_bc(const T* __restrict__ x, int64_t ldx, const float* __restrict__ s,
-                                                  int HW, int C, int64_t nvec, T* __restrict__ out, int64_t ldo) {
+                                                  int64_t lds, int HW, int C, int64_t nvec, T* __restrict__ out,
+                                                  int64_t ldo) {
   const int cv = C / 8;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
     int64_t row = i / cv;
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(256) void k_scale_bc(const T* __restrict__ x, int64
     int64_t b = row / HW;
     float v[8], sc[8];
     ld8(x + row * ldx + c, v);
-    ld8(s + b * C + c, sc);
+    ld8(s + b * lds + c, sc);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] *= sc[j];
     st8(out + row * ldo + c, v);
@@ -243,20 +244,20 @@ inline void vshape(int C, dim3& grid, dim3& block, int B) {
 
 }  // namespace
 
-extern "C" int mg_scale_bc(int dtype, const void* x, int64_t ldx, const float* s, int B, int HW, int C, void* out,
-                           int64_t ldo, void* stream) {
+extern "C" int mg_scale_bc(int dtype, const void* x, int64_t ldx, const float* s, int64_t lds, int B, int HW, int C,
+                           void* out, int64_t ldo, void* stream) {
   MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
-  MG_REQUIRE(C % 8 == 0 && ldx % 8 == 0 && ldo % 8 == 0, "C and pitches must be multiples of 8");
+  MG_REQUIRE(C % 8 == 0 && ldx % 8 == 0 && ldo % 8 == 0 && lds % 4 == 0, "C and pitches must be multiples of 8");
   MG_REQUIRE(mg_al16(x) && mg_al16(out) && mg_al16(s), "x/out/s must be 16-byte aligned");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t nvec = (int64_t)B * HW * (C / 8);
   if (nvec == 0) return MG_OK;
   int blocks = (int)std::min<int64_t>(cdiv(nvec, 256), 4096);
   if (dtype == MG_F32)
-    hipLaunchKernelGGL(k_scale_bc<float>, dim3(blocks), dim3(256), 0, st, (const float*)x, ldx, s, HW, C, nvec,
+    hipLaunchKernelGGL(k_scale_bc<float>, dim3(blocks), dim3(256), 0, st, (const float*)x, ldx, s, lds, HW, C, nvec,
                        (float*)out, ldo);
   else
-    hipLaunchKernelGGL(k_scale_bc<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)x, ldx, s, HW, C, nvec,
+    hipLaunchKernelGGL(k_scale_bc<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)x, ldx, s, lds, HW, C, nvec,
                        (bf16_t*)out, ldo);
   return mg_check_launch("mg_scale_bc");
 }
@@ -327,23 +328,23 @@ extern "C" int mg_modconv_bwd_out(int dtype, int gz_dtype, const void* gz, int64
 }
 
 extern "C" int mg_modconv_bwd_in(int gxt_dtype, const void* gxt, int64_t ld_gxt, int dtype, const void* x,
-                                 int64_t ld_x, const float* s, int B, int HW, int Cin, int gx_dtype, void* gx,
-                                 int64_t ld_gx, int accumulate, float* gs, void* stream) {
+                                 int64_t ld_x, const float* s, int64_t ld_s, int B, int HW, int Cin, int gx_dtype,
+                                 void* gx, int64_t ld_gx, int accumulate, float* gs, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(B, cdiv(Cin, 256));
   dim3 blk(std::min(256, ((Cin + 63) / 64) * 64));
-  bool vec = Cin % 8 == 0 && ld_gxt % 8 == 0 && ld_x % 8 == 0 && (!gx || ld_gx % 8 == 0) && mg_al16(gxt) &&
-             mg_al16(x) && mg_al16(s) && (!gx || mg_al16(gx)) && mg_al16(gs);
+  bool vec = Cin % 8 == 0 && ld_gxt % 8 == 0 && ld_x % 8 == 0 && (!gx || ld_gx % 8 == 0) && ld_s % 4 == 0 &&
+             mg_al16(gxt) && mg_al16(x) && mg_al16(s) && (!gx || mg_al16(gx)) && mg_al16(gs);
   int thr = blk.x;
   if (vec) vshape(Cin, grid, blk, B);
 #define L_(TG, T, TO)                                                                                              \
   do {                                                                                                             \
     if (vec)                                                                                                       \
       hipLaunchKernelGGL((k_bwd_in_v<TG, T, TO>), grid, blk, 0, st, (const TG*)gxt, ld_gxt, (const T*)x, ld_x, s, \
-                         HW, Cin, (TO*)gx, ld_gx, accumulate, gs);                                                 \
+                         ld_s, HW, Cin, (TO*)gx, ld_gx, accumulate, gs);                                           \
     else                                                                                                           \
       hipLaunchKernelGGL((k_bwd_in<TG, T, TO>), grid, dim3(thr), 0, st, (const TG*)gxt, ld_gxt, \
-                                         (const T*)x, ld_x, s, HW, Cin, (TO*)gx, ld_gx, accumulate, gs); \
+                                         (const T*)x, ld_x, s, ld_s, HW, Cin, (TO*)gx, ld_gx, accumulate, gs); \
   } while (0)
   if (dtype == MG_F32) {
     if (gxt_dtype == MG_F32) {

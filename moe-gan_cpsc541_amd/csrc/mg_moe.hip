@@ -434,6 +434,47 @@ __global__ void k_grouped_colsum(const T* __restrict__ X, int64_t ld, const int*
   atomicAdd(&out[(int64_t)g * N + n], s);
 }
 
+// KL of one router, two passes: per-block partial sums over the three (mu, rho) pairs, then one block
+// folds the partials and applies the reference's nan/inf/clamp rules.
+__global__ __launch_bounds__(256) void k_router_kl_part(const float* __restrict__ mf, const float* __restrict__ rf,
+                                                        int nf, const float* __restrict__ mt,
+                                                        const float* __restrict__ rt, int nt,
+                                                        const float* __restrict__ mc, const float* __restrict__ rc,
+                                                        int nc, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int64_t n = (int64_t)nf + nt + nc;
+  float ps = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float m, r;
+    if (i < nf) { m = mf[i]; r = rf[i]; }
+    else if (i < nf + nt) { m = mt[i - nf]; r = rt[i - nf]; }
+    else { m = mc[i - nf - nt]; r = rc[i - nf - nt]; }
+    float sg = softplusf(r);
+    float lv = 2.f * logf(sg);
+    ps += expf(lv) + m * m - 1.f - lv;
+  }
+  ps = wave_sum(ps);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ps;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = 0.5f * (red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ void k_router_kl_fin(const float* __restrict__ part, int nparts, float* __restrict__ out) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) {
+    float v = s;
+    float pass = 1.f;
+    if (isnan(v)) { v = 0.f; pass = 0.f; }
+    else if (isinf(v)) { v = v > 0 ? 200.f : 0.f; pass = 0.f; }
+    if (v > 120.f) { v = 120.f; pass = 0.f; }
+    if (v < 0.f) { v = 0.f; pass = 0.f; }
+    out[0] = v;
+    out[1] = pass;
+  }
+}
+
 // KL of one router (t2i_moe_gan.py:405-423): out[0] = clamp(nan_to_num(sum), 0, 120), out[1] = grad-pass flag
 __global__ void k_router_kl(const float* __restrict__ mf, const float* __restrict__ rf, int nf,
                             const float* __restrict__ mt, const float* __restrict__ rt, int nt,
@@ -679,7 +720,16 @@ extern "C" int mg_grouped_colsum(int dtype, const void* X, int64_t ld, const int
 extern "C" int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const float* mu_t, const float* rho_t,
                             int nt, const float* mu_c, const float* rho_c, int nc, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_router_kl, dim3(1), dim3(1024), 0, st, mu_f, rho_f, nf, mu_t, rho_t, nt, mu_c, rho_c, nc, out);
+  int64_t n = (int64_t)nf + nt + nc;
+  int nparts = (int)std::min<int64_t>(64, std::max<int64_t>(1, cdiv(n, 2048)));
+  static float* s_part = nullptr;  // 64 partials; reuse is ordered by the stream
+  if (!s_part && hipMalloc(&s_part, 64 * sizeof(float)) != hipSuccess) {
+    mg_set_error("mg_router_kl: scratch allocation failed");
+    return MG_ERR_LAUNCH;
+  }
+  hipLaunchKernelGGL(k_router_kl_part, dim3(nparts), dim3(256), 0, st, mu_f, rho_f, nf, mu_t, rho_t, nt, mu_c, rho_c,
+                     nc, s_part);
+  hipLaunchKernelGGL(k_router_kl_fin, dim3(1), dim3(64), 0, st, s_part, nparts, out);
   return mg_check_launch("mg_router_kl");
 }
 

@@ -110,6 +110,37 @@ __global__ void k_colsum(const T* __restrict__ X, int64_t ld, int R, int C, int 
   atomicAdd(out + c, s);
 }
 
+// vectorised column sums: 8 columns per thread, rows split over TY lanes x grid.y, LDS reduction,
+// one atomic per column per block.  C % 8 == 0, 16-B aligned rows.
+template <typename T>
+__global__ __launch_bounds__(256) void k_colsum_v(const T* __restrict__ X, int64_t ld, int R, int C,
+                                                  int rows_per_block, float* __restrict__ out) {
+  __shared__ float red[256 * 8];
+  const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
+  const int c = (blockIdx.x * TX + tx) * 8;
+  const bool live = c < C;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(R, r0 + rows_per_block);
+  float acc[8], t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int r = r0 + ty; live && r < r1; r += TY) {
+    ld8(X + (int64_t)r * ld + c, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += t[j];
+  }
+  const int tid = ty * TX + tx;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = acc[j];
+  __syncthreads();
+  if (ty == 0 && live) {
+    for (int y = 1; y < TY; ++y)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += red[(y * TX + tx) * 8 + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(out + c + j, acc[j]);
+  }
+}
+
 // weight norm: W[o] = g[o] * v[o] / ||v[o]||  (t2i_moe_gan.py:869-886, torch weight_norm dim=0)
 __global__ void k_wn_fwd(const float* __restrict__ v, const float* __restrict__ g, int O, int K,
                          float* __restrict__ W, float* __restrict__ norm) {
@@ -313,6 +344,19 @@ extern "C" int mg_copy2d(int in_dtype, const void* in, int64_t ldi, int out_dtyp
 extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (R == 0 || C == 0) return MG_OK;
+  if (C % 8 == 0 && ld % 8 == 0 && mg_al16(X) && mg_al16(out)) {
+    int cv = C / 8;
+    int tx = std::min(cv, 32);
+    int ty = 256 / tx;
+    int cblk = cdiv(cv, tx);
+    // ~512 blocks in total, at least 4 rows per lane
+    int rblk = std::max(1, std::min(cdiv(R, 4 * ty), 512 / cblk));
+    int rpb = cdiv(R, rblk);
+    dim3 grid(cblk, cdiv(R, rpb));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum_v<T>, grid, dim3(tx, ty), 0, st, reinterpret_cast<const T*>(X), ld,
+                                         R, C, rpb, out));
+    return mg_check_launch("mg_colsum");
+  }
   int rpb = std::max(16, R / 256);
   dim3 grid(cdiv(C, 256), cdiv(R, rpb));
   DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum<T>, grid, dim3(256), 0, st, reinterpret_cast<const T*>(X), ld, R, C,

@@ -44,6 +44,10 @@ class GeneratorEngine:
         self.dev = store.device
         self.packs = {}
         self._ones = None
+        self.style_cols = {}
+        self._S = self._S2 = self._GS = None  # batched styles of the running forward / style grads of a backward
+        self._mean_latent = None
+        self._want_kl = True
 
     # parameter access
     def P(self, n):
@@ -60,6 +64,17 @@ class GeneratorEngine:
     # ------------------------------------------------------------------
     def prep(self):
         self.st.refresh_shadow()
+        sb = self.st.style_block()
+        self.style_cols = None
+        if sb is not None:
+            (o0, nrows, K, b0), cols = sb
+            self.style_cols = cols
+            self.style_n = nrows
+            self.style_W = self.st.data[o0:o0 + nrows * K].view(nrows, K)
+            self.style_b = self.st.data[b0:b0 + nrows]
+            self.style_gW = self.st.grad[o0:o0 + nrows * K].view(nrows, K)
+            self.style_gb = self.st.grad[b0:b0 + nrows]
+        self._mean_latent = None  # truncation centre: mapping of zeros, a function of the weights only
         pk = {}
         for pre, k in _modconv_prefixes():
             W = self.P(pre + "weight")
@@ -84,6 +99,14 @@ class GeneratorEngine:
     # ------------------------------------------------------------------
     # ModulatedConv  (t2i_moe_gan.py:154-186), fused form
     # ------------------------------------------------------------------
+    def _style(self, pre, w, Cin):
+        """(s, s^2) for one modulated conv: column slices of the step's batched styles when available."""
+        if self._S is not None and pre in self.style_cols:
+            c = self.style_cols[pre]
+            return self._S[:, c:c + Cin], self._S2[:, c:c + Cin]
+        s = ops.linear(w, self.P(pre + "modulation.weight"), bias=self.P(pre + "modulation.bias"))  # :158
+        return s, ops.cast(s, square=1)
+
     def mc_fwd(self, pre, x, w, act=0, resid=None, save=True):
         B, H, W, Cin = x.shape
         HW = H * W
@@ -91,8 +114,7 @@ class GeneratorEngine:
         rows = pk["rows"]
         Wt = self.P(pre + "weight")
         k = Wt.shape[-1]
-        s = ops.linear(w, self.P(pre + "modulation.weight"), bias=self.P(pre + "modulation.bias"))  # :158
-        s2 = ops.cast(s, square=1)
+        s, s2 = self._style(pre, w, Cin)
         d = ops.gemm(s2, pk["wsq"], B, rows, Cin, ep=E_(act=RSQRT))  # demod coefficients [B, rows] (:165)
         ep = E_(scale=d, scale_shift=ops.ilog2(HW), scale_ld=rows, act=act, resid=resid,
                 ld_res=resid.shape[-1] if resid is not None else 0)
@@ -120,7 +142,12 @@ class GeneratorEngine:
             gxt = ops.conv2d(gyt.view(B, H, W, rows), pk["wflip"], Cin, 3, 3, 1, 1)
         else:
             gxt = ops.gemm(gyt, pk["w"], P, Cin, rows, b_kc=False)
-        gs = torch.zeros(B, Cin, device=self.dev, dtype=torch.float32)
+        batched = self._GS is not None and pre in self.style_cols
+        if batched:
+            c = self.style_cols[pre]
+            gs = self._GS[:, c:c + Cin]
+        else:
+            gs = torch.zeros(B, Cin, device=self.dev, dtype=torch.float32)
         ops.modconv_bwd_in(gxt.view(P, Cin), x.view(P, Cin), s, B, HW, Cin,
                            None if gx is None else gx.view(P, -1), gs, accumulate)
         # weight gradient (fp32, reference layout)
@@ -134,8 +161,9 @@ class GeneratorEngine:
         gwsq = ops.gemm(gdd, s2, rows, Cin, B, a_kc=False, b_kc=False)  # [rows, Cin] = gdd^T s^2
         ops.wsq_bwd(Wt, gwsq[:Cout], self.G(pre + "weight"))
         ops.gemm(gdd, pk["wsq"], B, Cin, rows, b_kc=False, out=gs,
-                 ep=E_(alpha=2.0, scale=s, scale_ld=Cin, accumulate=1))  # gs += 2 s (gdd @ wsq)
-        # style = modulation(w)
+                 ep=E_(alpha=2.0, scale=s, scale_ld=s.stride(0), accumulate=1))  # gs += 2 s (gdd @ wsq)
+        if batched:
+            return  # style = modulation(w): backpropagated for all modulated convs at once (_style_bwd)
         ops.linear_wgrad(gs, w, self.G(pre + "modulation.weight"))
         ops.colsum(gs, self.G(pre + "modulation.bias"))
         ops.gemm(gs, self.P(pre + "modulation.weight"), B, w.shape[1], Cin, b_kc=False, out=gw,
@@ -234,7 +262,7 @@ class GeneratorEngine:
         out = torch.empty(T, C, device=self.dev, dtype=self.cdt)
         ops.moe_combine(Y, pos_of, gate, resid, out)  # x_spatial + moe_out (:571)
         kl2 = None
-        if train:
+        if train and self._want_kl:
             kl2 = torch.empty(2, device=self.dev, dtype=torch.float32)
             ops.router_kl(self.P(r + "feature_mu"), self.P(r + "feature_rho"), self.P(r + "text_mu"),
                           self.P(r + "text_rho"), self.P(r + "combined_mu"), self.P(r + "combined_rho"), kl2)
@@ -374,8 +402,10 @@ class GeneratorEngine:
             hs.append(h)
         return h, hs
 
-    def forward(self, z, text, eps, anneal=1.0, psi=0.7, train=True, save=True, want_img8=False):
-        """Returns (img16 [B,16,16,8] padded NHWC, img8 or None, kl2 list, probs list, ctx)."""
+    def forward(self, z, text, eps, anneal=1.0, psi=0.7, train=True, save=True, want_img8=False, want_kl=True):
+        """Returns (img16 [B,16,16,8] padded NHWC, img8 or None, kl2 list, probs list, ctx).
+        ``want_kl=False`` skips the routers' KL terms (their kl2 entries are None)."""
+        self._want_kl = want_kl
         B = z.shape[0]
         dev = self.dev
         if text.shape[0] != B and text.shape[0] == 1:
@@ -391,15 +421,21 @@ class GeneratorEngine:
         ops.copy2d(text, zt[:, z.shape[1]:], B, text.shape[1], ldo=zt.shape[1])
         h3, hs = self._mapping(zt, save)
         if psi < 1.0:
-            zeros = torch.zeros(1, zt.shape[1], device=dev)
-            m3, _ = self._mapping(zeros, False)
-            mean = ops.linear(m3, self.P("mapping.6.weight"), bias=self.P("mapping.6.bias"))
+            if self._mean_latent is None:  # mapping(0): depends on the weights only -> once per prep()
+                zeros = torch.zeros(1, zt.shape[1], device=dev)
+                m3, _ = self._mapping(zeros, False)
+                self._mean_latent = ops.linear(m3, self.P("mapping.6.weight"), bias=self.P("mapping.6.bias"))
+            mean = self._mean_latent
             beff = torch.empty(512, device=dev)
             ops.copy2d(self.P("mapping.6.bias").view(1, -1), beff.view(1, -1), 1, 512, alpha=psi)
             ops.copy2d(mean, beff.view(1, -1), 1, 512, alpha=1.0 - psi, accumulate=1)
             w = ops.linear(h3, self.P("mapping.6.weight"), bias=beff, alpha=psi)
         else:
             w = ops.linear(h3, self.P("mapping.6.weight"), bias=self.P("mapping.6.bias"))
+        # every modulated conv's style in one GEMM: S = w @ [W_mod ...]^T + [b_mod ...] (:158)
+        if self.style_cols:
+            self._S = ops.linear(w, self.style_W, bias=self.style_b)
+            self._S2 = ops.cast(self._S, square=1)
         x = ops.const_fwd(self.P("constant"), B, self.cdt)
         probs, kl2s, topis, blocks = [], [], [], []
         img8, rgb8sv = None, None
@@ -416,6 +452,7 @@ class GeneratorEngine:
             if name == "gen_block_8" and want_img8:
                 img8, rgb8sv = self.mc_fwd("to_rgb_8.", x, w, save=save)
         img16, rgbsv = self.mc_fwd("to_rgb_16.", x, w, save=save)
+        self._S = self._S2 = None
         ctx = None
         if save:
             ctx = dict(B=B, text=text, z=z, t0=t0, t1=t1, tmu=tmu, trs=trs, text_seq=text_seq, hs=hs, h3=h3, w=w,
@@ -430,6 +467,8 @@ class GeneratorEngine:
         dev = self.dev
         gw = torch.zeros(B, 512, device=dev)
         g_ts = torch.zeros(B, 512, device=dev)
+        if self.style_cols:
+            self._GS = torch.zeros(B, self.style_n, device=dev)
         sv = ctx["rgbsv"]
         x_last = sv[0]
         gx = torch.empty(x_last.shape, device=dev, dtype=self.cdt)
@@ -455,6 +494,11 @@ class GeneratorEngine:
             else:
                 gx = g_in
         ops.const_bwd(gx, self.G("constant"))
+        if self._GS is not None:  # all modulated convs' style backward at once
+            GS, self._GS = self._GS, None
+            ops.linear_wgrad(GS, ctx["w"], self.style_gW)
+            ops.colsum(GS, self.style_gb)
+            ops.gemm(GS, self.style_W, B, gw.shape[1], self.style_n, b_kc=False, out=gw, ep=E_(accumulate=1))
         # truncation: w = mean + psi (w_full - mean), mean under no_grad
         psi = ctx["psi"]
         g6 = ops.cast(gw, alpha=psi if psi < 1.0 else 1.0)

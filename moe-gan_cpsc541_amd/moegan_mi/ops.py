@@ -259,13 +259,16 @@ def scale_bc(x, s, out=None):
     HW = x.numel() // (B * C)
     if out is None:
         out = torch.empty_like(x)
-    call("mg_scale_bc", dt(x), ptr(x), C, ptr(s), B, HW, C, ptr(out), C, S())
+    call("mg_scale_bc", dt(x), ptr(x), C, ptr(s), s.stride(0), B, HW, C, ptr(out), C, S())
     return out
 
 
 def modconv_bwd_in(gxt, x, s, B, HW, Cin, gx, gs, accumulate=0):
-    call("mg_modconv_bwd_in", dt(gxt), ptr(gxt), gxt.shape[-1], dt(x), ptr(x), x.shape[-1], ptr(s), B, HW, Cin,
-         dt(gx) if gx is not None else 0, ptr(gx), gx.shape[-1] if gx is not None else 0, accumulate, ptr(gs), S())
+    """gx (+)= gxt * s; gs += sum_pix gxt * x.  s / gs may be column slices sharing one row pitch."""
+    assert s.stride(0) == gs.stride(0) and s.stride(-1) == 1 and gs.stride(-1) == 1
+    call("mg_modconv_bwd_in", dt(gxt), ptr(gxt), gxt.shape[-1], dt(x), ptr(x), x.shape[-1], ptr(s), s.stride(0), B, HW,
+         Cin, dt(gx) if gx is not None else 0, ptr(gx), gx.shape[-1] if gx is not None else 0, accumulate, ptr(gs),
+         S())
 
 
 # ---------------------------------------------------------------------------

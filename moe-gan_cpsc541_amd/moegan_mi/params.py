@@ -25,13 +25,24 @@ ALIGN = 8  # elements: keeps every view 16-byte aligned for fp32 and bf16 vector
 
 
 def flat_order(shapes, frozen_prefixes=()):
-    """Reference names reordered: experts grouped per (block, layer, kind); frozen names last."""
+    """Reference names reordered: the modulated convs' style weights and then their biases first (one
+    [sum Cin, 512] matrix and one [sum Cin] vector: every style of a forward is ONE GEMM), experts grouped
+    per (block, layer, kind); frozen names last."""
     names = [n for n in shapes if not is_buffer(n)]
     groups = OrderedDict()
     order, frozen = [], []
+    is_frozen = lambda n: any(n.startswith(p) for p in frozen_prefixes)  # noqa: E731
+    style_w = [n for n in names if n.endswith("modulation.weight") and not is_frozen(n)]
+    style_b = [n[:-len("weight")] + "bias" for n in style_w]
+    if not all(b in shapes for b in style_b):
+        style_w, style_b = [], []
+    lead = set(style_w) | set(style_b)
+    order.extend(style_w + style_b)
     for n in names:
         m = _EXPERT.match(n)
-        if any(n.startswith(p) for p in frozen_prefixes):
+        if n in lead:
+            continue
+        if is_frozen(n):
             frozen.append(n)
         elif m:
             key = (m.group(1), m.group(3), m.group(4))
@@ -83,6 +94,28 @@ class ParamStore:
         self.shadow = None
         if shadow_dtype is not None and shadow_dtype != torch.float32:
             self.shadow = torch.zeros(self.total, device=self.device, dtype=shadow_dtype)
+
+    def style_block(self):
+        """(weight matrix view [sum Cin, 512], bias view [sum Cin], {prefix: column offset}) of the contiguous
+        style group, or None when this store has no modulated convs."""
+        ws = [n for n in self.offsets if n.endswith("modulation.weight")]
+        ws = [n for n in ws if self.offsets[n][0] < self.n_opt]
+        if not ws:
+            return None
+        o0 = self.offsets[ws[0]][0]
+        K = self.shapes[ws[0]][1]
+        cols, off = {}, 0
+        for n in ws:
+            o, numel = self.offsets[n]
+            if o != o0 + off * K:
+                return None
+            cols[n[:-len("modulation.weight")]] = off
+            off += self.shapes[n][0]
+        b0 = self.offsets[ws[0][:-len("weight")] + "bias"][0]
+        for n in ws:
+            if self.offsets[n[:-len("weight")] + "bias"][0] != b0 + cols[n[:-len("modulation.weight")]]:
+                return None
+        return (o0, off, K, b0), cols
 
     def rebind(self, data):
         """Adopt ``data`` (the flat fp32 buffer, possibly on a new device) and move the rest with it."""

@@ -99,7 +99,7 @@ class TrainStep:
         # ------------------------- D phase -------------------------
         if zero_grads:
             self.ds.zero_grad()
-        f16, _, _, _, _, _ = self.ge.forward(z, text, eps_d, anneal, c.psi, train=True, save=False)
+        f16, _, _, _, _, _ = self.ge.forward(z, text, eps_d, anneal, c.psi, train=True, save=False, want_kl=False)
         dres = self.de.d_phase(real, text, f16, ("nhwc", 8), perm, c.r1_gamma)
         d_sumsq = None
         if step_optim:
