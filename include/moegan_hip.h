@@ -158,6 +158,13 @@ int mg_im2col_4x4s2(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t
 /* Discriminator output_layer, image channels: out[b,o] = sum h1[b,o+tap,c] W2[c,tap] (t2i_moe_gan.py:885-907). */
 int mg_disc_head_fwd(int dtype, const void* h1, const float* W2, int B, int Hf, int Cf, float* out, void* stream);
 
+/* Discriminator head as GEMMs (t2i_moe_gan.py:901-907, output_layer: 4x4 valid conv to 1 channel):
+   mg_disc_head_gmat: tap-expanded gradient G[b,y,x,tap] = g[b, y-kh, x-kw] ([B*Hf*Hf, 16]; g_bstride 0
+   broadcasts one map, the R1 path); mg_disc_head_sum: out[b,oy,ox] = sum_tap P[b, oy+kh, ox+kw, tap]
+   for P = h1 @ W2 ([B*Hf*Hf, 16] fp32). */
+int mg_disc_head_gmat(int out_dtype, const float* g, int64_t g_bstride, int B, int Hf, void* G, void* stream);
+int mg_disc_head_sum(const float* P, int B, int Hf, float* out, void* stream);
+
 /* Head backward into features, fused with LeakyReLU' of a1 (g_bstride = 0 broadcasts: R1). */
 int mg_disc_head_bwd_data(int dtype, const float* g, int64_t g_bstride, const float* W2, const void* a1, int B, int Hf, int Cf, int out_dtype, void* ga1, void* stream);
 

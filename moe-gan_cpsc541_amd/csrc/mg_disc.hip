@@ -58,6 +58,45 @@ __global__ void k_head_fwd(const T* __restrict__ h1, const float* __restrict__ W
   if (lane == 0) out[o] = s;
 }
 
+// Head as GEMMs: the 4x4 valid conv to one channel is P = h1 @ W2 ([pixels, 16 taps], an MFMA GEMM)
+// followed by a shifted 16-tap sum, and its backward uses the tap-expanded gradient
+//   G[b, y, x, tap] = g[b, y - kh, x - kw]   (0 outside the Ho x Ho map)
+// so that g_a1 = G @ W2^T (epilogue: * lrelu') and dW2 = h1^T G are GEMMs as well.
+template <typename TO>
+__global__ __launch_bounds__(256) void k_head_gmat(const float* __restrict__ g, int64_t g_bstride, int B, int Hf,
+                                                   TO* __restrict__ G) {
+  const int Ho = Hf - 3;
+  const int n = B * Hf * Hf;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
+    int x = p % Hf, t = p / Hf, y = t % Hf, b = t / Hf;
+    const float* gb = g + (int64_t)b * g_bstride;
+    float v[16];
+#pragma unroll
+    for (int kh = 0; kh < 4; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 4; ++kw) {
+        int oy = y - kh, ox = x - kw;
+        v[kh * 4 + kw] = ((unsigned)oy < (unsigned)Ho && (unsigned)ox < (unsigned)Ho) ? gb[oy * Ho + ox] : 0.f;
+      }
+    st8(G + (int64_t)p * 16, v);
+    st8(G + (int64_t)p * 16 + 8, v + 8);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_head_sum(const float* __restrict__ P, int B, int Hf, float* __restrict__ out) {
+  const int Ho = Hf - 3;
+  const int n = B * Ho * Ho;
+  for (int o = blockIdx.x * 256 + threadIdx.x; o < n; o += gridDim.x * 256) {
+    int ox = o % Ho, t = o / Ho, oy = t % Ho, b = t / Ho;
+    float s = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 4; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 4; ++kw) s += P[((int64_t)(b * Hf + oy + kh) * Hf + ox + kw) * 16 + kh * 4 + kw];
+    out[o] = s;
+  }
+}
+
 // head backward into the image features, fused with conv_layers.2's LeakyReLU:
 //   g_a1[b, y, x, c] = lrelu'(a1[b,y,x,c]) * sum_{oy,ox} g[b, oy, ox] * W2[c, y-oy, x-ox]
 // g_bstride = 0 broadcasts one gradient map to every image (R1: gradient of sum(out)).
@@ -271,6 +310,28 @@ extern "C" int mg_disc_head_fwd(int dtype, const void* h1, const float* W2, int 
   if (dtype == MG_F32) hipLaunchKernelGGL(k_head_fwd<float>, grid, dim3(256), 0, st, (const float*)h1, W2, B, Hf, Cf, out);
   else hipLaunchKernelGGL(k_head_fwd<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)h1, W2, B, Hf, Cf, out);
   return mg_check_launch("mg_disc_head_fwd");
+}
+
+extern "C" int mg_disc_head_gmat(int out_dtype, const float* g, int64_t g_bstride, int B, int Hf, void* G,
+                                 void* stream) {
+  MG_REQUIRE(Hf >= 4, "Hf >= 4");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)B * Hf * Hf;
+  if (n == 0) return MG_OK;
+  if (out_dtype == MG_F32)
+    hipLaunchKernelGGL(k_head_gmat<float>, dim3(nblk(n)), dim3(256), 0, st, g, g_bstride, B, Hf, (float*)G);
+  else
+    hipLaunchKernelGGL(k_head_gmat<bf16_t>, dim3(nblk(n)), dim3(256), 0, st, g, g_bstride, B, Hf, (bf16_t*)G);
+  return mg_check_launch("mg_disc_head_gmat");
+}
+
+extern "C" int mg_disc_head_sum(const float* P, int B, int Hf, float* out, void* stream) {
+  MG_REQUIRE(Hf >= 4, "Hf >= 4");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t n = (int64_t)B * (Hf - 3) * (Hf - 3);
+  if (n == 0) return MG_OK;
+  hipLaunchKernelGGL(k_head_sum, dim3(nblk(n)), dim3(256), 0, st, P, B, Hf, out);
+  return mg_check_launch("mg_disc_head_sum");
 }
 
 extern "C" int mg_disc_head_bwd_data(int dtype, const float* g, int64_t g_bstride, const float* W2, const void* a1,

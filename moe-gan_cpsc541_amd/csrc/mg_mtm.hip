@@ -222,6 +222,72 @@ __global__ void k_up2_fwd(const T* __restrict__ x, int B, int H, int W, int C, T
   }
 }
 
+// 8-channel vector forms (C % 8 == 0); same arithmetic order as the scalar kernels
+template <typename T>
+__global__ __launch_bounds__(256) void k_up2_fwd_v(const T* __restrict__ x, int B, int H, int W, int C,
+                                                   T* __restrict__ out) {
+  const int OH = 2 * H, OW = 2 * W, cv = C >> 3;
+  const int n = B * OH * OW * cv;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    int c = (i % cv) * 8;
+    int pix = i / cv;
+    int ox = pix % OW, t = pix / OW, oy = t % OH, b = t / OH;
+    int y0, y1, x0, x1;
+    float ly, lx;
+    src_idx(oy, H, y0, y1, ly);
+    src_idx(ox, W, x0, x1, lx);
+    const T* xb = x + (int64_t)b * H * W * C + c;
+    float a[8], bb[8], cc[8], dd[8], v[8];
+    ld8(xb + (y0 * W + x0) * C, a);
+    ld8(xb + (y0 * W + x1) * C, bb);
+    ld8(xb + (y1 * W + x0) * C, cc);
+    ld8(xb + (y1 * W + x1) * C, dd);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = (1.f - ly) * ((1.f - lx) * a[j] + lx * bb[j]) + ly * ((1.f - lx) * cc[j] + lx * dd[j]);
+    st8(out + (int64_t)pix * C + c, v);
+  }
+}
+
+template <typename TG, typename T>
+__global__ __launch_bounds__(256) void k_up2_bwd_v(const TG* __restrict__ gout, int B, int H, int W, int C,
+                                                   T* __restrict__ gx, int accumulate) {
+  const int OH = 2 * H, OW = 2 * W, cv = C >> 3;
+  const int n = B * H * W * cv;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    int c = (i % cv) * 8;
+    int pix = i / cv;
+    int ix = pix % W, t = pix / W, iy = t % H, b = t / H;
+    float s[8], g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+    for (int oy = max(0, 2 * iy - 2); oy <= min(OH - 1, 2 * iy + 2); ++oy) {
+      int y0, y1;
+      float ly;
+      src_idx(oy, H, y0, y1, ly);
+      float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
+      if (wy == 0.f) continue;
+      for (int ox = max(0, 2 * ix - 2); ox <= min(OW - 1, 2 * ix + 2); ++ox) {
+        int x0, x1;
+        float lx;
+        src_idx(ox, W, x0, x1, lx);
+        float wx = (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f);
+        if (wx == 0.f) continue;
+        ld8(gout + (((int64_t)b * OH + oy) * OW + ox) * C + c, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += wy * wx * g[j];
+      }
+    }
+    T* dst = gx + (int64_t)pix * C + c;
+    if (accumulate) {
+      ld8(dst, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += g[j];
+    }
+    st8(dst, s);
+  }
+}
+
 template <typename TG, typename T>
 __global__ void k_up2_bwd(const TG* __restrict__ gout, int B, int H, int W, int C, T* __restrict__ gx,
                           int accumulate) {
@@ -298,6 +364,15 @@ extern "C" int mg_offset_head_bwd(int dtype, const float* goff, const void* o1, 
 extern "C" int mg_upsample2x_fwd(int dtype, const void* x, int B, int H, int W, int C, void* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t n = 4LL * B * H * W * C;
+  if (C % 8 == 0 && mg_al16(x) && mg_al16(out) && n / 8 < (1LL << 31)) {
+    int blocks = nblk(n / 8);
+    if (dtype == MG_F32)
+      hipLaunchKernelGGL(k_up2_fwd_v<float>, dim3(blocks), dim3(256), 0, st, (const float*)x, B, H, W, C, (float*)out);
+    else
+      hipLaunchKernelGGL(k_up2_fwd_v<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)x, B, H, W, C,
+                         (bf16_t*)out);
+    return mg_check_launch("mg_upsample2x_fwd");
+  }
   if (dtype == MG_F32)
     hipLaunchKernelGGL(k_up2_fwd<float>, dim3(nblk(n)), dim3(256), 0, st, (const float*)x, B, H, W, C, (float*)out);
   else
@@ -309,6 +384,13 @@ extern "C" int mg_upsample2x_bwd(int gout_dtype, const void* gout, int B, int H,
                                  int accumulate, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t n = (int64_t)B * H * W * C;
+  if (C % 8 == 0 && mg_al16(gout) && mg_al16(gx) && n / 8 < (1LL << 31)) {
+#define L_(TG, T) hipLaunchKernelGGL((k_up2_bwd_v<TG, T>), dim3(nblk(n / 8)), dim3(256), 0, st, (const TG*)gout, B, H, W, C, (T*)gx, accumulate)
+    if (gout_dtype == MG_F32) { if (gx_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+    else { if (gx_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+    return mg_check_launch("mg_upsample2x_bwd");
+  }
 #define L_(TG, T) hipLaunchKernelGGL((k_up2_bwd<TG, T>), dim3(nblk(n)), dim3(256), 0, st, (const TG*)gout, B, H, W, C, (T*)gx, accumulate)
   if (gout_dtype == MG_F32) { if (gx_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
   else { if (gx_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }

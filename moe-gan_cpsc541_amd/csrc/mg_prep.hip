@@ -110,11 +110,11 @@ __global__ void k_colsum(const T* __restrict__ X, int64_t ld, int R, int C, int 
   atomicAdd(out + c, s);
 }
 
-// vectorised column sums: 8 columns per thread, rows split over TY lanes x grid.y, LDS reduction,
-// one atomic per column per block.  C % 8 == 0, 16-B aligned rows.
+// vectorised column sums: 8 columns per thread, rows split over TY lanes x grid.y, LDS reduction into
+// one partial row per row-block (no same-address atomics), folded by k_colsum_fin.  C % 8 == 0.
 template <typename T>
 __global__ __launch_bounds__(256) void k_colsum_v(const T* __restrict__ X, int64_t ld, int R, int C,
-                                                  int rows_per_block, float* __restrict__ out) {
+                                                  int rows_per_block, float* __restrict__ part) {
   __shared__ float red[256 * 8];
   const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int c = (blockIdx.x * TX + tx) * 8;
@@ -137,8 +137,17 @@ __global__ __launch_bounds__(256) void k_colsum_v(const T* __restrict__ X, int64
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += red[(y * TX + tx) * 8 + j];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(out + c + j, acc[j]);
+    for (int j = 0; j < 8; ++j) part[(int64_t)blockIdx.y * C + c + j] = acc[j];
   }
+}
+
+__global__ __launch_bounds__(256) void k_colsum_fin(const float* __restrict__ part, int nparts, int C,
+                                                    float* __restrict__ out) {
+  int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < nparts; ++r) s += part[(int64_t)r * C + c];
+  out[c] += s;
 }
 
 // weight norm: W[o] = g[o] * v[o] / ||v[o]||  (t2i_moe_gan.py:869-886, torch weight_norm dim=0)
@@ -352,9 +361,16 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     // ~512 blocks in total, at least 4 rows per lane
     int rblk = std::max(1, std::min(cdiv(R, 4 * ty), 512 / cblk));
     int rpb = cdiv(R, rblk);
-    dim3 grid(cblk, cdiv(R, rpb));
+    rblk = cdiv(R, rpb);
+    float* part = reinterpret_cast<float*>(mg_workspace((size_t)rblk * C * sizeof(float)));
+    if (!part) {
+      mg_set_error("mg_colsum: workspace allocation failed");
+      return MG_ERR_LAUNCH;
+    }
+    dim3 grid(cblk, rblk);
     DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum_v<T>, grid, dim3(tx, ty), 0, st, reinterpret_cast<const T*>(X), ld,
-                                         R, C, rpb, out));
+                                         R, C, rpb, part));
+    hipLaunchKernelGGL(k_colsum_fin, dim3(cdiv(C, 256)), dim3(256), 0, st, part, rblk, C, out);
     return mg_check_launch("mg_colsum");
   }
   int rpb = std::max(16, R / 256);

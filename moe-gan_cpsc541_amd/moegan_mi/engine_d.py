@@ -60,6 +60,9 @@ class DiscriminatorEngine:
         self.W1cls = ops.pack_dgrad_s2(W["conv_layers.2."], cdt)  # [4, 128, 4*256]
         W2 = W["output_layer.0."].view(384, 16)
         self.W2img = W2[:256]
+        # head as GEMMs: P = h1 @ W2img ([pix, 16 taps]) and g_a1 = G @ W2img^T
+        self.W2img_c = ops.cast(self.W2img.contiguous(), cdt)  # [256 ch, 16 taps]  (KC B operand of g_a1)
+        self.W2t_c = ops.cast(self.W2img.t().contiguous(), cdt)  # [16 taps, 256 ch] (KC B operand of P)
         self.w2sum = ops.gemm(W2[256:], self._ones(16).view(1, 16), 128, 1, 16).view(128)
         self.Wt = W["text_projection.0."]
 
@@ -83,7 +86,9 @@ class DiscriminatorEngine:
 
     def forward(self, img, layout, text, B, H):
         cols, h0, h1 = self.conv_stack(img, layout, B, H)
-        img_part = ops.disc_head_fwd(h1, self.W2img)  # [B, (H/4-3)^2]
+        Hf = H // 4
+        P = ops.gemm(h1.view(-1, 256), self.W2t_c, B * Hf * Hf, 16, 256, out_dtype=torch.float32)
+        img_part = ops.disc_head_sum(P, B, Hf)  # [B, (H/4-3)^2]
         return dict(cols=cols, h0=h0, h1=h1, img_part=img_part, H=H, B=B)
 
     # ------------------------------------------------------------------
@@ -92,10 +97,8 @@ class DiscriminatorEngine:
         Accumulates dW (effective weights) into self.dW; optionally writes the image gradient."""
         B, H = f["B"], f["H"]
         Hf = H // 4
-        g_a1 = torch.empty(B, Hf, Hf, 256, device=self.dev, dtype=self.cdt)
-        ops.disc_head_bwd_data(g_img_part, g_img_part.shape[1], self.W2img, f["h1"], g_a1)
+        g_a1, _ = self._head_bwd(g_img_part, g_img_part.shape[1], f["h1"], B, Hf, want_params)
         if want_params:
-            ops.disc_head_bwd_w(g_img_part, g_img_part.shape[1], f["h1"], self.dW["output_layer.0."])
             ops.conv2d_wgrad(g_a1, f["h0"], 256, 4, 4, 2, 1, self.dW["conv_layers.2."])
             ops.colsum(g_a1.view(-1, 256), self.G("conv_layers.2.bias"))
         g_a0 = torch.empty(B, H // 2, H // 2, 128, device=self.dev, dtype=self.cdt)
@@ -107,6 +110,21 @@ class DiscriminatorEngine:
         if g_input is not None:
             ops.dgrad_s2(g_a0, self.W0cls, 3, g_input)
         return g_a1, g_a0
+
+    def _head_bwd(self, g, g_bstride, h1, B, Hf, want_w, wgrad_input=None):
+        """g_a1 = lrelu'(a1) * (G @ W2img^T) and (optionally) dW2img += X^T G, G the tap-expanded gradient;
+        X = h1 (or ``wgrad_input``, the R1 path's m1 v1)."""
+        Pn = B * Hf * Hf
+        G = ops.disc_head_gmat(g, g_bstride, B, Hf, self.cdt)
+        h1f = h1.view(Pn, 256)
+        g_a1 = torch.empty(B, Hf, Hf, 256, device=self.dev, dtype=self.cdt)
+        ops.gemm(G, self.W2img_c, Pn, 256, 16, out=g_a1.view(Pn, 256),
+                 ep=E_(act=MUL_LRELU_GRAD, aux=h1f, ld_aux=256))
+        if want_w:
+            X = h1f if wgrad_input is None else wgrad_input.view(Pn, 256)
+            dW2img = self.dW["output_layer.0."].view(384, 16)[:256]
+            ops.gemm(X, G, 256, 16, Pn, a_kc=False, b_kc=False, out=dW2img, ep=E_(atomic=1), splits=0)
+        return g_a1, G
 
     def begin_grads(self):
         self.dW = {pre: torch.zeros_like(self.W[pre]) for pre in WN_LAYERS}
@@ -148,8 +166,7 @@ class DiscriminatorEngine:
         Hf = Hr // 4
         Ho = Hf - 3
         g1 = self._ones(Ho * Ho).view(1, -1)
-        gA1 = torch.empty(B, Hf, Hf, 256, device=dev, dtype=self.cdt)
-        ops.disc_head_bwd_data(g1, 0, self.W2img, fr["h1"], gA1)  # m1 * Gh1
+        gA1, G1 = self._head_bwd(g1, 0, fr["h1"], B, Hf, False)  # m1 * Gh1
         gA0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
         ops.dgrad_s2(gA1, self.W1cls, 128, gA0, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
         gx = torch.zeros(B, Hr, Hr, 4, device=dev)
@@ -165,7 +182,9 @@ class DiscriminatorEngine:
         ops.gemm(gA0.view(-1, 128), cols_u, 128, 48, gA0.numel() // 128, a_kc=False, b_kc=False,
                  out=self.dW["conv_layers.0."].view(128, 48), ep=E_(atomic=1), splits=0)
         ops.conv2d_wgrad(gA1, m0v0, 256, 4, 4, 2, 1, self.dW["conv_layers.2."])
-        ops.disc_head_bwd_w(g1, 0, m1v1, self.dW["output_layer.0."])
+        dW2img = self.dW["output_layer.0."].view(384, 16)[:256]
+        ops.gemm(m1v1.view(-1, 256), G1, 256, 16, B * Hf * Hf, a_kc=False, b_kc=False, out=dW2img,
+                 ep=E_(atomic=1), splits=0)
         self._remap_w0()
         self.finish_grads()
         return dict(losses=out, r1=r1, real_pred=real_pred, mism_pred=mism_pred, fake_pred=fake_pred, r1_grad=gx)

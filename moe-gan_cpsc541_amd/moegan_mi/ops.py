@@ -454,6 +454,22 @@ def disc_head_fwd(h1, W2img):
     return out
 
 
+def disc_head_gmat(g, g_bstride, B, Hf, dtype):
+    """Tap-expanded head gradient G [B*Hf*Hf, 16] (mg_disc_head_gmat)."""
+    G = torch.empty(B * Hf * Hf, 16, device=g.device, dtype=dtype)
+    call("mg_disc_head_gmat", L.MG_F32 if dtype == torch.float32 else L.MG_BF16, ptr(g), g_bstride, B, Hf, ptr(G),
+         S())
+    return G
+
+
+def disc_head_sum(P, B, Hf):
+    """out[b, oy*Ho + ox] = sum_tap P[b, oy+kh, ox+kw, tap] (mg_disc_head_sum)."""
+    Ho = Hf - 3
+    out = torch.empty(B, Ho * Ho, device=P.device)
+    call("mg_disc_head_sum", ptr(P), B, Hf, ptr(out), S())
+    return out
+
+
 def disc_head_bwd_data(g, g_bstride, W2img, a1, out):
     B, Hf, _, Cf = out.shape
     call("mg_disc_head_bwd_data", dt(a1), ptr(g), g_bstride, ptr(W2img), ptr(a1), B, Hf, Cf, dt(out), ptr(out), S())
