@@ -277,12 +277,20 @@ extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t
   return mg_check_launch("mg_layernorm_bwd");
 }
 
+int mg_attn_fwd_mfma(const void* qkv, int B, int L, int C, int heads, void* out, float* lse, hipStream_t st);
+int mg_attn_bwd_mfma(const void* qkv, const void* out, const void* gout, const float* lse, int B, int L, int C,
+                     int heads, void* gqkv, hipStream_t st);
+
 extern "C" int mg_attn_fwd(int dtype, const void* qkv, int B, int L, int C, int heads, void* out, float* lse,
                            void* stream) {
   int D = C / heads;
   MG_REQUIRE(D == 16 || D == 32 || D == 64, "head dim must be 16, 32 or 64");
   MG_REQUIRE(L <= 1024, "at most 1024 tokens per image");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_BF16 && B > 0) {  // MFMA path for the model's shapes (exact fp32 parity mode stays scalar)
+    int rc = mg_attn_fwd_mfma(qkv, B, L, C, heads, out, lse, st);
+    if (rc != 1) return rc;
+  }
   int thr = std::max(64, ((L + 63) / 64) * 64);
   size_t sm = 2 * (size_t)L * D * sizeof(float);
 #define L_(T, DD) hipLaunchKernelGGL((k_attn_fwd<T, DD>), dim3(B * heads), dim3(thr), sm, st, (const T*)qkv, L, C, heads, (T*)out, lse)
@@ -301,6 +309,10 @@ extern "C" int mg_attn_bwd(int dtype, int gout_dtype, const void* qkv, const voi
   MG_REQUIRE(D == 16 || D == 32 || D == 64, "head dim must be 16, 32 or 64");
   MG_REQUIRE(L <= 1024, "at most 1024 tokens per image");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_BF16 && gout_dtype == MG_BF16 && B > 0) {
+    int rc = mg_attn_bwd_mfma(qkv, out, gout, lse, B, L, C, heads, gqkv, st);
+    if (rc != 1) return rc;
+  }
   int thr = std::max(64, ((L + 63) / 64) * 64);
   size_t sm = (2 * (size_t)L * D + 2 * (size_t)L) * sizeof(float);
 #define L_(T, TG, DD) hipLaunchKernelGGL((k_attn_bwd<T, TG, DD>), dim3(B * heads), dim3(thr), sm, st, (const T*)qkv, \

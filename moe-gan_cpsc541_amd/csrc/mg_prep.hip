@@ -141,13 +141,18 @@ __global__ __launch_bounds__(256) void k_colsum_v(const T* __restrict__ X, int64
   }
 }
 
+// block (64 columns x 4 partial lanes); out[c] += sum_r part[r, c]
 __global__ __launch_bounds__(256) void k_colsum_fin(const float* __restrict__ part, int nparts, int C,
                                                     float* __restrict__ out) {
-  int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
   float s = 0.f;
-  for (int r = 0; r < nparts; ++r) s += part[(int64_t)r * C + c];
-  out[c] += s;
+  if (c < C)
+    for (int r = ty; r < nparts; r += 4) s += part[(int64_t)r * C + c];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < C) out[c] += red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
 }
 
 // weight norm: W[o] = g[o] * v[o] / ||v[o]||  (t2i_moe_gan.py:869-886, torch weight_norm dim=0)
@@ -359,7 +364,7 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     int ty = 256 / tx;
     int cblk = cdiv(cv, tx);
     // ~512 blocks in total, at least 4 rows per lane
-    int rblk = std::max(1, std::min(cdiv(R, 4 * ty), 512 / cblk));
+    int rblk = std::max(1, std::min({cdiv(R, 4 * ty), 512 / cblk, 64}));
     int rpb = cdiv(R, rblk);
     rblk = cdiv(R, rpb);
     float* part = reinterpret_cast<float*>(mg_workspace((size_t)rblk * C * sizeof(float)));
@@ -370,7 +375,7 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     dim3 grid(cblk, rblk);
     DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum_v<T>, grid, dim3(tx, ty), 0, st, reinterpret_cast<const T*>(X), ld,
                                          R, C, rpb, part));
-    hipLaunchKernelGGL(k_colsum_fin, dim3(cdiv(C, 256)), dim3(256), 0, st, part, rblk, C, out);
+    hipLaunchKernelGGL(k_colsum_fin, dim3(cdiv(C, 64)), dim3(256), 0, st, part, rblk, C, out);
     return mg_check_launch("mg_colsum");
   }
   int rpb = std::max(16, R / 256);

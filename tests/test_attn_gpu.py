@@ -1,0 +1,39 @@
+"""bf16 MFMA self-attention (mg_attn_mfma.hip) vs a plain PyTorch fp32 reference on the same bf16 inputs."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from moegan_mi import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("L,C", [(16, 512), (64, 256), (256, 128), (64, 512), (16, 256), (64, 128)])
+def test_attention_bf16_mfma_vs_fp32(L, C):
+    B, heads = 5, 8
+    D = C // heads
+    g = torch.Generator(device=DEV).manual_seed(L + C)
+    qkv = (torch.randn(B * L, 3 * C, device=DEV, generator=g) * 1.5).bfloat16()
+    gout = torch.randn(B * L, C, device=DEV, generator=g).bfloat16()
+    out, lse = ops.attn_fwd(qkv, B, L, C)
+    g_qkv = ops.attn_bwd(qkv, out, gout, lse, B, L, C)
+    torch.cuda.synchronize()
+    x = qkv.float().view(B, L, 3, heads, D).permute(2, 0, 3, 1, 4).detach().requires_grad_(True)  # [3,B,h,L,D]
+    q, k, v = x[0], x[1], x[2]
+    s = q @ k.transpose(-1, -2) / D ** 0.5
+    o = torch.softmax(s, -1) @ v
+    ref = o.permute(0, 2, 1, 3).reshape(B * L, C)
+    assert rel(out, ref) < 2e-2
+    ref_lse = torch.logsumexp(s, -1)  # [B, h, L]
+    assert (lse.view(B, heads, L) - ref_lse).abs().max().item() < 2e-2
+    ref.backward(gout.float())
+    gref = x.grad.permute(1, 3, 0, 2, 4).reshape(B * L, 3 * C)
+    for part in range(3):
+        sl = slice(part * C, (part + 1) * C)
+        assert rel(g_qkv[:, sl], gref[:, sl]) < 3e-2, part
