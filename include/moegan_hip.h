@@ -77,8 +77,21 @@ typedef struct mg_epilogue {
 const char* mg_last_error(void);
 int mg_version(void);
 /* Tuning override for measurements (key: 0 conv-wgrad tile, 1 grouped-wgrad tile, 2 conv tile,
-   3 gemm tile [64 | 128], 4 conv-wgrad splits, 5 disable split-K slabs; value 0 = automatic). */
+   3 gemm tile [64 | 128], 4 conv-wgrad splits, 5 disable split-K slabs, 6 enable the XCD-aware tile
+   order; value 0 = automatic). */
 int mg_set_tuning(int key, int value);
+
+/* One problem of a batched GEMM launch (mg_gemm_batch): C[M,N] = epilogue(op(A) @ op(B)). */
+typedef struct mg_gemm_desc {
+  int32_t M, N, K;
+  const void* A;
+  int64_t lda;
+  const void* B;
+  int64_t ldb;
+  void* C;
+  int64_t ldc;
+  const mg_epilogue* ep; /* may be NULL */
+} mg_gemm_desc;
 
 /* Generic MFMA GEMM: C[M,N] = epilogue(op(A)[M,K] @ op(B)[K,N]).
  *   a_kc = 1 : A[m*lda + k]     a_kc = 0 : A[k*lda + m]
@@ -90,6 +103,11 @@ int mg_set_tuning(int key, int value);
  * (requires ep->atomic and an fp32 C). */
 int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t lda, int a_kc, const void* B, int64_t ldb,
             int b_kc, void* C, int64_t ldc, int c_dtype, const mg_epilogue* ep, int splits, void* stream);
+
+/* n independent GEMMs of one dtype / orientation / output dtype in as few launches as possible
+   (8 problems per launch, 64x64 tiles, no split-K): the per-layer small GEMMs of the generator (the
+   demodulation coefficients of every modulated conv, router / cross-attention projections). */
+int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, const mg_gemm_desc* descs, void* stream);
 
 /* Implicit-GEMM NHWC convolution (square kernel KHxKW, stride, pad):
  *   y[b,oh,ow,o] = epilogue( sum_{kh,kw,ci} x[b,ih,iw,ci] * in_scale[b,ci] * wpack[o][(kh*KW+kw)*Cin+ci] )

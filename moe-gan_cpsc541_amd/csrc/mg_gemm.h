@@ -26,6 +26,7 @@
 
 namespace mg {
 
+
 constexpr int NTHREADS = 256;
 
 template <typename T> struct Frag;
@@ -375,6 +376,7 @@ struct Grouping {
   const int* row_off;    // [ngroups+1] row (mode 1) / reduction (mode 2) offsets
   const int* tile_off;   // mode 1: [ngroups+1] prefix of ceil(rows_g / BM)
   int rows_per_group;    // mode 3: ngroups equal groups of this many rows (no tables)
+  int swz;               // mode 0: XCD-aware tile order
 };
 
 // ---------------------------------------------------------------------------
@@ -415,8 +417,10 @@ MG_DEV bf16x8_t mc_frag_bf16(const bf16_t* img, int ld, int kr0, int c0, int lan
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// One output tile: C[m0.., n0..] of rows [mrow_base, mrow_base + Mloc) over k in [kbeg, kend).
 template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
-__global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M, int N, int K, int kchunk, Grouping grp) {
+MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, int Mloc, int N, int kbeg, int kend,
+                      int mrow_base) {
   constexpr int VEC = VecOf<T>::N;
   typedef typename VecOf<T>::type vec_t;
   constexpr int TBK = Tile<T>::BK;
@@ -439,41 +443,6 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
-  // ---- resolve tile / group ----
-  int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  int mrow_base = 0;  // global row offset of this group (mode 1)
-  int Mloc = M;
-  int kbeg = blockIdx.z * kchunk, kend = min(K, kbeg + kchunk);
-  int g = 0;
-  if (grp.mode == 1) {
-    int t = blockIdx.x;
-    g = -1;
-    for (int i = 0; i < grp.ngroups; ++i)
-      if (t >= grp.tile_off[i] && t < grp.tile_off[i + 1]) { g = i; break; }
-    if (g < 0) return;
-    mrow_base = grp.row_off[g];
-    Mloc = grp.row_off[g + 1] - mrow_base;
-    m0 = (t - grp.tile_off[g]) * BM;
-  } else if (grp.mode == 3) {
-    int tpg = (grp.rows_per_group + BM - 1) / BM;
-    g = blockIdx.x / tpg;
-    if (g >= grp.ngroups) return;
-    mrow_base = g * grp.rows_per_group;
-    Mloc = grp.rows_per_group;
-    m0 = (blockIdx.x - g * tpg) * BM;
-  } else if (grp.mode == 2) {
-    int splits = gridDim.z / grp.ngroups;
-    g = blockIdx.z / splits;
-    int s = blockIdx.z - g * splits;
-    int r0 = grp.row_off[g], r1 = grp.row_off[g + 1];
-    int per = ((r1 - r0 + splits - 1) / splits + TBK - 1) / TBK * TBK;
-    kbeg = r0 + s * per;
-    kend = min(r1, kbeg + per);
-    if (kbeg >= kend) return;
-  }
-  A.set_group(g);
-  B.set_group(g);
-  ep.set_group(g);
   // in grouped-M mode the A loader / epilogue see absolute rows; clamp via Mloc
   const int mlimit = mrow_base + Mloc;
 
@@ -631,6 +600,84 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   }
 }
 
+
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
+__global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M, int N, int K, int kchunk, Grouping grp) {
+  constexpr int TBK = Tile<T>::BK;
+  // ---- resolve tile / group ----
+  int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  if (grp.mode == 0 && grp.swz) {
+    // XCD-aware tile order: blocks that share an XCD (linear id % 8) take a contiguous run of
+    // (m-tile, n-tile) work items, n fastest -- neighbouring m-tiles (overlapping implicit-conv input
+    // rows) and all n-tiles of one m-tile then meet in the same L2.
+    const int gx = gridDim.x, gy = gridDim.y, nb = gx * gy;
+    const int bid = blockIdx.x + blockIdx.y * gx;
+    const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
+    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    m0 = (w / gy) * BM;
+    n0 = (w - (w / gy) * gy) * BN;
+  }
+  int mrow_base = 0;  // global row offset of this group (mode 1)
+  int Mloc = M;
+  int kbeg = blockIdx.z * kchunk, kend = min(K, kbeg + kchunk);
+  int g = 0;
+  if (grp.mode == 1) {
+    int t = blockIdx.x;
+    g = -1;
+    for (int i = 0; i < grp.ngroups; ++i)
+      if (t >= grp.tile_off[i] && t < grp.tile_off[i + 1]) { g = i; break; }
+    if (g < 0) return;
+    mrow_base = grp.row_off[g];
+    Mloc = grp.row_off[g + 1] - mrow_base;
+    m0 = (t - grp.tile_off[g]) * BM;
+  } else if (grp.mode == 3) {
+    int tpg = (grp.rows_per_group + BM - 1) / BM;
+    g = blockIdx.x / tpg;
+    if (g >= grp.ngroups) return;
+    mrow_base = g * grp.rows_per_group;
+    Mloc = grp.rows_per_group;
+    m0 = (blockIdx.x - g * tpg) * BM;
+  } else if (grp.mode == 2) {
+    int splits = gridDim.z / grp.ngroups;
+    g = blockIdx.z / splits;
+    int s = blockIdx.z - g * splits;
+    int r0 = grp.row_off[g], r1 = grp.row_off[g + 1];
+    int per = ((r1 - r0 + splits - 1) / splits + TBK - 1) / TBK * TBK;
+    kbeg = r0 + s * per;
+    kend = min(r1, kbeg + per);
+    if (kbeg >= kend) return;
+  }
+  A.set_group(g);
+  B.set_group(g);
+  ep.set_group(g);
+  gemm_tile<T, BM, BN, A_KC, B_KC>(A, B, ep, m0, n0, Mloc, N, kbeg, kend, mrow_base);
+}
+
+// ---------------------------------------------------------------------------
+// Batched independent small GEMMs: up to MG_BATCH_MAX problems of one dtype / orientation per launch,
+// described in the kernel arguments; block -> (problem, tile) through a tile prefix.
+// ---------------------------------------------------------------------------
+constexpr int MG_BATCH_MAX = 8;
+template <typename TO, class AL, class BL>
+struct BatchArgs {
+  AL a[MG_BATCH_MAX];
+  BL b[MG_BATCH_MAX];
+  Epi<TO> e[MG_BATCH_MAX];
+  int M[MG_BATCH_MAX], N[MG_BATCH_MAX], K[MG_BATCH_MAX], tiles_n[MG_BATCH_MAX], tile_off[MG_BATCH_MAX + 1];
+  int n;
+};
+
+template <typename T, bool A_KC, bool B_KC, class AL, class BL, typename TO>
+__global__ __launch_bounds__(NTHREADS) void gemm_batch_kernel(BatchArgs<TO, AL, BL> args) {
+  const int t = blockIdx.x;
+  int p = 0;
+  while (p + 1 < args.n && t >= args.tile_off[p + 1]) ++p;
+  const int lt = t - args.tile_off[p];
+  const int tm = lt / args.tiles_n[p], tn = lt - tm * args.tiles_n[p];
+  gemm_tile<T, 64, 64, A_KC, B_KC>(args.a[p], args.b[p], args.e[p], tm * 64, tn * 64, args.M[p], args.N[p], 0,
+                                   args.K[p], 0);
+}
+
 // launch helper: picks the grid; grouped-M launches an upper bound of tiles.
 template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
 inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, int K, int splits, Grouping grp,
@@ -645,6 +692,7 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   dim3 grid(gx, cdiv(N, BN), gz);
   EP e2 = ep;
   e2.vec_ok = e2.host_vec_ok() ? 1 : 0;
+  if (grp.mode == 0) grp.swz = g_mg_tune[MG_TUNE_XCD] == 1 ? 1 : 0;  // measured: no gain at these shapes
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
                      K, kchunk, grp);
 }

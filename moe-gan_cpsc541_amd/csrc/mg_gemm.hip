@@ -201,6 +201,73 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
 }
 
 // ---------------------------------------------------------------------------
+// batched small GEMMs
+// ---------------------------------------------------------------------------
+namespace {
+template <typename T, typename TO, bool AK, bool BKc>
+int run_batch(int n, const mg_gemm_desc* d, hipStream_t st) {
+  using AL = typename std::conditional<AK, LdKC<T>, LdMC<T>>::type;
+  using BL = typename std::conditional<BKc, LdKC<T>, LdMC<T>>::type;
+  for (int i0 = 0; i0 < n; i0 += MG_BATCH_MAX) {
+    BatchArgs<TO, AL, BL> args;
+    int cnt = std::min(MG_BATCH_MAX, n - i0), tiles = 0, used = 0;
+    for (int j = 0; j < cnt; ++j) {
+      const mg_gemm_desc& q = d[i0 + j];
+      if (q.M == 0 || q.N == 0) continue;
+      const mg_epilogue* e = q.ep;
+      const int32_t* aidx = e ? e->a_idx : nullptr;
+      int adiv = (e && e->a_idx_div > 0) ? e->a_idx_div : 1;
+      const float* ars = e ? e->a_rowscale : nullptr;
+      int agelu = e ? e->a_gelu : 0;
+      const T* Ap = reinterpret_cast<const T*>(q.A);
+      const T* Bp = reinterpret_cast<const T*>(q.B);
+      if constexpr (AK) args.a[used] = AL{Ap, q.lda, q.M, q.K, aidx, adiv, ars, agelu};
+      else args.a[used] = AL{Ap, q.lda, q.M, q.K, aidx, adiv, ars, agelu, 0};
+      if constexpr (BKc) args.b[used] = BL{Bp, q.ldb, q.N, q.K, nullptr, 1, nullptr, 0};
+      else args.b[used] = BL{Bp, q.ldb, q.N, q.K, nullptr, 1, nullptr, 0, 0};
+      args.e[used] = make_epi<TO>(q.C, q.ldc, e);
+      args.e[used].vec_ok = args.e[used].host_vec_ok() ? 1 : 0;
+      args.M[used] = q.M;
+      args.N[used] = q.N;
+      args.K[used] = q.K;
+      args.tiles_n[used] = cdiv(q.N, 64);
+      args.tile_off[used] = tiles;
+      tiles += cdiv(q.M, 64) * cdiv(q.N, 64);
+      ++used;
+    }
+    if (!used) continue;
+    args.tile_off[used] = tiles;
+    args.n = used;
+    hipLaunchKernelGGL((gemm_batch_kernel<T, AK, BKc, AL, BL, TO>), dim3(tiles), dim3(NTHREADS), 0, st, args);
+  }
+  return mg_check_launch("mg_gemm_batch");
+}
+}  // namespace
+
+extern "C" int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, const mg_gemm_desc* d,
+                             void* stream) {
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
+  const int vec = dtype == MG_F32 ? 4 : 8;
+  for (int i = 0; i < n; ++i) {
+    const mg_gemm_desc& q = d[i];
+    MG_REQUIRE(q.M >= 0 && q.N >= 0 && q.K >= 0, "negative size");
+    MG_REQUIRE(aligned16(q.A) && aligned16(q.B), "A/B must be 16-byte aligned");
+    MG_REQUIRE(q.lda % vec == 0 && q.ldb % vec == 0, "lda/ldb must be multiples of the 16-byte vector");
+    MG_REQUIRE(a_kc ? (q.K % vec == 0) : (q.M % vec == 0), "A vector dim must be a multiple of the vector");
+    MG_REQUIRE(b_kc ? (q.K % vec == 0) : (q.N % vec == 0), "B vector dim must be a multiple of the vector");
+    MG_REQUIRE(!(q.ep && q.ep->atomic) || c_dtype == MG_F32, "atomic epilogue requires fp32 C");
+  }
+  if (n <= 0) return MG_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define B_(T, TO)                                                   \
+  (a_kc ? (b_kc ? run_batch<T, TO, true, true>(n, d, st) : run_batch<T, TO, true, false>(n, d, st)) \
+        : (b_kc ? run_batch<T, TO, false, true>(n, d, st) : run_batch<T, TO, false, false>(n, d, st)))
+  if (dtype == MG_F32) return c_dtype == MG_F32 ? B_(float, float) : B_(float, bf16_t);
+  return c_dtype == MG_F32 ? B_(bf16_t, float) : B_(bf16_t, bf16_t);
+#undef B_
+}
+
+// ---------------------------------------------------------------------------
 // implicit-GEMM convolution
 // ---------------------------------------------------------------------------
 namespace {

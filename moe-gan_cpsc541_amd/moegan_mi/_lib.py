@@ -28,11 +28,17 @@ class Epilogue(ctypes.Structure):
                 ("add_shift", _i32), ("add_ld", _i64), ("out_pre", _c_void_p), ("ld_pre", _i64)]
 
 
+class GemmDesc(ctypes.Structure):
+    """Mirror of ``mg_gemm_desc`` (include/moegan_hip.h)."""
+    _fields_ = [("M", _i32), ("N", _i32), ("K", _i32), ("A", _c_void_p), ("lda", _i64), ("B", _c_void_p),
+                ("ldb", _i64), ("C", _c_void_p), ("ldc", _i64), ("ep", ctypes.POINTER(Epilogue))]
+
+
 # Argument types are derived from include/moegan_hip.h itself, so the binding
 # cannot drift from the C ABI (the header travels with the library).
 _HEADER = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "moegan_hip.h"))
 _CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "float": _f32, "void": _c_void_p,
-          "mg_epilogue": ctypes.POINTER(Epilogue)}
+          "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc)}
 
 
 def _parse_header(path=_HEADER):
@@ -48,7 +54,7 @@ def _parse_header(path=_HEADER):
                 continue
             base = a.replace("const ", "").split()[0].rstrip("*")
             if "*" in a:
-                types.append(_CTYPE["mg_epilogue"] if base == "mg_epilogue" else _c_void_p)
+                types.append(_CTYPE[base] if base in ("mg_epilogue", "mg_gemm_desc") else _c_void_p)
             else:
                 types.append(_CTYPE[base])
         sigs[name] = types

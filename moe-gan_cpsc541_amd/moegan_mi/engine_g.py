@@ -46,6 +46,8 @@ class GeneratorEngine:
         self._ones = None
         self.style_cols = {}
         self._S = self._S2 = self._GS = None  # batched styles of the running forward / style grads of a backward
+        self._D = None  # demodulation coefficients of the running forward, {prefix: [B, rows]}
+        self._demod_bwd = []
         self._mean_latent = None
         self._want_kl = True
 
@@ -115,7 +117,9 @@ class GeneratorEngine:
         Wt = self.P(pre + "weight")
         k = Wt.shape[-1]
         s, s2 = self._style(pre, w, Cin)
-        d = ops.gemm(s2, pk["wsq"], B, rows, Cin, ep=E_(act=RSQRT))  # demod coefficients [B, rows] (:165)
+        d = self._D.get(pre) if self._D is not None else None
+        if d is None:
+            d = ops.gemm(s2, pk["wsq"], B, rows, Cin, ep=E_(act=RSQRT))  # demod coefficients [B, rows] (:165)
         ep = E_(scale=d, scale_shift=ops.ilog2(HW), scale_ld=rows, act=act, resid=resid,
                 ld_res=resid.shape[-1] if resid is not None else 0)
         xs = ops.scale_bc(x, s)  # x * style, shared by the conv and its weight gradient
@@ -158,12 +162,13 @@ class GeneratorEngine:
             ops.conv2d_wgrad(gyt, xs, rows, k, k, 1, k // 2, tmp)
             self.G(pre + "weight").add_(tmp[:Cout])
         # demodulation backward
+        if batched:  # deferred: all modulated convs' demod + style backward run batched at the end
+            self._demod_bwd.append((pre, gdd, s2, s, gs, Cin, rows, Cout))
+            return
         gwsq = ops.gemm(gdd, s2, rows, Cin, B, a_kc=False, b_kc=False)  # [rows, Cin] = gdd^T s^2
         ops.wsq_bwd(Wt, gwsq[:Cout], self.G(pre + "weight"))
         ops.gemm(gdd, pk["wsq"], B, Cin, rows, b_kc=False, out=gs,
                  ep=E_(alpha=2.0, scale=s, scale_ld=s.stride(0), accumulate=1))  # gs += 2 s (gdd @ wsq)
-        if batched:
-            return  # style = modulation(w): backpropagated for all modulated convs at once (_style_bwd)
         ops.linear_wgrad(gs, w, self.G(pre + "modulation.weight"))
         ops.colsum(gs, self.G(pre + "modulation.bias"))
         ops.gemm(gs, self.P(pre + "modulation.weight"), B, w.shape[1], Cin, b_kc=False, out=gw,
@@ -436,6 +441,15 @@ class GeneratorEngine:
         if self.style_cols:
             self._S = ops.linear(w, self.style_W, bias=self.style_b)
             self._S2 = ops.cast(self._S, square=1)
+            # and every demodulation d = rsqrt(s^2 @ wsq^T + 1e-8) in batched launches (:165)
+            self._D, probs = {}, []
+            for pre, c in self.style_cols.items():
+                pk = self.packs[pre]
+                rows, Cin = pk["rows"], self.P(pre + "weight").shape[1]
+                d = torch.empty(B, rows, device=dev)
+                self._D[pre] = d
+                probs.append(dict(A=self._S2[:, c:c + Cin], B=pk["wsq"], M=B, N=rows, K=Cin, out=d, ep=E_(act=RSQRT)))
+            ops.gemm_batch(probs)
         x = ops.const_fwd(self.P("constant"), B, self.cdt)
         probs, kl2s, topis, blocks = [], [], [], []
         img8, rgb8sv = None, None
@@ -452,7 +466,7 @@ class GeneratorEngine:
             if name == "gen_block_8" and want_img8:
                 img8, rgb8sv = self.mc_fwd("to_rgb_8.", x, w, save=save)
         img16, rgbsv = self.mc_fwd("to_rgb_16.", x, w, save=save)
-        self._S = self._S2 = None
+        self._S = self._S2 = self._D = None
         ctx = None
         if save:
             ctx = dict(B=B, text=text, z=z, t0=t0, t1=t1, tmu=tmu, trs=trs, text_seq=text_seq, hs=hs, h3=h3, w=w,
@@ -469,6 +483,7 @@ class GeneratorEngine:
         g_ts = torch.zeros(B, 512, device=dev)
         if self.style_cols:
             self._GS = torch.zeros(B, self.style_n, device=dev)
+            self._demod_bwd = []
         sv = ctx["rgbsv"]
         x_last = sv[0]
         gx = torch.empty(x_last.shape, device=dev, dtype=self.cdt)
@@ -494,7 +509,18 @@ class GeneratorEngine:
             else:
                 gx = g_in
         ops.const_bwd(gx, self.G("constant"))
-        if self._GS is not None:  # all modulated convs' style backward at once
+        if self._GS is not None:  # all modulated convs' demodulation and style backward at once
+            pw, pg = [], []
+            for pre, gdd, s2, s, gs, Cin, rows, Cout in self._demod_bwd:
+                gwsq = torch.empty(rows, Cin, device=dev)  # gdd^T s^2
+                pw.append(dict(A=gdd, B=s2, M=rows, N=Cin, K=B, out=gwsq, lda=rows, ldb=s2.stride(0)))
+                pg.append(dict(A=gdd, B=self.packs[pre]["wsq"], M=B, N=Cin, K=rows, out=gs, ldc=gs.stride(0),
+                               ep=E_(alpha=2.0, scale=s, scale_ld=s.stride(0), accumulate=1)))  # gs += 2 s (gdd@wsq)
+            ops.gemm_batch(pw, a_kc=False, b_kc=False)
+            ops.gemm_batch(pg, a_kc=True, b_kc=False)
+            for (pre, _, _, _, _, Cin, rows, Cout), q in zip(self._demod_bwd, pw):
+                ops.wsq_bwd(self.P(pre + "weight"), q["out"][:Cout], self.G(pre + "weight"))
+            self._demod_bwd = []
             GS, self._GS = self._GS, None
             ops.linear_wgrad(GS, ctx["w"], self.style_gW)
             ops.colsum(GS, self.style_gb)

@@ -4,6 +4,7 @@ Every function enqueues on torch's current stream and returns its output
 tensor(s).  Shapes follow include/moegan_hip.h: activations are NHWC/token
 rows, weights are in the reference layout unless a ``pack`` says otherwise.
 """
+import ctypes
 import math
 
 import torch
@@ -67,6 +68,23 @@ def gemm(A, B, M, N, K, *, a_kc=True, b_kc=True, out=None, out_dtype=None, lda=N
          ldb if ldb is not None else _ld(B), int(b_kc), ptr(out), ldc if ldc is not None else _ld(out),
          dt(out), ep, splits, S())
     return out
+
+
+def gemm_batch(problems, *, a_kc=True, b_kc=True):
+    """Independent GEMMs in few launches (mg_gemm_batch).  problems: list of dicts with keys
+    A, B, M, N, K, out (preallocated) and optional ep, lda, ldb, ldc.  All share dtype/orientation."""
+    n = len(problems)
+    if n == 0:
+        return
+    arr = (L.GemmDesc * n)()
+    keep = []
+    for i, q in enumerate(problems):
+        A, B, out = q["A"], q["B"], q["out"]
+        ep = q.get("ep")
+        keep.append(ep)
+        arr[i] = L.GemmDesc(q["M"], q["N"], q["K"], ptr(A), q.get("lda", _ld(A)), ptr(B), q.get("ldb", _ld(B)),
+                            ptr(out), q.get("ldc", _ld(out)), ctypes.pointer(ep) if ep is not None else None)
+    call("mg_gemm_batch", dt(problems[0]["A"]), int(a_kc), int(b_kc), dt(problems[0]["out"]), n, arr, S())
 
 
 def linear(x, W, bias=None, act=0, out=None, out_dtype=None, **epk):

@@ -115,3 +115,39 @@ def test_grouped_gemm_and_wgrad(dtype, tol):
     refw = torch.stack([gP[int(row_off[e]):int(row_off[e + 1])].T @ src[int(row_off[e]):int(row_off[e + 1])]
                         for e in range(E)])
     assert rel(gW, refw) < tol * 2
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (1, 0), (0, 0)])
+def test_gemm_batch_matches_individual(dtype, tol, a_kc, b_kc):
+    """mg_gemm_batch: 11 problems of different shapes / epilogues (two launches) == plain GEMMs."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    shapes = [(256, 512, 512), (256, 256, 128), (8, 64, 512), (200, 72, 96), (512, 16, 256), (64, 8, 8),
+              (256, 8, 128), (128, 512, 256), (256, 128, 512), (72, 40, 64), (256, 1024, 256)]
+    probs, refs = [], []
+    for i, (M, N, K) in enumerate(shapes):
+        A = torch.randn(M, K, device=DEV, generator=g)
+        Bm = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+        bias = torch.randn(N, device=DEV, generator=g)
+        As = A.to(dtype) if a_kc else A.T.contiguous().to(dtype)
+        Bs = Bm.to(dtype) if b_kc else Bm.T.contiguous().to(dtype)
+        act = [0, L.ACT_LRELU, L.ACT_RSQRT_EPS][i % 3]
+        Ad, Bd = A.to(dtype).double(), Bm.to(dtype).double()
+        r = Ad @ Bd.T + bias.double()
+        if act == L.ACT_LRELU:
+            r = torch.where(r > 0, r, 0.2 * r)
+        elif act == L.ACT_RSQRT_EPS:
+            r = torch.rsqrt(r.abs() + 1.0)
+            bias = bias + 0  # keep
+        out = torch.empty(M, N, device=DEV)
+        if act == L.ACT_RSQRT_EPS:  # keep the argument positive: add |min| through the bias
+            shift = (Ad @ Bd.T).min().item()
+            bias = bias * 0 + (1.0 - shift)
+            r = torch.rsqrt(Ad @ Bd.T + bias.double() + 1e-8)
+        ep = L.epilogue(bias=bias, act=act)
+        probs.append(dict(A=As, B=Bs, M=M, N=N, K=K, out=out, ep=ep))
+        refs.append(r)
+    ops.gemm_batch(probs, a_kc=a_kc, b_kc=b_kc)
+    torch.cuda.synchronize()
+    for q, r in zip(probs, refs):
+        assert rel(q["out"], r) < tol, (q["M"], q["N"], q["K"])
