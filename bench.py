@@ -42,13 +42,30 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--time-kernel", default="d_conv1",
                     help="kernel whose launches are timed with HIP events for the roofline field")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from Python each step instead of replaying the captured hipGraphs")
+    ap.add_argument("--backend", default="nccl", help="process-group backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box, with --backend gloo)")
     return ap.parse_args()
 
 
-def make_eps(E, dev, gen):
-    dims = [(512, 512), (256, 512), (128, 512)]
-    return [(torch.randn(c, 128, device=dev, generator=gen), torch.randn(t, 128, device=dev, generator=gen),
-             torch.randn(256, E, device=dev, generator=gen)) for c, t in dims]
+EPS_DIMS = [(512, 512), (256, 512), (128, 512)]  # (C, text) per MoE block: eps_f [C,128], eps_t [512,128], eps_c
+
+
+def eps_buffers(E, dev):
+    """One flat buffer holding the router epsilons of one generator forward (3 blocks x (f, t, c)), plus views."""
+    n = sum(c * 128 + t * 128 + 256 * E for c, t in EPS_DIMS)
+    flat = torch.empty(n, device=dev)
+    views, o = [], 0
+    for c, t in EPS_DIMS:
+        trip = []
+        for shp in ((c, 128), (t, 128), (256, E)):
+            k = shp[0] * shp[1]
+            trip.append(flat[o:o + k].view(shp))
+            o += k
+        views.append(tuple(trip))
+    return flat, views
 
 
 def cpu_baseline(args, E, k):
@@ -91,16 +108,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(args.backend, rank=rank, world_size=world)
         pg = dist.group.WORLD
 
     from moegan_mi import ops
+    from moegan_mi.graphs import SegmentedGraph
     from moegan_mi.init import init_discriminator, init_generator
     from moegan_mi.step import StepConfig, TrainStep
 
@@ -113,12 +136,50 @@ def main():
     text = torch.randn(B, 512, device=dev, generator=gen)
     z = torch.randn(B, 512, device=dev, generator=gen)
     eps_gen = torch.Generator(device=dev).manual_seed(3)  # identical router noise on every rank
+    # the step's random inputs live in fixed buffers, refilled before every step (eager or replayed)
+    eps_d_flat, eps_d = eps_buffers(E, dev)
+    eps_g_flat, eps_g = eps_buffers(E, dev)
+    perm = torch.empty(B, device=dev, dtype=torch.int32)
+
+    def refill():
+        eps_d_flat.normal_(generator=eps_gen)  # fresh router noise for both generator forwards (:349-351)
+        eps_g_flat.normal_(generator=eps_gen)
+        perm.copy_(torch.randperm(B, device=dev, generator=gen))
+
+    def run_step():
+        return ts.step(real, text, z, eps_d, eps_g, perm, anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8)
+
+    # live timing of the roofline kernel: D conv_layers.2 forward on the 64x64 real batch
+    # (implicit GEMM M = B*16*16, N = 256, K = 4*4*128); inactive until the timed region
+    want_dims = (B * 256, 256, 2048)
+    ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "conv2d" and dims == want_dims, active=False)
+
+    graph = None
+    if not args.eager:
+        refill()
+        t_w = time.perf_counter()
+        run_step()  # sizes every lazily allocated buffer / workspace
+        torch.cuda.synchronize()
+        t_h = time.perf_counter()
+        run_step()  # host enqueue time of one eager step (diagnostic)
+        t_e = time.perf_counter()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] eager step {(t_h - t_w) * 1e3:.1f} ms; host enqueue of one step {(t_e - t_h) * 1e3:.1f} ms, "
+                  f"with device {(time.perf_counter() - t_h) * 1e3:.1f} ms", file=sys.stderr, flush=True)
+        graph = SegmentedGraph()
+        out = graph.capture(run_step)
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] captured the step: {graph.n_graphs} graph segment(s), {len(graph.items)} items",
+                  file=sys.stderr, flush=True)
 
     def one_step():
-        eps_d = make_eps(E, dev, eps_gen)
-        eps_g = make_eps(E, dev, eps_gen)
-        perm = torch.randperm(B, device=dev, generator=gen).int()
-        return ts.step(real, text, z, eps_d, eps_g, perm, anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8)
+        refill()
+        if graph is not None:
+            graph.replay()
+            return out
+        return run_step()
 
     for i in range(args.warmup):
         t_w = time.perf_counter()
@@ -127,15 +188,11 @@ def main():
         if rank == 0:
             print(f"[bench] warmup step {i}: {(time.perf_counter() - t_w) * 1e3:.1f} ms", file=sys.stderr, flush=True)
 
-    # live timing of the roofline kernel: D conv_layers.2 forward on the 64x64 real batch
-    # (implicit GEMM M = B*16*16, N = 256, K = 4*4*128)
-    want_dims = (B * 256, 256, 2048)
-    ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "conv2d" and dims == want_dims)
+    ops.TIMER.active = True
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    out = None
     for i in range(args.steps):
         out = one_step()
         if rank == 0 and (i + 1) % max(1, args.steps // 4) == 0:
@@ -144,8 +201,8 @@ def main():
     if pg is not None:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    ops.TIMER.active = False
     kt = ops.TIMER.results()
-    ops.TIMER = None
     if pg is not None:
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -185,7 +242,8 @@ def main():
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                 "dtype": args.dtype, "data": "synthetic (U(-1,1) images, N(0,1) 512-d captions, random init)",
                 "config": {"workload": f"C2: 64x64, {E} experts top-{k}, batch {B}/GPU, {args.dtype}, R1 on",
-                           "global_batch": B * world, "experts": E, "topk": k, "parallelism": f"dp{world}"},
+                           "global_batch": B * world, "experts": E, "topk": k, "parallelism": f"dp{world}",
+                           "launch": "eager" if args.eager else "hipGraph replay"},
                 "step_tflops_algorithmic": round(step_tflops, 2),
                 "step_mfma_frac": round(step_tflops / peak, 4), "finite": finite,
                 "roofline": roof, "cpu_baseline": cpu}

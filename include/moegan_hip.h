@@ -309,6 +309,13 @@ int mg_sumsq(const float* x, int64_t n, float* out, void* stream);
 /* torch.optim.AdamW step over a flat fp32 range fused with clip_grad_norm_ (coef from *sumsq, max_norm); t2i_moe_gan.py:1101-1102. */
 int mg_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, int step, const float* sumsq, float max_norm, void* stream);
 
+/* Optimizer prologue for graph-replayable steps: sumsq[0] = 0, step[0] += 1 (the AdamW step counter
+   lives on the device so a captured hipGraph advances it on every replay; torch's state['step']). */
+int mg_opt_prologue(float* sumsq, int32_t* step, void* stream);
+
+/* mg_adamw with the step count read from device memory (*step >= 1); bias corrections on the device. */
+int mg_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, const int32_t* step, const float* sumsq, float max_norm, void* stream);
+
 /* generator constant [1,C,4,4] -> NHWC [B,4,4,C] (t2i_moe_gan.py:815). */
 int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, void* out, void* stream);
 

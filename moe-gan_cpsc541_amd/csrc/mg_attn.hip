@@ -237,6 +237,131 @@ __global__ void k_attn_bwd(const T* __restrict__ qkv, const T* __restrict__ out,
   }
 }
 
+// ---- vectorised LayerNorm: LPR = C/8 lanes per row, each lane 8 consecutive channels (16-B loads);
+// a wave covers 64/LPR rows at once.  Row statistics are reduced over the row's LPR lanes.
+template <int LPR>
+MG_DEV float row_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void k_ln_fwd_v(const T* __restrict__ x, int64_t ldx, int R,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  float eps, T* __restrict__ y, int64_t ldy, float* __restrict__ mean,
+                                                  float* __restrict__ rstd, int act) {
+  constexpr int C = LPR * 8, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sl = lane / LPR, c = (lane % LPR) * 8;
+  float ga[8], be[8];
+  ld8(gamma + c, ga);
+  ld8(beta + c, be);
+  const int nwaves = gridDim.x * (blockDim.x >> 6);
+  for (int r0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW; r0 < R; r0 += nwaves * RPW) {
+    const int r = r0 + sl;
+    const bool ok = r < R;
+    float v[8];
+    if (ok) ld8(x + (int64_t)r * ldx + c, v);
+    else
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j];
+    const float mu = row_sum<LPR>(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q += (v[j] - mu) * (v[j] - mu);
+    const float rs = rsqrtf(row_sum<LPR>(q) / C + eps);
+    if (ok) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = (v[j] - mu) * rs * ga[j] + be[j];
+        if (act) o[j] = lrelu(o[j]);
+      }
+      st8(y + (int64_t)r * ldy + c, o);
+      if (lane % LPR == 0) {
+        mean[r] = mu;
+        rstd[r] = rs;
+      }
+    }
+  }
+}
+
+// backward: each wave walks ROWS_PER_WAVE rows (RPW at a time); gamma/beta gradients are accumulated per lane
+// (fixed channels), folded over the wave's row slots and the block's waves in LDS, one atomic per channel/block.
+template <typename T, typename TG, int LPR>
+__global__ __launch_bounds__(256) void k_ln_bwd_v(const TG* __restrict__ gy, int64_t ldg, const T* __restrict__ x,
+                                                  int64_t ldx, int R, const float* __restrict__ mean,
+                                                  const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                  T* __restrict__ gx, int64_t ldgx, int accumulate,
+                                                  float* __restrict__ ggamma, float* __restrict__ gbeta,
+                                                  int rows_per_wave) {
+  constexpr int C = LPR * 8, RPW = 64 / LPR;
+  __shared__ float red[2][4][C];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sl = lane / LPR, c = (lane % LPR) * 8;
+  float ga[8], pg[8], pb[8];
+  ld8(gamma + c, ga);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pg[j] = pb[j] = 0.f;
+  const int w = blockIdx.x * (blockDim.x >> 6) + wv;
+  const int rbeg = w * rows_per_wave, rend = min(R, rbeg + rows_per_wave);
+  for (int r0 = rbeg; r0 < rend; r0 += RPW) {
+    const int r = r0 + sl;
+    if (r < rend) {
+      const float mu = mean[r], rs = rstd[r];
+      float g[8], xh[8], gh[8];
+      ld8(gy + (int64_t)r * ldg + c, g);
+      ld8(x + (int64_t)r * ldx + c, xh);
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xh[j] = (xh[j] - mu) * rs;
+        gh[j] = g[j] * ga[j];
+        pg[j] += g[j] * xh[j];
+        pb[j] += g[j];
+        s1 += gh[j];
+        s2 += gh[j] * xh[j];
+      }
+      s1 = row_sum<LPR>(s1) / C;
+      s2 = row_sum<LPR>(s2) / C;
+      if (gx) {
+        float o[8];
+        if (accumulate) ld8(gx + (int64_t)r * ldgx + c, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (gh[j] - s1 - xh[j] * s2) + (accumulate ? o[j] : 0.f);
+        st8(gx + (int64_t)r * ldgx + c, o);
+      }
+    }
+  }
+  if (!ggamma) return;
+  // fold the wave's row slots (lanes l, l+LPR, ...) then the block's waves
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1) {
+      pg[j] += __shfl_xor(pg[j], o, 64);
+      pb[j] += __shfl_xor(pb[j], o, 64);
+    }
+  }
+  if (sl == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][wv][c + j] = pg[j];
+      red[1][wv][c + j] = pb[j];
+    }
+  }
+  __syncthreads();
+  const int nw = blockDim.x >> 6;
+  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) {
+    const int k = i / C, cc = i - k * C;
+    float s = 0.f;
+    for (int q = 0; q < nw; ++q) s += red[k][q][cc];
+    atomicAdd((k ? gbeta : ggamma) + cc, s);
+  }
+}
+
 }  // namespace
 
 extern "C" int mg_layernorm_fwd(int dtype, const void* x, int64_t ldx, int R, int C, const float* gamma,
@@ -245,6 +370,18 @@ extern "C" int mg_layernorm_fwd(int dtype, const void* x, int64_t ldx, int R, in
   MG_REQUIRE(C == 128 || C == 256 || C == 512, "C must be 128, 256 or 512");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (R == 0) return MG_OK;
+  if (ldx % 8 == 0 && ldy % 8 == 0 && mg_al16(x) && mg_al16(y) && mg_al16(gamma) && mg_al16(beta)) {
+    const int lpr = C / 8, rpw = 64 / lpr;
+    dim3 g2(std::min(cdiv(R, 4 * rpw), 2048)), b2(256);
+#define LV_(T, P) hipLaunchKernelGGL((k_ln_fwd_v<T, P>), g2, b2, 0, st, (const T*)x, ldx, R, gamma, beta, eps, (T*)y, ldy, mean, rstd, act)
+    if (dtype == MG_F32) {
+      if (C == 128) LV_(float, 16); else if (C == 256) LV_(float, 32); else LV_(float, 64);
+    } else {
+      if (C == 128) LV_(bf16_t, 16); else if (C == 256) LV_(bf16_t, 32); else LV_(bf16_t, 64);
+    }
+#undef LV_
+    return mg_check_launch("mg_layernorm_fwd");
+  }
   dim3 grid(cdiv(R, 4)), blk(256);
 #define L_(T, N) hipLaunchKernelGGL((k_ln_fwd<T, N>), grid, blk, 0, st, (const T*)x, ldx, R, gamma, beta, eps, (T*)y, ldy, mean, rstd, act)
   if (dtype == MG_F32) {
@@ -262,6 +399,25 @@ extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t
   MG_REQUIRE(C == 128 || C == 256 || C == 512, "C must be 128, 256 or 512");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (R == 0) return MG_OK;
+  if (ldg % 8 == 0 && ldx % 8 == 0 && (!gx || ldgx % 8 == 0) && mg_al16(gy) && mg_al16(x) && (!gx || mg_al16(gx)) &&
+      mg_al16(gamma)) {
+    // ~1024 waves; each walks a multiple of the rows it covers at once
+    const int lpr = C / 8, rw = 64 / lpr;
+    int rows = std::max(rw, cdiv(R, 1024));
+    rows = cdiv(rows, rw) * rw;
+    dim3 g2(cdiv(cdiv(R, rows), 4)), b2(256);
+#define LV_(T, TG, P) hipLaunchKernelGGL((k_ln_bwd_v<T, TG, P>), g2, b2, 0, st, (const TG*)gy, ldg, (const T*)x, ldx, R, \
+                                         mean, rstd, gamma, (T*)gx, ldgx, accumulate, ggamma, gbeta, rows)
+#define LVC_(T, TG) if (C == 128) LV_(T, TG, 16); else if (C == 256) LV_(T, TG, 32); else LV_(T, TG, 64)
+    if (dtype == MG_F32) {
+      if (gy_dtype == MG_F32) { LVC_(float, float); } else { LVC_(float, bf16_t); }
+    } else {
+      if (gy_dtype == MG_F32) { LVC_(bf16_t, float); } else { LVC_(bf16_t, bf16_t); }
+    }
+#undef LVC_
+#undef LV_
+    return mg_check_launch("mg_layernorm_bwd");
+  }
   int rpw = std::max(1, std::min(64, R / 1024));
   dim3 grid(cdiv(cdiv(R, rpw), 4)), blk(256);
 #define L_(T, TG, N) hipLaunchKernelGGL((k_ln_bwd<T, TG, N>), grid, blk, 0, st, (const TG*)gy, ldg, (const T*)x, ldx, R, \

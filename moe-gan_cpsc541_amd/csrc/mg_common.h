@@ -48,7 +48,7 @@ MG_DEV void st8(bf16_t* p, const float* v) {
   for (int j = 0; j < 8; ++j) r[j] = f2bf(v[j]);
   *reinterpret_cast<u16x8_t*>(p) = r;
 }
-inline bool mg_al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+__host__ __device__ inline bool mg_al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 MG_DEV float lrelu(float x) { return x > 0.f ? x : 0.2f * x; }
 MG_DEV float lrelu_grad(float y) { return y > 0.f ? 1.f : 0.2f; }
@@ -75,7 +75,8 @@ void mg_set_error(const std::string& msg);
 int mg_check_launch(const char* what);
 // Tuning overrides (0 = automatic), set through mg_set_tuning for A/B measurements.
 enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, MG_TUNE_GEMM_TILE = 3,
-       MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_XCD = 6, MG_TUNE_COUNT = 16 };
+       MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_XCD = 6, MG_TUNE_WGRAD_MODE = 7,
+       MG_TUNE_COUNT = 16 };
 extern int g_mg_tune[MG_TUNE_COUNT];
 // Library-owned device scratch (grown on demand, never shrunk; stream-ordered reuse on one stream).
 void* mg_workspace(size_t bytes);

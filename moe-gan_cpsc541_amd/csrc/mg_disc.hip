@@ -235,16 +235,32 @@ __global__ void k_g_loss(const float* __restrict__ fake, int B, float scale, flo
 }
 
 // R1 (t2i_moe_gan.py:1285-1286): r1 = gamma/2 * mean_b ||g_b||^2; u = gamma/B * g  (d r1 / d g)
+// One block per image: a single same-address atomic per image (a grid of per-chunk blocks serialised
+// ~16k atomics on r1 at the memory side).
 template <typename T, typename TU>
 __global__ void k_r1(const T* __restrict__ g, int64_t per, int B, float gamma, float* __restrict__ r1,
                      TU* __restrict__ u) {
   __shared__ float red[16];
-  int b = blockIdx.y;
+  int b = blockIdx.x;
   float s = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < per; i += (int64_t)gridDim.x * blockDim.x) {
-    float v = ldf(g, (int64_t)b * per + i);
-    s += v * v;
-    if (u) stf(u, (int64_t)b * per + i, gamma / B * v);
+  const T* gb = g + (int64_t)b * per;
+  if ((per & 7) == 0 && mg_al16(gb) && (!u || mg_al16(u + (int64_t)b * per))) {
+    float v[8];
+    for (int64_t i = (int64_t)threadIdx.x * 8; i < per; i += (int64_t)blockDim.x * 8) {
+      ld8(gb + i, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s += v[j] * v[j];
+        v[j] *= gamma / B;
+      }
+      if (u) st8(u + (int64_t)b * per + i, v);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < per; i += blockDim.x) {
+      float v = ldf(gb, i);
+      s += v * v;
+      if (u) stf(u, (int64_t)b * per + i, gamma / B * v);
+    }
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -265,18 +281,32 @@ __global__ void k_mask_mul(const T* __restrict__ a, const TM* __restrict__ m, in
 
 // text branch of the head (t2i_moe_gan.py:895-902): tb[b] = sum_c t[b,c] * w2sum[c] (+ bias)
 //   g_tpre[b,c] = g_tb[b] * w2sum[c] * lrelu'(t[b,c]);  dW2[256+c, tap] += sum_b g_tb[b] * t[b,c]  (all 16 taps)
-__global__ void k_d_text_bwd(const float* __restrict__ g_tb, const float* __restrict__ t,
-                             const float* __restrict__ w2sum, int B, int Ct, int cofs, float* __restrict__ g_tpre,
-                             float* __restrict__ dW2) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= Ct) return;
+// block = 64 columns x 4 image lanes over a chunk of TB_CHUNK images; partial column sums folded in LDS,
+// then one atomic per (column, tap) per block.
+constexpr int TB_CHUNK = 32;
+__global__ __launch_bounds__(256) void k_d_text_bwd(const float* __restrict__ g_tb, const float* __restrict__ t,
+                                                    const float* __restrict__ w2sum, int B, int Ct, int cofs,
+                                                    float* __restrict__ g_tpre, float* __restrict__ dW2) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int b0 = blockIdx.y * TB_CHUNK, b1 = min(B, b0 + TB_CHUNK);
   float acc = 0.f;
-  for (int b = 0; b < B; ++b) {
-    float tv = t[(int64_t)b * Ct + c];
-    acc += g_tb[b] * tv;
-    g_tpre[(int64_t)b * Ct + c] = g_tb[b] * w2sum[c] * lrelu_grad(tv);
+  if (c < Ct) {
+    const float ws = w2sum[c];
+    for (int b = b0 + q; b < b1; b += 4) {
+      float tv = t[(int64_t)b * Ct + c];
+      float gb = g_tb[b];
+      acc += gb * tv;
+      g_tpre[(int64_t)b * Ct + c] = gb * ws * lrelu_grad(tv);
+    }
   }
-  for (int tap = 0; tap < 16; ++tap) dW2[(int64_t)(cofs + c) * 16 + tap] += acc;
+  red[q][cl] = acc;
+  __syncthreads();
+  if (q == 0 && c < Ct) {
+    float s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    for (int tap = 0; tap < 16; ++tap) atomicAdd(&dW2[(int64_t)(cofs + c) * 16 + tap], s);
+  }
 }
 
 inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
@@ -286,7 +316,8 @@ inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t -
 extern "C" int mg_d_text_bwd(const float* g_tb, const float* t, const float* w2sum, int B, int Ct, int cofs,
                              float* g_tpre, float* dW2, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_d_text_bwd, dim3(cdiv(Ct, 128)), dim3(128), 0, st, g_tb, t, w2sum, B, Ct, cofs, g_tpre, dW2);
+  hipLaunchKernelGGL(k_d_text_bwd, dim3(cdiv(Ct, 64), cdiv(B, TB_CHUNK)), dim3(256), 0, st, g_tb, t, w2sum, B, Ct,
+                     cofs, g_tpre, dW2);
   return mg_check_launch("mg_d_text_bwd");
 }
 
@@ -373,7 +404,7 @@ extern "C" int mg_g_loss(const float* fake, int B, float scale, float* out, floa
 extern "C" int mg_r1(int dtype, const void* g, int64_t per, int B, float gamma, float* r1, int u_dtype, void* u,
                      void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid((unsigned)std::min<int64_t>((per + 255) / 256, 64), B);
+  dim3 grid(B);
 #define L_(T, TU) hipLaunchKernelGGL((k_r1<T, TU>), grid, dim3(256), 0, st, (const T*)g, per, B, gamma, r1, (TU*)u)
   if (dtype == MG_F32) { if (u_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
   else { if (u_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }

@@ -369,6 +369,53 @@ void run_wgrad(const void* gy, int64_t ldg, const void* x, int B, int H, int W, 
   auto ep = make_epi<float>(gw, N, &e);
   launch_gemm<T, BM, BN, false, false>(la, lb, ep, Cout, N, P, splits, kNoGroup, 0, st);
 }
+
+// gw[o][ci][tap] += sum_s ws[s][o][tap * Cin + ci]: split-K slabs of a weight gradient folded and moved to the
+// reference [Cout][Cin][KH][KW] layout in one pass (threads walk gw in order: coalesced accumulate).
+__global__ __launch_bounds__(256) void k_wgrad_fold(const float* __restrict__ ws, int splits, int Cout, int lgCin,
+                                                    int taps, float* __restrict__ gw) {
+  const int Cin = 1 << lgCin, N = taps << lgCin;
+  const int64_t MN = (int64_t)Cout * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
+    const int tap = (int)(i % taps);
+    const int64_t oc = i / taps;  // o * Cin + ci
+    const int ci = (int)(oc & (Cin - 1));
+    const int64_t o = oc >> lgCin;
+    const float* src = ws + o * N + (int64_t)tap * Cin + ci;
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += src[s * MN];
+    gw[i] += v;
+  }
+}
+
+// Weight gradient with split-K into fp32 slabs written by the 8-column vector epilogue (coalesced, no atomics),
+// then k_wgrad_fold.  Returns false when the workspace cannot be had (caller falls back to atomics).
+template <typename T, int BM, int BN>
+bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin, const float* sc,
+                     int Cout, int KH, int KW, int stride, int pad, float* gw, int splits, hipStream_t st) {
+  constexpr int TBK = Tile<T>::BK;
+  int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  int P = B * OH * OW, N = KH * KW * Cin;
+  int kchunk = ((P + splits - 1) / splits + TBK - 1) / TBK * TBK;
+  splits = (P + kchunk - 1) / kchunk;
+  const int64_t MN = (int64_t)Cout * N;
+  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float)));
+  if (!ws) return false;
+  LdMC<T> la{reinterpret_cast<const T*>(gy), ldg, Cout, P, nullptr, 1, nullptr, 0, 0};
+  LdMCConv<T> lb{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), P,
+                 KW, stride, pad, N, sc};
+  mg_epilogue raw{};
+  raw.alpha = 1.f;
+  Epi<float> slab = make_epi<float>(ws, N, &raw);
+  slab.zstride = MN;
+  slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
+  dim3 grid(cdiv(Cout, BM), cdiv(N, BN), splits);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, false, LdMC<T>, LdMCConv<T>, Epi<float>>), grid, dim3(NTHREADS),
+                     0, st, la, lb, slab, Cout, N, P, kchunk, kNoGroup);
+  int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 4096);
+  hipLaunchKernelGGL(k_wgrad_fold, dim3(blocks), dim3(256), 0, st, ws, splits, Cout, ilog2(Cin), KH * KW, gw);
+  return true;
+}
 }  // namespace
 
 extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin,
@@ -389,13 +436,28 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
   const int tile = g_mg_tune[MG_TUNE_WGRAD_TILE];
   const bool big = dtype == MG_BF16 && Cout >= 128 && N >= 128 && tile == 128;
   const int64_t tiles = big ? (int64_t)cdiv(Cout, 128) * cdiv(N, 128) : (int64_t)cdiv(Cout, 64) * cdiv(N, 64);
+  const bool slabs = g_mg_tune[MG_TUNE_WGRAD_MODE] == 0;
   if (splits < 1 && g_mg_tune[MG_TUNE_WGRAD_SPLITS] > 0) splits = g_mg_tune[MG_TUNE_WGRAD_SPLITS];
-  if (splits < 1) {  // measured sweet spot: ~576 blocks, >= 2048 pixels per split
-    const int64_t want = big ? 288 : 576;
+  if (splits < 1) {
+    // atomics: measured sweet spot ~576 blocks, >= 2048 pixels per split (the remapped fp32 atomics are
+    // scattered, so few splits); slabs: ~2048 blocks, >= 1024 pixels and <= 16 slabs (measured at B=256:
+    // D conv1 / modconv 8x8 / modconv 16x16 weight gradients 1.36x / 1.2x / 1.6x over ~512 blocks)
+    const int64_t want = slabs ? (big ? 1024 : 2048) : (big ? 288 : 576);
     int64_t t = std::max<int64_t>(tiles, 1);
-    splits = (int)std::max<int64_t>(1, std::min<int64_t>((want + t / 2) / t, P / 2048));
+    splits = (int)std::max<int64_t>(1, std::min<int64_t>((want + t / 2) / t, slabs ? std::min<int64_t>(16, P / 1024)
+                                                                                      : P / 2048));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (slabs && dtype == MG_BF16) {
+    bool ok = big ? run_wgrad_slabs<bf16_t, 128, 128>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad,
+                                                       gw, splits, st)
+                  : run_wgrad_slabs<bf16_t, 64, 64>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw,
+                                                     splits, st);
+    if (ok) return mg_check_launch("mg_conv2d_wgrad (slabs)");
+  } else if (slabs) {
+    if (run_wgrad_slabs<float, 64, 64>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st))
+      return mg_check_launch("mg_conv2d_wgrad (slabs)");
+  }
   if (dtype == MG_F32) run_wgrad<float, 64, 64>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
   else if (big) run_wgrad<bf16_t, 128, 128>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
   else run_wgrad<bf16_t, 64, 64>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);

@@ -236,6 +236,63 @@ __global__ void k_combine(const T* __restrict__ Y, int64_t ldy, const int* __res
   }
 }
 
+// 8-channel vector form of k_combine (same arithmetic order)
+template <typename T>
+__global__ __launch_bounds__(256) void k_combine_v(const T* __restrict__ Y, int64_t ldy, const int* __restrict__ pos_of,
+                                                   const float* __restrict__ gate, int Tn, int k, int C,
+                                                   const T* __restrict__ resid, int64_t ldr, T* __restrict__ out,
+                                                   int64_t ldo) {
+  const int cv = C >> 3;
+  const int n = Tn * cv;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int t = i / cv, c = (i - t * cv) * 8;
+    float s[8], y[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] = 0.f;
+    for (int j = 0; j < k; ++j) {
+      const int a = t * k + j;
+      const float g = gate[a];
+      ld8(Y + (int64_t)pos_of[a] * ldy + c, y);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += g * y[q];
+    }
+    if (resid) {
+      ld8(resid + (int64_t)t * ldr + c, y);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] = y[q] + s[q];
+    }
+    st8(out + (int64_t)t * ldo + c, s);
+  }
+}
+
+// 8-channel vector form of k_token_grad
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void k_token_grad_v(const T* __restrict__ gX, int64_t ldx,
+                                                      const int* __restrict__ pos_of, int Tn, int k, int C,
+                                                      const float* __restrict__ g_raw, const float* __restrict__ Wfc,
+                                                      int E, TO* __restrict__ out, int64_t ldo) {
+  const int cv = C >> 3;
+  const int n = Tn * cv;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int t = i / cv, c = (i - t * cv) * 8;
+    float s[8], v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] = 0.f;
+    if (gX)
+      for (int j = 0; j < k; ++j) {
+        ld8(gX + (int64_t)pos_of[t * k + j] * ldx + c, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] += v[q];
+      }
+    for (int e = 0; e < E; ++e) {
+      const float gr = g_raw[(int64_t)t * E + e];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += gr * Wfc[(int64_t)(c + q) * E + e];
+    }
+    st8(out + (int64_t)t * ldo + c, s);
+  }
+}
+
 // g_gate[a] = <gout[t], Y[pos_of[a]]>, one wave per assignment
 template <typename T, typename TG>
 __global__ void k_gate_grad(const TG* __restrict__ gout, int64_t ldg, const T* __restrict__ Y, int64_t ldy,
@@ -432,6 +489,65 @@ __global__ void k_grouped_colsum(const T* __restrict__ X, int64_t ld, const int*
     s += rs ? v * rs[r] : v;
   }
   atomicAdd(&out[(int64_t)g * N + n], s);
+}
+
+// 8-column vector form: block = TX column vectors x TY row lanes over one chunk of rows.  A thread flushes its
+// running sum to global memory only when its rows cross a group boundary (rare: E boundaries in total); the
+// sums for the chunk's last group are folded over the row lanes in LDS and added once per column.
+template <typename T>
+__global__ __launch_bounds__(256) void k_grouped_colsum_v(const T* __restrict__ X, int64_t ld,
+                                                          const int* __restrict__ idx, int idx_div,
+                                                          const float* __restrict__ rs, const int* __restrict__ row_off,
+                                                          int G, int N, int rows_per_block, float* __restrict__ out) {
+  __shared__ float red[256 * 8];
+  const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
+  const int n = (blockIdx.x * TX + tx) * 8;
+  const int total = row_off[G];
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(total, r0 + rows_per_block);
+  if (r0 >= r1) return;
+  int glast = 0;
+  while (glast < G && row_off[glast + 1] <= r1 - 1) ++glast;
+  float s[8], v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  int g = -1;
+  const bool live = n < N;
+  for (int r = r0 + ty; live && r < r1; r += TY) {
+    if (g < 0 || r >= row_off[g + 1]) {
+      if (g >= 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          atomicAdd(&out[(int64_t)g * N + n + j], s[j]);
+          s[j] = 0.f;
+        }
+      }
+      g = 0;
+      while (g < G && row_off[g + 1] <= r) ++g;
+    }
+    const int src = idx ? idx[r] / idx_div : r;
+    ld8(X + (int64_t)src * ld + n, v);
+    const float sc = rs ? rs[r] : 1.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += rs ? v[j] * sc : v[j];
+  }
+  if (live && g >= 0 && g != glast) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(&out[(int64_t)g * N + n + j], s[j]);
+      s[j] = 0.f;
+    }
+  }
+  const int tid = ty * TX + tx;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = s[j];
+  __syncthreads();
+  if (ty == 0 && live) {
+    for (int y = 1; y < TY; ++y)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += red[(y * TX + tx) * 8 + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&out[(int64_t)glast * N + n + j], s[j]);
+  }
 }
 
 // KL of one router, two passes: per-block partial sums over the three (mu, rho) pairs, then one block
@@ -639,6 +755,17 @@ extern "C" int mg_moe_combine(int dtype, const void* Y, int64_t ldy, const int32
                               int k, int C, const void* resid, int64_t ldr, void* out, int64_t ldo, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t n = (int64_t)T * C;
+  if (C % 8 == 0 && ldy % 8 == 0 && ldo % 8 == 0 && (!resid || ldr % 8 == 0) && mg_al16(Y) && mg_al16(out) &&
+      (!resid || mg_al16(resid)) && n / 8 < (1LL << 31)) {
+    int blocks = nblk(n / 8);
+    if (dtype == MG_F32)
+      hipLaunchKernelGGL(k_combine_v<float>, dim3(blocks), dim3(256), 0, st, (const float*)Y, ldy, pos_of, gate, T, k,
+                         C, (const float*)resid, ldr, (float*)out, ldo);
+    else
+      hipLaunchKernelGGL(k_combine_v<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)Y, ldy, pos_of, gate, T,
+                         k, C, (const bf16_t*)resid, ldr, (bf16_t*)out, ldo);
+    return mg_check_launch("mg_moe_combine");
+  }
   if (dtype == MG_F32)
     hipLaunchKernelGGL(k_combine<float>, dim3(nblk(n)), dim3(256), 0, st, (const float*)Y, ldy, pos_of, gate, T, k, C,
                        (const float*)resid, ldr, (float*)out, ldo);
@@ -682,6 +809,13 @@ extern "C" int mg_moe_token_grad(int dtype, const void* gX, int64_t ldx, const i
                                  void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t n = (int64_t)T * C;
+  if (C % 8 == 0 && (!gX || (ldx % 8 == 0 && mg_al16(gX))) && ldo % 8 == 0 && mg_al16(out) && n / 8 < (1LL << 31)) {
+#define LV_(TT, TO) hipLaunchKernelGGL((k_token_grad_v<TT, TO>), dim3(nblk(n / 8)), dim3(256), 0, st, (const TT*)gX, ldx, pos_of, T, k, C, g_raw, Wfc, E, (TO*)out, ldo)
+    if (dtype == MG_F32) { if (out_dtype == MG_F32) LV_(float, float); else LV_(float, bf16_t); }
+    else { if (out_dtype == MG_F32) LV_(bf16_t, float); else LV_(bf16_t, bf16_t); }
+#undef LV_
+    return mg_check_launch("mg_moe_token_grad");
+  }
 #define L_(TT, TO) hipLaunchKernelGGL((k_token_grad<TT, TO>), dim3(nblk(n)), dim3(256), 0, st, (const TT*)gX, ldx, pos_of, T, k, C, g_raw, Wfc, E, (TO*)out, ldo)
   if (dtype == MG_F32) { if (out_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
   else { if (out_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
@@ -708,6 +842,20 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
 extern "C" int mg_grouped_colsum(int dtype, const void* X, int64_t ld, const int32_t* idx, int idx_div, const float* rs,
                                  const int32_t* row_off, int G, int N, int max_rows, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (N % 8 == 0 && ld % 8 == 0 && mg_al16(X) && max_rows > 0) {
+    const int cv = N / 8, tx = std::min(cv, 64), ty = 256 / tx;
+    const int cblk = cdiv(cv, tx);
+    // ~1024 blocks, at least 8 rows per row lane
+    int rpb = std::max(8 * ty, cdiv(max_rows, std::max(1, 1024 / cblk)));
+    dim3 grid(cblk, cdiv(max_rows, rpb)), blk(tx, ty);
+    if (dtype == MG_F32)
+      hipLaunchKernelGGL(k_grouped_colsum_v<float>, grid, blk, 0, st, (const float*)X, ld, idx,
+                         idx_div > 0 ? idx_div : 1, rs, row_off, G, N, rpb, out);
+    else
+      hipLaunchKernelGGL(k_grouped_colsum_v<bf16_t>, grid, blk, 0, st, (const bf16_t*)X, ld, idx,
+                         idx_div > 0 ? idx_div : 1, rs, row_off, G, N, rpb, out);
+    return mg_check_launch("mg_grouped_colsum");
+  }
   int rpb = std::max(64, max_rows / 512);
   dim3 grid(cdiv(N, 256), cdiv(max_rows, rpb));
   if (dtype == MG_F32)

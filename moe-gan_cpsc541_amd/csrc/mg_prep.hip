@@ -207,10 +207,18 @@ __global__ void k_wn_bwd(const float* __restrict__ v, const float* __restrict__ 
 }
 
 // sum of squares of n floats, accumulated into out[0]
+// (<= 256 blocks: every block ends in one same-address atomic, and those serialise at the memory side)
 __global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
   __shared__ float red[16];
   float s = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t nv = mg_al16(x) ? n / 4 : 0;
+  const f32x4_t* x4 = reinterpret_cast<const f32x4_t*>(x);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4_t v = x4[i];
+    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  for (int64_t i = nv * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
     float v = x[i];
     s += v * v;
   }
@@ -229,6 +237,38 @@ __global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restric
 __global__ void k_adamw(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                         float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
                         float bc1, float bc2_sqrt, const float* __restrict__ sumsq, float max_norm) {
+  float coef = 1.f;
+  if (sumsq) {
+    float tn = sqrtf(sumsq[0]);
+    coef = fminf(max_norm / (tn + 1e-6f), 1.f);
+  }
+  float step_size = lr / bc1;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * coef;
+    float pi = p[i] * (1.f - lr * wd);
+    float mi = m[i] + (gi - m[i]) * (1.f - b1);
+    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi - step_size * (mi / denom);
+  }
+}
+
+__global__ void k_opt_prologue(float* __restrict__ sumsq, int32_t* __restrict__ step) {
+  if (threadIdx.x == 0) {
+    sumsq[0] = 0.f;
+    step[0] += 1;
+  }
+}
+
+// k_adamw with the bias corrections derived on the device from the step counter
+__global__ void k_adamw_dev(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                            const int32_t* __restrict__ step, const float* __restrict__ sumsq, float max_norm) {
+  const float t = (float)step[0];
+  const float bc1 = 1.f - powf(b1, t);
+  const float bc2_sqrt = sqrtf(1.f - powf(b2, t));
   float coef = 1.f;
   if (sumsq) {
     float tn = sqrtf(sumsq[0]);
@@ -401,7 +441,7 @@ extern "C" int mg_weight_norm_bwd(const float* v, const float* g, const float* n
 extern "C" int mg_sumsq(const float* x, int64_t n, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (n == 0) return MG_OK;
-  hipLaunchKernelGGL(k_sumsq, dim3(std::min(nblk(n), 1024)), dim3(256), 0, st, x, n, out);
+  hipLaunchKernelGGL(k_sumsq, dim3(std::min(nblk(n / 4 + 1), 256)), dim3(256), 0, st, x, n, out);
   return mg_check_launch("mg_sumsq");
 }
 
@@ -415,6 +455,24 @@ extern "C" int mg_adamw(float* p, const float* g, float* m, float* v, int64_t n,
   hipLaunchKernelGGL(k_adamw, dim3(std::min(nblk(n), 4096)), dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps,
                      weight_decay, bc1, sqrtf(bc2), sumsq, max_norm);
   return mg_check_launch("mg_adamw");
+}
+
+extern "C" int mg_opt_prologue(float* sumsq, int32_t* step, void* stream) {
+  MG_REQUIRE(sumsq && step, "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_opt_prologue, dim3(1), dim3(64), 0, st, sumsq, step);
+  return mg_check_launch("mg_opt_prologue");
+}
+
+extern "C" int mg_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                            float beta2, float eps, float weight_decay, const int32_t* step, const float* sumsq,
+                            float max_norm, void* stream) {
+  MG_REQUIRE(step, "null step counter");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) return MG_OK;
+  hipLaunchKernelGGL(k_adamw_dev, dim3(std::min(nblk(n), 4096)), dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2,
+                     eps, weight_decay, step, sumsq, max_norm);
+  return mg_check_launch("mg_adamw_dev");
 }
 
 extern "C" int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, void* out, void* stream) {

@@ -257,10 +257,11 @@ class GeneratorEngine:
         Hd = 4 * C
         # tokens in dispatch order (k copies per token), shared by the expert GEMM and its weight gradient
         Xg = ops.gather_rows(tok, perm, k)
-        Pre = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+        # the pre-activation is kept only for the backward's GELU' (a no-grad forward skips that store)
+        Pre = torch.empty(n, Hd, device=self.dev, dtype=self.cdt) if save else None
         Hid = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
         ops.gemm_grouped(Xg, W1, row_off, tile_off, max_tiles, Hd, C, b_gstride=Hd * C, out=Hid, ldb=C,
-                         ep=E_(bias=b1, act=GELU, out_pre=Pre, ld_pre=Hd))
+                         ep=E_(bias=b1, act=GELU, out_pre=Pre, ld_pre=Hd if save else 0))
         Y = torch.empty(n, C, device=self.dev, dtype=self.cdt)
         ops.gemm_grouped(Hid, W2, row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y, ldb=Hd,
                          ep=E_(bias=b2))

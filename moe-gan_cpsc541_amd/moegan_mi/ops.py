@@ -20,18 +20,19 @@ def _ld(t):
 
 
 # Optional live kernel timer (bench.py): when set, launches whose (kind, dims) satisfy
-# TIMER.want(kind, dims) are bracketed by HIP events on the current stream.
+# TIMER.want(kind, dims) are bracketed by HIP events on the current stream while TIMER.active.
+# Under graph capture such a launch becomes an eager segment (graphs.eager), so the events
+# still bracket exactly that kernel on every replay.
 TIMER = None
 
 
 class KernelTimer:
-    def __init__(self, want):
+    def __init__(self, want, active=True):
         self.want = want
+        self.active = active
         self.events = []  # (kind, dims, start, end)
 
-    def wrap(self, kind, dims, fn):
-        if not self.want(kind, dims):
-            return fn()
+    def record(self, kind, dims, fn):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         r = fn()
@@ -44,10 +45,18 @@ class KernelTimer:
         return [(k, d, s.elapsed_time(e)) for k, d, s, e in self.events]
 
 
-def _timed(kind, dims, fn):
-    if TIMER is None:
+def _timed_run(kind, dims, fn):
+    t = TIMER
+    if t is None or not t.active:
         return fn()
-    return TIMER.wrap(kind, dims, fn)
+    return t.record(kind, dims, fn)
+
+
+def _timed(kind, dims, fn):
+    if TIMER is None or not TIMER.want(kind, dims):
+        return fn()
+    from . import graphs
+    return graphs.eager(lambda: _timed_run(kind, dims, fn))
 
 
 def ilog2(v):
@@ -239,6 +248,16 @@ def sumsq(x, out):
 def adamw(p, g, m, v, lr, beta1, beta2, eps, wd, step, sumsq_buf=None, max_norm=0.0):
     call("mg_adamw", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps, wd, step, ptr(sumsq_buf),
          max_norm, S())
+
+
+def opt_prologue(sumsq_buf, step_dev):
+    """sumsq_buf[0] = 0; step_dev[0] += 1 (device-side AdamW step counter, graph-replayable)."""
+    call("mg_opt_prologue", ptr(sumsq_buf), ptr(step_dev), S())
+
+
+def adamw_dev(p, g, m, v, lr, beta1, beta2, eps, wd, step_dev, sumsq_buf=None, max_norm=0.0):
+    call("mg_adamw_dev", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps, wd, ptr(step_dev),
+         ptr(sumsq_buf), max_norm, S())
 
 
 def const_fwd(cst, B, dtype):

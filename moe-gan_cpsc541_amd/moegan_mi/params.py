@@ -87,7 +87,8 @@ class ParamStore:
         self.grad = torch.zeros(self.total, device=self.device, dtype=torch.float32)
         self.m = torch.zeros(self.total, device=self.device, dtype=torch.float32)
         self.v = torch.zeros(self.total, device=self.device, dtype=torch.float32)
-        self.step_count = 0
+        self.step_count = 0  # host mirror (eager steps); the optimizer reads the device counter below
+        self.step_dev = torch.zeros(1, device=self.device, dtype=torch.int32)
         self.buffers = OrderedDict((n, torch.zeros(s, device=self.device)) for n, s in self.shapes.items()
                                    if is_buffer(n))
         self.shadow_dtype = shadow_dtype
@@ -125,6 +126,7 @@ class ParamStore:
             self.grad = self.grad.to(dev)
             self.m = self.m.to(dev)
             self.v = self.v.to(dev)
+            self.step_dev = self.step_dev.to(dev)
             self.buffers = OrderedDict((n, b.to(dev)) for n, b in self.buffers.items())
             if self.shadow is not None:
                 self.shadow = torch.zeros(self.total, device=dev, dtype=self.shadow_dtype)

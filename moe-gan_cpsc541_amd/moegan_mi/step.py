@@ -16,7 +16,7 @@ RCCL) all-reduces the flat D and G gradient buffers and the [E] expert-load vect
 """
 import torch
 
-from . import ops
+from . import graphs, ops
 from .engine_d import DiscriminatorEngine
 from .engine_g import GeneratorEngine
 from .layout import discriminator_shapes, generator_shapes
@@ -55,18 +55,22 @@ class TrainStep:
         self.clip_encoder = None  # optional image encoder for the (gradient-free) CLIP loss
 
     # ---- data-parallel reductions ----
+    # (collectives stay eager segments when the step is replayed as hipGraphs, graphs.py)
     def _allreduce_mean(self, t):
         if self.pg is None:
             return
         import torch.distributed as dist
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
-        t.mul_(1.0 / self.world)
+
+        def run():
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+            t.mul_(1.0 / self.world)
+        graphs.eager(run)
 
     def _allreduce_sum(self, t):
         if self.pg is None:
             return
         import torch.distributed as dist
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+        graphs.eager(lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg))
 
     # ---- optimizer ----
     def _adamw(self, store, lr, max_norm, n=None, grad_scale=1.0):
@@ -74,11 +78,12 @@ class TrainStep:
         store.step_count += 1
         if grad_scale != 1.0:  # (loss / accumulation_steps) of the reference == scaling the summed gradient
             store.grad[:n].mul_(grad_scale)
-        ss = torch.zeros(1, device=self.dev)
+        ss = torch.empty(1, device=self.dev)
+        ops.opt_prologue(ss, store.step_dev)  # ss = 0, device step counter += 1 (graph-replayable)
         ops.sumsq(store.grad[:n], ss)
         c = self.cfg
-        ops.adamw(store.data[:n], store.grad[:n], store.m[:n], store.v[:n], lr, c.beta1, c.beta2, c.eps,
-                  c.weight_decay, store.step_count, ss, max_norm)
+        ops.adamw_dev(store.data[:n], store.grad[:n], store.m[:n], store.v[:n], lr, c.beta1, c.beta2, c.eps,
+                      c.weight_decay, store.step_dev, ss, max_norm)
         return ss
 
     # ---- the step ----
