@@ -10,18 +10,17 @@
 //   T = float  : v_mfma_f32_16x16x4_f32   (exact fp32, the parity mode)
 //
 // Operand access is delegated to loader structs so one kernel body serves
-// plain / transposed operands, implicit NHWC convolutions (with the
-// modulated-conv style scale fused into the load), row gathers for expert
-// dispatch and GELU-on-load for expert hidden activations.
-//
-//   KC loader (reduction index contiguous in memory):
-//      RowState row(int r) const;  vec load(const RowState&, int k0, int kofs) const;
-//   MC loader (output index contiguous, reduction index strided):
-//      ColState col(int c0) const; vec load(const ColState&, int k) const;  (c0..c0+VEC-1)
+// plain / transposed operands, implicit NHWC convolutions, the parity-class
+// split of a stride-2 data gradient, per-group weights for expert batches and
+// (XF instantiations only) row gathers, GELU-on-load and modulation scales.
+// Loads are raw buffer loads with hardware zero-fill for out-of-range slots;
+// see the Loaders section.
 //
 // Grouping (expert batches) is resolved per block from device-side offset
 // tables, so no host synchronisation is needed to size the launch.
 #pragma once
+#include <type_traits>
+
 #include "mg_common.h"
 
 namespace mg {
@@ -61,120 +60,197 @@ MG_DEV u16x8_t vgelu(u16x8_t v) {
 // ---------------------------------------------------------------------------
 // Loaders
 // ---------------------------------------------------------------------------
-// KC, plain rows with optional row gather / per-row scale / GELU-on-load.
+// Every operand vector is fetched by a raw buffer load through a wave-uniform descriptor covering
+// [0, 2^31) bytes.  A slot that must read zeros (row past M, padding tap, K tail) is given the
+// out-of-range offset MG_OOB and the hardware returns 0: no exec-mask branches, no selects on the
+// loaded data.  Per-slot state (byte offset of the slot's row / column, valid-tap masks) is computed
+// once before the K loop, so a K step costs at most a few VALU per vector (0 for plain operands,
+// whose K advance rides in the scalar offset).
+//
+// XF = the operand needs a transform (row gather, GELU-on-load, row / channel scale).  Transforms
+// are applied by fix() when the staged registers are written to LDS -- after the MFMAs of the
+// step -- so they never wait on a load that is still in flight.  The fast instantiations (XF =
+// false) carry none of that code.
+//
+//   KC loader (reduction index contiguous): Slot slot(int row, int kofs, bool ok)
+//   MC loader (output index contiguous):   Slot slot(int col0, int kofs, bool ok)
+//   both:  template <bool TAIL, int TBK> vec load(rsrc, const Slot&, int k0, int kend)
+//          void fix(const Slot&, int k0, vec&)      (XF only)
+// Offsets are 32-bit: every operand tensor must be < 2 GiB (checked on the host).
+
+constexpr uint32_t MG_OOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+MG_DEV rsrc_t make_rsrc(const void* p) {
+  // the base is wave-uniform (kernel argument / block-derived); readfirstlane makes that provable so the
+  // compiler keeps the descriptor in SGPRs (no waterfall loops around the loads)
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+template <typename V> MG_DEV V bload(rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+// KC, plain rows with optional row gather / per-row scale / GELU-on-load (XF).
 //   row r -> source row (idx ? idx[r] / idx_div : r); value *= rs[r] if rs
-template <typename T>
+template <typename T, bool XF = false>
 struct LdKC {
+  typedef typename VecOf<T>::type vec_t;
   const T* p; int64_t ld; int rows; int K;
   const int* idx; int idx_div;   // gather: source row = idx[r] / idx_div
   const float* rs;               // optional per-row scale (indexed by r)
   int gelu;                      // apply GELU to loaded values
-  struct RowState { const T* base; float s; };
-  struct ColState {};
+  struct Slot { uint32_t off; int kofs; float s; };
   MG_DEV void set_group(int) {}
-  MG_DEV RowState row(int r) const {
-    RowState st{nullptr, 1.f};
-    if (r < rows) {
-      int src = idx ? idx[r] / idx_div : r;
-      st.base = p + (int64_t)src * ld;
-      if (rs) st.s = rs[r];
+  MG_DEV rsrc_t rsrc() const { return make_rsrc(p); }
+  MG_DEV Slot slot(int r, int kofs, bool ok) const {
+    Slot s{MG_OOB, kofs, 1.f};
+    if (ok && r < rows) {
+      int src = r;
+      if constexpr (XF) {
+        if (idx) src = idx[r] / idx_div;
+        if (rs) s.s = rs[r];
+      }
+      s.off = (uint32_t)(((int64_t)src * ld + kofs) * (int64_t)sizeof(T));
     }
-    return st;
+    return s;
   }
-  MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
-    int k = k0 + kofs;
-    if (!st.base || k >= K) return vzero<T>();
-    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(st.base + k);
-    if (gelu) v = vgelu(v);
-    if (rs) v = vscale1(v, st.s);
-    return v;
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+    uint32_t off = s.off;
+    if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
+    return bload<vec_t>(r, off, (uint32_t)k0 * (uint32_t)sizeof(T));
+  }
+  MG_DEV void fix(const Slot& s, int, vec_t& v) const {
+    if constexpr (XF) {
+      if (gelu) v = vgelu(v);
+      if (rs) v = vscale1(v, s.s);
+    }
   }
 };
 
 // KC, implicit NHWC convolution: row = output pixel (b, oh, ow), k = tap*Cin + ci.
-// Requires Cin % VEC == 0 (one tap per vector) and power-of-two OH/OW/Cin.
-template <typename T>
+// Requires Cin % VEC == 0 (one tap per vector) and power-of-two OH/OW/Cin; KH*KW <= 32.
+// The slot keeps the byte offset of its pixel's tap (0, 0) and a bit mask of the taps that fall
+// inside the image.  SC = false (Cin >= TBK): a K step lies inside one tap, so the tap and its offset
+// are wave-uniform scalars and a vector costs 4 VALU; SC = true (small Cin): per-lane tap.
+template <typename T, bool XF = false, bool SC = false>
 struct LdKCConv {
+  typedef typename VecOf<T>::type vec_t;
   const T* x; int H, W, Cin, lgCin, lgOW, lgOHW, M;
   int KW, stride, pad, K;
-  const float* scale;  // optional [B, Cin] per-sample input-channel scale (modulation)
+  const float* scale;  // optional [B, Cin] per-sample input-channel scale (modulation), XF only
   int kwinv;           // (tap * kwinv) >> 16 == tap / KW for every tap of the kernel
-  struct RowState { const T* base; int ih0, iw0, b; };
-  struct ColState {};
+  struct Slot { int32_t base; uint32_t mask; int kofs; int b; };
   MG_DEV void set_group(int) {}
-  MG_DEV RowState row(int r) const {
-    RowState st;
-    if (r >= M) { st.b = -1; st.base = x; st.ih0 = st.iw0 = 0; return st; }
-    st.b = r >> lgOHW;
-    int rem = r & ((1 << lgOHW) - 1);
-    int oh = rem >> lgOW, ow = rem & ((1 << lgOW) - 1);
-    st.ih0 = oh * stride - pad;
-    st.iw0 = ow * stride - pad;
-    // pointer of tap (0, 0), channel 0 (may point outside the image; only dereferenced in bounds)
-    st.base = x + ((((int64_t)st.b * H + st.ih0) * W + st.iw0) << lgCin);
-    return st;
+  MG_DEV rsrc_t rsrc() const { return make_rsrc(x); }
+  MG_DEV Slot slot(int r, int kofs, bool ok) const {
+    Slot s{0, 0u, kofs, 0};
+    if (!ok || r >= M) return s;
+    s.b = r >> lgOHW;
+    const int rem = r & ((1 << lgOHW) - 1);
+    const int oh = rem >> lgOW, ow = rem & ((1 << lgOW) - 1);
+    const int ih0 = oh * stride - pad, iw0 = ow * stride - pad;
+    s.base = (((s.b * H + ih0) * W + iw0) << lgCin) * (int)sizeof(T);
+    const int KH = (K >> lgCin) / KW;
+    uint32_t m = 0;
+    for (int kh = 0; kh < KH; ++kh)
+      for (int kw = 0; kw < KW; ++kw)
+        if ((unsigned)(ih0 + kh) < (unsigned)H && (unsigned)(iw0 + kw) < (unsigned)W) m |= 1u << (kh * KW + kw);
+    s.mask = m;
+    return s;
   }
-  MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
-    int k = k0 + kofs;
-    if (st.b < 0 || k >= K) return vzero<T>();
-    int tap = k >> lgCin;
-    int ci = k & (Cin - 1);
-    int kh = (tap * kwinv) >> 16, kw = tap - kh * KW;
-    if ((unsigned)(st.ih0 + kh) >= (unsigned)H || (unsigned)(st.iw0 + kw) >= (unsigned)W) return vzero<T>();
-    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(st.base + (((int64_t)(kh * W + kw)) << lgCin) + ci);
-    if (scale) v = vscale(v, scale + (int64_t)st.b * Cin + ci);
-    return v;
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+    const int k = k0 + s.kofs;
+    const int kk = SC ? k : k0;  // SC = false: k0 is a multiple of TBK <= Cin, the step stays inside tap k0 / Cin
+    const int tap = kk >> lgCin;
+    const int kh = (tap * kwinv) >> 16, kw = tap - kh * KW;
+    const int tapoff = (((kh * W + kw) << lgCin) + (kk & (Cin - 1))) * (int)sizeof(T);
+    // invalid tap -> bit 31 set (out of range); arithmetic, not a select, so no branch is formed
+    uint32_t off = (uint32_t)(s.base + tapoff + (SC ? 0 : s.kofs * (int)sizeof(T))) | ((~s.mask >> tap) << 31);
+    if constexpr (TAIL) off = k < kend ? off : MG_OOB;
+    return bload<vec_t>(r, off, 0);
+  }
+  MG_DEV void fix(const Slot& s, int k0, vec_t& v) const {
+    if constexpr (XF) {
+      if (scale) v = vscale(v, scale + (int64_t)s.b * Cin + ((k0 + s.kofs) & (Cin - 1)));
+    }
   }
 };
 
-// MC, plain: element (k, c) at p[k*ld + c]; optional row gather on k, per-k scale, GELU-on-load.
-template <typename T>
+// MC, plain: element (k, c) at p[k*ld + c]; optional row gather on k, per-k scale, GELU-on-load (XF).
+template <typename T, bool XF = false>
 struct LdMC {
+  typedef typename VecOf<T>::type vec_t;
   const T* p; int64_t ld; int cols; int K;
   const int* idx; int idx_div; const float* rs; int gelu;
-  int64_t group_stride;  // added per group (grouped-K mode: rows are absolute anyway)
-  struct ColState { int c0; };
-  struct RowState {};
+  struct Slot { uint32_t off; int kofs; bool ok; };
   MG_DEV void set_group(int) {}
-  MG_DEV ColState col(int c0) const { return ColState{c0}; }
-  MG_DEV typename VecOf<T>::type load(const ColState& st, int k) const {
-    if (st.c0 >= cols || k >= K) return vzero<T>();
-    int src = idx ? idx[k] / idx_div : k;
-    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(p + (int64_t)src * ld + st.c0);
-    if (gelu) v = vgelu(v);
-    if (rs) v = vscale1(v, rs[k]);
-    return v;
+  MG_DEV rsrc_t rsrc() const { return make_rsrc(p); }
+  MG_DEV Slot slot(int c0, int kofs, bool ok) const {
+    Slot s{MG_OOB, kofs, ok && c0 < cols};
+    if (s.ok) s.off = XF ? (uint32_t)(c0 * (int)sizeof(T)) : (uint32_t)(((int64_t)kofs * ld + c0) * (int64_t)sizeof(T));
+    return s;
+  }
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+    if constexpr (XF) {
+      const int k = k0 + s.kofs;
+      const bool ok = s.ok && (!TAIL || k < kend);
+      const int src = ok ? (idx ? idx[k] / idx_div : k) : 0;
+      return bload<vec_t>(r, ok ? (uint32_t)((int64_t)src * ld * (int64_t)sizeof(T)) + s.off : MG_OOB, 0);
+    } else {
+      uint32_t off = s.off;
+      if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
+      return bload<vec_t>(r, off, (uint32_t)((int64_t)k0 * ld * (int64_t)sizeof(T)));
+    }
+  }
+  MG_DEV void fix(const Slot& s, int k0, vec_t& v) const {
+    if constexpr (XF) {
+      const int k = k0 + s.kofs;
+      if (k >= K) return;
+      if (gelu) v = vgelu(v);
+      if (rs) v = vscale1(v, rs[k]);
+    }
   }
 };
 
-// MC, implicit conv columns for weight gradients: element (k = pixel, c = tap*Cin + ci).
-template <typename T>
+// MC, implicit conv columns for weight gradients: element (k = output pixel, c = tap*Cin + ci).
+template <typename T, bool XF = false>
 struct LdMCConv {
+  typedef typename VecOf<T>::type vec_t;
   const T* x; int H, W, Cin, lgCin, lgOW, lgOHW, K;  // K = number of output pixels
   int KW, stride, pad, cols;
-  const float* scale;
-  struct ColState { int kh, kw, ci; bool ok; };
-  struct RowState {};
+  const float* scale;  // XF only
+  struct Slot { int dh, dw, ci, kofs; uint32_t bad; };
   MG_DEV void set_group(int) {}
-  MG_DEV ColState col(int c0) const {
-    ColState st;
-    st.ok = c0 < cols;
-    int tap = c0 >> lgCin;
-    st.ci = c0 & (Cin - 1);
-    st.kh = tap / KW;
-    st.kw = tap - st.kh * KW;
-    return st;
+  MG_DEV rsrc_t rsrc() const { return make_rsrc(x); }
+  MG_DEV Slot slot(int c0, int kofs, bool ok) const {
+    Slot s;
+    s.bad = (ok && c0 < cols) ? 0u : 1u;
+    const int tap = c0 >> lgCin;
+    s.ci = c0 & (Cin - 1);
+    const int kh = tap / KW;
+    s.dh = kh - pad;
+    s.dw = tap - kh * KW - pad;
+    s.kofs = kofs;
+    return s;
   }
-  MG_DEV typename VecOf<T>::type load(const ColState& st, int k) const {
-    if (!st.ok || k >= K) return vzero<T>();
-    int b = k >> lgOHW;
-    int rem = k & ((1 << lgOHW) - 1);
-    int oh = rem >> lgOW, ow = rem & ((1 << lgOW) - 1);
-    int ih = oh * stride - pad + st.kh, iw = ow * stride - pad + st.kw;
-    if (ih < 0 || ih >= H || iw < 0 || iw >= W) return vzero<T>();
-    auto v = *reinterpret_cast<const typename VecOf<T>::type*>(x + (((int64_t)b * H + ih) * W + iw) * Cin + st.ci);
-    if (scale) v = vscale(v, scale + (int64_t)b * Cin + st.ci);
-    return v;
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+    const int k = k0 + s.kofs;
+    const int b = k >> lgOHW;
+    const int oh = (k >> lgOW) & ((1 << (lgOHW - lgOW)) - 1), ow = k & ((1 << lgOW) - 1);
+    const int ih = oh * stride + s.dh, iw = ow * stride + s.dw;
+    const uint32_t bad = (uint32_t)((unsigned)ih >= (unsigned)H) | (uint32_t)((unsigned)iw >= (unsigned)W) | s.bad;
+    uint32_t off = ((uint32_t)((((b * H + ih) * W + iw) << lgCin) + s.ci) * (uint32_t)sizeof(T)) | (bad << 31);
+    if constexpr (TAIL) off = k < kend ? off : MG_OOB;
+    return bload<vec_t>(r, off, 0);
+  }
+  MG_DEV void fix(const Slot& s, int k0, vec_t& v) const {
+    if constexpr (XF) {
+      const int k = k0 + s.kofs;
+      if (scale && k < K) v = vscale(v, scale + (int64_t)(k >> lgOHW) * Cin + s.ci);
+    }
   }
 };
 
@@ -182,64 +258,80 @@ struct LdMCConv {
 // split into the 4 output-parity classes (py, px).  Row r (class-major) =
 // (class, b, i, j) -> input-grid pixel (b, 2i+py, 2j+px); k = t*Cg + co with
 // t = ty*2 + tx the 2x2 taps of that class reading g[b, i+dy, j+dx, co].
-template <typename T>
+template <typename T, bool XF = false, bool SC = false>
 struct LdKCConvT {
+  typedef typename VecOf<T>::type vec_t;
   const T* g; int OH, OW, Cg, lgCg, lgOW, lgOHW, Mc, K;
   int cls;
-  struct RowState { int b, i, j; };
-  struct ColState {};
+  struct Slot { int32_t base; uint32_t mask; int kofs; };
   MG_DEV void set_group(int c) { cls = c; }
-  MG_DEV RowState row(int r) const {
-    RowState st;
-    if (r == 0x7fffffff) { st.b = -1; st.i = st.j = 0; return st; }
-    int rem = r - cls * Mc;
-    st.b = rem >> lgOHW;
-    st.i = (rem >> lgOW) & ((1 << (lgOHW - lgOW)) - 1);
-    st.j = rem & ((1 << lgOW) - 1);
-    return st;
+  MG_DEV rsrc_t rsrc() const { return make_rsrc(g); }
+  MG_DEV static int dy_of(int py, int ty) { return py ? (ty ? 0 : 1) : (ty ? -1 : 0); }
+  MG_DEV Slot slot(int r, int kofs, bool ok) const {
+    Slot s{0, 0u, kofs};
+    if (!ok) return s;
+    const int rem = r - cls * Mc;
+    const int b = rem >> lgOHW;
+    const int i = (rem >> lgOW) & ((1 << (lgOHW - lgOW)) - 1), j = rem & ((1 << lgOW) - 1);
+    s.base = (((b * OH + i) * OW + j) << lgCg) * (int)sizeof(T);
+    const int py = cls >> 1, px = cls & 1;
+    uint32_t m = 0;
+    for (int t = 0; t < 4; ++t) {
+      const int oh = i + dy_of(py, t >> 1), ow = j + dy_of(px, t & 1);
+      if ((unsigned)oh < (unsigned)OH && (unsigned)ow < (unsigned)OW) m |= 1u << t;
+    }
+    s.mask = m;
+    return s;
   }
-  MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
-    int k = k0 + kofs;
-    if (st.b < 0 || k >= K) return vzero<T>();
-    int t = k >> lgCg;
-    int co = k & (Cg - 1);
-    int ty = t >> 1, tx = t & 1;
-    int py = cls >> 1, px = cls & 1;
-    int dy = py ? (ty ? 0 : 1) : (ty ? -1 : 0);
-    int dx = px ? (tx ? 0 : 1) : (tx ? -1 : 0);
-    int oh = st.i + dy, ow = st.j + dx;
-    if (oh < 0 || oh >= OH || ow < 0 || ow >= OW) return vzero<T>();
-    return *reinterpret_cast<const typename VecOf<T>::type*>(g + (((int64_t)st.b * OH + oh) * OW + ow) * Cg + co);
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+    const int k = k0 + s.kofs;
+    const int kk = SC ? k : k0;  // SC = false: the step stays inside tap k0 / Cg (wave-uniform)
+    const int t = kk >> lgCg;
+    const int dy = dy_of(cls >> 1, t >> 1), dx = dy_of(cls & 1, t & 1);
+    const int tapoff = (((dy * OW + dx) << lgCg) + (kk & (Cg - 1))) * (int)sizeof(T);
+    uint32_t off = (uint32_t)(s.base + tapoff + (SC ? 0 : s.kofs * (int)sizeof(T))) | ((~s.mask >> t) << 31);
+    if constexpr (TAIL) off = k < kend ? off : MG_OOB;
+    return bload<vec_t>(r, off, 0);
   }
+  MG_DEV void fix(const Slot&, int, vec_t&) const {}
 };
 
 // Grouped B operand: KC rows of a per-group weight (base + g*gstride).
-template <typename T>
+template <typename T, bool XF = false>
 struct LdKCGroupW {
+  typedef typename VecOf<T>::type vec_t;
   const T* p0; int64_t ld; int rows; int K; int64_t gstride;
   const T* p;
-  struct RowState { const T* base; };
-  struct ColState {};
+  struct Slot { uint32_t off; int kofs; };
   MG_DEV void set_group(int g) { p = p0 + (int64_t)g * gstride; }
-  MG_DEV RowState row(int r) const { return RowState{r < rows ? p + (int64_t)r * ld : nullptr}; }
-  MG_DEV typename VecOf<T>::type load(const RowState& st, int k0, int kofs) const {
-    int k = k0 + kofs;
-    if (!st.base || k >= K) return vzero<T>();
-    return *reinterpret_cast<const typename VecOf<T>::type*>(st.base + k);
+  MG_DEV rsrc_t rsrc() const { return make_rsrc(p); }
+  MG_DEV Slot slot(int r, int kofs, bool ok) const {
+    return Slot{(ok && r < rows) ? (uint32_t)(((int64_t)r * ld + kofs) * (int64_t)sizeof(T)) : MG_OOB, kofs};
   }
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+    uint32_t off = s.off;
+    if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
+    return bload<vec_t>(r, off, (uint32_t)k0 * (uint32_t)sizeof(T));
+  }
+  MG_DEV void fix(const Slot&, int, vec_t&) const {}
 };
-template <typename T>
+template <typename T, bool XF = false>
 struct LdMCGroupW {
+  typedef typename VecOf<T>::type vec_t;
   const T* p0; int64_t ld; int cols; int K; int64_t gstride;
   const T* p;
-  struct ColState { int c0; };
-  struct RowState {};
+  struct Slot { uint32_t off; int kofs; };
   MG_DEV void set_group(int g) { p = p0 + (int64_t)g * gstride; }
-  MG_DEV ColState col(int c0) const { return ColState{c0}; }
-  MG_DEV typename VecOf<T>::type load(const ColState& st, int k) const {
-    if (st.c0 >= cols || k >= K) return vzero<T>();
-    return *reinterpret_cast<const typename VecOf<T>::type*>(p + (int64_t)k * ld + st.c0);
+  MG_DEV rsrc_t rsrc() const { return make_rsrc(p); }
+  MG_DEV Slot slot(int c0, int kofs, bool ok) const {
+    return Slot{(ok && c0 < cols) ? (uint32_t)(((int64_t)kofs * ld + c0) * (int64_t)sizeof(T)) : MG_OOB, kofs};
   }
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+    uint32_t off = s.off;
+    if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
+    return bload<vec_t>(r, off, (uint32_t)((int64_t)k0 * ld * (int64_t)sizeof(T)));
+  }
+  MG_DEV void fix(const Slot&, int, vec_t&) const {}
 };
 
 // ---------------------------------------------------------------------------
@@ -448,59 +540,53 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 
   // ---- per-thread load slots ----
   vec_t ra[A_VPT], rb[B_VPT];
-  typename AL::RowState ast[A_KC ? A_VPT : 1];
-  typename AL::ColState acs[A_KC ? 1 : A_VPT];
-  typename BL::RowState bst[B_KC ? B_VPT : 1];
-  typename BL::ColState bcs[B_KC ? 1 : B_VPT];
+  typename AL::Slot as_[A_VPT];
+  typename BL::Slot bs_[B_VPT];
   int a_r[A_VPT], a_k[A_VPT], b_r[B_VPT], b_k[B_VPT];
 #pragma unroll
   for (int i = 0; i < A_VPT; ++i) {
     int v = tid + i * NTHREADS;
-    if constexpr (A_KC) {
-      a_r[i] = v / (TBK / VEC); a_k[i] = (v % (TBK / VEC)) * VEC;
-      int r = mrow_base + m0 + a_r[i];
-      ast[i] = A.row(r < mlimit ? r : 0x7fffffff);
-    } else {
-      a_k[i] = v / (BM / VEC); a_r[i] = (v % (BM / VEC)) * VEC;
-      int c = mrow_base + m0 + a_r[i];
-      acs[i] = A.col(c < mlimit ? c : 0x7fffffff);
-    }
+    if constexpr (A_KC) { a_r[i] = v / (TBK / VEC); a_k[i] = (v % (TBK / VEC)) * VEC; }
+    else { a_k[i] = v / (BM / VEC); a_r[i] = (v % (BM / VEC)) * VEC; }
+    const int r = mrow_base + m0 + a_r[i];
+    as_[i] = A.slot(r, a_k[i], r < mlimit);
   }
 #pragma unroll
   for (int i = 0; i < B_VPT; ++i) {
     int v = tid + i * NTHREADS;
-    if constexpr (B_KC) {
-      b_r[i] = v / (TBK / VEC); b_k[i] = (v % (TBK / VEC)) * VEC;
-      bst[i] = B.row(n0 + b_r[i]);
-    } else {
-      b_k[i] = v / (BN / VEC); b_r[i] = (v % (BN / VEC)) * VEC;
-      bcs[i] = B.col(n0 + b_r[i]);
-    }
+    if constexpr (B_KC) { b_r[i] = v / (TBK / VEC); b_k[i] = (v % (TBK / VEC)) * VEC; }
+    else { b_k[i] = v / (BN / VEC); b_r[i] = (v % (BN / VEC)) * VEC; }
+    bs_[i] = B.slot(n0 + b_r[i], b_k[i], true);
   }
+  const rsrc_t rA = A.rsrc(), rB = B.rsrc();
 
-  auto gload = [&](int k0) {
+  // issue the buffer loads of K step k0 (TAIL: the step reaches past kend)
+  auto gload = [&](int k0, auto tail) {
+    constexpr bool TL = decltype(tail)::value;
+#pragma unroll
+    for (int i = 0; i < A_VPT; ++i) ra[i] = A.template load<TL, TBK>(rA, as_[i], k0, kend);
+#pragma unroll
+    for (int i = 0; i < B_VPT; ++i) rb[i] = B.template load<TL, TBK>(rB, bs_[i], k0, kend);
+  };
+  auto sstore = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < A_VPT; ++i) {
-      if constexpr (A_KC) ra[i] = (k0 + a_k[i] < kend) ? A.load(ast[i], k0, a_k[i]) : vzero<T>();
-      else ra[i] = (k0 + a_k[i] < kend) ? A.load(acs[i], k0 + a_k[i]) : vzero<T>();
+      vec_t v = ra[i];
+      A.fix(as_[i], k0, v);
+      if constexpr (A_KC) *reinterpret_cast<vec_t*>(&As[kc_off<T>(a_r[i], a_k[i], LDK)]) = v;
+      else *reinterpret_cast<vec_t*>(&As[a_k[i] * LDA + (a_r[i] ^ mc_swz<T>(a_k[i]))]) = v;
     }
 #pragma unroll
     for (int i = 0; i < B_VPT; ++i) {
-      if constexpr (B_KC) rb[i] = (k0 + b_k[i] < kend) ? B.load(bst[i], k0, b_k[i]) : vzero<T>();
-      else rb[i] = (k0 + b_k[i] < kend) ? B.load(bcs[i], k0 + b_k[i]) : vzero<T>();
+      vec_t v = rb[i];
+      B.fix(bs_[i], k0, v);
+      if constexpr (B_KC) *reinterpret_cast<vec_t*>(&Bs[kc_off<T>(b_r[i], b_k[i], LDK)]) = v;
+      else *reinterpret_cast<vec_t*>(&Bs[b_k[i] * LDB + (b_r[i] ^ mc_swz<T>(b_k[i]))]) = v;
     }
   };
-  auto sstore = [&]() {
-#pragma unroll
-    for (int i = 0; i < A_VPT; ++i) {
-      if constexpr (A_KC) *reinterpret_cast<vec_t*>(&As[kc_off<T>(a_r[i], a_k[i], LDK)]) = ra[i];
-      else *reinterpret_cast<vec_t*>(&As[a_k[i] * LDA + (a_r[i] ^ mc_swz<T>(a_k[i]))]) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_VPT; ++i) {
-      if constexpr (B_KC) *reinterpret_cast<vec_t*>(&Bs[kc_off<T>(b_r[i], b_k[i], LDK)]) = rb[i];
-      else *reinterpret_cast<vec_t*>(&Bs[b_k[i] * LDB + (b_r[i] ^ mc_swz<T>(b_k[i]))]) = rb[i];
-    }
+  auto gload_any = [&](int k0) {
+    if (k0 + TBK <= kend) gload(k0, std::false_type{});
+    else gload(k0, std::true_type{});
   };
 
   f32x4_t acc[FM][FN];
@@ -510,12 +596,12 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  if (kbeg < kend) gload(kbeg);
+  if (kbeg < kend) gload_any(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += TBK) {
     __syncthreads();
-    sstore();
+    sstore(k0);
     __syncthreads();
-    if (k0 + TBK < kend) gload(k0 + TBK);
+    if (k0 + TBK < kend) gload_any(k0 + TBK);
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int kk = 0; kk < TBK / 32; ++kk) {

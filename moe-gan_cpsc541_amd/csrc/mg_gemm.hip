@@ -56,7 +56,9 @@ inline int kwinv(int KW) { return 65536 / KW + 1; }  // exact tap / KW for tap <
 
 constexpr Grouping kNoGroup{0, 1, nullptr, nullptr, 0};
 
-template <typename T, typename TO, int BM, int BN, bool AK, bool BKc>
+inline bool a_xf(const mg_epilogue* e) { return e && (e->a_idx || e->a_rowscale || e->a_gelu); }
+
+template <typename T, typename TO, int BM, int BN, bool AK, bool BKc, bool XF>
 void run_plain(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                const mg_epilogue* e, int splits, hipStream_t st) {
   auto ep = make_epi<TO>(C, ldc, e);
@@ -65,38 +67,42 @@ void run_plain(int M, int N, int K, const void* A, int64_t lda, const void* B, i
   const float* ars = e ? e->a_rowscale : nullptr;
   int agelu = e ? e->a_gelu : 0;
   if constexpr (AK) {
-    LdKC<T> la{reinterpret_cast<const T*>(A), lda, M, K, aidx, adiv, ars, agelu};
+    LdKC<T, XF> la{reinterpret_cast<const T*>(A), lda, M, K, aidx, adiv, ars, agelu};
     if constexpr (BKc) {
       LdKC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
       launch_gemm<T, BM, BN, true, true>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
     } else {
-      LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0, 0};
+      LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
       launch_gemm<T, BM, BN, true, false>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
     }
   } else {
-    LdMC<T> la{reinterpret_cast<const T*>(A), lda, M, K, aidx, adiv, ars, agelu, 0};
+    LdMC<T, XF> la{reinterpret_cast<const T*>(A), lda, M, K, aidx, adiv, ars, agelu};
     if constexpr (BKc) {
       LdKC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
       launch_gemm<T, BM, BN, false, true>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
     } else {
-      LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0, 0};
+      LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
       launch_gemm<T, BM, BN, false, false>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
     }
   }
 }
 
-template <typename T, typename TO, int BM, int BN>
+template <typename T, typename TO, int BM, int BN, bool XF = false>
 void run_plain_orient(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
                       int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, int splits, hipStream_t st) {
-  if (a_kc && b_kc) run_plain<T, TO, BM, BN, true, true>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
-  else if (a_kc) run_plain<T, TO, BM, BN, true, false>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
-  else if (b_kc) run_plain<T, TO, BM, BN, false, true>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
-  else run_plain<T, TO, BM, BN, false, false>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  if (a_kc && b_kc) run_plain<T, TO, BM, BN, true, true, XF>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else if (a_kc) run_plain<T, TO, BM, BN, true, false, XF>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else if (b_kc) run_plain<T, TO, BM, BN, false, true, XF>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else run_plain<T, TO, BM, BN, false, false, XF>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
 }
 
 template <typename T, typename TO>
 void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
                      int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, int splits, hipStream_t st) {
+  if (a_xf(e)) {  // loader transforms: generic 64x64 instantiation
+    run_plain_orient<T, TO, 64, 64, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+    return;
+  }
   const int tile = g_mg_tune[MG_TUNE_GEMM_TILE];
   if (tile == 128 || (tile == 0 && (int64_t)cdiv(M, 128) * cdiv(N, 128) * splits >= 480))
     run_plain_orient<T, TO, 128, 128>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
@@ -112,7 +118,7 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
                       int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, hipStream_t st) {
   constexpr int TBK = Tile<T>::BK;
   int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
-  if (tiles >= 96 || K < 4 * TBK) return false;
+  if (tiles >= 96 || K < 4 * TBK || a_xf(e)) return false;
   int splits = (int)std::min<int64_t>(256 / tiles, K / (2 * TBK));
   if (splits < 2) return false;
   int kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
@@ -125,10 +131,6 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
   Epi<float> slab = make_epi<float>(ws, N, &raw);
   slab.zstride = MN;
   slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
-  const int32_t* aidx = e ? e->a_idx : nullptr;
-  int adiv = (e && e->a_idx_div > 0) ? e->a_idx_div : 1;
-  const float* ars = e ? e->a_rowscale : nullptr;
-  int agelu = e ? e->a_gelu : 0;
   auto go = [&](auto la, auto lb, auto akc, auto bkc) {
     dim3 grid(cdiv(M, 64), cdiv(N, 64), splits);
     hipLaunchKernelGGL((gemm_kernel<T, 64, 64, decltype(akc)::value, decltype(bkc)::value, decltype(la),
@@ -140,13 +142,13 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
   using TT = std::true_type;
   using FF = std::false_type;
   if (a_kc) {
-    LdKC<T> la{Ap, lda, M, K, aidx, adiv, ars, agelu};
+    LdKC<T> la{Ap, lda, M, K, nullptr, 1, nullptr, 0};
     if (b_kc) go(la, LdKC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, TT{}, TT{});
-    else go(la, LdMC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0, 0}, TT{}, FF{});
+    else go(la, LdMC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, TT{}, FF{});
   } else {
-    LdMC<T> la{Ap, lda, M, K, aidx, adiv, ars, agelu, 0};
+    LdMC<T> la{Ap, lda, M, K, nullptr, 1, nullptr, 0};
     if (b_kc) go(la, LdKC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, FF{}, TT{});
-    else go(la, LdMC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0, 0}, FF{}, FF{});
+    else go(la, LdMC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, FF{}, FF{});
   }
   auto ep = make_epi<TO>(C, ldc, e);
   int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
@@ -215,16 +217,10 @@ int run_batch(int n, const mg_gemm_desc* d, hipStream_t st) {
       const mg_gemm_desc& q = d[i0 + j];
       if (q.M == 0 || q.N == 0) continue;
       const mg_epilogue* e = q.ep;
-      const int32_t* aidx = e ? e->a_idx : nullptr;
-      int adiv = (e && e->a_idx_div > 0) ? e->a_idx_div : 1;
-      const float* ars = e ? e->a_rowscale : nullptr;
-      int agelu = e ? e->a_gelu : 0;
       const T* Ap = reinterpret_cast<const T*>(q.A);
       const T* Bp = reinterpret_cast<const T*>(q.B);
-      if constexpr (AK) args.a[used] = AL{Ap, q.lda, q.M, q.K, aidx, adiv, ars, agelu};
-      else args.a[used] = AL{Ap, q.lda, q.M, q.K, aidx, adiv, ars, agelu, 0};
-      if constexpr (BKc) args.b[used] = BL{Bp, q.ldb, q.N, q.K, nullptr, 1, nullptr, 0};
-      else args.b[used] = BL{Bp, q.ldb, q.N, q.K, nullptr, 1, nullptr, 0, 0};
+      args.a[used] = AL{Ap, q.lda, q.M, q.K, nullptr, 1, nullptr, 0};
+      args.b[used] = BL{Bp, q.ldb, q.N, q.K, nullptr, 1, nullptr, 0};
       args.e[used] = make_epi<TO>(q.C, q.ldc, e);
       args.e[used].vec_ok = args.e[used].host_vec_ok() ? 1 : 0;
       args.M[used] = q.M;
@@ -256,6 +252,7 @@ extern "C" int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, 
     MG_REQUIRE(a_kc ? (q.K % vec == 0) : (q.M % vec == 0), "A vector dim must be a multiple of the vector");
     MG_REQUIRE(b_kc ? (q.K % vec == 0) : (q.N % vec == 0), "B vector dim must be a multiple of the vector");
     MG_REQUIRE(!(q.ep && q.ep->atomic) || c_dtype == MG_F32, "atomic epilogue requires fp32 C");
+    MG_REQUIRE(!a_xf(q.ep), "A loader transforms (a_idx / a_rowscale / a_gelu) are not supported by mg_gemm_batch");
   }
   if (n <= 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -271,27 +268,27 @@ extern "C" int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, 
 // implicit-GEMM convolution
 // ---------------------------------------------------------------------------
 namespace {
-template <typename T, typename TO, int BM, int BN>
+template <typename T, typename TO, int BM, int BN, bool XF = false, bool SC = false>
 void run_conv(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW, int stride,
               int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int M = B * OH * OW, K = KH * KW * Cin;
-  LdKCConv<T> la{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), M,
-                 KW, stride, pad, K, sc, kwinv(KW)};
+  LdKCConv<T, XF, SC> la{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), M,
+                         KW, stride, pad, K, sc, kwinv(KW)};
   LdKC<T> lb{reinterpret_cast<const T*>(wpack), K, Cout, K, nullptr, 1, nullptr, 0};
   auto ep = make_epi<TO>(y, ldy, e);
   launch_gemm<T, BM, BN, true, true>(la, lb, ep, M, Cout, K, 1, kNoGroup, 0, st);
 }
 // Implicit conv with few output tiles (offset heads: Cout = 32 at 4x4 / 8x8) walks K = 9*Cin serially in
 // ~100 blocks; split K into fp32 slabs over ~512 blocks and apply the epilogue in the reduction.
-template <typename T, typename TO>
+template <typename T, typename TO, bool SC>
 bool conv_slabs(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW, int stride,
                 int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
   constexpr int TBK = Tile<T>::BK;
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int M = B * OH * OW, K = KH * KW * Cin;
   int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(Cout, 64);
-  if (tiles >= 256 || K < 8 * TBK || (e && e->atomic) || g_mg_tune[MG_TUNE_NO_SLABS]) return false;
+  if (tiles >= 256 || K < 8 * TBK || (e && e->atomic) || sc || g_mg_tune[MG_TUNE_NO_SLABS]) return false;
   int splits = (int)std::min<int64_t>(cdiv(512, tiles), K / (4 * TBK));
   if (splits < 2) return false;
   int kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
@@ -304,11 +301,11 @@ bool conv_slabs(const void* x, int B, int H, int W, int Cin, const void* wpack, 
   Epi<float> slab = make_epi<float>(ws, Cout, &raw);
   slab.zstride = MN;
   slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
-  LdKCConv<T> la{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), M,
-                 KW, stride, pad, K, sc, kwinv(KW)};
+  LdKCConv<T, false, SC> la{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), M,
+                            KW, stride, pad, K, sc, kwinv(KW)};
   LdKC<T> lb{reinterpret_cast<const T*>(wpack), K, Cout, K, nullptr, 1, nullptr, 0};
   dim3 grid(cdiv(M, 64), cdiv(Cout, 64), splits);
-  hipLaunchKernelGGL((gemm_kernel<T, 64, 64, true, true, LdKCConv<T>, LdKC<T>, Epi<float>>), grid, dim3(NTHREADS), 0,
+  hipLaunchKernelGGL((gemm_kernel<T, 64, 64, true, true, LdKCConv<T, false, SC>, LdKC<T>, Epi<float>>), grid, dim3(NTHREADS), 0,
                      st, la, lb, slab, M, Cout, K, kchunk, kNoGroup);
   auto ep = make_epi<TO>(y, ldy, e);
   int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
@@ -320,7 +317,15 @@ template <typename T, typename TO>
 void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW,
                     int stride, int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e,
                     hipStream_t st) {
-  if (conv_slabs<T, TO>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st)) return;
+  const bool small_c = Cin < Tile<T>::BK;  // a K step spans several taps: per-lane tap decode
+  if (small_c ? conv_slabs<T, TO, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st)
+              : conv_slabs<T, TO, false>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st))
+    return;
+  if (sc || small_c) {  // modulation scale on load / small Cin: generic 64x64 instantiations
+    if (sc) run_conv<T, TO, 64, 64, true, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+    else run_conv<T, TO, 64, 64, false, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+    return;
+  }
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int64_t M = (int64_t)B * OH * OW;
   const int tile = g_mg_tune[MG_TUNE_CONV_TILE];
@@ -353,14 +358,14 @@ extern "C" int mg_conv2d_fwd(int dtype, const void* x, int B, int H, int W, int 
 }
 
 namespace {
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool XF = false>
 void run_wgrad(const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin, const float* sc, int Cout,
                int KH, int KW, int stride, int pad, float* gw, int splits, hipStream_t st) {
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int P = B * OH * OW, N = KH * KW * Cin;
-  LdMC<T> la{reinterpret_cast<const T*>(gy), ldg, Cout, P, nullptr, 1, nullptr, 0, 0};
-  LdMCConv<T> lb{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), P,
-                 KW, stride, pad, N, sc};
+  LdMC<T> la{reinterpret_cast<const T*>(gy), ldg, Cout, P, nullptr, 1, nullptr, 0};
+  LdMCConv<T, XF> lb{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), P,
+                     KW, stride, pad, N, sc};
   mg_epilogue e{};
   e.alpha = 1.f;
   e.atomic = 1;
@@ -390,7 +395,7 @@ __global__ __launch_bounds__(256) void k_wgrad_fold(const float* __restrict__ ws
 
 // Weight gradient with split-K into fp32 slabs written by the 8-column vector epilogue (coalesced, no atomics),
 // then k_wgrad_fold.  Returns false when the workspace cannot be had (caller falls back to atomics).
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool XF = false>
 bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin, const float* sc,
                      int Cout, int KH, int KW, int stride, int pad, float* gw, int splits, hipStream_t st) {
   constexpr int TBK = Tile<T>::BK;
@@ -401,16 +406,16 @@ bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, i
   const int64_t MN = (int64_t)Cout * N;
   float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float)));
   if (!ws) return false;
-  LdMC<T> la{reinterpret_cast<const T*>(gy), ldg, Cout, P, nullptr, 1, nullptr, 0, 0};
-  LdMCConv<T> lb{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), P,
-                 KW, stride, pad, N, sc};
+  LdMC<T> la{reinterpret_cast<const T*>(gy), ldg, Cout, P, nullptr, 1, nullptr, 0};
+  LdMCConv<T, XF> lb{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), P,
+                     KW, stride, pad, N, sc};
   mg_epilogue raw{};
   raw.alpha = 1.f;
   Epi<float> slab = make_epi<float>(ws, N, &raw);
   slab.zstride = MN;
   slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
   dim3 grid(cdiv(Cout, BM), cdiv(N, BN), splits);
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, false, LdMC<T>, LdMCConv<T>, Epi<float>>), grid, dim3(NTHREADS),
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, false, LdMC<T>, LdMCConv<T, XF>, Epi<float>>), grid, dim3(NTHREADS),
                      0, st, la, lb, slab, Cout, N, P, kchunk, kNoGroup);
   int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 4096);
   hipLaunchKernelGGL(k_wgrad_fold, dim3(blocks), dim3(256), 0, st, ws, splits, Cout, ilog2(Cin), KH * KW, gw);
@@ -448,6 +453,17 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
                                                                                       : P / 2048));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (in_scale) {  // modulation scale on load: generic 64x64 instantiation (slabs, atomics if no workspace)
+    bool ok = dtype == MG_BF16 ? run_wgrad_slabs<bf16_t, 64, 64, true>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW,
+                                                                       stride, pad, gw, splits, st)
+                               : run_wgrad_slabs<float, 64, 64, true>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW,
+                                                                      stride, pad, gw, splits, st);
+    if (!ok) {
+      if (dtype == MG_BF16) run_wgrad<bf16_t, 64, 64, true>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
+      else run_wgrad<float, 64, 64, true>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw, splits, st);
+    }
+    return mg_check_launch("mg_conv2d_wgrad (scaled)");
+  }
   if (slabs && dtype == MG_BF16) {
     bool ok = big ? run_wgrad_slabs<bf16_t, 128, 128>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad,
                                                        gw, splits, st)
@@ -468,7 +484,7 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
 // grouped (per-expert) GEMMs
 // ---------------------------------------------------------------------------
 namespace {
-template <typename T, typename TO, bool BKc>
+template <typename T, typename TO, bool BKc, bool XF>
 void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_off, const int32_t* tile_off,
                  int max_tiles, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t b_gstride, void* C,
                  int64_t ldc, const mg_epilogue* e, hipStream_t st) {
@@ -476,8 +492,8 @@ void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_o
   ep.gstride_bias = N;
   const int32_t* aidx = e ? e->a_idx : nullptr;
   int adiv = (e && e->a_idx_div > 0) ? e->a_idx_div : 1;
-  LdKC<T> la{reinterpret_cast<const T*>(A), lda, total_rows, K, aidx, adiv, e ? e->a_rowscale : nullptr,
-             e ? e->a_gelu : 0};
+  LdKC<T, XF> la{reinterpret_cast<const T*>(A), lda, total_rows, K, aidx, adiv, e ? e->a_rowscale : nullptr,
+                 e ? e->a_gelu : 0};
   Grouping grp{1, ngroups, row_off, tile_off, 0};
   if constexpr (BKc) {
     LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
@@ -488,14 +504,14 @@ void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_o
   }
 }
 
-template <typename T>
+template <typename T, bool XF>
 void run_grouped_wgrad(int M, int N, int ngroups, const int32_t* row_off, int total_rows, const void* A, int64_t lda,
                        const void* B, int64_t ldb, const int32_t* b_idx, int b_idx_div, int b_gelu, float* C,
                        int splits, const mg_epilogue* e, hipStream_t st) {
-  LdMC<T> la{reinterpret_cast<const T*>(A), lda, M, total_rows, e ? e->a_idx : nullptr,
-             (e && e->a_idx_div > 0) ? e->a_idx_div : 1, e ? e->a_rowscale : nullptr, e ? e->a_gelu : 0, 0};
-  LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, total_rows, b_idx, b_idx_div > 0 ? b_idx_div : 1, nullptr,
-             b_gelu, 0};
+  LdMC<T, XF> la{reinterpret_cast<const T*>(A), lda, M, total_rows, e ? e->a_idx : nullptr,
+             (e && e->a_idx_div > 0) ? e->a_idx_div : 1, e ? e->a_rowscale : nullptr, e ? e->a_gelu : 0};
+  LdMC<T, XF> lb{reinterpret_cast<const T*>(B), ldb, N, total_rows, b_idx, b_idx_div > 0 ? b_idx_div : 1, nullptr,
+             b_gelu};
   mg_epilogue ee{};
   ee.alpha = e ? e->alpha : 1.f;
   ee.atomic = 1;
@@ -520,17 +536,19 @@ extern "C" int mg_gemm_grouped(int dtype, int total_rows, int N, int K, int ngro
   MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
   if (max_tiles <= 0 || N == 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define MG_GRP(T, TO)                                                                                           \
-  (b_kc ? run_grouped<T, TO, true>(total_rows, N, K, ngroups, row_off, tile_off, max_tiles, A, lda, B, ldb,     \
-                                   b_gstride, C, ldc, ep, st)                                                    \
-        : run_grouped<T, TO, false>(total_rows, N, K, ngroups, row_off, tile_off, max_tiles, A, lda, B, ldb,    \
-                                    b_gstride, C, ldc, ep, st))
+#define MG_GRP4(T, TO, X)                                                                                       \
+  (b_kc ? run_grouped<T, TO, true, X>(total_rows, N, K, ngroups, row_off, tile_off, max_tiles, A, lda, B, ldb,  \
+                                      b_gstride, C, ldc, ep, st)                                                 \
+        : run_grouped<T, TO, false, X>(total_rows, N, K, ngroups, row_off, tile_off, max_tiles, A, lda, B, ldb, \
+                                       b_gstride, C, ldc, ep, st))
+#define MG_GRP(T, TO) (a_xf(ep) ? MG_GRP4(T, TO, true) : MG_GRP4(T, TO, false))
   if (dtype == MG_F32) {
     if (c_dtype == MG_F32) MG_GRP(float, float); else MG_GRP(float, bf16_t);
   } else {
     if (c_dtype == MG_F32) MG_GRP(bf16_t, float); else MG_GRP(bf16_t, bf16_t);
   }
 #undef MG_GRP
+#undef MG_GRP4
   return mg_check_launch("mg_gemm_grouped");
 }
 
@@ -549,8 +567,11 @@ extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const
     splits = std::max(1, std::min({64, cdiv(big ? 512 : 1024, std::max(1, tiles)), std::max(1, rows_per_group / 1024)}));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (dtype == MG_F32) run_grouped_wgrad<float>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st);
-  else run_grouped_wgrad<bf16_t>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st);
+  const bool xf = a_xf(ep) || b_idx || b_gelu;
+#define MG_GW(T, X) run_grouped_wgrad<T, X>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st)
+  if (dtype == MG_F32) { if (xf) MG_GW(float, true); else MG_GW(float, false); }
+  else { if (xf) MG_GW(bf16_t, true); else MG_GW(bf16_t, false); }
+#undef MG_GW
   return mg_check_launch("mg_gemm_grouped_wgrad");
 }
 
@@ -558,11 +579,11 @@ extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const
 // data gradient of a 4x4 / stride-2 / pad-1 conv (discriminator convs, R1 path)
 // ---------------------------------------------------------------------------
 namespace {
-template <typename T, typename TO>
+template <typename T, typename TO, bool SC>
 void run_dgrad_s2(const void* g, int B, int OH, int OW, int Cg, const void* wcls, int Cin, void* out, int64_t ldo,
                   const mg_epilogue* e, hipStream_t st) {
   int Mc = B * OH * OW;
-  LdKCConvT<T> la{reinterpret_cast<const T*>(g), OH, OW, Cg, ilog2(Cg), ilog2(OW), ilog2(OH * OW), Mc, 4 * Cg, 0};
+  LdKCConvT<T, false, SC> la{reinterpret_cast<const T*>(g), OH, OW, Cg, ilog2(Cg), ilog2(OW), ilog2(OH * OW), Mc, 4 * Cg, 0};
   LdKCGroupW<T> lb{reinterpret_cast<const T*>(wcls), 4 * Cg, Cin, 4 * Cg, (int64_t)Cin * 4 * Cg, nullptr};
   auto ep = make_epi<TO>(out, ldo, e);
   ep.rm_mode = 1;
@@ -570,7 +591,7 @@ void run_dgrad_s2(const void* g, int B, int OH, int OW, int Cg, const void* wcls
   ep.rm_lgOW = ilog2(OW);
   ep.rm_lgOHW = ilog2(OH * OW);
   Grouping grp{3, 4, nullptr, nullptr, Mc};
-  if (Cin >= 128)
+  if (Cin >= 128 && !SC)
     launch_gemm<T, 128, 128, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);
   else
     launch_gemm<T, 64, 64, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);
@@ -587,11 +608,11 @@ extern "C" int mg_conv2d_dgrad_s2(int dtype, const void* g, int B, int OH, int O
   if (B == 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == MG_F32) {
-    if (out_dtype == MG_F32) run_dgrad_s2<float, float>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st);
-    else run_dgrad_s2<float, bf16_t>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st);
+    if (out_dtype == MG_F32) (Cg < Tile<float>::BK ? run_dgrad_s2<float, float, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<float, float, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
+    else (Cg < Tile<float>::BK ? run_dgrad_s2<float, bf16_t, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<float, bf16_t, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
   } else {
-    if (out_dtype == MG_F32) run_dgrad_s2<bf16_t, float>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st);
-    else run_dgrad_s2<bf16_t, bf16_t>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st);
+    if (out_dtype == MG_F32) (Cg < Tile<bf16_t>::BK ? run_dgrad_s2<bf16_t, float, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<bf16_t, float, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
+    else (Cg < Tile<bf16_t>::BK ? run_dgrad_s2<bf16_t, bf16_t, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<bf16_t, bf16_t, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
   }
   return mg_check_launch("mg_conv2d_dgrad_s2");
 }
