@@ -152,22 +152,22 @@ def main():
     # live timing of the roofline kernel: D conv_layers.2 forward on the 64x64 real batch
     # (implicit GEMM M = B*16*16, N = 256, K = 4*4*128); inactive until the timed region
     want_dims = (B * 256, 256, 2048)
-    ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "conv2d" and dims == want_dims, active=False)
+    ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "conv2d:d_conv1" and dims == want_dims, active=False)
 
     graph = None
     if not args.eager:
+        graph = SegmentedGraph()
         refill()
         t_w = time.perf_counter()
-        run_step()  # sizes every lazily allocated buffer / workspace
+        graph.run_eager(run_step)  # sizes every lazily allocated buffer / workspace (on the capture stream)
         torch.cuda.synchronize()
         t_h = time.perf_counter()
-        run_step()  # host enqueue time of one eager step (diagnostic)
+        graph.run_eager(run_step)  # host enqueue time of one eager step (diagnostic)
         t_e = time.perf_counter()
         torch.cuda.synchronize()
         if rank == 0:
             print(f"[bench] eager step {(t_h - t_w) * 1e3:.1f} ms; host enqueue of one step {(t_e - t_h) * 1e3:.1f} ms, "
                   f"with device {(time.perf_counter() - t_h) * 1e3:.1f} ms", file=sys.stderr, flush=True)
-        graph = SegmentedGraph()
         out = graph.capture(run_step)
         torch.cuda.synchronize()
         if rank == 0:

@@ -1,4 +1,5 @@
 // Error plumbing and version of libmoegan_hip.
+#include <mutex>
 #include <string>
 
 #include "mg_common.h"
@@ -16,26 +17,41 @@ int mg_check_launch(const char* what) {
   return MG_OK;
 }
 
-// Split-K slab workspace.  Growth frees the old block only after the device is idle, so an
-// in-flight launch never reads freed memory; steady-state training never grows it (and a
-// captured hipGraph keeps seeing the same pointer).
-static void* g_ws = nullptr;
-static size_t g_ws_bytes = 0;
+// Split-K slab / partial-sum workspace, one block per stream (launches on different streams may run
+// concurrently, launches on one stream are ordered, so per-stream reuse is race-free).  Growth frees the
+// old block only after the device is idle, so an in-flight launch never reads freed memory; steady-state
+// training never grows it (and a captured hipGraph keeps seeing the same pointers).
+namespace {
+struct WsEntry { hipStream_t stream; void* ptr; size_t bytes; };
+constexpr int kMaxWsStreams = 128;  // torch hands out streams from a fixed pool (32 per priority)
+WsEntry g_ws[kMaxWsStreams];
+int g_ws_n = 0;
+std::mutex g_ws_mu;
+}  // namespace
 
-void* mg_workspace(size_t bytes) {
-  if (bytes <= g_ws_bytes) return g_ws;
-  if (g_ws) {
+void* mg_workspace(size_t bytes, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  WsEntry* e = nullptr;
+  for (int i = 0; i < g_ws_n; ++i)
+    if (g_ws[i].stream == stream) e = &g_ws[i];
+  if (!e) {
+    if (g_ws_n == kMaxWsStreams) return nullptr;
+    e = &g_ws[g_ws_n++];
+    *e = WsEntry{stream, nullptr, 0};
+  }
+  if (bytes <= e->bytes) return e->ptr;
+  if (e->ptr) {
     (void)hipDeviceSynchronize();
-    (void)hipFree(g_ws);
+    (void)hipFree(e->ptr);
   }
   size_t want = bytes + (bytes >> 2);
-  if (hipMalloc(&g_ws, want) != hipSuccess) {
-    g_ws = nullptr;
-    g_ws_bytes = 0;
+  if (hipMalloc(&e->ptr, want) != hipSuccess) {
+    e->ptr = nullptr;
+    e->bytes = 0;
     return nullptr;
   }
-  g_ws_bytes = want;
-  return g_ws;
+  e->bytes = want;
+  return e->ptr;
 }
 
 int g_mg_tune[MG_TUNE_COUNT] = {0};

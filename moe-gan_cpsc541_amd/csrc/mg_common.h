@@ -78,8 +78,8 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_XCD = 6, MG_TUNE_WGRAD_MODE = 7,
        MG_TUNE_COUNT = 16 };
 extern int g_mg_tune[MG_TUNE_COUNT];
-// Library-owned device scratch (grown on demand, never shrunk; stream-ordered reuse on one stream).
-void* mg_workspace(size_t bytes);
+// Library-owned device scratch, one block per stream (grown on demand, never shrunk).
+void* mg_workspace(size_t bytes, hipStream_t stream);
 
 #define MG_REQUIRE(cond, msg)                       \
   do {                                              \

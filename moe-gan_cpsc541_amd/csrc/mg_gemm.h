@@ -2,8 +2,9 @@
 //
 // C[m, n] = sum_k A[m, k] * B[k, n], tiles staged through LDS with both
 // operands stored k-contiguous ([rows][BK+pad]) so every lane reads its MFMA
-// fragment with one 16-byte ds_read.  The K loop prefetches tile k+1 into
-// registers while the MFMAs consume tile k.  256 threads = 4 waves in a 2x2
+// fragment with one 16-byte ds_read.  When two LDS stages fit (bf16), the K loop
+// is double-buffered with two register stages: step t+3 is loaded while step t
+// is multiplied, one barrier per K step.  256 threads = 4 waves in a 2x2
 // arrangement; each wave owns a (BM/2)x(BN/2) sub-tile of 16x16 fragments.
 //
 //   T = bf16_t : v_mfma_f32_16x16x32_bf16 (fp32 accumulate)
@@ -27,6 +28,14 @@ namespace mg {
 
 
 constexpr int NTHREADS = 256;
+// K-loop pipeline (build-time): tiles of at most MG_DB_MAX_TILE outputs double-buffer LDS (one barrier
+// per K step) when two stages fit 64 KiB; MG_NSTAGE register stages in that mode.
+#ifndef MG_DB_MAX_TILE
+#define MG_DB_MAX_TILE 0  // measured: double buffering lost to the occupancy it costs (v0-v3 A/B)
+#endif
+#ifndef MG_NSTAGE
+#define MG_NSTAGE 1
+#endif
 
 template <typename T> struct Frag;
 template <> struct Frag<bf16_t> { static constexpr int PAD = 8; };
@@ -526,11 +535,13 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   constexpr int A_VPT = BM * TBK / VEC / NTHREADS;
   constexpr int B_VPT = BN * TBK / VEC / NTHREADS;
   static_assert(A_VPT >= 1 && B_VPT >= 1, "tile too small for 256 threads");
-  // one LDS array: A tile, B tile; reused by the epilogue to stage accumulators
-  __shared__ __attribute__((aligned(16))) T smem[A_ELEMS + B_ELEMS];
-  T* As = smem;
-  T* Bs = smem + A_ELEMS;
-  static_assert(4 * 16 * (WN + 4) * 4 <= (int)sizeof(T) * (A_ELEMS + B_ELEMS), "epilogue staging does not fit");
+  // LDS: NBUF stages of (A tile, B tile), reused by the epilogue to stage accumulators.  Double
+  // buffering (with a second register stage) when two stages fit the 64 KiB static limit.
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
+  constexpr int NBUF = (2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE) ? 2 : 1;
+  constexpr int NS = NBUF == 2 ? MG_NSTAGE : 1;
+  __shared__ __attribute__((aligned(16))) T smem[NBUF * STAGE];
+  static_assert(4 * 16 * (WN + 4) * 4 <= (int)sizeof(T) * STAGE, "epilogue staging does not fit");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -539,7 +550,6 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   const int mlimit = mrow_base + Mloc;
 
   // ---- per-thread load slots ----
-  vec_t ra[A_VPT], rb[B_VPT];
   typename AL::Slot as_[A_VPT];
   typename BL::Slot bs_[B_VPT];
   int a_r[A_VPT], a_k[A_VPT], b_r[B_VPT], b_k[B_VPT];
@@ -560,33 +570,38 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   }
   const rsrc_t rA = A.rsrc(), rB = B.rsrc();
 
-  // issue the buffer loads of K step k0 (TAIL: the step reaches past kend)
-  auto gload = [&](int k0, auto tail) {
+  // NS register stages: the loads of K step t + NS are issued while step t is multiplied
+  vec_t ra[NS][A_VPT], rb[NS][B_VPT];
+  // issue the buffer loads of K step k0 into register stage R (TAIL: the step reaches past kend)
+  auto gload = [&](auto R, int k0, auto tail) {
+    constexpr int r = decltype(R)::value;
     constexpr bool TL = decltype(tail)::value;
 #pragma unroll
-    for (int i = 0; i < A_VPT; ++i) ra[i] = A.template load<TL, TBK>(rA, as_[i], k0, kend);
+    for (int i = 0; i < A_VPT; ++i) ra[r][i] = A.template load<TL, TBK>(rA, as_[i], k0, kend);
 #pragma unroll
-    for (int i = 0; i < B_VPT; ++i) rb[i] = B.template load<TL, TBK>(rB, bs_[i], k0, kend);
+    for (int i = 0; i < B_VPT; ++i) rb[r][i] = B.template load<TL, TBK>(rB, bs_[i], k0, kend);
   };
-  auto sstore = [&](int k0) {
+  auto gload_any = [&](auto R, int k0) {
+    if (k0 + TBK <= kend) gload(R, k0, std::false_type{});
+    else gload(R, k0, std::true_type{});
+  };
+  // register stage R (K step k0) -> LDS buffer (As, Bs)
+  auto sstore = [&](auto R, int k0, T* As, T* Bs) {
+    constexpr int r = decltype(R)::value;
 #pragma unroll
     for (int i = 0; i < A_VPT; ++i) {
-      vec_t v = ra[i];
+      vec_t v = ra[r][i];
       A.fix(as_[i], k0, v);
       if constexpr (A_KC) *reinterpret_cast<vec_t*>(&As[kc_off<T>(a_r[i], a_k[i], LDK)]) = v;
       else *reinterpret_cast<vec_t*>(&As[a_k[i] * LDA + (a_r[i] ^ mc_swz<T>(a_k[i]))]) = v;
     }
 #pragma unroll
     for (int i = 0; i < B_VPT; ++i) {
-      vec_t v = rb[i];
+      vec_t v = rb[r][i];
       B.fix(bs_[i], k0, v);
       if constexpr (B_KC) *reinterpret_cast<vec_t*>(&Bs[kc_off<T>(b_r[i], b_k[i], LDK)]) = v;
       else *reinterpret_cast<vec_t*>(&Bs[b_k[i] * LDB + (b_r[i] ^ mc_swz<T>(b_k[i]))]) = v;
     }
-  };
-  auto gload_any = [&](int k0) {
-    if (k0 + TBK <= kend) gload(k0, std::false_type{});
-    else gload(k0, std::true_type{});
   };
 
   f32x4_t acc[FM][FN];
@@ -596,12 +611,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  if (kbeg < kend) gload_any(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += TBK) {
-    __syncthreads();
-    sstore(k0);
-    __syncthreads();
-    if (k0 + TBK < kend) gload_any(k0 + TBK);
+  // one K step of MFMAs from the LDS buffer (As, Bs)
+  auto compute = [&](const T* As, const T* Bs) {
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int kk = 0; kk < TBK / 32; ++kk) {
@@ -640,6 +651,54 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 #pragma unroll
           for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
       }
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  if constexpr (NBUF == 2) {
+    // Two LDS buffers, one barrier per K step.  Step t multiplies LDS[t & 1], then writes the register
+    // stage holding step t+1 into LDS[(t+1) & 1] (last read by step t-1, whose closing barrier freed it)
+    // and refills that stage with step t+1+NS.
+    if (kbeg < kend) {
+      gload_any(I0{}, kbeg);
+      if constexpr (NS == 2)
+        if (kbeg + TBK < kend) gload_any(I1{}, kbeg + TBK);
+      sstore(I0{}, kbeg, smem, smem + A_ELEMS);
+      if (kbeg + NS * TBK < kend) gload_any(I0{}, kbeg + NS * TBK);
+      __syncthreads();
+    }
+    // one multiply per loop body (so the accumulators keep their registers); with two register stages
+    // the parity of the stage being written back is a uniform branch between two static-index copies
+    const int nsteps = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
+    for (int t = 0; t < nsteps; ++t) {
+      const int k0 = kbeg + t * TBK;
+      const T* cur = smem + (t & 1) * STAGE;
+      compute(cur, cur + A_ELEMS);
+      const int kn = k0 + TBK;
+      if (kn < kend) {
+        T* nxt = smem + ((t + 1) & 1) * STAGE;
+        if (NS == 1 || (t & 1)) {
+          sstore(I0{}, kn, nxt, nxt + A_ELEMS);
+          if (kn + NS * TBK < kend) gload_any(I0{}, kn + NS * TBK);
+        } else if constexpr (NS == 2) {
+          sstore(I1{}, kn, nxt, nxt + A_ELEMS);
+          if (kn + NS * TBK < kend) gload_any(I1{}, kn + NS * TBK);
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    // one LDS buffer, one register stage: store, barrier, prefetch the next step, multiply
+    T* const As = smem;
+    T* const Bs = smem + A_ELEMS;
+    if (kbeg < kend) gload_any(I0{}, kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += TBK) {
+      __syncthreads();
+      sstore(I0{}, k0, As, Bs);
+      __syncthreads();
+      if (k0 + TBK < kend) gload_any(I0{}, k0 + TBK);
+      compute(As, Bs);
     }
   }
 

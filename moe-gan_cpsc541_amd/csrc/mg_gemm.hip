@@ -124,7 +124,7 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
   int kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
   splits = (K + kchunk - 1) / kchunk;
   const int64_t MN = (int64_t)M * N;
-  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float)));
+  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float), st));
   if (!ws) return false;
   mg_epilogue raw{};
   raw.alpha = 1.f;
@@ -294,7 +294,7 @@ bool conv_slabs(const void* x, int B, int H, int W, int Cin, const void* wpack, 
   int kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
   splits = (K + kchunk - 1) / kchunk;
   const int64_t MN = (int64_t)M * Cout;
-  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float)));
+  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float), st));
   if (!ws) return false;
   mg_epilogue raw{};
   raw.alpha = 1.f;
@@ -404,7 +404,7 @@ bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, i
   int kchunk = ((P + splits - 1) / splits + TBK - 1) / TBK * TBK;
   splits = (P + kchunk - 1) / kchunk;
   const int64_t MN = (int64_t)Cout * N;
-  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float)));
+  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float), st));
   if (!ws) return false;
   LdMC<T> la{reinterpret_cast<const T*>(gy), ldg, Cout, P, nullptr, 1, nullptr, 0};
   LdMCConv<T, XF> lb{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), P,

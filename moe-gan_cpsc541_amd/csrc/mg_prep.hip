@@ -407,7 +407,7 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     int rblk = std::max(1, std::min({cdiv(R, 4 * ty), 512 / cblk, 64}));
     int rpb = cdiv(R, rblk);
     rblk = cdiv(R, rpb);
-    float* part = reinterpret_cast<float*>(mg_workspace((size_t)rblk * C * sizeof(float)));
+    float* part = reinterpret_cast<float*>(mg_workspace((size_t)rblk * C * sizeof(float), st));
     if (!part) {
       mg_set_error("mg_colsum: workspace allocation failed");
       return MG_ERR_LAUNCH;

@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmoegan_hip.so")
+LIB_PATH = os.environ.get("MOEGAN_HIP_LIB") or os.path.join(_HERE, "libmoegan_hip.so")  # override: A/B builds
 
 MG_F32, MG_BF16 = 0, 1
 ACT_NONE, ACT_LRELU, ACT_GELU, ACT_MUL_GELU_GRAD, ACT_MUL_LRELU_GRAD, ACT_RSQRT_EPS = 0, 1, 2, 3, 4, 5

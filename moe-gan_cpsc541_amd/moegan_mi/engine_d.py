@@ -21,7 +21,7 @@ All weights are weight-normed (g * v / ||v||); gradients flow back to g and v.
 import torch
 
 from . import _lib as L
-from . import ops
+from . import graphs, ops
 
 E_ = ops.E
 MUL_LRELU_GRAD, LRELU = L.ACT_MUL_LRELU_GRAD, L.ACT_LRELU
@@ -34,6 +34,8 @@ class DiscriminatorEngine:
         self.cdt = cdt
         self.dev = store.device
         self.ones_cache = {}
+        # weight gradients on a side stream, overlapping the data-gradient chain (joined before finish_grads)
+        self.side = graphs.SideStream(self.dev, enabled=graphs.side_streams_enabled(self.dev))
 
     def P(self, n):
         return self.st.view(n)
@@ -81,7 +83,8 @@ class DiscriminatorEngine:
             strides = (H * H * ld, H * ld, ld, 1)
         cols = ops.im2col_4x4s2(img, strides, B, H, H, 3, 48, self.cdt)  # [B*(H/2)^2, 48]
         h0 = ops.linear(cols, self.W0p, bias=self.P("conv_layers.0.bias"), act=LRELU).view(B, H // 2, H // 2, 128)
-        h1 = ops.conv2d(h0, self.W1p, 256, 4, 4, 2, 1, ep=E_(bias=self.P("conv_layers.2.bias"), act=LRELU))
+        h1 = ops.conv2d(h0, self.W1p, 256, 4, 4, 2, 1, ep=E_(bias=self.P("conv_layers.2.bias"), act=LRELU),
+                        tag="d_conv1")
         return cols, h0, h1
 
     def forward(self, img, layout, text, B, H):
@@ -99,14 +102,16 @@ class DiscriminatorEngine:
         Hf = H // 4
         g_a1, _ = self._head_bwd(g_img_part, g_img_part.shape[1], f["h1"], B, Hf, want_params)
         if want_params:
-            ops.conv2d_wgrad(g_a1, f["h0"], 256, 4, 4, 2, 1, self.dW["conv_layers.2."])
-            ops.colsum(g_a1.view(-1, 256), self.G("conv_layers.2.bias"))
+            dW1, gb1 = self.dW["conv_layers.2."], self.G("conv_layers.2.bias")
+            self.side.run(lambda: (ops.conv2d_wgrad(g_a1, f["h0"], 256, 4, 4, 2, 1, dW1),
+                                   ops.colsum(g_a1.view(-1, 256), gb1)), g_a1, f["h0"])
         g_a0 = torch.empty(B, H // 2, H // 2, 128, device=self.dev, dtype=self.cdt)
         ops.dgrad_s2(g_a1, self.W1cls, 128, g_a0, ep=E_(act=MUL_LRELU_GRAD, aux=f["h0"], ld_aux=128))
         if want_params:
-            ops.gemm(g_a0.view(-1, 128), f["cols"], 128, 48, g_a0.numel() // 128, a_kc=False, b_kc=False,
-                     out=self.dW["conv_layers.0."].view(128, 48), ep=E_(atomic=1), splits=0)
-            ops.colsum(g_a0.view(-1, 128), self.G("conv_layers.0.bias"))
+            dW0, gb0 = self.dW["conv_layers.0."].view(128, 48), self.G("conv_layers.0.bias")
+            self.side.run(lambda: (ops.gemm(g_a0.view(-1, 128), f["cols"], 128, 48, g_a0.numel() // 128, a_kc=False,
+                                            b_kc=False, out=dW0, ep=E_(atomic=1), splits=0),
+                                   ops.colsum(g_a0.view(-1, 128), gb0)), g_a0, f["cols"])
         if g_input is not None:
             ops.dgrad_s2(g_a0, self.W0cls, 3, g_input)
         return g_a1, g_a0
@@ -123,7 +128,8 @@ class DiscriminatorEngine:
         if want_w:
             X = h1f if wgrad_input is None else wgrad_input.view(Pn, 256)
             dW2img = self.dW["output_layer.0."].view(384, 16)[:256]
-            ops.gemm(X, G, 256, 16, Pn, a_kc=False, b_kc=False, out=dW2img, ep=E_(atomic=1), splits=0)
+            self.side.run(lambda: ops.gemm(X, G, 256, 16, Pn, a_kc=False, b_kc=False, out=dW2img, ep=E_(atomic=1),
+                                           splits=0), X, G)
         return g_a1, G
 
     def begin_grads(self):
@@ -179,12 +185,17 @@ class DiscriminatorEngine:
         ops.gemm(cols_u, self.W0p, cols_u.shape[0], 128, 48, out=m0v0.view(-1, 128),
                  ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
         m1v1 = ops.conv2d(m0v0, self.W1p, 256, 4, 4, 2, 1, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h1"], ld_aux=256))
-        ops.gemm(gA0.view(-1, 128), cols_u, 128, 48, gA0.numel() // 128, a_kc=False, b_kc=False,
-                 out=self.dW["conv_layers.0."].view(128, 48), ep=E_(atomic=1), splits=0)
-        ops.conv2d_wgrad(gA1, m0v0, 256, 4, 4, 2, 1, self.dW["conv_layers.2."])
+        dW0, dW1 = self.dW["conv_layers.0."].view(128, 48), self.dW["conv_layers.2."]
         dW2img = self.dW["output_layer.0."].view(384, 16)[:256]
-        ops.gemm(m1v1.view(-1, 256), G1, 256, 16, B * Hf * Hf, a_kc=False, b_kc=False, out=dW2img,
-                 ep=E_(atomic=1), splits=0)
+
+        def r1_wgrads():
+            ops.gemm(gA0.view(-1, 128), cols_u, 128, 48, gA0.numel() // 128, a_kc=False, b_kc=False, out=dW0,
+                     ep=E_(atomic=1), splits=0)
+            ops.conv2d_wgrad(gA1, m0v0, 256, 4, 4, 2, 1, dW1)
+            ops.gemm(m1v1.view(-1, 256), G1, 256, 16, B * Hf * Hf, a_kc=False, b_kc=False, out=dW2img,
+                     ep=E_(atomic=1), splits=0)
+        self.side.run(r1_wgrads, gA0, cols_u, gA1, m0v0, m1v1, G1)
+        self.side.join()
         self._remap_w0()
         self.finish_grads()
         return dict(losses=out, r1=r1, real_pred=real_pred, mism_pred=mism_pred, fake_pred=fake_pred, r1_grad=gx)
@@ -215,6 +226,7 @@ class DiscriminatorEngine:
         self.stack_backward(f, g, want_params=want_d_params, g_input=g_img)
         if want_d_params:
             self._text_head_bwd(g.view(-1), t, text)
+            self.side.join()
             self._remap_w0()
             self.finish_grads()
         return loss, fake_pred, g_img
@@ -250,6 +262,7 @@ class DiscriminatorEngine:
         g_img = torch.zeros(B, H, H, 4, device=self.dev, dtype=torch.float32) if want_input else None
         self.stack_backward(f, g_logits, want_params=True, g_input=g_img)
         self._text_head_bwd(g_tb, ctx["t"], ctx["text"])
+        self.side.join()
         self._remap_w0()
         self.finish_grads()
         return None if g_img is None else g_img[..., :3].permute(0, 3, 1, 2).contiguous()

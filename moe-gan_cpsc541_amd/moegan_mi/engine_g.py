@@ -15,7 +15,7 @@ permutation are inputs (SURVEY.md §7 "Randomness parity").
 import torch
 
 from . import _lib as L
-from . import ops
+from . import graphs, ops
 from .layout import GEN_BLOCKS
 
 E_ = ops.E
@@ -50,6 +50,8 @@ class GeneratorEngine:
         self._demod_bwd = []
         self._mean_latent = None
         self._want_kl = True
+        # weight gradients run on a side stream, overlapping the data-gradient chain (joined in backward)
+        self.side = graphs.SideStream(self.dev, enabled=graphs.side_streams_enabled(self.dev))
 
     # parameter access
     def P(self, n):
@@ -154,18 +156,22 @@ class GeneratorEngine:
             gs = torch.zeros(B, Cin, device=self.dev, dtype=torch.float32)
         ops.modconv_bwd_in(gxt.view(P, Cin), x.view(P, Cin), s, B, HW, Cin,
                            None if gx is None else gx.view(P, -1), gs, accumulate)
-        # weight gradient (fp32, reference layout)
+        # weight gradient (fp32, reference layout), on the side stream
+        gW = self.G(pre + "weight")
         if rows == Cout:
-            ops.conv2d_wgrad(gyt, xs, Cout, k, k, 1, k // 2, self.G(pre + "weight"))
+            self.side.run(lambda: ops.conv2d_wgrad(gyt, xs, Cout, k, k, 1, k // 2, gW), gyt, xs)
         else:
-            tmp = torch.zeros(rows, Cin, k, k, device=self.dev)
-            ops.conv2d_wgrad(gyt, xs, rows, k, k, 1, k // 2, tmp)
-            self.G(pre + "weight").add_(tmp[:Cout])
+            def wgrad_padded():
+                tmp = torch.zeros(rows, Cin, k, k, device=self.dev)
+                ops.conv2d_wgrad(gyt, xs, rows, k, k, 1, k // 2, tmp)
+                gW.add_(tmp[:Cout])
+            self.side.run(wgrad_padded, gyt, xs)
         # demodulation backward
         if batched:  # deferred: all modulated convs' demod + style backward run batched at the end
             self._demod_bwd.append((pre, gdd, s2, s, gs, Cin, rows, Cout))
             return
         gwsq = ops.gemm(gdd, s2, rows, Cin, B, a_kc=False, b_kc=False)  # [rows, Cin] = gdd^T s^2
+        self.side.join()  # the side stream's conv weight gradient accumulates into the same tensor
         ops.wsq_bwd(Wt, gwsq[:Cout], self.G(pre + "weight"))
         ops.gemm(gdd, pk["wsq"], B, Cin, rows, b_kc=False, out=gs,
                  ep=E_(alpha=2.0, scale=s, scale_ld=s.stride(0), accumulate=1))  # gs += 2 s (gdd @ wsq)
@@ -301,17 +307,17 @@ class GeneratorEngine:
         ops.gemm_grouped(gG, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
                          out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd))
         gW2 = self.st.group_view(ex + "0.net.2.weight", f"{ex}{E-1}.net.2.weight", self.st.grad)
-        ops.gemm_grouped_wgrad(gG, sv["Hid"], row_off, n, C, Hd, gW2)
         gb2 = self.st.group_view(ex + "0.net.2.bias", f"{ex}{E-1}.net.2.bias", self.st.grad)
-        ops.grouped_colsum(gG, row_off, C, n, gb2)
+        self.side.run(lambda: (ops.gemm_grouped_wgrad(gG, sv["Hid"], row_off, n, C, Hd, gW2),
+                               ops.grouped_colsum(gG, row_off, C, n, gb2)), gG)
         # expert layer 1
         gX = torch.empty(n, C, device=self.dev, dtype=self.cdt)
         ops.gemm_grouped(gP, sv["W1"], row_off, tile_off, sv["max_tiles"], C, Hd, b_kc=False, b_gstride=Hd * C,
                          out=gX, ldb=C)
         gW1 = self.st.group_view(ex + "0.net.0.weight", f"{ex}{E-1}.net.0.weight", self.st.grad)
-        ops.gemm_grouped_wgrad(gP, sv["Xg"], row_off, n, Hd, C, gW1)
         gb1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias", self.st.grad)
-        ops.grouped_colsum(gP, row_off, Hd, n, gb1)
+        self.side.run(lambda: (ops.gemm_grouped_wgrad(gP, sv["Xg"], row_off, n, Hd, C, gW1),
+                               ops.grouped_colsum(gP, row_off, Hd, n, gb1)), gP)
         # router
         g_raw, gsum = ops.router_bwd(sv["probs"], sv["zlog"], sv["topi"], sv["gate"], g_gate, g_probs, coef,
                                      sv["HW"], self.P(r + "temperature"), sv["anneal"], self.G(r + "temperature"), B)
@@ -390,8 +396,8 @@ class GeneratorEngine:
         ops.colsum(g_xf1, self.G(pre + "self_attn.out_proj.bias"))
         g_qkv = ops.attn_bwd(sv["qkv"], sv["att"], g_att, sv["lse"], B, L_, C)
         g_n1 = ops.linear_dgrad(g_qkv, self.Pc(pre + "self_attn.in_proj_weight"))
-        ops.linear_wgrad(g_qkv, sv["n1"], self.G(pre + "self_attn.in_proj_weight"))
-        ops.colsum(g_qkv, self.G(pre + "self_attn.in_proj_bias"))
+        gWqkv, gbqkv = self.G(pre + "self_attn.in_proj_weight"), self.G(pre + "self_attn.in_proj_bias")
+        self.side.run(lambda: (ops.linear_wgrad(g_qkv, sv["n1"], gWqkv), ops.colsum(g_qkv, gbqkv)), g_qkv)
         g_xf0 = g_xf1
         ops.layernorm_bwd(g_n1, sv["xf0"], sv["mu1"], sv["rs1"], self.P(pre + "norm1.weight"), g_xf0,
                           self.G(pre + "norm1.weight"), self.G(pre + "norm1.bias"), accumulate=1)
@@ -510,6 +516,7 @@ class GeneratorEngine:
             else:
                 gx = g_in
         ops.const_bwd(gx, self.G("constant"))
+        self.side.join()  # every weight gradient is in place before the demodulation backward adds to it
         if self._GS is not None:  # all modulated convs' demodulation and style backward at once
             pw, pg = [], []
             for pre, gdd, s2, s, gs, Cin, rows, Cout in self._demod_bwd:

@@ -13,9 +13,13 @@ memory pool, so addresses baked into the graphs stay valid for every replay.
 
 Inputs are fixed buffers: refill them (``copy_`` / ``normal_``) before ``replay()``.
 """
+import os
+import weakref
+
 import torch
 
 ACTIVE = None  # the SegmentedGraph being captured, if any
+_SIDES = weakref.WeakSet()  # live SideStreams: joined at every eager boundary (a segment must end joined)
 
 
 def eager(fn):
@@ -30,15 +34,23 @@ class SegmentedGraph:
         self.items = []  # ("graph", CUDAGraph) | ("eager", fn)
         self.pool = None
         self._cur = None
-        self.stream = None
+        self.stream = torch.cuda.Stream()  # capture stream (the library keeps one workspace per stream)
+
+    def run_eager(self, fn, *args, **kwargs):
+        """Run ``fn`` eagerly on the capture stream: the warm-up that sizes every lazily allocated buffer,
+        including the library's per-stream workspace, for the stream the capture will use."""
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            r = fn(*args, **kwargs)
+        torch.cuda.current_stream().wait_stream(self.stream)
+        return r
 
     def capture(self, fn, *args, **kwargs):
-        """Capture ``fn(*args, **kwargs)`` (which must already have run eagerly once with the same shapes,
-        so every lazily sized buffer exists).  Returns fn's result (tensors in the graph pool)."""
+        """Capture ``fn(*args, **kwargs)`` (which must already have run once through ``run_eager`` with the
+        same shapes, so every lazily sized buffer exists).  Returns fn's result (tensors in the graph pool)."""
         global ACTIVE
         assert ACTIVE is None, "nested capture"
         self.pool = torch.cuda.graph_pool_handle()
-        self.stream = torch.cuda.Stream()
         self.stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.stream):
             ACTIVE = self
@@ -63,6 +75,8 @@ class SegmentedGraph:
         self._cur = None
 
     def _eager(self, fn):
+        for side in list(_SIDES):
+            side.join()
         self._end()
         r = fn()
         self.items.append(("eager", fn))
@@ -79,3 +93,43 @@ class SegmentedGraph:
                 x.replay()
             else:
                 x()
+
+
+def side_streams_enabled(device):
+    """Side streams only on request (MOEGAN_SIDE_STREAM=1): measured on the C2 step with hipGraph replay,
+    overlapping the weight gradients with the data-gradient chain was slower (13.42 vs 13.02 ms/step)."""
+    return torch.device(device).type == "cuda" and os.environ.get("MOEGAN_SIDE_STREAM", "0") == "1"
+
+
+class SideStream:
+    """Fork independent work (weight gradients) onto a second HIP stream and join it back.
+
+    ``run(fn, *keep)`` makes the side stream wait for everything enqueued so far on the current
+    stream, then enqueues ``fn`` on the side stream; ``keep`` are tensors allocated on the current
+    stream that ``fn`` reads -- they are held until ``join()``, so the caching allocator cannot hand
+    their memory to later current-stream work while the side stream may still read it.
+    ``join()`` makes the current stream wait for the side stream.  Under capture the fork/join
+    become graph edges (the side stream joins the capture through the event it waits on); a
+    segment must be joined before it ends (``eager`` boundaries, the end of the step)."""
+
+    def __init__(self, device, enabled=True):
+        self.s = torch.cuda.Stream(device) if enabled else None
+        self.keep = []
+        self.pending = False
+        _SIDES.add(self)
+
+    def run(self, fn, *keep):
+        if self.s is None:
+            return fn()
+        self.s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.s):
+            r = fn()
+        self.keep.extend(keep)
+        self.pending = True
+        return r
+
+    def join(self):
+        if self.pending:
+            torch.cuda.current_stream().wait_stream(self.s)
+            self.pending = False
+            self.keep.clear()

@@ -118,14 +118,16 @@ def linear_wgrad(g, x, gW, alpha=1.0):
                 ep=E(alpha=alpha, atomic=1), splits=0)
 
 
-def conv2d(x, wpack, Cout, KH, KW, stride=1, pad=0, in_scale=None, out=None, out_dtype=None, ep=None, ldy=None):
-    """NHWC implicit-GEMM conv (mg_conv2d_fwd): x [B,H,W,Cin] -> [B,OH,OW,Cout]."""
+def conv2d(x, wpack, Cout, KH, KW, stride=1, pad=0, in_scale=None, out=None, out_dtype=None, ep=None, ldy=None,
+           tag=None):
+    """NHWC implicit-GEMM conv (mg_conv2d_fwd): x [B,H,W,Cin] -> [B,OH,OW,Cout].  ``tag`` names the call site
+    for the live kernel timer (kind "conv2d:<tag>")."""
     B, H, W, Cin = x.shape
     OH = (H + 2 * pad - KH) // stride + 1
     OW = (W + 2 * pad - KW) // stride + 1
     if out is None:
         out = torch.empty(B, OH, OW, ldy or Cout, device=x.device, dtype=out_dtype or x.dtype)
-    _timed("conv2d", (B * OH * OW, Cout, KH * KW * Cin),
+    _timed("conv2d" if tag is None else "conv2d:" + tag, (B * OH * OW, Cout, KH * KW * Cin),
            lambda: call("mg_conv2d_fwd", dt(x), ptr(x), B, H, W, Cin, ptr(wpack), Cout, KH, KW, stride, pad,
                         ptr(in_scale), ptr(out), ldy or out.shape[-1], dt(out), ep, S()))
     return out
