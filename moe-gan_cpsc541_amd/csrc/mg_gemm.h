@@ -36,6 +36,10 @@ constexpr int NTHREADS = 256;
 #ifndef MG_NSTAGE
 #define MG_NSTAGE 1
 #endif
+// LDS-DMA (buffer_load ... lds) staging for bf16 KC x KC tiles
+#ifndef MG_GLDS
+#define MG_GLDS 0  // measured: on par with register staging at C2 (gemm 4096^3 +9%, expert GEMMs -20%)
+#endif
 
 template <typename T> struct Frag;
 template <> struct Frag<bf16_t> { static constexpr int PAD = 8; };
@@ -101,6 +105,23 @@ MG_DEV rsrc_t make_rsrc(const void* p) {
 template <typename V> MG_DEV V bload(rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
+// LDS-DMA form (buffer_load_dwordx4 ... lds): the wave's 64 x 16 B land contiguously at the wave-uniform
+// LDS address `lds` (lane order); out-of-range offsets write zeros.
+MG_DEV void bload_lds(rsrc_t r, uint32_t voff, uint32_t soff, void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+// KC loaders define offs<TAIL, TBK>(slot, k0, kend, voff, soff); load / glds derive from it.
+#define MG_KC_LOADS                                                                                           \
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {          \
+    uint32_t o, so;                                                                                           \
+    offs<TAIL, TBK>(s, k0, kend, o, so);                                                                      \
+    return bload<vec_t>(r, o, so);                                                                            \
+  }                                                                                                           \
+  template <bool TAIL, int TBK> MG_DEV void glds(rsrc_t r, const Slot& s, int k0, int kend, void* lds) const { \
+    uint32_t o, so;                                                                                           \
+    offs<TAIL, TBK>(s, k0, kend, o, so);                                                                      \
+    bload_lds(r, o, so, lds);                                                                                 \
+  }
 
 // KC, plain rows with optional row gather / per-row scale / GELU-on-load (XF).
 //   row r -> source row (idx ? idx[r] / idx_div : r); value *= rs[r] if rs
@@ -126,11 +147,13 @@ struct LdKC {
     }
     return s;
   }
-  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
-    uint32_t off = s.off;
+  static constexpr bool kGlds = !XF;  // no transform: may stage by LDS-DMA
+  template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
+    off = s.off;
     if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
-    return bload<vec_t>(r, off, (uint32_t)k0 * (uint32_t)sizeof(T));
+    soff = (uint32_t)k0 * (uint32_t)sizeof(T);
   }
+  MG_KC_LOADS
   MG_DEV void fix(const Slot& s, int, vec_t& v) const {
     if constexpr (XF) {
       if (gelu) v = vgelu(v);
@@ -170,17 +193,19 @@ struct LdKCConv {
     s.mask = m;
     return s;
   }
-  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+  static constexpr bool kGlds = !XF;
+  template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
     const int k = k0 + s.kofs;
     const int kk = SC ? k : k0;  // SC = false: k0 is a multiple of TBK <= Cin, the step stays inside tap k0 / Cin
     const int tap = kk >> lgCin;
     const int kh = (tap * kwinv) >> 16, kw = tap - kh * KW;
     const int tapoff = (((kh * W + kw) << lgCin) + (kk & (Cin - 1))) * (int)sizeof(T);
     // invalid tap -> bit 31 set (out of range); arithmetic, not a select, so no branch is formed
-    uint32_t off = (uint32_t)(s.base + tapoff + (SC ? 0 : s.kofs * (int)sizeof(T))) | ((~s.mask >> tap) << 31);
+    off = (uint32_t)(s.base + tapoff + (SC ? 0 : s.kofs * (int)sizeof(T))) | ((~s.mask >> tap) << 31);
     if constexpr (TAIL) off = k < kend ? off : MG_OOB;
-    return bload<vec_t>(r, off, 0);
+    soff = 0;
   }
+  MG_KC_LOADS
   MG_DEV void fix(const Slot& s, int k0, vec_t& v) const {
     if constexpr (XF) {
       if (scale) v = vscale(v, scale + (int64_t)s.b * Cin + ((k0 + s.kofs) & (Cin - 1)));
@@ -195,6 +220,7 @@ struct LdMC {
   const T* p; int64_t ld; int cols; int K;
   const int* idx; int idx_div; const float* rs; int gelu;
   struct Slot { uint32_t off; int kofs; bool ok; };
+  static constexpr bool kGlds = false;
   MG_DEV void set_group(int) {}
   MG_DEV rsrc_t rsrc() const { return make_rsrc(p); }
   MG_DEV Slot slot(int c0, int kofs, bool ok) const {
@@ -232,6 +258,7 @@ struct LdMCConv {
   int KW, stride, pad, cols;
   const float* scale;  // XF only
   struct Slot { int dh, dw, ci, kofs; uint32_t bad; };
+  static constexpr bool kGlds = false;
   MG_DEV void set_group(int) {}
   MG_DEV rsrc_t rsrc() const { return make_rsrc(x); }
   MG_DEV Slot slot(int c0, int kofs, bool ok) const {
@@ -292,16 +319,18 @@ struct LdKCConvT {
     s.mask = m;
     return s;
   }
-  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+  static constexpr bool kGlds = !XF;
+  template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
     const int k = k0 + s.kofs;
     const int kk = SC ? k : k0;  // SC = false: the step stays inside tap k0 / Cg (wave-uniform)
     const int t = kk >> lgCg;
     const int dy = dy_of(cls >> 1, t >> 1), dx = dy_of(cls & 1, t & 1);
     const int tapoff = (((dy * OW + dx) << lgCg) + (kk & (Cg - 1))) * (int)sizeof(T);
-    uint32_t off = (uint32_t)(s.base + tapoff + (SC ? 0 : s.kofs * (int)sizeof(T))) | ((~s.mask >> t) << 31);
+    off = (uint32_t)(s.base + tapoff + (SC ? 0 : s.kofs * (int)sizeof(T))) | ((~s.mask >> t) << 31);
     if constexpr (TAIL) off = k < kend ? off : MG_OOB;
-    return bload<vec_t>(r, off, 0);
+    soff = 0;
   }
+  MG_KC_LOADS
   MG_DEV void fix(const Slot&, int, vec_t&) const {}
 };
 
@@ -317,11 +346,13 @@ struct LdKCGroupW {
   MG_DEV Slot slot(int r, int kofs, bool ok) const {
     return Slot{(ok && r < rows) ? (uint32_t)(((int64_t)r * ld + kofs) * (int64_t)sizeof(T)) : MG_OOB, kofs};
   }
-  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
-    uint32_t off = s.off;
+  static constexpr bool kGlds = !XF;
+  template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
+    off = s.off;
     if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
-    return bload<vec_t>(r, off, (uint32_t)k0 * (uint32_t)sizeof(T));
+    soff = (uint32_t)k0 * (uint32_t)sizeof(T);
   }
+  MG_KC_LOADS
   MG_DEV void fix(const Slot&, int, vec_t&) const {}
 };
 template <typename T, bool XF = false>
@@ -330,6 +361,7 @@ struct LdMCGroupW {
   const T* p0; int64_t ld; int cols; int K; int64_t gstride;
   const T* p;
   struct Slot { uint32_t off; int kofs; };
+  static constexpr bool kGlds = false;
   MG_DEV void set_group(int g) { p = p0 + (int64_t)g * gstride; }
   MG_DEV rsrc_t rsrc() const { return make_rsrc(p); }
   MG_DEV Slot slot(int c0, int kofs, bool ok) const {
@@ -538,7 +570,10 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   // LDS: NBUF stages of (A tile, B tile), reused by the epilogue to stage accumulators.  Double
   // buffering (with a second register stage) when two stages fit the 64 KiB static limit.
   constexpr int STAGE = A_ELEMS + B_ELEMS;
-  constexpr int NBUF = (2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE) ? 2 : 1;
+  // LDS-DMA staging (bf16, both operands k-contiguous without transforms): two LDS stages, no registers
+  constexpr bool GLDS = MG_GLDS && sizeof(T) == 2 && A_KC && B_KC && AL::kGlds && BL::kGlds &&
+                        2 * STAGE * (int)sizeof(T) <= 65536;
+  constexpr int NBUF = (GLDS || (2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE)) ? 2 : 1;
   constexpr int NS = NBUF == 2 ? MG_NSTAGE : 1;
   __shared__ __attribute__((aligned(16))) T smem[NBUF * STAGE];
   static_assert(4 * 16 * (WN + 4) * 4 <= (int)sizeof(T) * STAGE, "epilogue staging does not fit");
@@ -553,10 +588,14 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   typename AL::Slot as_[A_VPT];
   typename BL::Slot bs_[B_VPT];
   int a_r[A_VPT], a_k[A_VPT], b_r[B_VPT], b_k[B_VPT];
+  // GLDS: wave-instruction i of wave w fills LDS rows (4i + w) * 8 .. +8 (1 KiB, lane order); lane L takes
+  // row +(L >> 3) and stores physical chunk L & 7, so it loads logical chunk (L & 7) ^ (row & 7) (the swizzle
+  // moves to the source address; fragment reads use kc_off unchanged).
 #pragma unroll
   for (int i = 0; i < A_VPT; ++i) {
     int v = tid + i * NTHREADS;
-    if constexpr (A_KC) { a_r[i] = v / (TBK / VEC); a_k[i] = (v % (TBK / VEC)) * VEC; }
+    if constexpr (GLDS) { a_r[i] = (i * 4 + wid) * 8 + (lane >> 3); a_k[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7)); }
+    else if constexpr (A_KC) { a_r[i] = v / (TBK / VEC); a_k[i] = (v % (TBK / VEC)) * VEC; }
     else { a_k[i] = v / (BM / VEC); a_r[i] = (v % (BM / VEC)) * VEC; }
     const int r = mrow_base + m0 + a_r[i];
     as_[i] = A.slot(r, a_k[i], r < mlimit);
@@ -564,7 +603,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 #pragma unroll
   for (int i = 0; i < B_VPT; ++i) {
     int v = tid + i * NTHREADS;
-    if constexpr (B_KC) { b_r[i] = v / (TBK / VEC); b_k[i] = (v % (TBK / VEC)) * VEC; }
+    if constexpr (GLDS) { b_r[i] = (i * 4 + wid) * 8 + (lane >> 3); b_k[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7)); }
+    else if constexpr (B_KC) { b_r[i] = v / (TBK / VEC); b_k[i] = (v % (TBK / VEC)) * VEC; }
     else { b_k[i] = v / (BN / VEC); b_r[i] = (v % (BN / VEC)) * VEC; }
     bs_[i] = B.slot(n0 + b_r[i], b_k[i], true);
   }
@@ -656,7 +696,42 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
-  if constexpr (NBUF == 2) {
+  if constexpr (GLDS) {
+    // LDS-DMA, two stages: step t+1's loads are issued before step t is multiplied; a counted vmcnt
+    // retires only step t's (issued earlier), a raw barrier publishes them, and a second barrier keeps
+    // step t+2's DMA from overwriting the buffer while another wave still reads it.
+    static_assert(A_VPT + B_VPT < 64, "vmcnt range");
+    auto issue = [&](int k0, T* buf) {
+      if (k0 + TBK <= kend) {
+#pragma unroll
+        for (int i = 0; i < A_VPT; ++i) A.template glds<false, TBK>(rA, as_[i], k0, kend, buf + (i * 4 + wid) * 8 * LDK);
+#pragma unroll
+        for (int i = 0; i < B_VPT; ++i)
+          B.template glds<false, TBK>(rB, bs_[i], k0, kend, buf + A_ELEMS + (i * 4 + wid) * 8 * LDK);
+      } else {
+#pragma unroll
+        for (int i = 0; i < A_VPT; ++i) A.template glds<true, TBK>(rA, as_[i], k0, kend, buf + (i * 4 + wid) * 8 * LDK);
+#pragma unroll
+        for (int i = 0; i < B_VPT; ++i)
+          B.template glds<true, TBK>(rB, bs_[i], k0, kend, buf + A_ELEMS + (i * 4 + wid) * 8 * LDK);
+      }
+    };
+    const int nsteps = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
+    if (nsteps > 0) issue(kbeg, smem);
+    for (int t = 0; t < nsteps; ++t) {
+      T* cur = smem + (t & 1) * STAGE;
+      if (t + 1 < nsteps) {
+        issue(kbeg + (t + 1) * TBK, smem + ((t + 1) & 1) * STAGE);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_VPT + B_VPT) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      compute(cur, cur + A_ELEMS);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of cur have landed (WAR)
+      __builtin_amdgcn_s_barrier();
+    }
+  } else if constexpr (NBUF == 2) {
     // Two LDS buffers, one barrier per K step.  Step t multiplies LDS[t & 1], then writes the register
     // stage holding step t+1 into LDS[(t+1) & 1] (last read by step t-1, whose closing barrier freed it)
     // and refills that stage with step t+1+NS.

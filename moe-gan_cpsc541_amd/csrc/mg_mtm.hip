@@ -75,6 +75,100 @@ __global__ void k_warp_fwd(const T* __restrict__ x, const T* __restrict__ o1, co
   }
 }
 
+// Vectorised warp forward: one 16-B channel vector per thread, G = C / VEC threads per output pixel
+// (contiguous lanes), 256 / G pixels per block.  The pixel's G threads split the 9 taps x 32 channels of
+// the offset conv, reduce (s0, s1) with lane shuffles, then each gathers the 4 bilinear taps of its own
+// channel vector with 16-B loads and stores 16 B.  Same math as k_warp_fwd.
+template <typename T>
+__global__ __launch_bounds__(256) void k_warp_fwd_v(const T* __restrict__ x, const T* __restrict__ o1,
+                                                    const float* __restrict__ w2, const float* __restrict__ b2,
+                                                    int B, int H, int W, int C, int lgG, T* __restrict__ out,
+                                                    float* __restrict__ samp) {
+  constexpr int VEC = VecOf<T>::N;
+  typedef typename VecOf<T>::type vec_t;
+  constexpr int OV = 32 / VEC;  // offset-conv input vectors per tap
+  __shared__ float sw[9 * 32 * 2];  // [tap][c][j]
+  for (int i = threadIdx.x; i < 576; i += 256) {
+    const int j = i / 288, c = (i / 9) % 32, tap = i % 9;
+    sw[(tap * 32 + c) * 2 + j] = w2[i];
+  }
+  __syncthreads();
+  const int G = 1 << lgG;
+  const int g = threadIdx.x & (G - 1);
+  const int64_t p = (int64_t)blockIdx.x * (256 >> lgG) + (threadIdx.x >> lgG);
+  const int64_t P = (int64_t)B * H * W;
+  const bool live = p < P;
+  const int64_t pp = live ? p : 0;
+  const int b = (int)(pp / (H * W));
+  const int rem = (int)(pp - (int64_t)b * H * W);
+  const int h = rem / W, w = rem - (rem / W) * W;
+  float s0 = 0.f, s1 = 0.f;
+  for (int v = g; v < 9 * OV; v += G) {
+    const int tap = v / OV, c0 = (v - tap * OV) * VEC;
+    const int kh = tap / 3, kw = tap - kh * 3;
+    const int yy = h + kh - 1, xx = w + kw - 1;
+    if (live && yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      float t[VEC];
+      const vec_t raw = *reinterpret_cast<const vec_t*>(o1 + (((int64_t)b * H + yy) * W + xx) * 32 + c0);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) t[e] = sizeof(T) == 2 ? bf2f((bf16_t)raw[e]) : (float)raw[e];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        s0 += t[e] * sw[(tap * 32 + c0 + e) * 2];
+        s1 += t[e] * sw[(tap * 32 + c0 + e) * 2 + 1];
+      }
+    }
+  }
+  for (int o = G >> 1; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o, 64);
+    s1 += __shfl_xor(s1, o, 64);
+  }
+  if (!live) return;
+  s0 += b2[0];
+  s1 += b2[1];
+  float gx = linspace_pm1(w, W) + s0 * 0.05f;
+  float gy = linspace_pm1(h, H) + s1 * 0.05f;
+  const float mx = (gx >= -1.f && gx <= 1.f) ? 1.f : 0.f;
+  const float my = (gy >= -1.f && gy <= 1.f) ? 1.f : 0.f;
+  gx = fminf(fmaxf(gx, -1.f), 1.f);
+  gy = fminf(fmaxf(gy, -1.f), 1.f);
+  const float ix = ((gx + 1.f) * W - 1.f) * 0.5f;
+  const float iy = ((gy + 1.f) * H - 1.f) * 0.5f;
+  if (g == 0) *reinterpret_cast<f32x4_t*>(samp + p * 4) = f32x4_t{ix, iy, mx, my};
+  const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+  const int x1 = x0 + 1, y1 = y0 + 1;
+  const float wnw = ((float)x1 - ix) * ((float)y1 - iy);
+  const float wne = (ix - (float)x0) * ((float)y1 - iy);
+  const float wsw = ((float)x1 - ix) * (iy - (float)y0);
+  const float wse = (ix - (float)x0) * (iy - (float)y0);
+  const bool vx0 = x0 >= 0 && x0 < W, vx1 = x1 >= 0 && x1 < W, vy0 = y0 >= 0 && y0 < H, vy1 = y1 >= 0 && y1 < H;
+  const T* xb = x + (int64_t)b * H * W * C;
+  for (int c = g * VEC; c < C; c += G * VEC) {
+    float acc[VEC], t[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+    auto tap = [&](bool ok, int yy, int xx, float wt) {
+      if (!ok) return;
+      const vec_t raw = *reinterpret_cast<const vec_t*>(xb + ((int64_t)yy * W + xx) * C + c);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) t[e] = sizeof(T) == 2 ? bf2f((bf16_t)raw[e]) : (float)raw[e];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[e] += wt * t[e];
+    };
+    tap(vy0 && vx0, y0, x0, wnw);
+    tap(vy0 && vx1, y0, x1, wne);
+    tap(vy1 && vx0, y1, x0, wsw);
+    tap(vy1 && vx1, y1, x1, wse);
+    vec_t r;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      if constexpr (sizeof(T) == 2) r[e] = f2bf(acc[e]);
+      else r[e] = acc[e];
+    }
+    *reinterpret_cast<vec_t*>(out + p * C + c) = r;
+  }
+}
+
 template <typename T, typename TG>
 __global__ void k_warp_bwd(const TG* __restrict__ gout, const T* __restrict__ x, const float* __restrict__ samp,
                            int B, int H, int W, int C, float* __restrict__ gx, float* __restrict__ goff) {
@@ -127,6 +221,74 @@ __global__ void k_warp_bwd(const TG* __restrict__ gout, const T* __restrict__ x,
   if (lane == 0) {
     goff[p * 2 + 0] = gix * (0.5f * W) * mx * 0.05f;
     goff[p * 2 + 1] = giy * (0.5f * H) * my * 0.05f;
+  }
+}
+
+// Warp backward for images of at most 256 pixels: one block per (image, 64-channel chunk) owns that slice
+// of dL/dx, so the bilinear scatter accumulates in LDS (ds_add_f32, lane = channel: conflict-free) and is
+// added to gx once with plain stores -- instead of four global fp32 atomics per element.  dL/dgrid is
+// reduced across the wave per pixel and added to goff (zeroed by the launcher) with one atomic per chunk.
+template <typename T, typename TG>
+__global__ __launch_bounds__(512) void k_warp_bwd_lds(const TG* __restrict__ gout, const T* __restrict__ x,
+                                                      const float* __restrict__ samp, int B, int H, int W, int C,
+                                                      float* __restrict__ gx, float* __restrict__ goff) {
+  extern __shared__ float acc[];  // [H*W][64]
+  const int b = blockIdx.x, c0 = blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int HW = H * W;
+  for (int i = threadIdx.x; i < HW * 64; i += blockDim.x) acc[i] = 0.f;
+  __syncthreads();
+  const T* xb = x + (int64_t)b * HW * C + c0 + lane;
+  for (int q = wv; q < HW; q += nw) {
+    const int64_t p = (int64_t)b * HW + q;
+    const f32x4_t sp = *reinterpret_cast<const f32x4_t*>(samp + p * 4);
+    const float ix = sp[0], iy = sp[1], mx = sp[2], my = sp[3];
+    const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+    const int x1 = x0 + 1, y1 = y0 + 1;
+    const float ax1 = (float)x1 - ix, ax0 = ix - (float)x0, ay1 = (float)y1 - iy, ay0 = iy - (float)y0;
+    const bool vx0 = x0 >= 0 && x0 < W, vx1 = x1 >= 0 && x1 < W, vy0 = y0 >= 0 && y0 < H, vy1 = y1 >= 0 && y1 < H;
+    const float g = ldf(gout, p * C + c0 + lane);
+    float gix = 0.f, giy = 0.f;
+    if (vy0 && vx0) {
+      const int o = y0 * W + x0;
+      const float v = ldf(xb, (int64_t)o * C);
+      gix -= v * ay1 * g;
+      giy -= v * ax1 * g;
+      atomicAdd(&acc[o * 64 + lane], ax1 * ay1 * g);
+    }
+    if (vy0 && vx1) {
+      const int o = y0 * W + x1;
+      const float v = ldf(xb, (int64_t)o * C);
+      gix += v * ay1 * g;
+      giy -= v * ax0 * g;
+      atomicAdd(&acc[o * 64 + lane], ax0 * ay1 * g);
+    }
+    if (vy1 && vx0) {
+      const int o = y1 * W + x0;
+      const float v = ldf(xb, (int64_t)o * C);
+      gix -= v * ay0 * g;
+      giy += v * ax1 * g;
+      atomicAdd(&acc[o * 64 + lane], ax1 * ay0 * g);
+    }
+    if (vy1 && vx1) {
+      const int o = y1 * W + x1;
+      const float v = ldf(xb, (int64_t)o * C);
+      gix += v * ay0 * g;
+      giy += v * ax0 * g;
+      atomicAdd(&acc[o * 64 + lane], ax0 * ay0 * g);
+    }
+    gix = wave_sum(gix);
+    giy = wave_sum(giy);
+    if (lane == 0) {
+      atomicAdd(&goff[p * 2 + 0], gix * (0.5f * W) * mx * 0.05f);
+      atomicAdd(&goff[p * 2 + 1], giy * (0.5f * H) * my * 0.05f);
+    }
+  }
+  __syncthreads();
+  float* gb = gx + (int64_t)b * HW * C + c0;
+  for (int i = threadIdx.x; i < HW * 64; i += blockDim.x) {
+    const int q = i >> 6, l = i & 63;
+    gb[(int64_t)q * C + l] += acc[i];
   }
 }
 
@@ -191,6 +353,79 @@ __global__ void k_offset_head_bwd(const float* __restrict__ goff, const T* __res
     if (i < 576) atomicAdd(&gw2[i], red[i]);
     else atomicAdd(&gb2[i - 576], red[i]);
   }
+}
+
+// Offset-head backward for images of at most 256 pixels: a block owns 256 consecutive pixels (whole
+// images), stages their goff in LDS (every in-image 3x3 neighbour is inside the block), and writes its
+// (gw2, gb2) partial sums to a workspace row instead of same-address global atomics; k_offset_head_fin
+// reduces the rows.  Same math as k_offset_head_bwd.
+template <typename T>
+__global__ __launch_bounds__(256) void k_offset_head_bwd_blk(const float* __restrict__ goff, const T* __restrict__ o1,
+                                                             const float* __restrict__ w2, int B, int H, int W,
+                                                             T* __restrict__ ga1, float* __restrict__ part) {
+  __shared__ float sw[576];
+  __shared__ float red[578];
+  __shared__ float sg[256 * 2];
+  const int64_t P = (int64_t)B * H * W;
+  const int64_t q0 = (int64_t)blockIdx.x * 256;
+  for (int i = threadIdx.x; i < 578; i += 256) {
+    if (i < 576) sw[i] = w2[i];
+    red[i] = 0.f;
+  }
+  for (int i = threadIdx.x; i < 512; i += 256) sg[i] = (q0 * 2 + i < P * 2) ? goff[q0 * 2 + i] : 0.f;
+  __syncthreads();
+  const int c = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  float accw[18];
+#pragma unroll
+  for (int i = 0; i < 18; ++i) accw[i] = 0.f;
+  float accb0 = 0.f, accb1 = 0.f;
+  for (int it = pl; it < 256; it += 8) {
+    const int64_t q = q0 + it;
+    if (q >= P) break;
+    const int b = (int)(q / (H * W));
+    const int rem = (int)(q - (int64_t)b * H * W);
+    const int h = rem / W, w = rem - (rem / W) * W;
+    const float ov = ldf(o1, q * 32 + c);
+    float g = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap % 3;
+      const int yy = h - (kh - 1), xx = w - (kw - 1);  // output pixel that reads q through this tap
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const int lp = it + (yy - h) * W + (xx - w);  // same image: inside this block
+        const float g0 = sg[lp * 2], g1 = sg[lp * 2 + 1];
+        g += g0 * sw[c * 9 + tap] + g1 * sw[(32 + c) * 9 + tap];
+        accw[tap] += g0 * ov;
+        accw[9 + tap] += g1 * ov;
+      }
+    }
+    stf(ga1, q * 32 + c, ov > 0.f ? g : 0.2f * g);
+    if (c == 0) {
+      accb0 += sg[it * 2];
+      accb1 += sg[it * 2 + 1];
+    }
+  }
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    atomicAdd(&red[c * 9 + tap], accw[tap]);
+    atomicAdd(&red[(32 + c) * 9 + tap], accw[9 + tap]);
+  }
+  if (c == 0) {
+    atomicAdd(&red[576], accb0);
+    atomicAdd(&red[577], accb1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 578; i += 256) part[(int64_t)blockIdx.x * 578 + i] = red[i];
+}
+
+__global__ __launch_bounds__(256) void k_offset_head_fin(const float* __restrict__ part, int nblk,
+                                                         float* __restrict__ gw2, float* __restrict__ gb2) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 578) return;
+  float s = 0.f;
+  for (int r = 0; r < nblk; ++r) s += part[(int64_t)r * 578 + i];
+  if (i < 576) gw2[i] += s;
+  else gb2[i - 576] += s;
 }
 
 // bilinear x2 source index (align_corners=False, scale 0.5): clamped at 0
@@ -328,6 +563,20 @@ extern "C" int mg_warp_fwd(int dtype, const void* x, const void* o1, const float
                            int W, int C, void* out, float* samp, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t P = (int64_t)B * H * W;
+  const int vec = dtype == MG_F32 ? 4 : 8;
+  const int G = C / vec;
+  if (C % vec == 0 && G <= 64 && (G & (G - 1)) == 0 && mg_al16(x) && mg_al16(o1) && mg_al16(out) && mg_al16(samp)) {
+    int lgG = 0;
+    while ((1 << lgG) < G) ++lgG;
+    dim3 gv((unsigned)((P + (256 >> lgG) - 1) / (256 >> lgG)));
+    if (dtype == MG_F32)
+      hipLaunchKernelGGL(k_warp_fwd_v<float>, gv, dim3(256), 0, st, (const float*)x, (const float*)o1, w2, b2, B, H, W,
+                         C, lgG, (float*)out, samp);
+    else
+      hipLaunchKernelGGL(k_warp_fwd_v<bf16_t>, gv, dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)o1, w2, b2, B, H,
+                         W, C, lgG, (bf16_t*)out, samp);
+    return mg_check_launch("mg_warp_fwd");
+  }
   dim3 grid((unsigned)((P + 3) / 4));
   if (dtype == MG_F32)
     hipLaunchKernelGGL(k_warp_fwd<float>, grid, dim3(256), 0, st, (const float*)x, (const float*)o1, w2, b2, B, H, W, C, (float*)out, samp);
@@ -340,6 +589,17 @@ extern "C" int mg_warp_bwd(int dtype, int gout_dtype, const void* gout, const vo
                            int W, int C, float* gx, float* goff, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t P = (int64_t)B * H * W;
+  // measured slower than the atomic kernel at C2 (latency-bound per-pixel chain): opt-in via tuning key 8
+  if (g_mg_tune[MG_TUNE_WARP_LDS] == 1 && C % 64 == 0 && H * W <= 256 && mg_al16(samp)) {
+    if (hipMemsetAsync(goff, 0, (size_t)P * 2 * sizeof(float), st) != hipSuccess) return mg_check_launch("mg_warp_bwd");
+    dim3 gl(B, C / 64);
+    const size_t lds = (size_t)H * W * 64 * sizeof(float);
+#define L_(T, TG) hipLaunchKernelGGL((k_warp_bwd_lds<T, TG>), gl, dim3(512), lds, st, (const TG*)gout, (const T*)x, samp, B, H, W, C, gx, goff)
+    if (dtype == MG_F32) { if (gout_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+    else { if (gout_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+    return mg_check_launch("mg_warp_bwd");
+  }
   dim3 grid((unsigned)((P + 3) / 4));
 #define L_(T, TG) hipLaunchKernelGGL((k_warp_bwd<T, TG>), grid, dim3(256), 0, st, (const TG*)gout, (const T*)x, samp, B, H, W, C, gx, goff)
   if (dtype == MG_F32) { if (gout_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
@@ -352,6 +612,23 @@ extern "C" int mg_offset_head_bwd(int dtype, const float* goff, const void* o1, 
                                   void* ga1, float* gw2, float* gb2, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t P = (int64_t)B * H * W;
+  // block-partial variant: measured slower at C2 (few blocks at 4x4 / 8x8); opt-in via tuning key 8
+  if (g_mg_tune[MG_TUNE_WARP_LDS] == 1 && H * W <= 256 && 256 % (H * W) == 0) {
+    const int nb = (int)((P + 255) / 256);
+    float* part = reinterpret_cast<float*>(mg_workspace((size_t)nb * 578 * sizeof(float), st));
+    if (!part) {
+      mg_set_error("mg_offset_head_bwd: workspace allocation failed");
+      return MG_ERR_LAUNCH;
+    }
+    if (dtype == MG_F32)
+      hipLaunchKernelGGL(k_offset_head_bwd_blk<float>, dim3(nb), dim3(256), 0, st, goff, (const float*)o1, w2, B, H, W,
+                         (float*)ga1, part);
+    else
+      hipLaunchKernelGGL(k_offset_head_bwd_blk<bf16_t>, dim3(nb), dim3(256), 0, st, goff, (const bf16_t*)o1, w2, B, H,
+                         W, (bf16_t*)ga1, part);
+    hipLaunchKernelGGL(k_offset_head_fin, dim3(3), dim3(256), 0, st, part, nb, gw2, gb2);
+    return mg_check_launch("mg_offset_head_bwd");
+  }
   int ppb = 64;
   dim3 grid((unsigned)((P + ppb - 1) / ppb));
   if (dtype == MG_F32)
