@@ -50,6 +50,7 @@ class GeneratorEngine:
         self._demod_bwd = []
         self._mean_latent = None
         self._want_kl = True
+        self._bv = None  # per-block vectors of the running forward (_block_vectors)
         # weight gradients run on a side stream, overlapping the data-gradient chain (joined in backward)
         self.side = graphs.SideStream(self.dev, enabled=graphs.side_streams_enabled(self.dev))
 
@@ -241,15 +242,14 @@ class GeneratorEngine:
         T, C = tok.shape
         B = w.shape[0]
         E, k = self.E, (self.k if train else 1)
-        if train:
-            Wf = ops.reparam(self.P(r + "feature_mu"), self.P(r + "feature_rho"), eps[0])
-            Wt = ops.reparam(self.P(r + "text_mu"), self.P(r + "text_rho"), eps[1])
-            Wc = ops.reparam(self.P(r + "combined_mu"), self.P(r + "combined_rho"), eps[2])
+        bv = self._bv.get(pre) if self._bv is not None else None
+        if bv is not None:  # computed for every block at once (_block_vectors)
+            Wf, Wt, Wc, Wfc, u, Lt = bv["Wf"], bv["Wt"], bv["Wc"], bv["Wfc"], bv["u"], bv["Lt"]
         else:
-            Wf, Wt, Wc = self.P(r + "feature_mu"), self.P(r + "text_mu"), self.P(r + "combined_mu")
-        Wfc = ops.gemm(Wf, Wc[:128], C, E, 128, b_kc=False)  # [C, E]
-        u = ops.gemm(w, Wt, B, 128, w.shape[1], b_kc=False)  # [B, 128]
-        Lt = ops.gemm(u, Wc[128:], B, E, 128, b_kc=False)  # [B, E]
+            Wf, Wt, Wc = self._router_weights(r, eps, train)
+            Wfc = ops.gemm(Wf, Wc[:128], C, E, 128, b_kc=False)  # [C, E]
+            u = ops.gemm(w, Wt, B, 128, w.shape[1], b_kc=False)  # [B, 128]
+            Lt = ops.gemm(u, Wc[128:], B, E, 128, b_kc=False)  # [B, E]
         probs, zlog, topi, gate = ops.router_fwd(tok, Wfc, Lt, E, k, HW, self.P(r + "temperature"), anneal,
                                                  eval_mode=0 if train else 1)
         row_off, tile_off, perm, pos_of, gate_pos = ops.moe_dispatch(topi, gate, E)
@@ -284,6 +284,55 @@ class GeneratorEngine:
                       zlog=zlog, topi=topi, gate=gate, row_off=row_off, tile_off=tile_off, perm=perm, pos_of=pos_of,
                       gate_pos=gate_pos, Pre=Pre, Hid=Hid, Xg=Xg, Y=Y, W1=W1, W2=W2, max_tiles=max_tiles)
         return out, probs, kl2, topi, sv
+
+    def _router_weights(self, r, eps, train):
+        """Reparameterised router weights (t2i_moe_gan.py:302-333) in train mode, the means in eval mode."""
+        if train:
+            return (ops.reparam(self.P(r + "feature_mu"), self.P(r + "feature_rho"), eps[0]),
+                    ops.reparam(self.P(r + "text_mu"), self.P(r + "text_rho"), eps[1]),
+                    ops.reparam(self.P(r + "combined_mu"), self.P(r + "combined_rho"), eps[2]))
+        return self.P(r + "feature_mu"), self.P(r + "text_mu"), self.P(r + "combined_mu")
+
+    def _block_vectors(self, w, text_seq, eps, train):
+        """Everything per block that depends only on (w, text_seq, router eps) -- the cross-attention value
+        chain tp -> v -> out_proj (t2i_moe_gan.py:549-556) and the router's text logits and feature-combine
+        matrix (:364-389) -- for all blocks at once: five batched launches instead of eighteen GEMMs."""
+        B = w.shape[0]
+        dev = self.dev
+        pres = [name + ".attn_block." for name, *_ in GEN_BLOCKS]
+        Cs = [self.P(p + "text_proj.weight").shape[0] for p in pres]
+        bv = {p + "moe.": {} for p in pres}
+        chain = {}
+        src = [text_seq] * len(pres)
+        for key, wname, bname, sl in (("tp", "text_proj.weight", "text_proj.bias", False),
+                                      ("vv", "cross_attn.in_proj_weight", "cross_attn.in_proj_bias", True),
+                                      ("ca", "cross_attn.out_proj.weight", "cross_attn.out_proj.bias", False)):
+            probs, outs = [], []
+            for p, C, a in zip(pres, Cs, src):
+                Wm, bm = self.P(p + wname), self.P(p + bname)
+                if sl:  # value rows of the packed in-projection
+                    Wm, bm = Wm[2 * C:], bm[2 * C:]
+                o = torch.empty(B, C, device=dev)
+                probs.append(dict(A=a, B=Wm, M=B, N=C, K=a.shape[1], out=o, ep=E_(bias=bm)))
+                outs.append(o)
+            ops.gemm_batch(probs)
+            chain[key] = outs
+            src = outs
+        E = self.E
+        probs1, probs2 = [], []
+        for i, (p, C) in enumerate(zip(pres, Cs)):
+            d = bv[p + "moe."]
+            Wf, Wt, Wc = self._router_weights(p + "moe.router.", None if eps is None else eps[i], train)
+            d.update(Wf=Wf, Wt=Wt, Wc=Wc, Wfc=torch.empty(C, E, device=dev), u=torch.empty(B, 128, device=dev),
+                     Lt=torch.empty(B, E, device=dev))
+            probs1.append(dict(A=Wf, B=Wc[:128], M=C, N=E, K=128, out=d["Wfc"]))  # Wf @ Wc1
+            probs1.append(dict(A=w, B=Wt, M=B, N=128, K=w.shape[1], out=d["u"]))  # w @ Wt
+            probs2.append(dict(A=d["u"], B=Wc[128:], M=B, N=E, K=128, out=d["Lt"]))  # u @ Wc2
+        ops.gemm_batch(probs1, b_kc=False)
+        ops.gemm_batch(probs2, b_kc=False)
+        for i, p in enumerate(pres):
+            bv[p] = dict(tp=chain["tp"][i], vv=chain["vv"][i], ca=chain["ca"][i])
+        return bv
 
     def _cbuf(self):
         return self.st.shadow if self.st.shadow is not None else self.st.data
@@ -349,11 +398,16 @@ class GeneratorEngine:
         qkv = ops.linear(n1, self.Pc(pre + "self_attn.in_proj_weight"), bias=self.P(pre + "self_attn.in_proj_bias"))
         att, lse = ops.attn_fwd(qkv, B, L_, C)
         # cross-attention against the single text token: softmax over one key == 1 (:553-555)
-        ca_W = self.P(pre + "cross_attn.in_proj_weight")
-        ca_b = self.P(pre + "cross_attn.in_proj_bias")
-        tp = ops.linear(text_seq, self.P(pre + "text_proj.weight"), bias=self.P(pre + "text_proj.bias"))
-        vv = ops.linear(tp, ca_W[2 * C:], bias=ca_b[2 * C:])
-        ca = ops.linear(vv, self.P(pre + "cross_attn.out_proj.weight"), bias=self.P(pre + "cross_attn.out_proj.bias"))
+        bv = self._bv.get(pre) if self._bv is not None else None
+        if bv is not None:
+            tp, vv, ca = bv["tp"], bv["vv"], bv["ca"]
+        else:
+            ca_W = self.P(pre + "cross_attn.in_proj_weight")
+            ca_b = self.P(pre + "cross_attn.in_proj_bias")
+            tp = ops.linear(text_seq, self.P(pre + "text_proj.weight"), bias=self.P(pre + "text_proj.bias"))
+            vv = ops.linear(tp, ca_W[2 * C:], bias=ca_b[2 * C:])
+            ca = ops.linear(vv, self.P(pre + "cross_attn.out_proj.weight"),
+                            bias=self.P(pre + "cross_attn.out_proj.bias"))
         xf1 = ops.linear(att, self.Pc(pre + "self_attn.out_proj.weight"), bias=self.P(pre + "self_attn.out_proj.bias"),
                          resid=xf0, ld_res=C, addvec=ca, add_shift=ops.ilog2(L_), add_ld=C)
         n3, mu3, rs3 = ops.layernorm_fwd(xf1, self.P(pre + "norm3.weight"), self.P(pre + "norm3.bias"))
@@ -457,6 +511,7 @@ class GeneratorEngine:
                 self._D[pre] = d
                 probs.append(dict(A=self._S2[:, c:c + Cin], B=pk["wsq"], M=B, N=rows, K=Cin, out=d, ep=E_(act=RSQRT)))
             ops.gemm_batch(probs)
+        self._bv = self._block_vectors(w, text_seq, eps, train)
         x = ops.const_fwd(self.P("constant"), B, self.cdt)
         probs, kl2s, topis, blocks = [], [], [], []
         img8, rgb8sv = None, None
@@ -474,6 +529,7 @@ class GeneratorEngine:
                 img8, rgb8sv = self.mc_fwd("to_rgb_8.", x, w, save=save)
         img16, rgbsv = self.mc_fwd("to_rgb_16.", x, w, save=save)
         self._S = self._S2 = self._D = None
+        self._bv = None
         ctx = None
         if save:
             ctx = dict(B=B, text=text, z=z, t0=t0, t1=t1, tmu=tmu, trs=trs, text_seq=text_seq, hs=hs, h3=h3, w=w,
