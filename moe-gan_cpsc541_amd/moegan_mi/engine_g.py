@@ -48,6 +48,8 @@ class GeneratorEngine:
         self._S = self._S2 = self._GS = None  # batched styles of the running forward / style grads of a backward
         self._D = None  # demodulation coefficients of the running forward, {prefix: [B, rows]}
         self._demod_bwd = []
+        self._router_bwd, self._xattn_bwd = [], []  # per-block small backward GEMMs, batched at the end
+        self._defer = False
         self._mean_latent = None
         self._want_kl = True
         self._bv = None  # per-block vectors of the running forward (_block_vectors)
@@ -334,6 +336,76 @@ class GeneratorEngine:
             bv[p] = dict(tp=chain["tp"][i], vv=chain["vv"][i], ca=chain["ca"][i])
         return bv
 
+    def _flush_xattn_bwd(self):
+        """Cross-attention value-chain backward of every block (t2i_moe_gan.py:549-556), level by level in
+        batched launches: weight gradients (fp32 atomics), bias gradients, data gradients; the text-sequence
+        gradient of all blocks accumulates with fp32 atomics."""
+        items, self._xattn_bwd = self._xattn_bwd, []
+        if not items:
+            return
+        dev = self.dev
+        for q in items:
+            C, pre = q["C"], q["pre"]
+            q["Wo"] = self.P(pre + "cross_attn.out_proj.weight")
+            q["Wv"] = self.P(pre + "cross_attn.in_proj_weight")[2 * C:]
+            q["Wt"] = self.P(pre + "text_proj.weight")
+            q["gWo"] = self.G(pre + "cross_attn.out_proj.weight")
+            q["gWv"] = self.G(pre + "cross_attn.in_proj_weight")[2 * C:]
+            q["gWt"] = self.G(pre + "text_proj.weight")
+            q["gbo"] = self.G(pre + "cross_attn.out_proj.bias")
+            q["gbv"] = self.G(pre + "cross_attn.in_proj_bias")[2 * C:]
+            q["gbt"] = self.G(pre + "text_proj.bias")
+        # (gradient in, saved input, weight, weight grad, bias grad, gradient out)
+        levels = (("g_ca", "vv", "Wo", "gWo", "gbo", "g_vv"), ("g_vv", "tp", "Wv", "gWv", "gbv", "g_tp"),
+                  ("g_tp", "text_seq", "Wt", "gWt", "gbt", None))
+        for gin, xin, Wk, gWk, gbk, gout in levels:
+            wg, dg = [], []
+            for q in items:
+                g, x, Wm = q[gin], q[xin], q[Wk]
+                M, N = g.shape
+                K = x.shape[1]
+                wg.append(dict(A=g, B=x, M=N, N=K, K=M, out=q[gWk], ldc=q[gWk].stride(0), ep=E_(atomic=1)))
+                if gout is None:  # d text_seq, shared by the blocks
+                    dg.append(dict(A=g, B=Wm, M=M, N=Wm.shape[1], K=N, out=q["g_text_seq"], ep=E_(atomic=1)))
+                else:
+                    q[gout] = torch.empty(M, Wm.shape[1], device=dev)
+                    dg.append(dict(A=g, B=Wm, M=M, N=Wm.shape[1], K=N, out=q[gout]))
+                ops.colsum(g, q[gbk])
+            ops.gemm_batch(wg, a_kc=False, b_kc=False)
+            ops.gemm_batch(dg, a_kc=True, b_kc=False)
+
+    def _flush_router_bwd(self):
+        """Router parameter backward of every block (t2i_moe_gan.py:364-389 through :302-333) in batched
+        launches: dWf, dWc, dWt, d w (fp32 atomics into the shared latent gradient), then the per-parameter
+        reparameterisation / KL backward."""
+        items, self._router_bwd = self._router_bwd, []
+        if not items:
+            return
+        dev = self.dev
+        pa, pb, pc, pd = [], [], [], []
+        for q in items:
+            C, E, B, Wc = q["C"], q["E"], q["B"], q["Wc"]
+            q["gWf"] = torch.empty(C, 128, device=dev)
+            q["gWc"] = torch.empty(256, E, device=dev)
+            q["g_u"] = torch.empty(B, 128, device=dev)
+            q["gWt"] = torch.empty(q["w"].shape[1], 128, device=dev)
+            pa.append(dict(A=q["G1"], B=Wc[:128], M=C, N=128, K=E, out=q["gWf"]))  # G1 @ Wc1^T
+            pa.append(dict(A=q["gsum"], B=Wc[128:], M=B, N=128, K=E, out=q["g_u"]))  # gsum @ Wc2^T
+            pb.append(dict(A=q["Wf"], B=q["G1"], M=128, N=E, K=C, out=q["gWc"][:128]))  # Wf^T G1
+            pb.append(dict(A=q["u"], B=q["gsum"], M=128, N=E, K=B, out=q["gWc"][128:]))  # u^T gsum
+            pc.append(dict(A=q["w"], B=q["g_u"], M=q["w"].shape[1], N=128, K=B, out=q["gWt"]))  # w^T g_u
+            pd.append(dict(A=q["g_u"], B=q["Wt"], M=B, N=q["w"].shape[1], K=128, out=q["gw"],
+                           ep=E_(atomic=1)))  # gw += g_u Wt^T
+        ops.gemm_batch(pa)
+        ops.gemm_batch(pb, a_kc=False, b_kc=False)
+        ops.gemm_batch(pc, a_kc=False, b_kc=False)
+        ops.gemm_batch(pd)
+        for q in items:
+            r = q["r"]
+            for nm, gWx, epi in (("feature", q["gWf"], 0), ("text", q["gWt"], 1), ("combined", q["gWc"], 2)):
+                ops.router_param_bwd(self.P(r + nm + "_mu"), self.P(r + nm + "_rho"), q["eps"][epi], gWx,
+                                     q["kl_coef"], self.G(r + nm + "_mu"), self.G(r + nm + "_rho"))
+
     def _cbuf(self):
         return self.st.shadow if self.st.shadow is not None else self.st.data
 
@@ -373,17 +445,10 @@ class GeneratorEngine:
         ops.moe_token_grad(gX, sv["pos_of"], g_raw, sv["Wfc"], g_tok, k)
         G1 = torch.zeros(C, E, device=self.dev, dtype=torch.float32)
         ops.router_feat_grad(tok, g_raw, G1)
-        Wf, Wt, Wc, u = sv["Wf"], sv["Wt"], sv["Wc"], sv["u"]
-        gWf = ops.gemm(G1, Wc[:128], C, 128, E)  # G1 @ Wc1^T
-        gWc = torch.empty(256, E, device=self.dev, dtype=torch.float32)
-        ops.gemm(Wf, G1, 128, E, C, a_kc=False, b_kc=False, out=gWc[:128])  # Wf^T G1
-        g_u = ops.gemm(gsum, Wc[128:], B, 128, E)  # gsum @ Wc2^T
-        ops.gemm(u, gsum, 128, E, B, a_kc=False, b_kc=False, out=gWc[128:])  # u^T gsum
-        gWt = ops.gemm(w, g_u, w.shape[1], 128, B, a_kc=False, b_kc=False)  # w^T g_u
-        ops.gemm(g_u, Wt, B, w.shape[1], 128, out=gw, ep=E_(accumulate=1))  # gw += g_u Wt^T
-        for nm, gWx, epi in (("feature", gWf, 0), ("text", gWt, 1), ("combined", gWc, 2)):
-            ops.router_param_bwd(self.P(r + nm + "_mu"), self.P(r + nm + "_rho"), sv["eps"][epi], gWx, kl_coef,
-                                 self.G(r + nm + "_mu"), self.G(r + nm + "_rho"))
+        # the router's parameter GEMMs depend only on (G1, gsum) and saved vectors: run for every block at
+        # the end of the backward, batched (_flush_router_bwd)
+        self._router_bwd.append(dict(r=r, C=C, E=E, B=B, G1=G1, gsum=gsum, Wf=sv["Wf"], Wt=sv["Wt"], Wc=sv["Wc"],
+                                     u=sv["u"], w=w, gw=gw, eps=sv["eps"], kl_coef=kl_coef))
 
     # ------------------------------------------------------------------
     # AttentionBlock  (t2i_moe_gan.py:493-576)
@@ -433,17 +498,10 @@ class GeneratorEngine:
         # cross-attention vector: sum over each image's tokens
         g_ca = torch.zeros(B, C, device=self.dev, dtype=torch.float32)
         ops.segsum(g_xf1, B, L_, C, g_ca)
-        ca_W = self.P(pre + "cross_attn.in_proj_weight")
-        gca_W = self.G(pre + "cross_attn.in_proj_weight")
-        ops.linear_wgrad(g_ca, sv["vv"], self.G(pre + "cross_attn.out_proj.weight"))
-        ops.colsum(g_ca, self.G(pre + "cross_attn.out_proj.bias"))
-        g_vv = ops.linear_dgrad(g_ca, self.P(pre + "cross_attn.out_proj.weight"))
-        ops.linear_wgrad(g_vv, sv["tp"], gca_W[2 * C:])
-        ops.colsum(g_vv, self.G(pre + "cross_attn.in_proj_bias")[2 * C:])
-        g_tp = ops.linear_dgrad(g_vv, ca_W[2 * C:])
-        ops.linear_wgrad(g_tp, sv["text_seq"], self.G(pre + "text_proj.weight"))
-        ops.colsum(g_tp, self.G(pre + "text_proj.bias"))
-        ops.linear_dgrad(g_tp, self.P(pre + "text_proj.weight"), out=g_text_seq, accumulate=1)
+        # the rest of the cross-attention chain depends only on g_ca and saved vectors: batched over the
+        # blocks at the end of the backward (_flush_xattn_bwd)
+        self._xattn_bwd.append(dict(pre=pre, C=C, B=B, g_ca=g_ca, vv=sv["vv"], tp=sv["tp"], text_seq=sv["text_seq"],
+                                    g_text_seq=g_text_seq))
         # self-attention
         g_att = ops.linear_dgrad(g_xf1, self.Pc(pre + "self_attn.out_proj.weight"))
         ops.linear_wgrad(g_xf1, sv["att"], self.G(pre + "self_attn.out_proj.weight"))
@@ -456,6 +514,9 @@ class GeneratorEngine:
         ops.layernorm_bwd(g_n1, sv["xf0"], sv["mu1"], sv["rs1"], self.P(pre + "norm1.weight"), g_xf0,
                           self.G(pre + "norm1.weight"), self.G(pre + "norm1.bias"), accumulate=1)
         self.mc_bwd(pre + "proj_in.", sv["sv_in"], g_xf0, gx, gw)
+        if not self._defer:  # called on its own: complete this block's gradients now
+            self._flush_router_bwd()
+            self._flush_xattn_bwd()
 
     # ------------------------------------------------------------------
     # AuroraGenerator  (t2i_moe_gan.py:762-855)
@@ -544,6 +605,8 @@ class GeneratorEngine:
         dev = self.dev
         gw = torch.zeros(B, 512, device=dev)
         g_ts = torch.zeros(B, 512, device=dev)
+        self._router_bwd, self._xattn_bwd = [], []
+        self._defer = True  # per-block small GEMMs are batched over the blocks after the block loop
         if self.style_cols:
             self._GS = torch.zeros(B, self.style_n, device=dev)
             self._demod_bwd = []
@@ -572,6 +635,9 @@ class GeneratorEngine:
             else:
                 gx = g_in
         ops.const_bwd(gx, self.G("constant"))
+        self._flush_router_bwd()
+        self._flush_xattn_bwd()
+        self._defer = False
         self.side.join()  # every weight gradient is in place before the demodulation backward adds to it
         if self._GS is not None:  # all modulated convs' demodulation and style backward at once
             pw, pg = [], []
