@@ -510,10 +510,11 @@ __global__ __launch_bounds__(256) void k_grouped_colsum_v(const T* __restrict__ 
   float s[8], v[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = 0.f;
-  int g = -1;
+  int g = -1, gend = -1;
   const bool live = n < N;
-  for (int r = r0 + ty; live && r < r1; r += TY) {
-    if (g < 0 || r >= row_off[g + 1]) {
+  int r = r0 + ty;
+  while (live && r < r1) {
+    if (r >= gend) {
       if (g >= 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -523,12 +524,25 @@ __global__ __launch_bounds__(256) void k_grouped_colsum_v(const T* __restrict__ 
       }
       g = 0;
       while (g < G && row_off[g + 1] <= r) ++g;
+      gend = row_off[g + 1];
+    }
+    if (!idx && !rs && r + 3 * TY < min(gend, r1)) {  // four rows of one group: independent loads in flight
+      float v1[8], v2[8], v3[8];
+      ld8(X + (int64_t)r * ld + n, v);
+      ld8(X + (int64_t)(r + TY) * ld + n, v1);
+      ld8(X + (int64_t)(r + 2 * TY) * ld + n, v2);
+      ld8(X + (int64_t)(r + 3 * TY) * ld + n, v3);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += (v[j] + v1[j]) + (v2[j] + v3[j]);
+      r += 4 * TY;
+      continue;
     }
     const int src = idx ? idx[r] / idx_div : r;
     ld8(X + (int64_t)src * ld + n, v);
     const float sc = rs ? rs[r] : 1.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] += rs ? v[j] * sc : v[j];
+    r += TY;
   }
   if (live && g >= 0 && g != glast) {
 #pragma unroll
@@ -828,7 +842,8 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
   MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
   MG_REQUIRE(C <= 512, "C <= 512");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  int chunk = std::max(256, ((T / 128) + 63) / 64 * 64);
+  // ~512 blocks (a 64-token step per LDS refill); the per-block partials meet in fp32 atomics
+  int chunk = std::max(64, std::min(256, (T / 512) / 64 * 64));
   dim3 grid(cdiv(T, chunk));
   int thr = ((C + 63) / 64) * 64;
 #define L_(TT, EE) hipLaunchKernelGGL((k_router_feat_grad<TT, EE>), grid, dim3(thr), 0, st, (const TT*)tok, ld, T, C, g_raw, chunk, G1)

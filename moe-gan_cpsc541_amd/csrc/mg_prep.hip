@@ -120,10 +120,19 @@ __global__ __launch_bounds__(256) void k_colsum_v(const T* __restrict__ X, int64
   const int c = (blockIdx.x * TX + tx) * 8;
   const bool live = c < C;
   const int r0 = blockIdx.y * rows_per_block, r1 = min(R, r0 + rows_per_block);
-  float acc[8], t[8];
+  float acc[8], t[8], t1[8], t2[8], t3[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  for (int r = r0 + ty; live && r < r1; r += TY) {
+  int r = r0 + ty;
+  for (; live && r + 3 * TY < r1; r += 4 * TY) {  // four independent row loads in flight
+    ld8(X + (int64_t)r * ld + c, t);
+    ld8(X + (int64_t)(r + TY) * ld + c, t1);
+    ld8(X + (int64_t)(r + 2 * TY) * ld + c, t2);
+    ld8(X + (int64_t)(r + 3 * TY) * ld + c, t3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += (t[j] + t1[j]) + (t2[j] + t3[j]);
+  }
+  for (; live && r < r1; r += TY) {
     ld8(X + (int64_t)r * ld + c, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] += t[j];
@@ -403,8 +412,8 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     int tx = std::min(cv, 32);
     int ty = 256 / tx;
     int cblk = cdiv(cv, tx);
-    // ~512 blocks in total, at least 4 rows per lane
-    int rblk = std::max(1, std::min({cdiv(R, 4 * ty), 512 / cblk, 64}));
+    // ~1024 blocks in total (every CU busy), at least 8 rows per lane
+    int rblk = std::max(1, std::min({cdiv(R, 8 * ty), 1024 / cblk, 256}));
     int rpb = cdiv(R, rblk);
     rblk = cdiv(R, rpb);
     float* part = reinterpret_cast<float*>(mg_workspace((size_t)rblk * C * sizeof(float), st));
