@@ -260,6 +260,9 @@ int mg_balance(const float* load, int E, float T, float weight, float grad_scale
 
 /* MTM offset head (conv 32->2) + linspace grid + clamp + bilinear grid_sample (zeros, align_corners=False), t2i_moe_gan.py:222-239. samp [P,4] saved. */
 int mg_warp_fwd(int dtype, const void* x, const void* o1, const float* w2, const float* b2, int B, int H, int W, int C, void* out, float* samp, void* stream);
+/* mg_warp_fwd that also writes out_scaled[b,..,c] = out[b,..,c] * s[b*lds + c] in the same pass: the following
+ * modulated conv's prescaled input (t2i_moe_gan.py:158-161, as mg_scale_bc). s fp32. */
+int mg_warp_fwd_scaled(int dtype, const void* x, const void* o1, const float* w2, const float* b2, int B, int H, int W, int C, const float* s, int64_t lds, void* out, void* out_scaled, float* samp, void* stream);
 
 /* grid_sample backward: gx (fp32, +=, atomics) and goff [P,2] = d loss / d offsets. */
 int mg_warp_bwd(int dtype, int gout_dtype, const void* gout, const void* x, const float* samp, int B, int H, int W, int C, float* gx, float* goff, void* stream);

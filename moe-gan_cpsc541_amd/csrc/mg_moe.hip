@@ -436,7 +436,8 @@ __global__ void k_token_grad(const T* __restrict__ gX, int64_t ldx, const int* _
 // G1[c, e] += sum_t tok[t, c] * g_raw[t, e]
 template <typename T, int E>
 __global__ void k_router_feat_grad(const T* __restrict__ tok, int64_t ld, int Tn, int C,
-                                   const float* __restrict__ g_raw, int chunk, float* __restrict__ G1) {
+                                   const float* __restrict__ g_raw, int chunk, float* __restrict__ G1,
+                                   float* __restrict__ part) {
   __shared__ float gr[64 * E];
   int c = threadIdx.x;
   int t0 = blockIdx.x * chunk, t1 = min(Tn, t0 + chunk);
@@ -460,9 +461,23 @@ __global__ void k_router_feat_grad(const T* __restrict__ tok, int64_t ld, int Tn
     }
   }
   if (c < C) {
+    if (part) {  // per-block partial row (no same-address atomics); k_feat_grad_fin folds the rows
 #pragma unroll
-    for (int e = 0; e < E; ++e) atomicAdd(&G1[(int64_t)c * E + e], acc[e]);
+      for (int e = 0; e < E; ++e) part[(int64_t)blockIdx.x * C * E + (int64_t)c * E + e] = acc[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) atomicAdd(&G1[(int64_t)c * E + e], acc[e]);
+    }
   }
+}
+
+__global__ __launch_bounds__(256) void k_feat_grad_fin(const float* __restrict__ part, int nparts, int n,
+                                                       float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int r = 0; r < nparts; ++r) s += part[(int64_t)r * n + i];
+  out[i] += s;
 }
 
 // out[g][n] += sum_{r in group g} X[src(r)][n] * rs[r]  (grouped bias gradients)
@@ -842,15 +857,17 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
   MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
   MG_REQUIRE(C <= 512, "C <= 512");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // ~512 blocks (a 64-token step per LDS refill); the per-block partials meet in fp32 atomics
+  // ~512 blocks (a 64-token step per LDS refill); per-block partial rows folded by k_feat_grad_fin
   int chunk = std::max(64, std::min(256, (T / 512) / 64 * 64));
   dim3 grid(cdiv(T, chunk));
   int thr = ((C + 63) / 64) * 64;
-#define L_(TT, EE) hipLaunchKernelGGL((k_router_feat_grad<TT, EE>), grid, dim3(thr), 0, st, (const TT*)tok, ld, T, C, g_raw, chunk, G1)
+  float* part = reinterpret_cast<float*>(mg_workspace((size_t)grid.x * C * E * sizeof(float), st));
+#define L_(TT, EE) hipLaunchKernelGGL((k_router_feat_grad<TT, EE>), grid, dim3(thr), 0, st, (const TT*)tok, ld, T, C, g_raw, chunk, G1, part)
 #define LE_(TT) if (E == 4) L_(TT, 4); else if (E == 8) L_(TT, 8); else if (E == 16) L_(TT, 16); else L_(TT, 32)
   if (dtype == MG_F32) { LE_(float); } else { LE_(bf16_t); }
 #undef LE_
 #undef L_
+  if (part) hipLaunchKernelGGL(k_feat_grad_fin, dim3(cdiv(C * E, 256)), dim3(256), 0, st, part, (int)grid.x, C * E, G1);
   return mg_check_launch("mg_router_feat_grad");
 }
 

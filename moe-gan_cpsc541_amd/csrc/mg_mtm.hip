@@ -83,7 +83,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_warp_fwd_v(const T* __restrict__ x, const T* __restrict__ o1,
                                                     const float* __restrict__ w2, const float* __restrict__ b2,
                                                     int B, int H, int W, int C, int lgG, T* __restrict__ out,
-                                                    float* __restrict__ samp) {
+                                                    float* __restrict__ samp, const float* __restrict__ sc,
+                                                    int64_t lds, T* __restrict__ xs) {
   constexpr int VEC = VecOf<T>::N;
   typedef typename VecOf<T>::type vec_t;
   constexpr int OV = 32 / VEC;  // offset-conv input vectors per tap
@@ -166,6 +167,17 @@ __global__ __launch_bounds__(256) void k_warp_fwd_v(const T* __restrict__ x, con
       else r[e] = acc[e];
     }
     *reinterpret_cast<vec_t*>(out + p * C + c) = r;
+    if (xs) {  // the next modulated conv's prescaled input, from the stored (rounded) value as mg_scale_bc does
+      const float* sp = sc + (int64_t)b * lds + c;
+      vec_t r2;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float v = (sizeof(T) == 2 ? bf2f((bf16_t)r[e]) : (float)r[e]) * sp[e];
+        if constexpr (sizeof(T) == 2) r2[e] = f2bf(v);
+        else r2[e] = v;
+      }
+      *reinterpret_cast<vec_t*>(xs + p * C + c) = r2;
+    }
   }
 }
 
@@ -571,10 +583,10 @@ extern "C" int mg_warp_fwd(int dtype, const void* x, const void* o1, const float
     dim3 gv((unsigned)((P + (256 >> lgG) - 1) / (256 >> lgG)));
     if (dtype == MG_F32)
       hipLaunchKernelGGL(k_warp_fwd_v<float>, gv, dim3(256), 0, st, (const float*)x, (const float*)o1, w2, b2, B, H, W,
-                         C, lgG, (float*)out, samp);
+                         C, lgG, (float*)out, samp, (const float*)nullptr, (int64_t)0, (float*)nullptr);
     else
       hipLaunchKernelGGL(k_warp_fwd_v<bf16_t>, gv, dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)o1, w2, b2, B, H,
-                         W, C, lgG, (bf16_t*)out, samp);
+                         W, C, lgG, (bf16_t*)out, samp, (const float*)nullptr, (int64_t)0, (bf16_t*)nullptr);
     return mg_check_launch("mg_warp_fwd");
   }
   dim3 grid((unsigned)((P + 3) / 4));
@@ -583,6 +595,31 @@ extern "C" int mg_warp_fwd(int dtype, const void* x, const void* o1, const float
   else
     hipLaunchKernelGGL(k_warp_fwd<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)o1, w2, b2, B, H, W, C, (bf16_t*)out, samp);
   return mg_check_launch("mg_warp_fwd");
+}
+
+extern "C" int mg_warp_fwd_scaled(int dtype, const void* x, const void* o1, const float* w2, const float* b2, int B,
+                                  int H, int W, int C, const float* s, int64_t lds, void* out, void* out_scaled,
+                                  float* samp, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t P = (int64_t)B * H * W;
+  const int vec = dtype == MG_F32 ? 4 : 8;
+  const int G = C / vec;
+  if (C % vec == 0 && G <= 64 && (G & (G - 1)) == 0 && mg_al16(x) && mg_al16(o1) && mg_al16(out) && mg_al16(samp) &&
+      mg_al16(s) && lds % 4 == 0 && mg_al16(out_scaled)) {
+    int lgG = 0;
+    while ((1 << lgG) < G) ++lgG;
+    dim3 gv((unsigned)((P + (256 >> lgG) - 1) / (256 >> lgG)));
+    if (dtype == MG_F32)
+      hipLaunchKernelGGL(k_warp_fwd_v<float>, gv, dim3(256), 0, st, (const float*)x, (const float*)o1, w2, b2, B, H, W,
+                         C, lgG, (float*)out, samp, s, lds, (float*)out_scaled);
+    else
+      hipLaunchKernelGGL(k_warp_fwd_v<bf16_t>, gv, dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)o1, w2, b2, B, H,
+                         W, C, lgG, (bf16_t*)out, samp, s, lds, (bf16_t*)out_scaled);
+    return mg_check_launch("mg_warp_fwd_scaled");
+  }
+  int rc = mg_warp_fwd(dtype, x, o1, w2, b2, B, H, W, C, out, samp, stream);
+  if (rc != MG_OK) return rc;
+  return mg_scale_bc(dtype, out, C, s, lds, B, H * W, C, out_scaled, C, stream);
 }
 
 extern "C" int mg_warp_bwd(int dtype, int gout_dtype, const void* gout, const void* x, const float* samp, int B, int H,

@@ -114,7 +114,7 @@ class GeneratorEngine:
         s = ops.linear(w, self.P(pre + "modulation.weight"), bias=self.P(pre + "modulation.bias"))  # :158
         return s, ops.cast(s, square=1)
 
-    def mc_fwd(self, pre, x, w, act=0, resid=None, save=True):
+    def mc_fwd(self, pre, x, w, act=0, resid=None, save=True, xs=None):
         B, H, W, Cin = x.shape
         HW = H * W
         pk = self.packs[pre]
@@ -127,7 +127,8 @@ class GeneratorEngine:
             d = ops.gemm(s2, pk["wsq"], B, rows, Cin, ep=E_(act=RSQRT))  # demod coefficients [B, rows] (:165)
         ep = E_(scale=d, scale_shift=ops.ilog2(HW), scale_ld=rows, act=act, resid=resid,
                 ld_res=resid.shape[-1] if resid is not None else 0)
-        xs = ops.scale_bc(x, s)  # x * style, shared by the conv and its weight gradient
+        if xs is None:  # x * style, shared by the conv and its weight gradient (the MTM warp writes it itself)
+            xs = ops.scale_bc(x, s)
         y = ops.conv2d(xs, pk["w"], rows, k, k, 1, k // 2, ep=ep, out_dtype=self.cdt)
         sv = (x, xs, w, s, s2, d, y, resid, act) if save else None
         return y, sv
@@ -190,8 +191,10 @@ class GeneratorEngine:
         opk = self.packs[pre + "offset_net.0."]
         o1 = ops.conv2d(x, opk["w"], 32, 3, 3, 1, 1, out_dtype=self.cdt,
                         ep=E_(bias=self.P(pre + "offset_net.0.bias"), act=LRELU))
-        xw, samp = ops.warp_fwd(x, o1, self.P(pre + "offset_net.2.weight"), self.P(pre + "offset_net.2.bias"))
-        y, msv = self.mc_fwd(pre + "modulated_conv.", xw, w, act=1, resid=resid, save=save)
+        s, _ = self._style(pre + "modulated_conv.", w, x.shape[-1])
+        xw, samp, xs = ops.warp_fwd(x, o1, self.P(pre + "offset_net.2.weight"), self.P(pre + "offset_net.2.bias"),
+                                    s=s)
+        y, msv = self.mc_fwd(pre + "modulated_conv.", xw, w, act=1, resid=resid, save=save, xs=xs)
         return y, ((x, o1, samp, xw, msv) if save else None)
 
     def mtm_bwd(self, pre, sv, gz, gx, gw, accumulate=0):

@@ -445,12 +445,20 @@ def balance(load, E_, T, weight, grad_scale, out, coef):
 # ---------------------------------------------------------------------------
 # MTM warp / upsample
 # ---------------------------------------------------------------------------
-def warp_fwd(x, o1, w2, b2):
+def warp_fwd(x, o1, w2, b2, s=None):
+    """MTM warp (mg_warp_fwd).  With ``s`` [B, C] (fp32, row stride s.stride(0)) also returns the warped map
+    scaled per (image, channel) -- the next modulated conv's input -- from the same pass (mg_warp_fwd_scaled):
+    (out, samp) or (out, samp, out_scaled)."""
     B, H, W, C = x.shape
     out = torch.empty_like(x)
     samp = torch.empty(B * H * W, 4, device=x.device, dtype=torch.float32)
-    call("mg_warp_fwd", dt(x), ptr(x), ptr(o1), ptr(w2), ptr(b2), B, H, W, C, ptr(out), ptr(samp), S())
-    return out, samp
+    if s is None:
+        call("mg_warp_fwd", dt(x), ptr(x), ptr(o1), ptr(w2), ptr(b2), B, H, W, C, ptr(out), ptr(samp), S())
+        return out, samp
+    xs = torch.empty_like(x)
+    call("mg_warp_fwd_scaled", dt(x), ptr(x), ptr(o1), ptr(w2), ptr(b2), B, H, W, C, ptr(s), s.stride(0), ptr(out),
+         ptr(xs), ptr(samp), S())
+    return out, samp, xs
 
 
 def warp_bwd(gout, x, samp, gx32, goff):
