@@ -439,7 +439,11 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
   // 128^2 tiles (half the operand traffic per flop) when both output dims fill them; split K so the grid
   // covers the chip about twice (occupancy-2 kernels) without cutting a split below 1024 pixels
   const int tile = g_mg_tune[MG_TUNE_WGRAD_TILE];
-  const bool big = dtype == MG_BF16 && Cout >= 128 && N >= 128 && tile == 128;
+  // 128^2 tiles pay off on long per-split reductions (measured at B=256: the discriminator's 4x4/s2 conv
+  // weight gradient, Cout 256 x 2048 over 65536 pixels, 137 -> 106 us; the generator's modulated convs
+  // stay faster on 64^2 tiles)
+  const bool big = dtype == MG_BF16 && Cout >= 128 && N >= 128 &&
+                   (tile == 128 || (tile == 0 && Cout >= 256 && N >= 1024 && P >= 32768));
   const int64_t tiles = big ? (int64_t)cdiv(Cout, 128) * cdiv(N, 128) : (int64_t)cdiv(Cout, 64) * cdiv(N, 64);
   const bool slabs = g_mg_tune[MG_TUNE_WGRAD_MODE] == 0;
   if (splits < 1 && g_mg_tune[MG_TUNE_WGRAD_SPLITS] > 0) splits = g_mg_tune[MG_TUNE_WGRAD_SPLITS];
@@ -449,7 +453,8 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
     // D conv1 / modconv 8x8 / modconv 16x16 weight gradients 1.36x / 1.2x / 1.6x over ~512 blocks)
     const int64_t want = slabs ? (big ? 1024 : 2048) : (big ? 288 : 576);
     int64_t t = std::max<int64_t>(tiles, 1);
-    splits = (int)std::max<int64_t>(1, std::min<int64_t>((want + t / 2) / t, slabs ? std::min<int64_t>(16, P / 1024)
+    const int64_t cap = (!big && tiles < 64) ? 32 : 16;  // few 64^2 tiles: up to 32 slabs (modconv 16x16 wgrad 65 -> 58 us)
+    splits = (int)std::max<int64_t>(1, std::min<int64_t>((want + t / 2) / t, slabs ? std::min<int64_t>(cap, P / 1024)
                                                                                       : P / 2048));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
