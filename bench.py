@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--topk", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU-oracle steps (B=8; ~10-20 s of CPU work)")
     ap.add_argument("--time-kernel", default="d_conv1",
                     help="kernel whose launches are timed with HIP events for the roofline field")
     ap.add_argument("--eager", action="store_true",

@@ -265,29 +265,43 @@ __global__ __launch_bounds__(256) void k_combine_v(const T* __restrict__ Y, int6
   }
 }
 
-// 8-channel vector form of k_token_grad
-template <typename T, typename TO>
+// 8-channel vector form of k_token_grad; Wfc [C, E] staged in LDS (dynamic, C * E floats), the token's
+// g_raw row read as 16-B vectors
+template <typename T, typename TO, int E>
 __global__ __launch_bounds__(256) void k_token_grad_v(const T* __restrict__ gX, int64_t ldx,
                                                       const int* __restrict__ pos_of, int Tn, int k, int C,
                                                       const float* __restrict__ g_raw, const float* __restrict__ Wfc,
-                                                      int E, TO* __restrict__ out, int64_t ldo) {
+                                                      TO* __restrict__ out, int64_t ldo) {
+  extern __shared__ float sW[];  // [E][C]: a lane's 8 channels are contiguous (16-B reads, no bank conflicts)
+  for (int i = threadIdx.x; i < C * E; i += 256) sW[(i % E) * C + i / E] = Wfc[i];
+  __syncthreads();
   const int cv = C >> 3;
   const int n = Tn * cv;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int t = i / cv, c = (i - t * cv) * 8;
-    float s[8], v[8];
+    float s[8], v[8], gr[E];
 #pragma unroll
     for (int q = 0; q < 8; ++q) s[q] = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; e += 4) {
+      const f32x4_t g4 = *reinterpret_cast<const f32x4_t*>(g_raw + (int64_t)t * E + e);
+      gr[e] = g4[0]; gr[e + 1] = g4[1]; gr[e + 2] = g4[2]; gr[e + 3] = g4[3];
+    }
     if (gX)
       for (int j = 0; j < k; ++j) {
         ld8(gX + (int64_t)pos_of[t * k + j] * ldx + c, v);
 #pragma unroll
         for (int q = 0; q < 8; ++q) s[q] += v[q];
       }
-    for (int e = 0; e < E; ++e) {
-      const float gr = g_raw[(int64_t)t * E + e];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) s[q] += gr * Wfc[(int64_t)(c + q) * E + e];
+    for (int e = 0; e < E; ++e) {
+      const f32x4_t w0 = *reinterpret_cast<const f32x4_t*>(sW + e * C + c);
+      const f32x4_t w1 = *reinterpret_cast<const f32x4_t*>(sW + e * C + c + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s[q] += gr[e] * w0[q];
+        s[q + 4] += gr[e] * w1[q];
+      }
     }
     st8(out + (int64_t)t * ldo + c, s);
   }
@@ -471,13 +485,23 @@ __global__ void k_router_feat_grad(const T* __restrict__ tok, int64_t ld, int Tn
   }
 }
 
-__global__ __launch_bounds__(256) void k_feat_grad_fin(const float* __restrict__ part, int nparts, int n,
-                                                       float* __restrict__ out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+// out[i] += sum_r part[r * n + i]: 64 columns x 16 row lanes per block, LDS fold
+__global__ __launch_bounds__(1024) void k_feat_grad_fin(const float* __restrict__ part, int nparts, int n,
+                                                        float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + cx;
   float s = 0.f;
-  for (int r = 0; r < nparts; ++r) s += part[(int64_t)r * n + i];
-  out[i] += s;
+  if (i < n)
+    for (int r = ry; r < nparts; r += 16) s += part[(int64_t)r * n + i];
+  red[ry][cx] = s;
+  __syncthreads();
+  if (ry == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) t += red[y][cx];
+    out[i] += t;
+  }
 }
 
 // out[g][n] += sum_{r in group g} X[src(r)][n] * rs[r]  (grouped bias gradients)
@@ -838,10 +862,16 @@ extern "C" int mg_moe_token_grad(int dtype, const void* gX, int64_t ldx, const i
                                  void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t n = (int64_t)T * C;
-  if (C % 8 == 0 && (!gX || (ldx % 8 == 0 && mg_al16(gX))) && ldo % 8 == 0 && mg_al16(out) && n / 8 < (1LL << 31)) {
-#define LV_(TT, TO) hipLaunchKernelGGL((k_token_grad_v<TT, TO>), dim3(nblk(n / 8)), dim3(256), 0, st, (const TT*)gX, ldx, pos_of, T, k, C, g_raw, Wfc, E, (TO*)out, ldo)
-    if (dtype == MG_F32) { if (out_dtype == MG_F32) LV_(float, float); else LV_(float, bf16_t); }
-    else { if (out_dtype == MG_F32) LV_(bf16_t, float); else LV_(bf16_t, bf16_t); }
+  if (C % 8 == 0 && (!gX || (ldx % 8 == 0 && mg_al16(gX))) && ldo % 8 == 0 && mg_al16(out) && n / 8 < (1LL << 31) &&
+      (E == 4 || E == 8 || E == 16 || E == 32) && mg_al16(g_raw) && (size_t)C * E * 4 <= 65536) {
+    const size_t lds = (size_t)C * E * sizeof(float);
+    // grid sized to fill the chip once (each block stages Wfc), grid-stride over the rest
+    const int blocks = (int)std::min<int64_t>(nblk(n / 8), 2048);
+#define LV_(TT, TO, EE) hipLaunchKernelGGL((k_token_grad_v<TT, TO, EE>), dim3(blocks), dim3(256), lds, st, (const TT*)gX, ldx, pos_of, T, k, C, g_raw, Wfc, (TO*)out, ldo)
+#define LVE_(TT, TO) if (E == 4) LV_(TT, TO, 4); else if (E == 8) LV_(TT, TO, 8); else if (E == 16) LV_(TT, TO, 16); else LV_(TT, TO, 32)
+    if (dtype == MG_F32) { if (out_dtype == MG_F32) { LVE_(float, float); } else { LVE_(float, bf16_t); } }
+    else { if (out_dtype == MG_F32) { LVE_(bf16_t, float); } else { LVE_(bf16_t, bf16_t); } }
+#undef LVE_
 #undef LV_
     return mg_check_launch("mg_moe_token_grad");
   }
@@ -867,7 +897,7 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
   if (dtype == MG_F32) { LE_(float); } else { LE_(bf16_t); }
 #undef LE_
 #undef L_
-  if (part) hipLaunchKernelGGL(k_feat_grad_fin, dim3(cdiv(C * E, 256)), dim3(256), 0, st, part, (int)grid.x, C * E, G1);
+  if (part) hipLaunchKernelGGL(k_feat_grad_fin, dim3(cdiv(C * E, 64)), dim3(1024), 0, st, part, (int)grid.x, C * E, G1);
   return mg_check_launch("mg_router_feat_grad");
 }
 
