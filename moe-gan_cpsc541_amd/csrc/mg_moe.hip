@@ -39,11 +39,17 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
                              int* __restrict__ topi, float* __restrict__ gate) {
   constexpr int TEAM = 8;
   constexpr int VEC = VecOf<T>::N;
-  extern __shared__ float wsm[];  // Wfc [C][E]
-  for (int i = threadIdx.x; i < C * E; i += blockDim.x) wsm[i] = Wfc[i];
+  // Wfc [C][E] in LDS with element e of row c at (e + c / VEC) mod E: the 8 lanes of a team read rows
+  // VEC apart, which the rotation puts on distinct banks
+  extern __shared__ float wsm[];
+  for (int i = threadIdx.x; i < C * E; i += blockDim.x) {
+    const int c = i / E, e = i - c * E;
+    wsm[c * E + ((e + c / VEC) & (E - 1))] = Wfc[i];
+  }
   __syncthreads();
   int team = threadIdx.x / TEAM, tl = threadIdx.x % TEAM;
-  int t = blockIdx.x * (blockDim.x / TEAM) + team;
+  // grid-stride over tokens: each block stages Wfc once for many tokens
+  for (int t = blockIdx.x * (blockDim.x / TEAM) + team; t - team < Tn; t += gridDim.x * (blockDim.x / TEAM)) {
   bool ok = t < Tn;
   float acc[E];
 #pragma unroll
@@ -51,13 +57,14 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
   if (ok) {
     for (int c0 = tl * VEC; c0 < C; c0 += TEAM * VEC) {
       auto v = *reinterpret_cast<const typename VecOf<T>::type*>(tok + (int64_t)t * ld + c0);
+      const int rot = c0 / VEC;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         float x;
         if constexpr (sizeof(T) == 4) x = v[j]; else x = bf2f(v[j]);
         const float* wr = wsm + (c0 + j) * E;
 #pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] += x * wr[e];
+        for (int e = 0; e < E; ++e) acc[e] += x * wr[(e + rot) & (E - 1)];
       }
     }
   }
@@ -67,7 +74,7 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
     acc[e] += __shfl_xor(acc[e], 2, 64);
     acc[e] += __shfl_xor(acc[e], 4, 64);
   }
-  if (!ok || tl != 0) return;
+  if (ok && tl == 0) {
   int b = t >> lgHW;
   float te = teff_of(temp, anneal);
   float z[E], p[E];
@@ -127,6 +134,8 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
 #pragma unroll
     for (int e = 0; e < E; ++e) probs[(int64_t)t * E + e] = p[e];
   }
+  }  // ok && tl == 0
+  }  // token loop
 }
 
 // ---- dispatch: deterministic per-expert position lists ----
@@ -777,7 +786,7 @@ extern "C" int mg_router_fwd(int dtype, const void* tok, int64_t ld, int T, int 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int lg = 0;
   while ((1 << lg) < HW) ++lg;
-  dim3 grid(cdiv(T, 32));
+  dim3 grid(std::min(cdiv(T, 32), 1024));
   size_t sm = (size_t)C * E * sizeof(float);
 #define L_(TT, EE) hipLaunchKernelGGL((k_router_fwd<TT, EE>), grid, dim3(256), sm, st, (const TT*)tok, ld, T, C, Wfc, Lt, lg, \
                                       temperature, anneal, k, eval_mode, probs, zlog, topi, gate)
