@@ -379,19 +379,21 @@ void run_wgrad(const void* gy, int64_t ldg, const void* x, int B, int H, int W, 
 // reference [Cout][Cin][KH][KW] layout in one pass (threads walk gw in order: coalesced accumulate).
 __global__ __launch_bounds__(256) void k_wgrad_fold(const float* __restrict__ ws, int splits, int Cout, int lgCin,
                                                     int taps, float* __restrict__ gw) {
+  // threads walk the slabs in their own order (o, tap, ci): the split reads are coalesced; the reference
+  // layout write gw[o][ci][tap] is strided by taps (one read-modify-write per element)
   const int Cin = 1 << lgCin, N = taps << lgCin;
   const int64_t MN = (int64_t)Cout * N;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
-    const int tap = (int)(i % taps);
-    const int64_t oc = i / taps;  // o * Cin + ci
-    const int ci = (int)(oc & (Cin - 1));
-    const int64_t o = oc >> lgCin;
-    const float* src = ws + o * N + (int64_t)tap * Cin + ci;
+    const int ci = (int)(i & (Cin - 1));
+    const int64_t t = i >> lgCin;  // o * taps + tap
+    const int tap = (int)(t % taps);
+    const int64_t o = t / taps;
     float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += src[s * MN];
-    gw[i] += v;
+    for (int s = 0; s < splits; ++s) v += ws[s * MN + i];
+    gw[((o << lgCin) + ci) * taps + tap] += v;
   }
 }
+
 
 // Weight gradient with split-K into fp32 slabs written by the 8-column vector epilogue (coalesced, no atomics),
 // then k_wgrad_fold.  Returns false when the workspace cannot be had (caller falls back to atomics).
