@@ -1,0 +1,89 @@
+"""Router / MoE token kernels across expert counts (E = 4, 8, 16, 32; the C5 config uses 32 top-4) and the
+fused MTM warp + modulation prescale, against plain PyTorch fp32 on the GPU.
+
+The router math follows the oracle (oracle/aurora_cpu.py `router` / `topk_route`, t2i_moe_gan.py:364-402);
+top-k indices must match exactly (inputs are drawn so that no two probabilities of a token tie).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from moegan_mi import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12)).item()
+
+
+def ref_router(tok, Wfc, Lt, HW, temp, anneal, k):
+    T = tok.shape[0]
+    b = torch.arange(T, device=tok.device) // HW
+    z = (tok.double() @ Wfc.double() + Lt.double()[b]) / min(max(temp * anneal, 0.5), 5.0)
+    p = torch.softmax(z.clamp(-20.0, 20.0), dim=1).clamp(1e-6, 1.0)
+    p = p / p.sum(dim=1, keepdim=True)
+    top = torch.topk(p, k, dim=1, sorted=True)
+    gate = top.values if k == p.shape[1] else top.values / top.values.sum(dim=1, keepdim=True)
+    return p, z, top.indices, gate
+
+
+@pytest.mark.parametrize("E,k", [(4, 2), (8, 2), (16, 2), (32, 4), (8, 8)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_router_fwd_across_experts(E, k, dtype):
+    g = torch.Generator(device=DEV).manual_seed(E * 7 + k)
+    B, HW, C = 8, 64, 128
+    T = B * HW
+    tok = torch.randn(T, C, device=DEV, generator=g).to(dtype)
+    Wfc = torch.randn(C, E, device=DEV, generator=g) * 0.2
+    Lt = torch.randn(B, E, device=DEV, generator=g)
+    temp = torch.tensor([1.3], device=DEV)
+    probs, zlog, topi, gate = ops.router_fwd(tok, Wfc, Lt, E, k, HW, temp, 1.0)
+    p, z, ti, gt = ref_router(tok.float(), Wfc, Lt, HW, 1.3, 1.0, k)
+    assert rel(zlog, z) < 1e-5
+    assert rel(probs, p) < 1e-5
+    # exact indices wherever the k-th and (k+1)-th probabilities are not within rounding of each other
+    srt = torch.sort(p, dim=1, descending=True).values
+    clear = (srt[:, k - 1] - srt[:, k]).abs() > 1e-6 if k < E else torch.ones(T, dtype=torch.bool, device=DEV)
+    order = torch.sort(topi.long(), dim=1).values
+    assert torch.equal(order[clear], torch.sort(ti, dim=1).values[clear])
+    assert clear.float().mean() > 0.95
+    assert rel(torch.sort(gate, dim=1).values[clear], torch.sort(gt, dim=1).values.float()[clear]) < 1e-5
+
+
+@pytest.mark.parametrize("E", [4, 8, 16, 32])
+def test_token_and_feature_grad_across_experts(E):
+    g = torch.Generator(device=DEV).manual_seed(100 + E)
+    T, C, k = 2048, 128, 2
+    gX = torch.randn(T * k, C, device=DEV, generator=g).to(torch.bfloat16)
+    pos_of = torch.randperm(T * k, device=DEV, generator=g).to(torch.int32)
+    g_raw = torch.randn(T, E, device=DEV, generator=g)
+    Wfc = torch.randn(C, E, device=DEV, generator=g)
+    out = torch.empty(T, C, device=DEV)
+    ops.moe_token_grad(gX, pos_of, g_raw, Wfc, out, k)
+    ref = gX.float()[pos_of.long().view(T, k)].sum(1) + g_raw @ Wfc.T
+    assert rel(out, ref) < 1e-5
+    tok = torch.randn(T, C, device=DEV, generator=g).to(torch.bfloat16)
+    G1 = torch.zeros(C, E, device=DEV)
+    ops.router_feat_grad(tok, g_raw, G1)
+    assert rel(G1, tok.float().T @ g_raw) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H,C", [(16, 128), (8, 256), (4, 512)])
+def test_warp_fwd_scaled_matches_warp_then_scale(dtype, H, C):
+    """mg_warp_fwd_scaled == mg_warp_fwd followed by mg_scale_bc, bit for bit (same rounding order)."""
+    g = torch.Generator(device=DEV).manual_seed(H + C)
+    B = 4
+    x = torch.randn(B, H, H, C, device=DEV, generator=g).to(dtype)
+    o1 = torch.randn(B, H, H, 32, device=DEV, generator=g).to(dtype)
+    w2 = torch.randn(2, 32, 3, 3, device=DEV, generator=g) * 0.5
+    b2 = torch.randn(2, device=DEV, generator=g)
+    S = torch.randn(B, 3 * C, device=DEV, generator=g)
+    s = S[:, C:2 * C]  # a column slice of a batched style matrix (row stride 3C)
+    out, samp = ops.warp_fwd(x, o1, w2, b2)
+    xs_ref = ops.scale_bc(out, s)
+    out2, samp2, xs = ops.warp_fwd(x, o1, w2, b2, s=s)
+    assert torch.equal(out, out2) and torch.equal(samp, samp2)
+    assert torch.equal(xs, xs_ref)
