@@ -267,6 +267,11 @@ int mg_warp_fwd_scaled(int dtype, const void* x, const void* o1, const float* w2
 /* grid_sample backward: gx (fp32, +=, atomics) and goff [P,2] = d loss / d offsets. */
 int mg_warp_bwd(int dtype, int gout_dtype, const void* gout, const void* x, const float* samp, int B, int H, int W, int C, float* gx, float* goff, void* stream);
 
+/* Fused MTM backward for images of at most 1024 pixels (t2i_moe_gan.py:222-239 backward; replaces mg_warp_bwd +
+   mg_offset_head_bwd there): grid_sample data gradient by gather into gx (dtype gx_dtype, = or += when accumulate;
+   no atomics), dL/doffsets per pixel, and the offset head backward: ga1, gw2 +=, gb2 +=.  C = 8 * 2^k <= 512. */
+int mg_mtm_bwd_fused(int dtype, int gout_dtype, const void* gout, const void* x, const float* samp, const void* o1, const float* w2, int B, int H, int W, int C, int gx_dtype, void* gx, int accumulate, void* ga1, float* gw2, float* gb2, void* stream);
+
 /* offset_net second conv backward fused with the first conv's LeakyReLU: ga1, gw2 +=, gb2 +=. */
 int mg_offset_head_bwd(int dtype, const float* goff, const void* o1, const float* w2, int B, int H, int W, void* ga1, float* gw2, float* gb2, void* stream);
 

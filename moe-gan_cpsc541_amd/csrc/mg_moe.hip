@@ -542,12 +542,12 @@ __global__ void k_grouped_colsum(const T* __restrict__ X, int64_t ld, const int*
 // 8-column vector form: block = TX column vectors x TY row lanes over one chunk of rows.  A thread flushes its
 // running sum to global memory only when its rows cross a group boundary (rare: E boundaries in total); the
 // sums for the chunk's last group are folded over the row lanes in LDS and added once per column.
-template <typename T>
-__global__ __launch_bounds__(256) void k_grouped_colsum_v(const T* __restrict__ X, int64_t ld,
-                                                          const int* __restrict__ idx, int idx_div,
-                                                          const float* __restrict__ rs, const int* __restrict__ row_off,
-                                                          int G, int N, int rows_per_block, float* __restrict__ out) {
-  __shared__ float red[256 * 8];
+template <typename T, int NT>
+__global__ __launch_bounds__(NT) void k_grouped_colsum_v(const T* __restrict__ X, int64_t ld,
+                                                         const int* __restrict__ idx, int idx_div,
+                                                         const float* __restrict__ rs, const int* __restrict__ row_off,
+                                                         int G, int N, int rows_per_block, float* __restrict__ out) {
+  __shared__ float red[NT * 8];
   const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int n = (blockIdx.x * TX + tx) * 8;
   const int total = row_off[G];
@@ -914,16 +914,17 @@ extern "C" int mg_grouped_colsum(int dtype, const void* X, int64_t ld, const int
                                  const int32_t* row_off, int G, int N, int max_rows, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (N % 8 == 0 && ld % 8 == 0 && mg_al16(X) && max_rows > 0) {
-    const int cv = N / 8, tx = std::min(cv, 64), ty = 256 / tx;
+    // 1024-thread blocks, ~256 of them (one per CU, 64 KiB of loads in flight each): a quarter of the
+    // same-address atomics of 1024 small blocks, at least 8 rows per row lane
+    const int cv = N / 8, tx = std::min(cv, 64), ty = 1024 / tx;
     const int cblk = cdiv(cv, tx);
-    // ~1024 blocks, at least 8 rows per row lane
-    int rpb = std::max(8 * ty, cdiv(max_rows, std::max(1, 1024 / cblk)));
+    int rpb = std::max(8 * ty, cdiv(max_rows, std::max(1, 256 / cblk)));
     dim3 grid(cblk, cdiv(max_rows, rpb)), blk(tx, ty);
     if (dtype == MG_F32)
-      hipLaunchKernelGGL(k_grouped_colsum_v<float>, grid, blk, 0, st, (const float*)X, ld, idx,
+      hipLaunchKernelGGL((k_grouped_colsum_v<float, 1024>), grid, blk, 0, st, (const float*)X, ld, idx,
                          idx_div > 0 ? idx_div : 1, rs, row_off, G, N, rpb, out);
     else
-      hipLaunchKernelGGL(k_grouped_colsum_v<bf16_t>, grid, blk, 0, st, (const bf16_t*)X, ld, idx,
+      hipLaunchKernelGGL((k_grouped_colsum_v<bf16_t, 1024>), grid, blk, 0, st, (const bf16_t*)X, ld, idx,
                          idx_div > 0 ? idx_div : 1, rs, row_off, G, N, rpb, out);
     return mg_check_launch("mg_grouped_colsum");
   }

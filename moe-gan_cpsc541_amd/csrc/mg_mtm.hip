@@ -569,6 +569,213 @@ __global__ void k_up2_bwd(const TG* __restrict__ gout, int B, int H, int W, int 
 
 inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
 
+
+// Fused MTM backward for images of at most 1024 pixels, one 1024-thread block per image: grid_sample's data
+// gradient as a GATHER instead of a scatter, then the offset head's backward from the image's dL/doffsets held
+// in LDS (t2i_moe_gan.py:222-239 backward).
+//  1. every output pixel p registers itself with the (up to 4) in-image source pixels q its bilinear sample
+//     touches (LDS atomics give the slot), a block scan turns the counts into a CSR list per q;
+//  2. items (pixel, 8-channel vector): gx[q] = sum over q's list of w(p->q) * gout[p]  (16-B loads, one plain
+//     store: no fp32 atomics, no zero fill, optional accumulate into gx), and dL/dgrid of p = dot products of
+//     gout[p] with x at its corners, reduced over the pixel's C/8 vector lanes with shuffles;
+//  3. offset head (32 -> 2 conv, 3x3) backward fused with the first conv's LeakyReLU: ga1 for the image, and
+//     the image's partial (gw2, gb2) row written to a workspace row (folded over images by k_rows_fin).
+template <typename T, typename TG, typename TX>
+__global__ __launch_bounds__(1024) void k_mtm_bwd_img(const TG* __restrict__ gout, const T* __restrict__ x,
+                                                      const float* __restrict__ samp, const T* __restrict__ o1,
+                                                      const float* __restrict__ w2, int H, int W, int C, int lgV,
+                                                      TX* __restrict__ gx, int accumulate, T* __restrict__ ga1,
+                                                      float* __restrict__ part) {
+  extern __shared__ float smem[];
+  const int HW = H * W, tid = threadIdx.x, nt = blockDim.x;
+  const int b = blockIdx.x;
+  f32x4_t* sinf = reinterpret_cast<f32x4_t*>(smem);   // [HW] (ix, iy, mx, my)
+  float* sgo = smem + 4 * HW;                          // [HW][2] dL/doffsets
+  float* sw = sgo + 2 * HW;                            // [576] offset_net.2 weight
+  float* red = sw + 576;                               // [578] (gw2, gb2) partials
+  int* cnt = reinterpret_cast<int*>(red + 578);        // [HW + 1] counts -> CSR offsets
+  int* slot = cnt + HW + 1;                            // [4 HW] slot of (p, corner) in q's list, -1 = none
+  int* ent = slot + 4 * HW;                            // [4 HW] p * 4 + corner
+  const int64_t row0 = (int64_t)b * HW;
+  for (int i = tid; i <= HW; i += nt) cnt[i] = 0;
+  for (int i = tid; i < 578; i += nt) {
+    if (i < 576) sw[i] = w2[i];
+    red[i] = 0.f;
+  }
+  __syncthreads();
+  for (int p = tid; p < HW; p += nt) {
+    const f32x4_t sp = *reinterpret_cast<const f32x4_t*>(samp + (row0 + p) * 4);
+    sinf[p] = sp;
+    const int x0 = (int)floorf(sp[0]), y0 = (int)floorf(sp[1]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
+      slot[p * 4 + k] = (xx >= 0 && xx < W && yy >= 0 && yy < H) ? atomicAdd(&cnt[yy * W + xx], 1) : -1;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of cnt[0..HW) by wave 0, 64 entries per pass
+    int carry = 0;
+    for (int base = 0; base < HW; base += 64) {
+      const int i = base + tid;
+      const int v = i < HW ? cnt[i] : 0;
+      int s = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(s, o, 64);
+        if (tid >= o) s += t;
+      }
+      if (i < HW) cnt[i] = carry + s - v;
+      carry += __shfl(s, 63, 64);
+    }
+    if (tid == 0) cnt[HW] = carry;
+  }
+  __syncthreads();
+  for (int p = tid; p < HW; p += nt) {
+    const f32x4_t sp = sinf[p];
+    const int x0 = (int)floorf(sp[0]), y0 = (int)floorf(sp[1]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int sl = slot[p * 4 + k];
+      if (sl >= 0) ent[cnt[(y0 + (k >> 1)) * W + x0 + (k & 1)] + sl] = p * 4 + k;
+    }
+  }
+  __syncthreads();
+  const int V = 1 << lgV, items = HW << lgV;
+  const TG* gb = gout + row0 * C;
+  const T* xb = x + row0 * C;
+  for (int base = 0; base < items; base += nt) {
+    const int it = base + tid;
+    const bool live = it < items;
+    const int p = live ? it >> lgV : 0, c = (it & (V - 1)) * 8;
+    float gix = 0.f, giy = 0.f, mx = 0.f, my = 0.f;
+    if (live) {
+      // gather: q = p
+      float acc[8], g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      for (int e = cnt[p], e1 = cnt[p + 1]; e < e1; ++e) {
+        const int en = ent[e], pe = en >> 2, k = en & 3;
+        const f32x4_t sp = sinf[pe];
+        const float fx0 = floorf(sp[0]), fy0 = floorf(sp[1]);
+        const float ax = (k & 1) ? sp[0] - fx0 : (fx0 + 1.f) - sp[0];
+        const float ay = (k >> 1) ? sp[1] - fy0 : (fy0 + 1.f) - sp[1];
+        const float wgt = ax * ay;
+        ld8(gb + (int64_t)pe * C + c, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += wgt * g[j];
+      }
+      TX* gq = gx + (row0 + p) * C + c;
+      if (accumulate) {
+        float o[8];
+        ld8(gq, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += o[j];
+      }
+      st8(gq, acc);
+      // dL/dgrid of p
+      const f32x4_t sp = sinf[p];
+      mx = sp[2];
+      my = sp[3];
+      const int x0 = (int)floorf(sp[0]), y0 = (int)floorf(sp[1]);
+      const float ax1 = (float)(x0 + 1) - sp[0], ax0 = sp[0] - (float)x0;
+      const float ay1 = (float)(y0 + 1) - sp[1], ay0 = sp[1] - (float)y0;
+      ld8(gb + (int64_t)p * C + c, g);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
+        if (xx >= 0 && xx < W && yy >= 0 && yy < H) {
+          float xv[8];
+          ld8(xb + (int64_t)(yy * W + xx) * C + c, xv);
+          float d = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d += xv[j] * g[j];
+          gix += ((k & 1) ? 1.f : -1.f) * ((k >> 1) ? ay0 : ay1) * d;
+          giy += ((k >> 1) ? 1.f : -1.f) * ((k & 1) ? ax0 : ax1) * d;
+        }
+      }
+    }
+    for (int o = 1; o < V; o <<= 1) {
+      gix += __shfl_xor(gix, o, 64);
+      giy += __shfl_xor(giy, o, 64);
+    }
+    if (live && (it & (V - 1)) == 0) {
+      sgo[p * 2 + 0] = gix * (0.5f * W) * mx * 0.05f;
+      sgo[p * 2 + 1] = giy * (0.5f * H) * my * 0.05f;
+    }
+  }
+  __syncthreads();
+  // offset head backward: items (q, c), c = tid & 31 fixed per thread
+  const int c = tid & 31;
+  float accw[18];
+#pragma unroll
+  for (int i = 0; i < 18; ++i) accw[i] = 0.f;
+  for (int it = tid; it < HW * 32; it += nt) {
+    const int q = it >> 5;
+    const int h = q / W, w = q - (q / W) * W;
+    const float ov = ldf(o1, (row0 + q) * 32 + c);
+    float g = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int yy = h - (tap / 3 - 1), xx = w - (tap % 3 - 1);  // output pixel that reads q through this tap
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const int pp = yy * W + xx;
+        const float g0 = sgo[pp * 2], g1 = sgo[pp * 2 + 1];
+        g += g0 * sw[c * 9 + tap] + g1 * sw[(32 + c) * 9 + tap];
+        accw[tap] += g0 * ov;
+        accw[9 + tap] += g1 * ov;
+      }
+    }
+    stf(ga1, (row0 + q) * 32 + c, ov > 0.f ? g : 0.2f * g);
+  }
+#pragma unroll
+  for (int i = 0; i < 18; ++i) {
+    accw[i] += __shfl_xor(accw[i], 32, 64);
+  }
+  if ((tid & 63) < 32) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      atomicAdd(&red[c * 9 + tap], accw[tap]);
+      atomicAdd(&red[(32 + c) * 9 + tap], accw[9 + tap]);
+    }
+  }
+  if (tid < 64) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int p = tid; p < HW; p += 64) {
+      s0 += sgo[p * 2];
+      s1 += sgo[p * 2 + 1];
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (tid == 0) {
+      red[576] = s0;
+      red[577] = s1;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 578; i += nt) part[(int64_t)b * 578 + i] = red[i];
+}
+
+// out_a[i] += sum_r part[r][i] for i < na, out_b[i - na] += ... for na <= i < ncols  (64 columns x 16 row lanes)
+__global__ __launch_bounds__(1024) void k_rows_fin(const float* __restrict__ part, int nrows, int ncols, int na,
+                                                   float* __restrict__ out_a, float* __restrict__ out_b) {
+  __shared__ float red[16][64];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + cx;
+  float s = 0.f;
+  if (i < ncols)
+    for (int r = ry; r < nrows; r += 16) s += part[(int64_t)r * ncols + i];
+  red[ry][cx] = s;
+  __syncthreads();
+  if (ry == 0 && i < ncols) {
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) t += red[y][cx];
+    if (i < na) out_a[i] += t;
+    else out_b[i - na] += t;
+  }
+}
+
 }  // namespace
 
 extern "C" int mg_warp_fwd(int dtype, const void* x, const void* o1, const float* w2, const float* b2, int B, int H,
@@ -643,6 +850,37 @@ extern "C" int mg_warp_bwd(int dtype, int gout_dtype, const void* gout, const vo
   else { if (gout_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
 #undef L_
   return mg_check_launch("mg_warp_bwd");
+}
+
+extern "C" int mg_mtm_bwd_fused(int dtype, int gout_dtype, const void* gout, const void* x, const float* samp,
+                                const void* o1, const float* w2, int B, int H, int W, int C, int gx_dtype, void* gx,
+                                int accumulate, void* ga1, float* gw2, float* gb2, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int HW = H * W;
+  int lgV = 0;
+  while ((8 << lgV) < C) ++lgV;
+  MG_REQUIRE(B > 0 && HW > 0 && HW <= 1024 && C == (8 << lgV) && C <= 512, "needs H*W <= 1024 and C = 8 * 2^k <= 512");
+  MG_REQUIRE(mg_al16(gout) && mg_al16(x) && mg_al16(samp) && mg_al16(gx), "16-B aligned gout / x / samp / gx");
+  MG_REQUIRE(gx_dtype == dtype || gx_dtype == MG_F32, "gx dtype must be the activation dtype or fp32");
+  float* part = reinterpret_cast<float*>(mg_workspace((size_t)B * 578 * sizeof(float), st));
+  if (!part) {
+    mg_set_error("mg_mtm_bwd_fused: workspace allocation failed");
+    return MG_ERR_LAUNCH;
+  }
+  const size_t lds = (size_t)HW * 6 * sizeof(float) + (576 + 578) * sizeof(float) + (size_t)(9 * HW + 1) * sizeof(int);
+  MG_REQUIRE(lds <= 65536, "image too large for the per-image LDS lists");
+#define L_(T, TG, TX) hipLaunchKernelGGL((k_mtm_bwd_img<T, TG, TX>), dim3(B), dim3(1024), lds, st, (const TG*)gout, \
+    (const T*)x, samp, (const T*)o1, w2, H, W, C, lgV, (TX*)gx, accumulate, (T*)ga1, part)
+  if (dtype == MG_F32) {
+    if (gout_dtype == MG_F32) L_(float, float, float); else L_(float, bf16_t, float);
+  } else if (gx_dtype == MG_F32) {
+    if (gout_dtype == MG_F32) L_(bf16_t, float, float); else L_(bf16_t, bf16_t, float);
+  } else {
+    if (gout_dtype == MG_F32) L_(bf16_t, float, bf16_t); else L_(bf16_t, bf16_t, bf16_t);
+  }
+#undef L_
+  hipLaunchKernelGGL(k_rows_fin, dim3(cdiv(578, 64)), dim3(1024), 0, st, part, B, 578, 576, gw2, gb2);
+  return mg_check_launch("mg_mtm_bwd_fused");
 }
 
 extern "C" int mg_offset_head_bwd(int dtype, const float* goff, const void* o1, const float* w2, int B, int H, int W,

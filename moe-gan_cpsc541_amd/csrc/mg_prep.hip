@@ -114,7 +114,7 @@ __global__ void k_colsum(const T* __restrict__ X, int64_t ld, int R, int C, int 
 // one partial row per row-block (no same-address atomics), folded by k_colsum_fin.  C % 8 == 0.
 template <typename T>
 __global__ __launch_bounds__(256) void k_colsum_v(const T* __restrict__ X, int64_t ld, int R, int C,
-                                                  int rows_per_block, float* __restrict__ part) {
+                                                  int rows_per_block, float* __restrict__ part, int atomic_out) {
   __shared__ float red[256 * 8];
   const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int c = (blockIdx.x * TX + tx) * 8;
@@ -145,8 +145,13 @@ __global__ __launch_bounds__(256) void k_colsum_v(const T* __restrict__ X, int64
     for (int y = 1; y < TY; ++y)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += red[(y * TX + tx) * 8 + j];
+    if (atomic_out) {  // few row blocks: add straight into out (shallow same-address atomics, no fold launch)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) part[(int64_t)blockIdx.y * C + c + j] = acc[j];
+      for (int j = 0; j < 8; ++j) atomicAdd(part + c + j, acc[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part[(int64_t)blockIdx.y * C + c + j] = acc[j];
+    }
   }
 }
 
@@ -416,14 +421,19 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     int rblk = std::max(1, std::min({cdiv(R, 8 * ty), 1024 / cblk, 256}));
     int rpb = cdiv(R, rblk);
     rblk = cdiv(R, rpb);
+    dim3 grid(cblk, rblk);
+    if (rblk <= 16) {
+      DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum_v<T>, grid, dim3(tx, ty), 0, st, reinterpret_cast<const T*>(X),
+                                           ld, R, C, rpb, out, 1));
+      return mg_check_launch("mg_colsum");
+    }
     float* part = reinterpret_cast<float*>(mg_workspace((size_t)rblk * C * sizeof(float), st));
     if (!part) {
       mg_set_error("mg_colsum: workspace allocation failed");
       return MG_ERR_LAUNCH;
     }
-    dim3 grid(cblk, rblk);
     DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum_v<T>, grid, dim3(tx, ty), 0, st, reinterpret_cast<const T*>(X), ld,
-                                         R, C, rpb, part));
+                                         R, C, rpb, part, 0));
     hipLaunchKernelGGL(k_colsum_fin, dim3(cdiv(C, 64)), dim3(256), 0, st, part, rblk, C, out);
     return mg_check_launch("mg_colsum");
   }

@@ -203,13 +203,21 @@ class GeneratorEngine:
         P = B * H * W
         g_xw = torch.empty(P, Cin, device=self.dev, dtype=self.cdt)
         self.mc_bwd(pre + "modulated_conv.", msv, gz, g_xw, gw)
+        opk = self.packs[pre + "offset_net.0."]
+        if ops.mtm_bwd_fusable(x) and gx.is_contiguous():
+            ga1 = torch.empty(B, H, W, 32, device=self.dev, dtype=self.cdt)
+            ops.mtm_bwd_fused(g_xw, x, samp, o1, self.P(pre + "offset_net.2.weight"), gx, ga1,
+                              self.G(pre + "offset_net.2.weight"), self.G(pre + "offset_net.2.bias"), accumulate)
+            ops.conv2d(ga1, opk["wflip"], Cin, 3, 3, 1, 1, out=gx.view(B, H, W, Cin), ep=E_(accumulate=1))
+            ops.conv2d_wgrad(ga1, x, 32, 3, 3, 1, 1, self.G(pre + "offset_net.0.weight"))
+            ops.colsum(ga1.view(P, 32), self.G(pre + "offset_net.0.bias"))
+            return
         gx32 = torch.zeros(B, H, W, Cin, device=self.dev, dtype=torch.float32)
         goff = torch.empty(P, 2, device=self.dev, dtype=torch.float32)
         ops.warp_bwd(g_xw, x, samp, gx32, goff)
         ga1 = torch.empty(B, H, W, 32, device=self.dev, dtype=self.cdt)
         ops.offset_head_bwd(goff, o1, self.P(pre + "offset_net.2.weight"), ga1,
                             self.G(pre + "offset_net.2.weight"), self.G(pre + "offset_net.2.bias"))
-        opk = self.packs[pre + "offset_net.0."]
         ops.conv2d(ga1, opk["wflip"], Cin, 3, 3, 1, 1, out=gx32, ep=E_(accumulate=1))
         ops.conv2d_wgrad(ga1, x, 32, 3, 3, 1, 1, self.G(pre + "offset_net.0.weight"))
         ops.colsum(ga1.view(P, 32), self.G(pre + "offset_net.0.bias"))

@@ -7,6 +7,8 @@ rows, weights are in the reference layout unless a ``pack`` says otherwise.
 import ctypes
 import math
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -464,6 +466,20 @@ def warp_fwd(x, o1, w2, b2, s=None):
 def warp_bwd(gout, x, samp, gx32, goff):
     B, H, W, C = x.shape
     call("mg_warp_bwd", dt(x), dt(gout), ptr(gout), ptr(x), ptr(samp), B, H, W, C, ptr(gx32), ptr(goff), S())
+
+
+def mtm_bwd_fused(gout, x, samp, o1, w2, gx, ga1, gw2, gb2, accumulate=0):
+    """Per-image fused MTM backward (mg_mtm_bwd_fused): gather-form grid_sample data gradient into gx
+    (= or +=, gx's dtype), dL/doffsets in LDS, offset head backward -> ga1, gw2 +=, gb2 +=."""
+    B, H, W, C = x.shape
+    call("mg_mtm_bwd_fused", dt(x), dt(gout), ptr(gout), ptr(x), ptr(samp), ptr(o1), ptr(w2), B, H, W, C, dt(gx),
+         ptr(gx), accumulate, ptr(ga1), ptr(gw2), ptr(gb2), S())
+
+
+def mtm_bwd_fusable(x):
+    B, H, W, C = x.shape
+    return (H * W <= 512 and C % 8 == 0 and C <= 512 and (C // 8) & (C // 8 - 1) == 0 and x.is_contiguous()
+            and os.environ.get("MOEGAN_MTM_FUSED", "1") != "0")
 
 
 def offset_head_bwd(goff, o1, w2, ga1, gw2, gb2):
