@@ -133,7 +133,7 @@ class DiscriminatorEngine:
         return g_a1, G
 
     def begin_grads(self):
-        self.dW = {pre: torch.zeros_like(self.W[pre]) for pre in WN_LAYERS}
+        self.dW = {pre: ops.zeros(*self.W[pre].shape, device=self.dev) for pre in WN_LAYERS}
 
     def finish_grads(self):
         # reference weight layout: conv_layers.0 packed as [o][tap*3+c] in the GEMM -> remap to [o][c][kh][kw]
@@ -157,7 +157,7 @@ class DiscriminatorEngine:
         out = torch.zeros(4, device=dev)
         g_img = torch.empty(B, No, device=dev)
         g_fake = torch.empty(B, ff["img_part"].shape[1], device=dev)
-        g_tb = torch.zeros(B, device=dev)
+        g_tb = ops.zeros(B, device=dev)
         real_pred = torch.empty(B, No, device=dev)
         mism_pred = torch.empty(B, No, device=dev)
         fake_pred = torch.empty(B, device=dev)
@@ -175,7 +175,7 @@ class DiscriminatorEngine:
         gA1, G1 = self._head_bwd(g1, 0, fr["h1"], B, Hf, False)  # m1 * Gh1
         gA0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
         ops.dgrad_s2(gA1, self.W1cls, 128, gA0, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
-        gx = torch.zeros(B, Hr, Hr, 4, device=dev)
+        gx = ops.zeros(B, Hr, Hr, 4, device=dev)
         ops.dgrad_s2(gA0, self.W0cls, 3, gx)  # d sum(real_pred) / d real  (NHWC, channel-padded)
         r1 = torch.zeros(1, device=dev)
         u = torch.empty(B, Hr, Hr, 4, device=dev, dtype=self.cdt)
@@ -220,7 +220,7 @@ class DiscriminatorEngine:
         loss = torch.zeros(1, device=self.dev)
         g = torch.empty(B, 1, device=self.dev)
         ops.g_loss(fake_pred, loss, g.view(-1), scale)
-        g_img = torch.zeros(fake_img.shape, device=self.dev, dtype=self.cdt)
+        g_img = ops.zeros(*fake_img.shape, device=self.dev, dtype=self.cdt)
         if want_d_params:
             self.begin_grads()
         self.stack_backward(f, g, want_params=want_d_params, g_input=g_img)
@@ -256,7 +256,7 @@ class DiscriminatorEngine:
         f = ctx["f"]
         B, H = f["B"], f["H"]
         g_logits = g_logits.contiguous().float()
-        g_tb = torch.zeros(B, device=self.dev)
+        g_tb = ops.zeros(B, device=self.dev)
         ops.segsum(g_logits, B, g_logits.shape[1], 1, g_tb.view(B, 1), ld=1)
         self.begin_grads()
         g_img = torch.zeros(B, H, H, 4, device=self.dev, dtype=torch.float32) if want_input else None

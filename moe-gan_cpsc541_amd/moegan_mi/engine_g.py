@@ -157,7 +157,7 @@ class GeneratorEngine:
             c = self.style_cols[pre]
             gs = self._GS[:, c:c + Cin]
         else:
-            gs = torch.zeros(B, Cin, device=self.dev, dtype=torch.float32)
+            gs = ops.zeros(B, Cin, device=self.dev)
         ops.modconv_bwd_in(gxt.view(P, Cin), x.view(P, Cin), s, B, HW, Cin,
                            None if gx is None else gx.view(P, -1), gs, accumulate)
         # weight gradient (fp32, reference layout), on the side stream
@@ -166,7 +166,7 @@ class GeneratorEngine:
             self.side.run(lambda: ops.conv2d_wgrad(gyt, xs, Cout, k, k, 1, k // 2, gW), gyt, xs)
         else:
             def wgrad_padded():
-                tmp = torch.zeros(rows, Cin, k, k, device=self.dev)
+                tmp = ops.zeros(rows, Cin, k, k, device=self.dev)
                 ops.conv2d_wgrad(gyt, xs, rows, k, k, 1, k // 2, tmp)
                 gW.add_(tmp[:Cout])
             self.side.run(wgrad_padded, gyt, xs)
@@ -212,7 +212,7 @@ class GeneratorEngine:
             ops.conv2d_wgrad(ga1, x, 32, 3, 3, 1, 1, self.G(pre + "offset_net.0.weight"))
             ops.colsum(ga1.view(P, 32), self.G(pre + "offset_net.0.bias"))
             return
-        gx32 = torch.zeros(B, H, W, Cin, device=self.dev, dtype=torch.float32)
+        gx32 = ops.zeros(B, H, W, Cin, device=self.dev)
         goff = torch.empty(P, 2, device=self.dev, dtype=torch.float32)
         ops.warp_bwd(g_xw, x, samp, gx32, goff)
         ga1 = torch.empty(B, H, W, 32, device=self.dev, dtype=self.cdt)
@@ -454,7 +454,7 @@ class GeneratorEngine:
         g_raw, gsum = ops.router_bwd(sv["probs"], sv["zlog"], sv["topi"], sv["gate"], g_gate, g_probs, coef,
                                      sv["HW"], self.P(r + "temperature"), sv["anneal"], self.G(r + "temperature"), B)
         ops.moe_token_grad(gX, sv["pos_of"], g_raw, sv["Wfc"], g_tok, k)
-        G1 = torch.zeros(C, E, device=self.dev, dtype=torch.float32)
+        G1 = ops.zeros(C, E, device=self.dev)
         ops.router_feat_grad(tok, g_raw, G1)
         # the router's parameter GEMMs depend only on (G1, gsum) and saved vectors: run for every block at
         # the end of the backward, batched (_flush_router_bwd)
@@ -507,7 +507,7 @@ class GeneratorEngine:
         ops.layernorm_bwd(g_n3, sv["xf1"], sv["mu3"], sv["rs3"], self.P(pre + "norm3.weight"), g_xf1,
                           self.G(pre + "norm3.weight"), self.G(pre + "norm3.bias"), accumulate=1)
         # cross-attention vector: sum over each image's tokens
-        g_ca = torch.zeros(B, C, device=self.dev, dtype=torch.float32)
+        g_ca = ops.zeros(B, C, device=self.dev)
         ops.segsum(g_xf1, B, L_, C, g_ca)
         # the rest of the cross-attention chain depends only on g_ca and saved vectors: batched over the
         # blocks at the end of the backward (_flush_xattn_bwd)
@@ -614,12 +614,12 @@ class GeneratorEngine:
         and d loss / d img8 (needs forward(..., want_img8=True, save=True)).  Returns (gz, gtext) if requested."""
         B = ctx["B"]
         dev = self.dev
-        gw = torch.zeros(B, 512, device=dev)
-        g_ts = torch.zeros(B, 512, device=dev)
+        gw = ops.zeros(B, 512, device=dev)
+        g_ts = ops.zeros(B, 512, device=dev)
         self._router_bwd, self._xattn_bwd = [], []
         self._defer = True  # per-block small GEMMs are batched over the blocks after the block loop
         if self.style_cols:
-            self._GS = torch.zeros(B, self.style_n, device=dev)
+            self._GS = ops.zeros(B, self.style_n, device=dev)
             self._demod_bwd = []
         sv = ctx["rgbsv"]
         x_last = sv[0]

@@ -61,6 +61,51 @@ def _timed(kind, dims, fn):
     return graphs.eager(lambda: _timed_run(kind, dims, fn))
 
 
+# ---------------------------------------------------------------------------
+# Per-step pool of zero-initialised scratch (accumulation targets of atomics / accumulating epilogues):
+# TrainStep.step zeroes the used prefix of ONE buffer per step instead of one fill launch per buffer.
+# Outside an active step (module API, tests) zeros() is plain torch.zeros.
+# ---------------------------------------------------------------------------
+class ZeroArena:
+    ALIGN = 256
+
+    def __init__(self):
+        self.buf = None
+        self.off = 0
+        self.need = 0
+        self.active = False
+
+    def begin(self, device):
+        if self.need > 0 and (self.buf is None or self.buf.numel() < self.need or self.buf.device != device):
+            self.buf = torch.empty(self.need, device=device, dtype=torch.uint8)
+        if self.buf is not None:
+            self.buf[:min(self.need, self.buf.numel())].zero_()
+        self.off = 0
+        self.active = True
+
+    def end(self):
+        self.need = max(self.need, self.off)
+        self.active = False
+
+    def zeros(self, shape, dtype, device):
+        n = math.prod(shape) * torch.empty((), dtype=dtype).element_size()
+        a = (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        o = self.off
+        if self.active:
+            self.off += a
+        if (not self.active or self.buf is None or o + a > self.buf.numel() or o + a > self.need
+                or self.buf.device != torch.device(device)):
+            return torch.zeros(shape, device=device, dtype=dtype)
+        return self.buf[o:o + n].view(dtype).view(shape)
+
+
+ARENA = ZeroArena()
+
+
+def zeros(*shape, device, dtype=torch.float32):
+    return ARENA.zeros(tuple(shape), dtype, device)
+
+
 def ilog2(v):
     r = int(math.log2(v))
     assert 1 << r == v, v
@@ -399,7 +444,7 @@ def router_bwd(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, 
     T, E_ = probs.shape
     k = topi.shape[1]
     g_raw = torch.empty(T, E_, device=probs.device, dtype=torch.float32)
-    gsum = torch.zeros(B, E_, device=probs.device, dtype=torch.float32)
+    gsum = zeros(B, E_, device=probs.device)
     call("mg_router_bwd", ptr(probs), ptr(zlog), ptr(topi), ptr(gate), ptr(g_gate), ptr(g_probs), ptr(coef), T, E_,
          k, HW, ptr(temperature), anneal, ptr(g_raw), ptr(gsum), ptr(g_temp), S())
     return g_raw, gsum

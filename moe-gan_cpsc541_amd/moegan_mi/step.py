@@ -98,6 +98,17 @@ class TrainStep:
         matters only when the D optimizer has not stepped yet in the window (acc > 1)."""
         c = self.cfg
         B = real.shape[0]
+        ops.ARENA.begin(self.dev)
+        try:
+            return self._step(real, text, z, eps_d, eps_g, perm, anneal, lr_g, lr_d, eff_kl_weight, prep, acc,
+                              zero_grads, step_optim)
+        finally:
+            ops.ARENA.end()
+
+    def _step(self, real, text, z, eps_d, eps_g, perm, anneal, lr_g, lr_d, eff_kl_weight, prep, acc, zero_grads,
+              step_optim):
+        c = self.cfg
+        B = real.shape[0]
         if prep:
             self.ge.prep()
             self.de.prep()
@@ -120,7 +131,7 @@ class TrainStep:
         g_gan, fake_pred, g_img = self.de.g_phase(img16, ("nhwc", 8), text, want_d_params=(acc > 1 and not step_optim))
         # balance loss on the last MoE layer, over the GLOBAL batch (t2i_moe_gan.py:951-1000)
         last = probs[-1]
-        load = torch.zeros(c.E, device=self.dev)
+        load = ops.zeros(c.E, device=self.dev)
         ops.colsum(last, load)
         self._allreduce_sum(load)
         bal = torch.zeros(1, device=self.dev)
