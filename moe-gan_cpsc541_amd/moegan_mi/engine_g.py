@@ -66,6 +66,11 @@ class GeneratorEngine:
     def G(self, n):
         return self.st.gview(n)
 
+    def _c(self, x, alpha=1.0):
+        """x in the compute dtype (the mapping / text / style GEMMs run on bf16 operands in bf16 mode, as the
+        reference's AMP autocast runs its Linear layers in half precision, t2i_moe_gan.py:1267)."""
+        return x if (x.dtype == self.cdt and alpha == 1.0) else ops.cast(x, self.cdt, alpha=alpha)
+
     # ------------------------------------------------------------------
     # per-step weight preparation (after every optimizer step)
     # ------------------------------------------------------------------
@@ -78,6 +83,7 @@ class GeneratorEngine:
             self.style_cols = cols
             self.style_n = nrows
             self.style_W = self.st.data[o0:o0 + nrows * K].view(nrows, K)
+            self.style_Wc = self._cbuf()[o0:o0 + nrows * K].view(nrows, K)
             self.style_b = self.st.data[b0:b0 + nrows]
             self.style_gW = self.st.grad[o0:o0 + nrows * K].view(nrows, K)
             self.style_gb = self.st.grad[b0:b0 + nrows]
@@ -536,7 +542,7 @@ class GeneratorEngine:
         hs = [zt]
         h = zt
         for i in (0, 2, 4):
-            h = ops.linear(h, self.P(f"mapping.{i}.weight"), bias=self.P(f"mapping.{i}.bias"), act=LRELU)
+            h = ops.linear(h, self.Pc(f"mapping.{i}.weight"), bias=self.P(f"mapping.{i}.bias"), act=LRELU)
             hs.append(h)
         return h, hs
 
@@ -549,30 +555,36 @@ class GeneratorEngine:
         if text.shape[0] != B and text.shape[0] == 1:
             text = text.expand(B, -1).contiguous()
         # text projection (:682-687, :790)
-        t0 = ops.linear(text, self.P("text_projection.0.weight"), bias=self.P("text_projection.0.bias"))
+        text_c = self._c(text)
+        t0 = ops.linear(text_c, self.Pc("text_projection.0.weight"), bias=self.P("text_projection.0.bias"),
+                        out_dtype=torch.float32)
         t1, tmu, trs = ops.layernorm_fwd(t0, self.P("text_projection.1.weight"), self.P("text_projection.1.bias"),
                                          act=1)
-        text_seq = ops.linear(t1, self.P("text_projection.3.weight"), bias=self.P("text_projection.3.bias"))
+        t1c = self._c(t1)
+        text_seq = ops.linear(t1c, self.Pc("text_projection.3.weight"), bias=self.P("text_projection.3.bias"),
+                              out_dtype=torch.float32)
         # mapping + truncation (:793-808)
-        zt = torch.empty(B, z.shape[1] + text.shape[1], device=dev)
+        zt = torch.empty(B, z.shape[1] + text.shape[1], device=dev, dtype=self.cdt)
         ops.copy2d(z, zt, B, z.shape[1], ldo=zt.shape[1])
         ops.copy2d(text, zt[:, z.shape[1]:], B, text.shape[1], ldo=zt.shape[1])
         h3, hs = self._mapping(zt, save)
         if psi < 1.0:
             if self._mean_latent is None:  # mapping(0): depends on the weights only -> once per prep()
-                zeros = torch.zeros(1, zt.shape[1], device=dev)
+                zeros = torch.zeros(1, zt.shape[1], device=dev, dtype=self.cdt)
                 m3, _ = self._mapping(zeros, False)
-                self._mean_latent = ops.linear(m3, self.P("mapping.6.weight"), bias=self.P("mapping.6.bias"))
+                self._mean_latent = ops.linear(m3, self.Pc("mapping.6.weight"), bias=self.P("mapping.6.bias"),
+                                               out_dtype=torch.float32)
             mean = self._mean_latent
             beff = torch.empty(512, device=dev)
             ops.copy2d(self.P("mapping.6.bias").view(1, -1), beff.view(1, -1), 1, 512, alpha=psi)
             ops.copy2d(mean, beff.view(1, -1), 1, 512, alpha=1.0 - psi, accumulate=1)
-            w = ops.linear(h3, self.P("mapping.6.weight"), bias=beff, alpha=psi)
+            w = ops.linear(h3, self.Pc("mapping.6.weight"), bias=beff, alpha=psi, out_dtype=torch.float32)
         else:
-            w = ops.linear(h3, self.P("mapping.6.weight"), bias=self.P("mapping.6.bias"))
+            w = ops.linear(h3, self.Pc("mapping.6.weight"), bias=self.P("mapping.6.bias"), out_dtype=torch.float32)
+        w_c = self._c(w)
         # every modulated conv's style in one GEMM: S = w @ [W_mod ...]^T + [b_mod ...] (:158)
         if self.style_cols:
-            self._S = ops.linear(w, self.style_W, bias=self.style_b)
+            self._S = ops.linear(w_c, self.style_Wc, bias=self.style_b, out_dtype=torch.float32)
             self._S2 = ops.cast(self._S, square=1)
             # and every demodulation d = rsqrt(s^2 @ wsq^T + 1e-8) in batched launches (:165)
             self._D, probs = {}, []
@@ -604,7 +616,8 @@ class GeneratorEngine:
         self._bv = None
         ctx = None
         if save:
-            ctx = dict(B=B, text=text, z=z, t0=t0, t1=t1, tmu=tmu, trs=trs, text_seq=text_seq, hs=hs, h3=h3, w=w,
+            ctx = dict(B=B, text=text, text_c=text_c, z=z, t0=t0, t1=t1, t1c=t1c, tmu=tmu, trs=trs, text_seq=text_seq,
+                       hs=hs, h3=h3, w=w, w_c=w_c,
                        psi=psi, blocks=blocks, rgbsv=rgbsv, rgb8sv=rgb8sv)
         return img16, img8, kl2s, probs, topis, ctx
 
@@ -663,37 +676,39 @@ class GeneratorEngine:
                 ops.wsq_bwd(self.P(pre + "weight"), q["out"][:Cout], self.G(pre + "weight"))
             self._demod_bwd = []
             GS, self._GS = self._GS, None
-            ops.linear_wgrad(GS, ctx["w"], self.style_gW)
+            GSc = self._c(GS)
+            ops.linear_wgrad(GSc, ctx["w_c"], self.style_gW)
             ops.colsum(GS, self.style_gb)
-            ops.gemm(GS, self.style_W, B, gw.shape[1], self.style_n, b_kc=False, out=gw, ep=E_(accumulate=1))
+            ops.gemm(GSc, self.style_Wc, B, gw.shape[1], self.style_n, b_kc=False, out=gw, ep=E_(accumulate=1))
         # truncation: w = mean + psi (w_full - mean), mean under no_grad
         psi = ctx["psi"]
-        g6 = ops.cast(gw, alpha=psi if psi < 1.0 else 1.0)
+        g6 = ops.cast(gw, self.cdt, alpha=psi if psi < 1.0 else 1.0)
         hs = ctx["hs"]
         ops.linear_wgrad(g6, hs[3], self.G("mapping.6.weight"))
         ops.colsum(g6, self.G("mapping.6.bias"))
-        g = ops.linear_dgrad(g6, self.P("mapping.6.weight"))
+        g = ops.linear_dgrad(g6, self.Pc("mapping.6.weight"))
         for j, i in enumerate((4, 2, 0)):
             ops.lrelu_mask_mul(g, hs[3 - j], g)
             ops.linear_wgrad(g, hs[2 - j], self.G(f"mapping.{i}.weight"))
             ops.colsum(g, self.G(f"mapping.{i}.bias"))
             if i != 0 or want_input_grads:
-                g = ops.linear_dgrad(g, self.P(f"mapping.{i}.weight"))
+                g = ops.linear_dgrad(g, self.Pc(f"mapping.{i}.weight"))
         g_zt = g if want_input_grads else None
         # text projection backward
-        ops.linear_wgrad(g_ts, ctx["t1"], self.G("text_projection.3.weight"))
+        g_tsc = self._c(g_ts)
+        ops.linear_wgrad(g_tsc, ctx["t1c"], self.G("text_projection.3.weight"))
         ops.colsum(g_ts, self.G("text_projection.3.bias"))
-        g_t1 = ops.linear_dgrad(g_ts, self.P("text_projection.3.weight"))
+        g_t1 = ops.linear_dgrad(g_tsc, self.Pc("text_projection.3.weight"), out_dtype=torch.float32)
         ops.lrelu_mask_mul(g_t1, ctx["t1"], g_t1)
         g_t0 = torch.empty_like(g_t1)
         ops.layernorm_bwd(g_t1, ctx["t0"], ctx["tmu"], ctx["trs"], self.P("text_projection.1.weight"), g_t0,
                           self.G("text_projection.1.weight"), self.G("text_projection.1.bias"))
-        ops.linear_wgrad(g_t0, ctx["text"], self.G("text_projection.0.weight"))
+        ops.linear_wgrad(self._c(g_t0), ctx["text_c"], self.G("text_projection.0.weight"))
         ops.colsum(g_t0, self.G("text_projection.0.bias"))
         if not want_input_grads:
             return None, None
         gtext = ops.linear_dgrad(g_t0, self.P("text_projection.0.weight"))
         zd = ctx["z"].shape[1]
-        gz = g_zt[:, :zd].contiguous()
-        gtext = gtext + g_zt[:, zd:]
+        gz = g_zt[:, :zd].float().contiguous()
+        gtext = gtext + g_zt[:, zd:].float()
         return gz, gtext
