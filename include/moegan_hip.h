@@ -323,6 +323,9 @@ int mg_opt_prologue(float* sumsq, int32_t* step, void* stream);
 
 /* mg_adamw with the step count read from device memory (*step >= 1); bias corrections on the device. */
 int mg_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, const int32_t* step, const float* sumsq, float max_norm, void* stream);
+/* Same update (t2i_moe_gan.py:1333-1421), 16-B vectors, and (shadow_bf16 != NULL) the bf16 compute copy of the
+   updated parameters written in the same pass (replaces the next step's fp32 -> bf16 parameter cast). */
+int mg_adamw_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, const int32_t* step, const float* sumsq, float max_norm, void* shadow_bf16, void* stream);
 
 /* generator constant [1,C,4,4] -> NHWC [B,4,4,C] (t2i_moe_gan.py:815). */
 int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, void* out, void* stream);

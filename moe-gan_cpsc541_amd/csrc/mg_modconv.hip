@@ -139,7 +139,9 @@ __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, in
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (live) ld8(s + (int64_t)b * ld_s + c, sc);
-  for (int p = ty; live && p < HW; p += TY) {
+  // pixels split over grid.z (more blocks in flight for few images x large maps)
+  const int ppz = (HW + gridDim.z - 1) / gridDim.z, p1 = min(HW, ((int)blockIdx.z + 1) * ppz);
+  for (int p = blockIdx.z * ppz + ty; live && p < p1; p += TY) {
     int64_t row = (int64_t)b * HW + p;
     ld8(gxt + row * ld_gxt + c, g);
     ld8(x + row * ld_x + c, xx);
@@ -160,8 +162,13 @@ __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, in
     for (int y = 1; y < TY; ++y)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += red[(y * TX + tx) * 8 + j];
+    if (gridDim.z > 1) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gs[(int64_t)b * ld_s + c + j] += acc[j];
+      for (int j = 0; j < 8; ++j) atomicAdd(&gs[(int64_t)b * ld_s + c + j], acc[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gs[(int64_t)b * ld_s + c + j] += acc[j];
+    }
   }
 }
 
@@ -336,7 +343,10 @@ extern "C" int mg_modconv_bwd_in(int gxt_dtype, const void* gxt, int64_t ld_gxt,
   bool vec = Cin % 8 == 0 && ld_gxt % 8 == 0 && ld_x % 8 == 0 && (!gx || ld_gx % 8 == 0) && ld_s % 4 == 0 &&
              mg_al16(gxt) && mg_al16(x) && mg_al16(s) && (!gx || mg_al16(gx)) && mg_al16(gs);
   int thr = blk.x;
-  if (vec) vshape(Cin, grid, blk, B);
+  if (vec) {
+    vshape(Cin, grid, blk, B);
+    grid.z = std::max(1, std::min(cdiv(HW, (int)blk.y * 4), cdiv(1024, (int)(grid.x * grid.y))));
+  }
 #define L_(TG, T, TO)                                                                                              \
   do {                                                                                                             \
     if (vec)                                                                                                       \

@@ -155,18 +155,29 @@ __global__ __launch_bounds__(256) void k_colsum_v(const T* __restrict__ X, int64
   }
 }
 
-// block (64 columns x 4 partial lanes); out[c] += sum_r part[r, c]
-__global__ __launch_bounds__(256) void k_colsum_fin(const float* __restrict__ part, int nparts, int C,
-                                                    float* __restrict__ out) {
-  __shared__ float red[4][64];
+// block (64 columns x 16 partial lanes, 1024 threads); out[c] += sum_r part[r, c]
+__global__ __launch_bounds__(1024) void k_colsum_fin(const float* __restrict__ part, int nparts, int C,
+                                                     float* __restrict__ out) {
+  __shared__ float red[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
-  float s = 0.f;
-  if (c < C)
-    for (int r = ty; r < nparts; r += 4) s += part[(int64_t)r * C + c];
-  red[ty][tx] = s;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    int r = ty;
+    for (; r + 16 < nparts; r += 32) {  // two independent loads in flight per lane
+      s0 += part[(int64_t)r * C + c];
+      s1 += part[(int64_t)(r + 16) * C + c];
+    }
+    if (r < nparts) s0 += part[(int64_t)r * C + c];
+  }
+  red[ty][tx] = s0 + s1;
   __syncthreads();
-  if (ty == 0 && c < C) out[c] += red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+  if (ty == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) t += red[y][tx];
+    out[c] += t;
+  }
 }
 
 // weight norm: W[o] = g[o] * v[o] / ||v[o]||  (t2i_moe_gan.py:869-886, torch weight_norm dim=0)
@@ -298,6 +309,64 @@ __global__ void k_adamw_dev(float* __restrict__ p, const float* __restrict__ g, 
     v[i] = vi;
     float denom = sqrtf(vi) / bc2_sqrt + eps;
     p[i] = pi - step_size * (mi / denom);
+  }
+}
+
+// AdamW + clip coefficient, 4 parameters per thread (16-B loads / stores), optionally also writing the
+// bf16 compute shadow of the updated parameters (the next step's per-step cast, fused away).
+__global__ __launch_bounds__(256) void k_adamw_dev_v(float* __restrict__ p, const float* __restrict__ g,
+                                                     float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                     float lr, float b1, float b2, float eps, float wd,
+                                                     const int32_t* __restrict__ step,
+                                                     const float* __restrict__ sumsq, float max_norm,
+                                                     bf16_t* __restrict__ shadow) {
+  const float t = (float)step[0];
+  const float bc1 = 1.f - powf(b1, t);
+  const float bc2_sqrt = sqrtf(1.f - powf(b2, t));
+  float coef = 1.f;
+  if (sumsq) {
+    float tn = sqrtf(sumsq[0]);
+    coef = fminf(max_norm / (tn + 1e-6f), 1.f);
+  }
+  const float step_size = lr / bc1;
+  auto upd = [&](float gi, float& pi, float& mi, float& vi) {
+    gi *= coef;
+    pi *= (1.f - lr * wd);
+    mi = mi + (gi - mi) * (1.f - b1);
+    vi = vi * b2 + (1.f - b2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+  };
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4_t pv = reinterpret_cast<const f32x4_t*>(p)[i], gv = reinterpret_cast<const f32x4_t*>(g)[i];
+    f32x4_t mv = reinterpret_cast<const f32x4_t*>(m)[i], vv = reinterpret_cast<const f32x4_t*>(v)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float pj = pv[j], mj = mv[j], vj = vv[j];
+      upd(gv[j], pj, mj, vj);
+      pv[j] = pj;
+      mv[j] = mj;
+      vv[j] = vj;
+    }
+    reinterpret_cast<f32x4_t*>(p)[i] = pv;
+    reinterpret_cast<f32x4_t*>(m)[i] = mv;
+    reinterpret_cast<f32x4_t*>(v)[i] = vv;
+    if (shadow) {
+      u16x4_t h;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[j] = f2bf(pv[j]);
+      reinterpret_cast<u16x4_t*>(shadow)[i] = h;
+    }
+  }
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    upd(g[i], pi, mi, vi);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+    if (shadow) shadow[i] = f2bf(pi);
   }
 }
 
@@ -434,7 +503,7 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     }
     DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum_v<T>, grid, dim3(tx, ty), 0, st, reinterpret_cast<const T*>(X), ld,
                                          R, C, rpb, part, 0));
-    hipLaunchKernelGGL(k_colsum_fin, dim3(cdiv(C, 64)), dim3(256), 0, st, part, rblk, C, out);
+    hipLaunchKernelGGL(k_colsum_fin, dim3(cdiv(C, 64)), dim3(1024), 0, st, part, rblk, C, out);
     return mg_check_launch("mg_colsum");
   }
   int rpb = std::max(16, R / 256);
@@ -492,6 +561,19 @@ extern "C" int mg_adamw_dev(float* p, const float* g, float* m, float* v, int64_
   hipLaunchKernelGGL(k_adamw_dev, dim3(std::min(nblk(n), 4096)), dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2,
                      eps, weight_decay, step, sumsq, max_norm);
   return mg_check_launch("mg_adamw_dev");
+}
+
+extern "C" int mg_adamw_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                                   float beta2, float eps, float weight_decay, const int32_t* step,
+                                   const float* sumsq, float max_norm, void* shadow_bf16, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) return MG_OK;
+  MG_REQUIRE(mg_al16(p) && mg_al16(g) && mg_al16(m) && mg_al16(v) &&
+             (!shadow_bf16 || (reinterpret_cast<uintptr_t>(shadow_bf16) & 7) == 0), "16-B aligned p/g/m/v, 8-B shadow");
+  hipLaunchKernelGGL(k_adamw_dev_v, dim3(std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4 + 1, 256), 4096))),
+                     dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, sumsq, max_norm,
+                     reinterpret_cast<bf16_t*>(shadow_bf16));
+  return mg_check_launch("mg_adamw_dev_shadow");
 }
 
 extern "C" int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, void* out, void* stream) {

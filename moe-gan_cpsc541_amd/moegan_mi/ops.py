@@ -304,9 +304,11 @@ def opt_prologue(sumsq_buf, step_dev):
     call("mg_opt_prologue", ptr(sumsq_buf), ptr(step_dev), S())
 
 
-def adamw_dev(p, g, m, v, lr, beta1, beta2, eps, wd, step_dev, sumsq_buf=None, max_norm=0.0):
-    call("mg_adamw_dev", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps, wd, ptr(step_dev),
-         ptr(sumsq_buf), max_norm, S())
+def adamw_dev(p, g, m, v, lr, beta1, beta2, eps, wd, step_dev, sumsq_buf=None, max_norm=0.0, shadow=None):
+    """AdamW with the device step counter and clip coefficient; ``shadow`` (bf16, same length) also receives the
+    updated parameters (mg_adamw_dev_shadow)."""
+    call("mg_adamw_dev_shadow", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps, wd, ptr(step_dev),
+         ptr(sumsq_buf), max_norm, ptr(shadow), S())
 
 
 def const_fwd(cst, B, dtype):

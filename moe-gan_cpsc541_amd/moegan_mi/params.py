@@ -131,7 +131,7 @@ class ParamStore:
             if self.shadow is not None:
                 self.shadow = torch.zeros(self.total, device=dev, dtype=self.shadow_dtype)
         self.device = dev
-        self.refresh_shadow()
+        self.refresh_shadow(force=True)
 
     # ---- views ----
     def _v(self, buf, name):
@@ -156,9 +156,19 @@ class ParamStore:
         return buf[a:b + n]
 
     # ---- per-step ----
-    def refresh_shadow(self):
+    def refresh_shadow(self, force=False):
         if self.shadow is not None and self.data.is_cuda:
+            fresh = getattr(self, "_shadow_version", None) == self.data._version
+            self._shadow_version = None
+            if fresh and not force:  # the optimizer wrote the shadow with the parameters (mg_adamw_dev_shadow)
+                return
             ops.cast(self.data, out=self.shadow)
+
+    def mark_shadow_written(self):
+        """Called after an optimizer step that also wrote the bf16 shadow of every optimised parameter.  Any
+        torch-level write to the fp32 buffer afterwards (load_state_dict, copy_) bumps its version counter and
+        makes the next refresh_shadow() cast again."""
+        self._shadow_version = self.data._version
 
     def zero_grad(self):
         self.grad.zero_()
@@ -182,4 +192,4 @@ class ParamStore:
                     continue
                 dst = self.buffers[n] if is_buffer(n) else self.view(n)
                 dst.copy_(torch.as_tensor(t).reshape(dst.shape).to(dst.device, torch.float32))
-        self.refresh_shadow()
+        self.refresh_shadow(force=True)

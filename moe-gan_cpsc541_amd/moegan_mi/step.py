@@ -82,8 +82,11 @@ class TrainStep:
         ops.opt_prologue(ss, store.step_dev)  # ss = 0, device step counter += 1 (graph-replayable)
         ops.sumsq(store.grad[:n], ss)
         c = self.cfg
+        shadow = store.shadow[:n] if (store.shadow is not None and store.shadow.dtype == torch.bfloat16) else None
         ops.adamw_dev(store.data[:n], store.grad[:n], store.m[:n], store.v[:n], lr, c.beta1, c.beta2, c.eps,
-                      c.weight_decay, store.step_dev, ss, max_norm)
+                      c.weight_decay, store.step_dev, ss, max_norm, shadow=shadow)
+        if shadow is not None:
+            store.mark_shadow_written()
         return ss
 
     # ---- the step ----
