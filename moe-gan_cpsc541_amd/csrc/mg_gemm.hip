@@ -329,6 +329,17 @@ void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpa
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int64_t M = (int64_t)B * OH * OW;
   const int tile = g_mg_tune[MG_TUNE_CONV_TILE];
+  if constexpr (sizeof(T) == 2) {
+    // 8-fragment-row wave tiles (128 x 64 / 64 x 128 per wave): 25 % fewer LDS bytes per MFMA
+    if (tile == 256) {
+      run_conv<T, TO, 256, 128>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+      return;
+    }
+    if (tile == 257) {
+      run_conv<T, TO, 128, 256>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+      return;
+    }
+  }
   if (tile == 128 || (tile == 0 && cdiv(M, 128) * (int64_t)cdiv(Cout, 128) >= 480 && Cout > 64))
     run_conv<T, TO, 128, 128>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
   else

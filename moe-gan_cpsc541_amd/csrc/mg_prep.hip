@@ -257,6 +257,20 @@ __global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restric
   }
 }
 
+// One AdamW element update (torch.optim.AdamW single-tensor math, t2i_moe_gan.py:1101-1102), with every
+// multiply-add spelled out: all three AdamW kernels run the identical instruction sequence (bit-exact to
+// each other whatever the surrounding code lets the compiler contract).
+MG_DEV void adamw_elem(float gi, float& pi, float& mi, float& vi, float coef, float lr, float b1, float b2,
+                       float eps, float wd, float step_size, float bc2_sqrt) {
+#pragma clang fp contract(off)
+  gi = gi * coef;
+  pi = pi * (1.f - lr * wd);
+  mi = mi + (gi - mi) * (1.f - b1);
+  vi = vi * b2 + (1.f - b2) * gi * gi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  pi = pi - step_size * (mi / denom);
+}
+
 // torch.optim.AdamW (single-tensor semantics, t2i_moe_gan.py:1101-1102) fused with
 // clip_grad_norm_ (t2i_moe_gan.py:1333-1337 / :1417-1421): coef = min(1, max_norm / (||g|| + 1e-6)).
 __global__ void k_adamw(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
@@ -269,14 +283,11 @@ __global__ void k_adamw(float* __restrict__ p, const float* __restrict__ g, floa
   }
   float step_size = lr / bc1;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float gi = g[i] * coef;
-    float pi = p[i] * (1.f - lr * wd);
-    float mi = m[i] + (gi - m[i]) * (1.f - b1);
-    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(g[i], pi, mi, vi, coef, lr, b1, b2, eps, wd, step_size, bc2_sqrt);
     m[i] = mi;
     v[i] = vi;
-    float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = pi - step_size * (mi / denom);
+    p[i] = pi;
   }
 }
 
@@ -301,14 +312,11 @@ __global__ void k_adamw_dev(float* __restrict__ p, const float* __restrict__ g, 
   }
   float step_size = lr / bc1;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float gi = g[i] * coef;
-    float pi = p[i] * (1.f - lr * wd);
-    float mi = m[i] + (gi - m[i]) * (1.f - b1);
-    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(g[i], pi, mi, vi, coef, lr, b1, b2, eps, wd, step_size, bc2_sqrt);
     m[i] = mi;
     v[i] = vi;
-    float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = pi - step_size * (mi / denom);
+    p[i] = pi;
   }
 }
 
@@ -330,12 +338,7 @@ __global__ __launch_bounds__(256) void k_adamw_dev_v(float* __restrict__ p, cons
   }
   const float step_size = lr / bc1;
   auto upd = [&](float gi, float& pi, float& mi, float& vi) {
-    gi *= coef;
-    pi *= (1.f - lr * wd);
-    mi = mi + (gi - mi) * (1.f - b1);
-    vi = vi * b2 + (1.f - b2) * gi * gi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    pi = pi - step_size * (mi / denom);
+    adamw_elem(gi, pi, mi, vi, coef, lr, b1, b2, eps, wd, step_size, bc2_sqrt);
   };
   const int64_t n4 = n >> 2;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {

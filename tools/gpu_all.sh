@@ -3,7 +3,7 @@
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 B=${B:-256}
-timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 400 python bench.py --steps 5 --warmup 2 --batch $B --no-cpu-baseline 2>&1 | tee gpurun_out/bench_quick.log || exit 1
