@@ -104,6 +104,14 @@ void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int
     return;
   }
   const int tile = g_mg_tune[MG_TUNE_GEMM_TILE];
+  if constexpr (sizeof(T) == 2) {
+    // 128 x 256 when N fills it and the grid covers the chip (measured: 4096^3 bf16 816 -> 920 TF/s;
+    // the step's few-tile projections stay on 128^2 / 64^2)
+    if (tile == 257 || (tile == 0 && N % 256 == 0 && (int64_t)cdiv(M, 128) * (N / 256) * splits >= 480)) {
+      run_plain_orient<T, TO, 128, 256>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+      return;
+    }
+  }
   if (tile == 128 || (tile == 0 && (int64_t)cdiv(M, 128) * cdiv(N, 128) * splits >= 480))
     run_plain_orient<T, TO, 128, 128>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
   else
@@ -321,6 +329,21 @@ void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpa
   if (small_c ? conv_slabs<T, TO, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st)
               : conv_slabs<T, TO, false>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st))
     return;
+  const int tile = g_mg_tune[MG_TUNE_CONV_TILE];
+  if constexpr (sizeof(T) == 2) {
+    // modulation-scaled loads on 128^2 tiles when the grid still covers the chip (measured at B=256: the
+    // 16x16 modulated 3x3 conv, 128 -> 128 channels, 58 -> 47 us; the 8x8 one stays on 64^2)
+    if (sc && !small_c && (tile == 128 || (tile == 0 && cdiv(B * ((H + 2 * pad - KH) / stride + 1) *
+                                                                  ((W + 2 * pad - KW) / stride + 1), 128) *
+                                                             (int64_t)cdiv(Cout, 128) >= 480))) {
+      run_conv<T, TO, 128, 128, true, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+      return;
+    }
+    if (sc && !small_c && tile == 257) {
+      run_conv<T, TO, 128, 256, true, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+      return;
+    }
+  }
   if (sc || small_c) {  // modulation scale on load / small Cin: generic 64x64 instantiations
     if (sc) run_conv<T, TO, 64, 64, true, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
     else run_conv<T, TO, 64, 64, false, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
@@ -328,15 +351,16 @@ void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpa
   }
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int64_t M = (int64_t)B * OH * OW;
-  const int tile = g_mg_tune[MG_TUNE_CONV_TILE];
   if constexpr (sizeof(T) == 2) {
-    // 8-fragment-row wave tiles (128 x 64 / 64 x 128 per wave): 25 % fewer LDS bytes per MFMA
-    if (tile == 256) {
-      run_conv<T, TO, 256, 128>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+    // 8-fragment wave tiles (128 x 64 / 64 x 128 per wave): 25 % fewer LDS bytes per MFMA.  128 x 256 by
+    // default when Cout fills it and the grid still covers the chip (measured at B=256: the
+    // discriminator's 4x4/s2 conv, N = 256, 100 -> 92 us; one column tile also reads the input once)
+    if (tile == 257 || (tile == 0 && Cout % 256 == 0 && cdiv(M, 128) * (int64_t)(Cout / 256) >= 256)) {
+      run_conv<T, TO, 128, 256>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
       return;
     }
-    if (tile == 257) {
-      run_conv<T, TO, 128, 256>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+    if (tile == 256) {
+      run_conv<T, TO, 256, 128>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
       return;
     }
   }
@@ -471,6 +495,17 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
                                                                                       : P / 2048));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_BF16 && slabs && in_scale && tile == 128 && Cout >= 128 && N >= 128 &&
+      run_wgrad_slabs<bf16_t, 128, 128, true>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw,
+                                               splits, st))
+    return mg_check_launch("mg_conv2d_wgrad (scaled, 128)");
+  if (dtype == MG_BF16 && slabs && !in_scale && (tile == 256 || tile == 257)) {
+    bool ok = tile == 256 ? run_wgrad_slabs<bf16_t, 256, 128>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride,
+                                                              pad, gw, splits, st)
+                          : run_wgrad_slabs<bf16_t, 128, 256>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride,
+                                                              pad, gw, splits, st);
+    if (ok) return mg_check_launch("mg_conv2d_wgrad (slabs, wide)");
+  }
   if (in_scale) {  // modulation scale on load: generic 64x64 instantiation (slabs, atomics if no workspace)
     bool ok = dtype == MG_BF16 ? run_wgrad_slabs<bf16_t, 64, 64, true>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW,
                                                                        stride, pad, gw, splits, st)
@@ -513,6 +548,19 @@ void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_o
   LdKC<T, XF> la{reinterpret_cast<const T*>(A), lda, total_rows, K, aidx, adiv, e ? e->a_rowscale : nullptr,
                  e ? e->a_gelu : 0};
   Grouping grp{1, ngroups, row_off, tile_off, 0};
+  if constexpr (sizeof(T) == 2) {
+    // 128 x 256 tiles (same 128-row tile prefix, half the column tiles)
+    if (g_mg_tune[MG_TUNE_GEMM_TILE] == 257 && N >= 256) {
+      if constexpr (BKc) {
+        LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
+        launch_gemm<T, 128, 256, true, true>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+      } else {
+        LdMCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
+        launch_gemm<T, 128, 256, true, false>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+      }
+      return;
+    }
+  }
   if constexpr (BKc) {
     LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
     launch_gemm<T, 128, 128, true, true>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);

@@ -151,3 +151,54 @@ def test_gemm_batch_matches_individual(dtype, tol, a_kc, b_kc):
     torch.cuda.synchronize()
     for q, r in zip(probs, refs):
         assert rel(q["out"], r) < tol, (q["M"], q["N"], q["K"])
+
+
+# tuning slots (mg_common.h): 0 = conv weight-gradient tile, 2 = conv forward tile, 3 = plain GEMM tile
+@pytest.mark.parametrize("tile", [128, 256, 257])
+@pytest.mark.parametrize("B,H,Cin,Cout,k,stride,pad", [(3, 8, 64, 96, 3, 1, 1), (4, 32, 128, 256, 4, 2, 1),
+                                                       (2, 8, 256, 512, 3, 1, 1)])
+@pytest.mark.parametrize("scaled", [False, True])
+def test_conv_wide_tiles_bf16(tile, B, H, Cin, Cout, k, stride, pad, scaled):
+    """Forced 128x128 / 256x128 / 128x256 tiles (ragged M / N tails included) vs fp32 PyTorch."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(B, Cin, H, H, device=DEV, generator=g)
+    w = torch.randn(Cout, Cin, k, k, device=DEV, generator=g) / (Cin * k * k) ** 0.5
+    s = torch.rand(B, Cin, device=DEV, generator=g) + 0.5 if scaled else None
+    xs = x * s[:, :, None, None] if scaled else x
+    xn = x.permute(0, 2, 3, 1).contiguous().bfloat16()
+    wp = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().bfloat16()
+    ref = F.conv2d(xs, w, stride=stride, padding=pad)
+    gy = torch.randn_like(ref)
+    xr = xs.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    (F.conv2d(xr, wr, stride=stride, padding=pad) * gy).sum().backward()
+    try:
+        L.call("mg_set_tuning", 0, tile)
+        L.call("mg_set_tuning", 2, tile)
+        y = ops.conv2d(xn, wp, Cout, k, k, stride, pad, in_scale=s, out_dtype=torch.float32)
+        gw = torch.zeros_like(w)
+        ops.conv2d_wgrad(gy.permute(0, 2, 3, 1).contiguous().bfloat16(), xn, Cout, k, k, stride, pad, gw, in_scale=s)
+        torch.cuda.synchronize()
+    finally:
+        L.call("mg_set_tuning", 0, 0)
+        L.call("mg_set_tuning", 2, 0)
+    assert rel(y.permute(0, 3, 1, 2), ref) < 2e-2
+    assert rel(gw, wr.grad) < 4e-2
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("M,N,K", [(1000, 520, 264), (512, 256, 64)])
+def test_gemm_wide_tile_bf16(a_kc, b_kc, M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(6)
+    A = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    Bm = torch.randn(N, K, device=DEV, generator=g).bfloat16()
+    ref = A.float() @ Bm.float().T
+    Aa = A if a_kc else A.T.contiguous()
+    Bb = Bm if b_kc else Bm.T.contiguous()
+    try:
+        L.call("mg_set_tuning", 3, 257)
+        C = ops.gemm(Aa, Bb, M, N, K, a_kc=a_kc, b_kc=b_kc, out_dtype=torch.float32)
+        torch.cuda.synchronize()
+    finally:
+        L.call("mg_set_tuning", 3, 0)
+    assert rel(C, ref) < 1e-2
