@@ -37,6 +37,10 @@ constexpr int NTHREADS = 256;
 #define MG_NSTAGE 1
 #endif
 // LDS-DMA (buffer_load ... lds) staging for bf16 KC x KC tiles
+// epilogue staging synchronised per block (1) or per wave (0: each wave owns its staging band)
+#ifndef MG_EPI_BLOCK_SYNC
+#define MG_EPI_BLOCK_SYNC 0
+#endif
 #ifndef MG_GLDS
 #define MG_GLDS 0  // measured: on par with register staging at C2 (gemm 4096^3 +9%, expert GEMMs -20%)
 #endif
@@ -782,14 +786,19 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   // Static indexing keeps acc in registers; the loop keeps the inlined epilogue code small.
   constexpr int CSP = WN + 4;  // staging pitch in floats (16-B aligned rows)
   float* cs = reinterpret_cast<float*>(smem) + wid * 16 * CSP;
+  // each wave stages through its own LDS band: one block barrier retires the K loop's reads of the
+  // tiles, after that a wave only orders its own LDS writes and reads (wave-scope fence)
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    __syncthreads();
+    if (MG_EPI_BLOCK_SYNC) __syncthreads();
+    else { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) cs[(fq * 4 + r) * CSP + j * 16 + fr] = acc[i][j][r];
-    __syncthreads();
+    if (MG_EPI_BLOCK_SYNC) __syncthreads();
+    else { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
     const int mb = m0 + wm * WM + i * 16, nb = n0 + wn * WN;
     if (ep.vec_ok) {
       // 8 consecutive columns per lane: vector loads of the epilogue operands, one 16-B store (bf16)
