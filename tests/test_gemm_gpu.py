@@ -87,9 +87,10 @@ def test_conv_fwd_wgrad(dtype, tol, B, H, Cin, Cout, k, stride, pad):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
-def test_grouped_gemm_and_wgrad(dtype, tol):
+@pytest.mark.parametrize("C", [64, 96, 128, 192])  # one / two K steps take the short-reduction path
+def test_grouped_gemm_and_wgrad(dtype, tol, C):
     g = torch.Generator(device=DEV).manual_seed(3)
-    E, C, H4 = 4, 64, 256
+    E, H4 = 4, 256
     counts = [37, 0, 300, 129]
     rows = sum(counts)
     row_off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=DEV)
