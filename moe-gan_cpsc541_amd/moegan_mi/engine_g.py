@@ -546,10 +546,11 @@ class GeneratorEngine:
             hs.append(h)
         return h, hs
 
-    def forward(self, z, text, eps, anneal=1.0, psi=0.7, train=True, save=True, want_img8=False, want_kl=True):
-        """Returns (img16 [B,16,16,8] padded NHWC, img8 or None, kl2 list, probs list, ctx).
-        ``want_kl=False`` skips the routers' KL terms (their kl2 entries are None)."""
-        self._want_kl = want_kl
+    def _prefix_fwd(self, z, text, psi, save):
+        """The part of the forward that does not depend on the router samples: text projection, mapping,
+        truncation, every style / demodulation, the constant and gen_block_4's convolution block.  Given the
+        same z, text and weights it is identical in the D-phase and G-phase forwards of one step
+        (t2i_moe_gan.py:1288-1296 and :1351-1357 feed the same z; G is not updated in between)."""
         B = z.shape[0]
         dev = self.dev
         if text.shape[0] != B and text.shape[0] == 1:
@@ -583,26 +584,54 @@ class GeneratorEngine:
             w = ops.linear(h3, self.Pc("mapping.6.weight"), bias=self.P("mapping.6.bias"), out_dtype=torch.float32)
         w_c = self._c(w)
         # every modulated conv's style in one GEMM: S = w @ [W_mod ...]^T + [b_mod ...] (:158)
+        S = S2 = D = None
         if self.style_cols:
-            self._S = ops.linear(w_c, self.style_Wc, bias=self.style_b, out_dtype=torch.float32)
-            self._S2 = ops.cast(self._S, square=1)
+            S = ops.linear(w_c, self.style_Wc, bias=self.style_b, out_dtype=torch.float32)
+            S2 = ops.cast(S, square=1)
             # and every demodulation d = rsqrt(s^2 @ wsq^T + 1e-8) in batched launches (:165)
-            self._D, probs = {}, []
+            D, probs = {}, []
             for pre, c in self.style_cols.items():
                 pk = self.packs[pre]
                 rows, Cin = pk["rows"], self.P(pre + "weight").shape[1]
                 d = torch.empty(B, rows, device=dev)
-                self._D[pre] = d
-                probs.append(dict(A=self._S2[:, c:c + Cin], B=pk["wsq"], M=B, N=rows, K=Cin, out=d, ep=E_(act=RSQRT)))
+                D[pre] = d
+                probs.append(dict(A=S2[:, c:c + Cin], B=pk["wsq"], M=B, N=rows, K=Cin, out=d, ep=E_(act=RSQRT)))
             ops.gemm_batch(probs)
-        self._bv = self._block_vectors(w, text_seq, eps, train)
+        self._S, self._S2, self._D = S, S2, D
         x = ops.const_fwd(self.P("constant"), B, self.cdt)
+        name0, _, _, _, up0 = GEN_BLOCKS[0]
+        assert not up0
+        x0, cbsv0 = self.cb_fwd(name0 + ".conv_block.", x, w, save=save)
+        return dict(B=B, text=text, text_c=text_c, t0=t0, t1=t1, t1c=t1c, tmu=tmu, trs=trs, text_seq=text_seq,
+                    hs=hs, h3=h3, w=w, w_c=w_c, psi=psi, S=S, S2=S2, D=D, x0=x0, cbsv0=cbsv0, save=save)
+
+    def forward(self, z, text, eps, anneal=1.0, psi=0.7, train=True, save=True, want_img8=False, want_kl=True,
+                keep_prefix=False, prefix=None):
+        """Returns (img16 [B,16,16,8] padded NHWC, img8 or None, kl2 list, probs list, ctx).
+        ``want_kl=False`` skips the routers' KL terms (their kl2 entries are None).
+        ``keep_prefix=True`` computes the router-independent prefix (``_prefix_fwd``) with its saved
+        activations and returns it as ``self.last_prefix``; ``prefix=`` reuses such a prefix (same z, text,
+        psi and weights) instead of recomputing it."""
+        self._want_kl = want_kl
+        if prefix is None:
+            prefix = self._prefix_fwd(z, text, psi, save or keep_prefix)
+        else:
+            assert prefix["B"] == z.shape[0] and prefix["psi"] == psi and (prefix["save"] or not save)
+            self._S, self._S2, self._D = prefix["S"], prefix["S2"], prefix["D"]
+        self.last_prefix = prefix if keep_prefix else None
+        B = prefix["B"]
+        w, text_seq = prefix["w"], prefix["text_seq"]
+        self._bv = self._block_vectors(w, text_seq, eps, train)
         probs, kl2s, topis, blocks = [], [], [], []
         img8, rgb8sv = None, None
+        x = None
         for i, (name, cin, cout, res, up) in enumerate(GEN_BLOCKS):
-            if up:
-                x = ops.upsample2x(x)
-            x, cbsv = self.cb_fwd(name + ".conv_block.", x, w, save=save)
+            if i == 0:
+                x, cbsv = prefix["x0"], (prefix["cbsv0"] if save else None)
+            else:
+                if up:
+                    x = ops.upsample2x(x)
+                x, cbsv = self.cb_fwd(name + ".conv_block.", x, w, save=save)
             x, p, kl2, topi, asv = self.attn_fwd(name + ".attn_block.", x, w, text_seq,
                                                  None if eps is None else eps[i], anneal, train, save)
             probs.append(p)
@@ -616,9 +645,9 @@ class GeneratorEngine:
         self._bv = None
         ctx = None
         if save:
-            ctx = dict(B=B, text=text, text_c=text_c, z=z, t0=t0, t1=t1, t1c=t1c, tmu=tmu, trs=trs, text_seq=text_seq,
-                       hs=hs, h3=h3, w=w, w_c=w_c,
-                       psi=psi, blocks=blocks, rgbsv=rgbsv, rgb8sv=rgb8sv)
+            ctx = {k: prefix[k] for k in ("B", "text", "text_c", "t0", "t1", "t1c", "tmu", "trs", "text_seq", "hs",
+                                          "h3", "w", "w_c", "psi")}
+            ctx.update(z=z, blocks=blocks, rgbsv=rgbsv, rgb8sv=rgb8sv)
         return img16, img8, kl2s, probs, topis, ctx
 
     def backward(self, ctx, g_img16, coef=None, kl_coef=None, want_input_grads=False, g_probs=None, g_img8=None):

@@ -118,7 +118,11 @@ class TrainStep:
         # ------------------------- D phase -------------------------
         if zero_grads:
             self.ds.zero_grad()
-        f16, _, _, _, _, _ = self.ge.forward(z, text, eps_d, anneal, c.psi, train=True, save=False, want_kl=False)
+        # the router-independent prefix of this forward (mapping, styles, gen_block_4's convolution block) is
+        # kept with its saved activations and reused by the G-phase forward: same z / text, G not yet updated
+        f16, _, _, _, _, _ = self.ge.forward(z, text, eps_d, anneal, c.psi, train=True, save=False, want_kl=False,
+                                             keep_prefix=True)
+        prefix, self.ge.last_prefix = self.ge.last_prefix, None
         dres = self.de.d_phase(real, text, f16, ("nhwc", 8), perm, c.r1_gamma)
         d_sumsq = None
         if step_optim:
@@ -130,7 +134,8 @@ class TrainStep:
             self.gs.zero_grad()
         want8 = self.clip_encoder is not None
         img16, img8, kl2s, probs, _, ctx = self.ge.forward(z, text, eps_g, anneal, c.psi, train=True, save=True,
-                                                           want_img8=want8)
+                                                           want_img8=want8, prefix=prefix)
+        prefix = None
         g_gan, fake_pred, g_img = self.de.g_phase(img16, ("nhwc", 8), text, want_d_params=(acc > 1 and not step_optim))
         # balance loss on the last MoE layer, over the GLOBAL batch (t2i_moe_gan.py:951-1000)
         last = probs[-1]

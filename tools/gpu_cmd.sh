@@ -1,3 +1,5 @@
 mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit 1
-bash tools/gpu_ab.sh wave blk wave blk
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1 || exit 1
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline 2>&1 | tail -1
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline 2>&1 | tail -1
