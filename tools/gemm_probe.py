@@ -47,6 +47,14 @@ def main():
     s8 = rn(B, 256) + 1
     w8 = ops.pack_conv(rn(256, 256, 3, 3, sc=0.02), bf)
     cases.append(("modconv8_fwd", 2.0 * B * 64 * 256 * 2304, lambda: ops.conv2d(x8, w8, 256, 3, 3, 1, 1, in_scale=s8)))
+    # plain (prescaled-input) 3x3 convs at 8x8 and 4x4
+    x8p = rn(B, 8, 8, 256, dt=bf)
+    cases.append(("conv8_fwd", 2.0 * B * 64 * 256 * 2304, lambda: ops.conv2d(x8p, w8, 256, 3, 3, 1, 1)))
+    x4p = rn(B, 4, 4, 512, dt=bf)
+    w4 = ops.pack_conv(rn(512, 512, 3, 3, sc=0.02), bf)
+    cases.append(("conv4_fwd", 2.0 * B * 16 * 512 * 4608, lambda: ops.conv2d(x4p, w4, 512, 3, 3, 1, 1)))
+    x16p = rn(B, 16, 16, 128, dt=bf)
+    cases.append(("conv16_fwd", 2.0 * B * 256 * 128 * 1152, lambda: ops.conv2d(x16p, w16, 128, 3, 3, 1, 1)))
     # weight gradients
     gy16 = rn(B * 256, 128, dt=bf)
     gw16 = torch.zeros(128, 128, 3, 3, device=dev)
