@@ -444,11 +444,11 @@ struct Epi {
       for (int j = 0; j < 8; ++j) v[j] = lrelu(v[j]);
     } else if (act == ACT_GELU) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+      for (int j = 0; j < 8; ++j) v[j] = sizeof(TO) == 2 ? gelu_fast(v[j]) : gelu_erf(v[j]);
     } else if (act == ACT_MUL_GELU_GRAD) {
       ld8(aux + (int64_t)m * ld_aux + n, t);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= gelu_erf_grad(t[j]);
+      for (int j = 0; j < 8; ++j) v[j] *= sizeof(TO) == 2 ? gelu_fast_grad(t[j]) : gelu_erf_grad(t[j]);
     } else if (act == ACT_MUL_LRELU_GRAD) {
       ld8(aux + (int64_t)m * ld_aux + n, t);
 #pragma unroll
@@ -487,8 +487,11 @@ struct Epi {
     if (bias) v += bias[(int64_t)g * gstride_bias + n];
     if (Cpre) stf(Cpre, (int64_t)m * ldc_pre + n, v);
     if (act == ACT_LRELU) v = lrelu(v);
-    else if (act == ACT_GELU) v = gelu_erf(v);
-    else if (act == ACT_MUL_GELU_GRAD) v *= gelu_erf_grad(ldf(aux, (int64_t)m * ld_aux + n));
+    else if (act == ACT_GELU) v = sizeof(TO) == 2 ? gelu_fast(v) : gelu_erf(v);
+    else if (act == ACT_MUL_GELU_GRAD) {
+      const float x = ldf(aux, (int64_t)m * ld_aux + n);
+      v *= sizeof(TO) == 2 ? gelu_fast_grad(x) : gelu_erf_grad(x);
+    }
     else if (act == ACT_MUL_LRELU_GRAD) v *= lrelu_grad(ldf(aux, (int64_t)m * ld_aux + n));
     else if (act == ACT_RSQRT_EPS) v = rsqrtf(v + 1e-8f);
     if (rowscale) v *= rowscale[m];

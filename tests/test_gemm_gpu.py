@@ -203,3 +203,28 @@ def test_gemm_wide_tile_bf16(a_kc, b_kc, M, N, K):
     finally:
         L.call("mg_set_tuning", 3, 0)
     assert rel(C, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 128), (4096, 512, 128)])
+def test_bf16_gelu_epilogues(M, N, K):
+    """bf16 GELU / GELU' epilogues (polynomial erf, |err| <= 1.5e-7) vs exact fp32 on the same bf16 operands:
+    the only difference left is the bf16 rounding of the result."""
+    g = torch.Generator(device=DEV).manual_seed(7)
+    A = (torch.randn(M, K, device=DEV, generator=g) * 0.5).bfloat16()
+    W = (torch.randn(N, K, device=DEV, generator=g) / 8).bfloat16()
+    b = torch.randn(N, device=DEV, generator=g)
+    pre_ref = A.float() @ W.float().T + b
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y = ops.gemm(A, W, M, N, K, out_dtype=torch.bfloat16, ep=L.epilogue(bias=b, act=L.ACT_GELU, out_pre=pre, ld_pre=N))
+    torch.cuda.synchronize()
+    ref = F.gelu(pre_ref)
+    assert ((y.float() - ref).abs() <= 1e-2 * ref.abs() + 2e-3).all()
+    # GELU' times an upstream gradient, with the bf16 pre-activation as aux
+    x = pre
+    xg = x.float()
+    cdf = 0.5 * (1 + torch.erf(xg / 2 ** 0.5))
+    dref = cdf + xg * torch.exp(-0.5 * xg * xg) / (2 * torch.pi) ** 0.5
+    gy = ops.gemm(A, W, M, N, K, out_dtype=torch.bfloat16, ep=L.epilogue(act=L.ACT_MUL_GELU_GRAD, aux=x, ld_aux=N))
+    torch.cuda.synchronize()
+    gref = (A.float() @ W.float().T) * dref
+    assert ((gy.float() - gref).abs() <= 1e-2 * gref.abs() + 2e-3).all()
