@@ -659,6 +659,8 @@ void run_dgrad_s2(const void* g, int B, int OH, int OW, int Cg, const void* wcls
   Grouping grp{3, 4, nullptr, nullptr, Mc};
   if (Cin >= 128 && !SC)
     launch_gemm<T, 128, 128, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);
+  else if (sizeof(T) == 2 && Cin <= 32 && !SC)  // image gradient (Cin = 3): 128 x 32 tiles waste 8x, not 16x, MFMA work
+    launch_gemm<T, 128, 32, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);
   else
     launch_gemm<T, 64, 64, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);
 }

@@ -228,3 +228,22 @@ def test_bf16_gelu_epilogues(M, N, K):
     torch.cuda.synchronize()
     gref = (A.float() @ W.float().T) * dref
     assert ((gy.float() - gref).abs() <= 1e-2 * gref.abs() + 2e-3).all()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("Cin,Cg,OH", [(3, 128, 32), (128, 256, 16), (16, 64, 8)])
+def test_dgrad_s2(dtype, tol, Cin, Cg, OH):
+    """4x4 / stride-2 / pad-1 conv data gradient (parity-class split) vs torch's conv autograd, incl. the
+    128 x 32 tiles of the image gradient (Cin = 3, output channel-padded to 4)."""
+    g = torch.Generator(device=DEV).manual_seed(8)
+    B = 4
+    W = torch.randn(Cg, Cin, 4, 4, device=DEV, generator=g) / (Cin * 16) ** 0.5
+    gy = torch.randn(B, Cg, OH, OH, device=DEV, generator=g)
+    x = torch.zeros(B, Cin, 2 * OH, 2 * OH, device=DEV, requires_grad=True)
+    (F.conv2d(x, W, stride=2, padding=1) * gy).sum().backward()
+    ld = (Cin + 3) // 4 * 4 if Cin < 8 else Cin
+    out = torch.zeros(B, 2 * OH, 2 * OH, ld, device=DEV)
+    wcls = ops.pack_dgrad_s2(W, dtype, rows=Cin)
+    ops.dgrad_s2(gy.permute(0, 2, 3, 1).contiguous().to(dtype), wcls, Cin, out)
+    torch.cuda.synchronize()
+    assert rel(out[..., :Cin].permute(0, 3, 1, 2), x.grad) < tol

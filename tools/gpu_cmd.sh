@@ -1,3 +1,2 @@
 mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit 1
-bash tools/gpu_ab.sh old new old new
+for v in old new old new; do MOEGAN_HIP_LIB=$PWD/moe-gan_cpsc541_amd/moegan_mi/libmoegan_hip_$v.so timeout -k 10 120 python -u tools/dgrad_probe.py 2>&1 | grep -v amdgpu.ids | sed "s/^/$v /" || exit 1; done
