@@ -355,6 +355,11 @@ void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpa
     // 8-fragment wave tiles (128 x 64 / 64 x 128 per wave): 25 % fewer LDS bytes per MFMA.  128 x 256 by
     // default when Cout fills it and the grid still covers the chip (measured at B=256: the
     // discriminator's 4x4/s2 conv, N = 256, 100 -> 92 us; one column tile also reads the input once)
+    // narrow outputs (the MTM offset heads, Cout = 32) over many pixels: 128 x 32 tiles, no MFMA columns wasted
+    if (tile == 0 && Cout <= 32 && M >= 32768) {
+      run_conv<T, TO, 128, 32>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+      return;
+    }
     if (tile == 257 || (tile == 0 && Cout % 256 == 0 && cdiv(M, 128) * (int64_t)(Cout / 256) >= 480)) {
       run_conv<T, TO, 128, 256>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
       return;

@@ -247,3 +247,21 @@ def test_dgrad_s2(dtype, tol, Cin, Cg, OH):
     ops.dgrad_s2(gy.permute(0, 2, 3, 1).contiguous().to(dtype), wcls, Cin, out)
     torch.cuda.synchronize()
     assert rel(out[..., :Cin].permute(0, 3, 1, 2), x.grad) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("Cout", [32, 24])
+def test_conv_narrow_output(dtype, tol, Cout):
+    """Narrow implicit convs over many pixels (the MTM offset heads: 128 -> 32, 3x3 at 16x16, B = 128) take
+    128 x 32 tiles; ragged Cout included."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    B, H, Cin = 128, 16, 128
+    x = torch.randn(B, Cin, H, H, device=DEV, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV, generator=g) / (Cin * 9) ** 0.5
+    bias = torch.randn(Cout, device=DEV, generator=g)
+    ref = F.leaky_relu(F.conv2d(x.to(dtype).float(), w.to(dtype).float(), bias, padding=1), 0.2)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(dtype)
+    wp = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().to(dtype)
+    y = ops.conv2d(xn, wp, Cout, 3, 3, 1, 1, out_dtype=torch.float32, ep=ops.E(bias=bias, act=L.ACT_LRELU))
+    torch.cuda.synchronize()
+    assert rel(y.permute(0, 3, 1, 2), ref) < tol

@@ -55,6 +55,9 @@ def main():
     cases.append(("conv4_fwd", 2.0 * B * 16 * 512 * 4608, lambda: ops.conv2d(x4p, w4, 512, 3, 3, 1, 1)))
     x16p = rn(B, 16, 16, 128, dt=bf)
     cases.append(("conv16_fwd", 2.0 * B * 256 * 128 * 1152, lambda: ops.conv2d(x16p, w16, 128, 3, 3, 1, 1)))
+    woff = ops.pack_conv(rn(32, 128, 3, 3, sc=0.03), bf)
+    cases.append(("offset_head16_fwd", 2.0 * B * 256 * 32 * 1152,
+                  lambda: ops.conv2d(x16p, woff, 32, 3, 3, 1, 1, ep=ops.E(act=L.ACT_LRELU))))
     # weight gradients
     gy16 = rn(B * 256, 128, dt=bf)
     gw16 = torch.zeros(128, 128, 3, 3, device=dev)
