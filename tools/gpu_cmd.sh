@@ -1,4 +1,6 @@
 mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit 1
-timeout -k 10 200 python -u tools/gemm_probe.py --only offset_head16_fwd --variants '2=0;2=64;2=0;2=64' 2>&1 | grep -v amdgpu.ids || exit 1
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline 2>&1 | tail -1
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1 || exit 1
+timeout -k 10 500 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.log || { tail -5 gpurun_out/bench_full.log; exit 1; }
+cat gpurun_out/bench_full.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_full -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_full.log 2>&1 || { echo "rocprof stats failed"; exit 1; }
+echo stats ok
