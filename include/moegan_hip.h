@@ -6,17 +6,30 @@
  * it with ctypes.  Each entry cites the reference code it replaces.
  *
  * Conventions
- *  - Plain pointers + sizes, no framework types.  The caller owns every buffer
- *    (device memory) and the library never allocates, frees or synchronises.
+ *  - Plain pointers + sizes, no framework types.  The caller owns every input
+ *    and output buffer (device memory).
+ *  - Scratch: split-K slabs and reduction partials live in one workspace block
+ *    per (device, stream).  By default the library owns it and grows it on
+ *    demand (hipStreamSynchronize on that stream, hipFree, hipMalloc), so size
+ *    it with mg_workspace_reserve() before capturing a hipGraph.  A caller that
+ *    wants the library never to allocate registers its own block with
+ *    mg_set_workspace(); a call needing more than that block then fails with
+ *    MG_ERR_ARG instead of allocating.  No entry point synchronises otherwise.
  *  - Activations are NHWC ("token") layout: [B, H, W, C] == [B*H*W, C] rows.
  *  - dtype: MG_F32 (exact fp32 parity mode) or MG_BF16 (bf16 storage, fp32
  *    accumulate).  Weight gradients and all reductions are fp32.
+ *  - Operands of the GEMM/convolution entry points are read through 32-bit
+ *    buffer offsets: each must be smaller than 2 GiB (checked, MG_ERR_ARG).
  *  - Every call is enqueued on `stream` (a hipStream_t; NULL = default).
  *  - Return 0 on success or a negative MG_ERR_*; mg_last_error() gives the
- *    thread-local message.  Thread-safe / reentrant (no global state).
+ *    thread-local message.
+ *  - Thread safety: entry points may be called concurrently from several
+ *    threads.  Process-wide state is limited to the workspace table (mutex
+ *    guarded) and the mg_set_tuning switches (atomic; meant for A/B runs).
  */
 #ifndef MOEGAN_HIP_H
 #define MOEGAN_HIP_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -76,6 +89,17 @@ typedef struct mg_epilogue {
 
 const char* mg_last_error(void);
 int mg_version(void);
+/* sha256 prefix of the sources this library was built from (csrc/srchash.py): lets a caller prove the
+   binary it loaded matches the sources it ships with. */
+const char* mg_source_hash(void);
+
+/* Workspace control (see Conventions).  mg_set_workspace: use the caller-owned block [ptr, ptr+bytes) for
+   `stream` on the current device (ptr = NULL returns the stream to a library-owned block).
+   mg_workspace_reserve: grow this stream's library-owned block to at least `bytes` now.
+   mg_workspace_bytes: current size of this stream's block (0 = none yet). */
+int mg_set_workspace(void* ptr, size_t bytes, void* stream);
+int mg_workspace_reserve(size_t bytes, void* stream);
+int64_t mg_workspace_bytes(void* stream);
 /* Tuning override for measurements (key: 0 conv-wgrad tile, 1 grouped-wgrad tile, 2 conv tile,
    3 gemm tile [64 | 128], 4 conv-wgrad splits, 5 disable split-K slabs, 6 enable the XCD-aware tile
    order; value 0 = automatic). */
@@ -252,8 +276,10 @@ int mg_grouped_colsum(int dtype, const void* X, int64_t ld, const int32_t* idx, 
 /* BayesianRouter.kl_divergence (t2i_moe_gan.py:405-423): out[0] = clamped KL, out[1] = gradient-pass flag. */
 int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const float* mu_t, const float* rho_t, int nt, const float* mu_c, const float* rho_c, int nc, float* out, void* stream);
 
-/* Router parameter gradients: reparameterisation chain + KL term (coefficient *kl_coef). */
-int mg_router_param_bwd(const float* mu, const float* rho, const float* eps, const float* gW, int64_t n, const float* kl_coef, float* gmu, float* grho, void* stream);
+/* Router parameter gradients: reparameterisation chain (gW, NULL = none) + KL term (coefficient *kl_coef).
+   flags[0] & mask (optional): drop the gW chain -- a non-finite generator loss was replaced by 0 and only the
+   KL term keeps a gradient (t2i_moe_gan.py:1396-1404). */
+int mg_router_param_bwd(const float* mu, const float* rho, const float* eps, const float* gW, int64_t n, const float* kl_coef, float* gmu, float* grho, const int32_t* flags, int32_t mask, void* stream);
 
 /* moe_balance_loss from global per-expert prob sums (t2i_moe_gan.py:951-1000): out[0] = loss, coef[e] = d loss/d probs[t,e] * grad_scale. */
 int mg_balance(const float* load, int E, float T, float weight, float grad_scale, float* out, float* coef, void* stream);
@@ -311,21 +337,44 @@ int mg_weight_norm_fwd(const float* v, const float* g, int O, int K, float* W, f
 /* weight_norm backward: gg += sum gW v/||v||, gv += (g/||v||)(gW - gg_o v/||v||). */
 int mg_weight_norm_bwd(const float* v, const float* g, const float* norm, const float* gW, int O, int K, float* gv, float* gg, void* stream);
 
-/* out[0] += sum x^2 (clip_grad_norm_ total norm, t2i_moe_gan.py:1336/1420). */
+/* out[0] += sum x^2 (clip_grad_norm_ total norm, t2i_moe_gan.py:1336/1420); deterministic (fixed-order fold). */
 int mg_sumsq(const float* x, int64_t n, float* out, void* stream);
 
 /* torch.optim.AdamW step over a flat fp32 range fused with clip_grad_norm_ (coef from *sumsq, max_norm); t2i_moe_gan.py:1101-1102. */
 int mg_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, int step, const float* sumsq, float max_norm, void* stream);
 
-/* Optimizer prologue for graph-replayable steps: sumsq[0] = 0, step[0] += 1 (the AdamW step counter
-   lives on the device so a captured hipGraph advances it on every replay; torch's state['step']). */
-int mg_opt_prologue(float* sumsq, int32_t* step, void* stream);
+/* Optimizer prologue for graph-replayable steps: sumsq[0] = 0 (if sumsq), step[0] += 1 (if step and the gate
+   below passes; the AdamW step counter lives on the device so a captured hipGraph advances it on every replay:
+   torch's state['step']).
+   Gate (loss guards, mg_finite_flag / mg_flag_window): the update is skipped when flags[0] & skip_mask, and
+   when run_mask != 0 and !(win[0] & run_mask); flags = NULL: always run. */
+int mg_opt_prologue(float* sumsq, int32_t* step, const int32_t* flags, int32_t skip_mask, const int32_t* win,
+                    int32_t run_mask, void* stream);
 
 /* mg_adamw with the step count read from device memory (*step >= 1); bias corrections on the device. */
 int mg_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, const int32_t* step, const float* sumsq, float max_norm, void* stream);
 /* Same update (t2i_moe_gan.py:1333-1421), 16-B vectors, and (shadow_bf16 != NULL) the bf16 compute copy of the
    updated parameters written in the same pass (replaces the next step's fp32 -> bf16 parameter cast). */
-int mg_adamw_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, const int32_t* step, const float* sumsq, float max_norm, void* shadow_bf16, void* stream);
+int mg_adamw_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, const int32_t* step, const float* sumsq, float max_norm, void* shadow_bf16, const int32_t* flags, int32_t skip_mask, const int32_t* win, int32_t run_mask, void* stream);
+
+/* ---- loss guards (t2i_moe_gan.py:1315-1320 NaN/Inf d_loss -> skip the batch; :1367-1376 NaN KL -> 0;
+   :1396-1399 NaN/Inf g_loss -> 0) as device-side flags, read by the gated optimizer calls above ---- */
+#define MG_FLAG_D_BAD 1  /* discriminator loss (GAN + R1) non-finite: the whole batch is skipped */
+#define MG_FLAG_G_BAD 2  /* generator loss (GAN + CLIP + balance) non-finite: replaced by 0 (KL term kept) */
+#define MG_WIN_D 1       /* accumulation window: the discriminator received a gradient */
+#define MG_WIN_G_MAIN 2  /* ... the generator's non-KL parameters received a gradient */
+#define MG_WIN_G_KL 4    /* ... the routers' KL parameters (mu / rho) received a gradient */
+/* flags[0] |= bit if any of x[0..n) is NaN or Inf. */
+int mg_finite_flag(const float* x, int n, int32_t bit, int32_t* flags, void* stream);
+/* Window word update: win[0] &= ~reset_bits unless flags[0] & keep_mask (a skipped batch does not reach the
+   reference's zero_grad, t2i_moe_gan.py:1353); then win[0] |= set_bits unless flags[0] & bad_mask. */
+int mg_flag_window(const int32_t* flags, int32_t reset_bits, int32_t keep_mask, int32_t bad_mask, int32_t set_bits, int32_t* win, void* stream);
+/* x[0..bytes) = 0 when ((flags[0] & mask) != 0) == (when_set != 0). */
+int mg_zero_if(void* x, int64_t bytes, const int32_t* flags, int32_t mask, int when_set, void* stream);
+/* acc[i] += g[i] unless flags[0] & mask (gradient accumulation of a batch that may be skipped). */
+int mg_gated_axpy(float* acc, const float* g, int64_t n, const int32_t* flags, int32_t mask, void* stream);
+/* out[i] = (flags[0] & mask) ? src[i] : 0  (n <= 4096). */
+int mg_select_if(const float* src, int n, const int32_t* flags, int32_t mask, float* out, void* stream);
 
 /* generator constant [1,C,4,4] -> NHWC [B,4,4,C] (t2i_moe_gan.py:815). */
 int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, void* out, void* stream);

@@ -1,8 +1,13 @@
-// Error plumbing and version of libmoegan_hip.
+// Error plumbing, scratch workspace, tuning switches and version of libmoegan_hip.
+#include <atomic>
 #include <mutex>
 #include <string>
 
 #include "mg_common.h"
+
+#ifndef MG_SRC_HASH
+#define MG_SRC_HASH "unknown"
+#endif
 
 static thread_local std::string g_last_error;
 
@@ -17,31 +22,48 @@ int mg_check_launch(const char* what) {
   return MG_OK;
 }
 
-// Split-K slab / partial-sum workspace, one block per stream (launches on different streams may run
-// concurrently, launches on one stream are ordered, so per-stream reuse is race-free).  Growth frees the
-// old block only after the device is idle, so an in-flight launch never reads freed memory; steady-state
-// training never grows it (and a captured hipGraph keeps seeing the same pointers).
+// Scratch for split-K slabs and reduction partials: one block per (device, stream).  Launches on one
+// stream are ordered, so reusing the block across the calls enqueued on that stream is race-free, and
+// launches on different streams or devices never share a block.  A block is either caller-owned
+// (mg_set_workspace: the library never allocates or frees it; a request larger than it fails with
+// MG_ERR_ARG) or library-owned (grown on demand: hipStreamSynchronize on that stream, hipFree, hipMalloc
+// -- so grow it with mg_workspace_reserve before capturing a hipGraph; steady-state training never grows).
 namespace {
-struct WsEntry { hipStream_t stream; void* ptr; size_t bytes; };
-constexpr int kMaxWsStreams = 128;  // torch hands out streams from a fixed pool (32 per priority)
+struct WsEntry {
+  int device;
+  hipStream_t stream;
+  void* ptr;
+  size_t bytes;
+  bool caller_owned;
+};
+constexpr int kMaxWsStreams = 256;  // torch hands out streams from a fixed pool (32 per priority per device)
 WsEntry g_ws[kMaxWsStreams];
 int g_ws_n = 0;
 std::mutex g_ws_mu;
+
+WsEntry* ws_entry(int dev, hipStream_t stream) {
+  for (int i = 0; i < g_ws_n; ++i)
+    if (g_ws[i].device == dev && g_ws[i].stream == stream) return &g_ws[i];
+  if (g_ws_n == kMaxWsStreams) return nullptr;
+  WsEntry* e = &g_ws[g_ws_n++];
+  *e = WsEntry{dev, stream, nullptr, 0, false};
+  return e;
+}
 }  // namespace
 
 void* mg_workspace(size_t bytes, hipStream_t stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(g_ws_mu);
-  WsEntry* e = nullptr;
-  for (int i = 0; i < g_ws_n; ++i)
-    if (g_ws[i].stream == stream) e = &g_ws[i];
-  if (!e) {
-    if (g_ws_n == kMaxWsStreams) return nullptr;
-    e = &g_ws[g_ws_n++];
-    *e = WsEntry{stream, nullptr, 0};
-  }
+  WsEntry* e = ws_entry(dev, stream);
+  if (!e) return nullptr;
   if (bytes <= e->bytes) return e->ptr;
+  if (e->caller_owned) {
+    mg_set_error("caller-provided workspace too small: " + std::to_string(bytes) + " bytes needed");
+    return nullptr;
+  }
   if (e->ptr) {
-    (void)hipDeviceSynchronize();
+    (void)hipStreamSynchronize(stream);  // the only user of this block is `stream`
     (void)hipFree(e->ptr);
   }
   size_t want = bytes + (bytes >> 2);
@@ -54,13 +76,50 @@ void* mg_workspace(size_t bytes, hipStream_t stream) {
   return e->ptr;
 }
 
-int g_mg_tune[MG_TUNE_COUNT] = {0};
+extern "C" int mg_set_workspace(void* ptr, size_t bytes, void* stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return MG_ERR_LAUNCH;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  WsEntry* e = ws_entry(dev, st);
+  MG_REQUIRE(e, "too many streams");
+  if (e->ptr && !e->caller_owned) {
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(e->ptr);
+  }
+  *e = ptr ? WsEntry{dev, st, ptr, bytes, true} : WsEntry{dev, st, nullptr, 0, false};
+  return MG_OK;
+}
+
+extern "C" int mg_workspace_reserve(size_t bytes, void* stream) {
+  if (!mg_workspace(bytes, reinterpret_cast<hipStream_t>(stream))) {
+    if (g_last_error.empty()) mg_set_error("mg_workspace_reserve: allocation failed");
+    return MG_ERR_LAUNCH;
+  }
+  return MG_OK;
+}
+
+extern "C" int64_t mg_workspace_bytes(void* stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  for (int i = 0; i < g_ws_n; ++i)
+    if (g_ws[i].device == dev && g_ws[i].stream == st) return (int64_t)g_ws[i].bytes;
+  return 0;
+}
+
+std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 
 extern "C" int mg_set_tuning(int key, int value) {
-  if (key < 0 || key >= MG_TUNE_COUNT) return MG_ERR_ARG;
-  g_mg_tune[key] = value;
+  if (key < 0 || key >= MG_TUNE_COUNT) {
+    mg_set_error("mg_set_tuning: key out of range");
+    return MG_ERR_ARG;
+  }
+  g_mg_tune[key].store(value, std::memory_order_relaxed);
   return MG_OK;
 }
 
 extern "C" const char* mg_last_error(void) { return g_last_error.c_str(); }
-extern "C" int mg_version(void) { return 1; }
+extern "C" int mg_version(void) { return 2; }
+extern "C" const char* mg_source_hash(void) { return MG_SRC_HASH; }

@@ -2,6 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
+#include <atomic>
 #include <string>
 
 #include "../../include/moegan_hip.h"
@@ -50,6 +53,10 @@ MG_DEV void st8(bf16_t* p, const float* v) {
 }
 __host__ __device__ inline bool mg_al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// torch.clamp semantics: NaN passes through (fminf/fmaxf alone would map NaN to a bound, hiding the
+// non-finite values the training loop's guards must see, t2i_moe_gan.py:1315, :1396)
+MG_DEV float clampf(float x, float lo, float hi) { return x != x ? x : fminf(fmaxf(x, lo), hi); }
+
 MG_DEV float lrelu(float x) { return x > 0.f ? x : 0.2f * x; }
 MG_DEV float lrelu_grad(float y) { return y > 0.f ? 1.f : 0.2f; }
 MG_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
@@ -96,8 +103,9 @@ int mg_check_launch(const char* what);
 enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, MG_TUNE_GEMM_TILE = 3,
        MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_XCD = 6, MG_TUNE_WGRAD_MODE = 7,
        MG_TUNE_WARP_LDS = 8, MG_TUNE_COUNT = 16 };
-extern int g_mg_tune[MG_TUNE_COUNT];
-// Library-owned device scratch, one block per stream (grown on demand, never shrunk).
+extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
+// Device scratch, one block per (device, stream): caller-owned (mg_set_workspace) or library-owned
+// (grown on demand, never shrunk).  NULL when it cannot be provided (mg_last_error says why).
 void* mg_workspace(size_t bytes, hipStream_t stream);
 
 #define MG_REQUIRE(cond, msg)                       \

@@ -46,6 +46,11 @@ Epi<TO> make_epi(void* C, int64_t ldc, const mg_epilogue* e) {
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+// Operands are fetched through buffer descriptors with 32-bit byte offsets (mg_gemm.h): every operand's
+// byte extent must stay below 2 GiB, or loads past it would silently return zeros.
+inline bool under2g(int64_t elems, int dtype) {
+  return elems >= 0 && elems * (dtype == MG_F32 ? 4 : 2) < (int64_t)0x7fffff00;
+}
 inline int ilog2(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -177,6 +182,9 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
   MG_REQUIRE(lda % vec == 0 && ldb % vec == 0, "lda/ldb must be multiples of the 16-byte vector");
   MG_REQUIRE(a_kc ? (K % vec == 0) : (M % vec == 0), "A vector dim must be a multiple of the 16-byte vector");
   MG_REQUIRE(b_kc ? (K % vec == 0) : (N % vec == 0), "B vector dim must be a multiple of the 16-byte vector");
+  MG_REQUIRE(under2g((a_kc ? (int64_t)M : K) * lda, dtype) && under2g((b_kc ? (int64_t)N : K) * ldb, dtype) &&
+                 under2g((int64_t)M * ldc, c_dtype),
+             "an operand exceeds 2 GiB (32-bit buffer offsets)");
   if (splits < 1) {  // auto split-K (atomic fp32 epilogues only): ~512 blocks, >= 256 of K per split
     if (ep && ep->atomic) {
       int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
@@ -261,6 +269,9 @@ extern "C" int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, 
     MG_REQUIRE(b_kc ? (q.K % vec == 0) : (q.N % vec == 0), "B vector dim must be a multiple of the vector");
     MG_REQUIRE(!(q.ep && q.ep->atomic) || c_dtype == MG_F32, "atomic epilogue requires fp32 C");
     MG_REQUIRE(!a_xf(q.ep), "A loader transforms (a_idx / a_rowscale / a_gelu) are not supported by mg_gemm_batch");
+    MG_REQUIRE(under2g((a_kc ? (int64_t)q.M : q.K) * q.lda, dtype) &&
+                   under2g((b_kc ? (int64_t)q.N : q.K) * q.ldb, dtype) && under2g((int64_t)q.M * q.ldc, c_dtype),
+               "an operand exceeds 2 GiB (32-bit buffer offsets)");
   }
   if (n <= 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -385,6 +396,9 @@ extern "C" int mg_conv2d_fwd(int dtype, const void* x, int B, int H, int W, int 
   MG_REQUIRE(pow2(H) && pow2(W) && pow2(OH) && pow2(OW), "spatial sizes must be powers of two");
   MG_REQUIRE(aligned16(x) && aligned16(wpack), "x/wpack must be 16-byte aligned");
   MG_REQUIRE(!(ep && ep->atomic) || y_dtype == MG_F32, "atomic epilogue requires fp32 output");
+  MG_REQUIRE(under2g((int64_t)B * H * W * Cin, dtype) && under2g((int64_t)Cout * KH * KW * Cin, dtype) &&
+                 under2g((int64_t)B * OH * OW * ldy, y_dtype),
+             "an operand exceeds 2 GiB (32-bit buffer offsets)");
   if (B == 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == MG_F32) {
@@ -474,6 +488,8 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
   MG_REQUIRE(pow2(Cin) && Cin >= vec, "Cin must be a power of two >= vector width");
   MG_REQUIRE(pow2(OH) && pow2(OW), "output spatial sizes must be powers of two");
   MG_REQUIRE(Cout % vec == 0 && ldg % vec == 0, "Cout / ldg must be multiples of the vector width");
+  MG_REQUIRE(under2g((int64_t)B * H * W * Cin, dtype) && under2g((int64_t)B * OH * OW * ldg, dtype),
+             "an operand exceeds 2 GiB (32-bit buffer offsets)");
   MG_REQUIRE(aligned16(gy) && aligned16(x), "gy/x must be 16-byte aligned");
   if (B == 0) return MG_OK;
   const int64_t P = (int64_t)B * OH * OW;
@@ -604,6 +620,9 @@ extern "C" int mg_gemm_grouped(int dtype, int total_rows, int N, int K, int ngro
   const int vec = dtype == MG_F32 ? 4 : 8;
   MG_REQUIRE(K % vec == 0 && lda % vec == 0 && ldb % vec == 0, "K/lda/ldb must be multiples of the vector width");
   MG_REQUIRE(b_kc || N % vec == 0, "N must be a multiple of the vector width for b_kc=0");
+  MG_REQUIRE(under2g((int64_t)total_rows * lda, dtype) && under2g((int64_t)ngroups * b_gstride, dtype) &&
+                 under2g((int64_t)total_rows * ldc, c_dtype),
+             "an operand exceeds 2 GiB (32-bit buffer offsets)");
   MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
   if (max_tiles <= 0 || N == 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -630,6 +649,8 @@ extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const
   MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
   const int vec = dtype == MG_F32 ? 4 : 8;
   MG_REQUIRE(M % vec == 0 && N % vec == 0 && lda % vec == 0 && ldb % vec == 0, "M/N/lda/ldb must be vector multiples");
+  MG_REQUIRE(under2g((int64_t)total_rows * lda, dtype) && under2g((int64_t)total_rows * ldb, dtype),
+             "an operand exceeds 2 GiB (32-bit buffer offsets)");
   MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
   if (splits < 1) {
     const bool big = dtype == MG_BF16 && M >= 128 && N >= 128 && g_mg_tune[MG_TUNE_GWGRAD_TILE] != 64;
@@ -677,6 +698,8 @@ extern "C" int mg_conv2d_dgrad_s2(int dtype, const void* g, int B, int OH, int O
   MG_REQUIRE(pow2(Cg) && Cg >= 8, "Cg must be a power of two >= 8");
   MG_REQUIRE(pow2(OH) && pow2(OW), "OH, OW must be powers of two");
   MG_REQUIRE(aligned16(g) && aligned16(wcls), "g/wcls must be 16-byte aligned");
+  MG_REQUIRE(under2g((int64_t)B * OH * OW * Cg, dtype) && under2g((int64_t)B * 4 * OH * OW * ldo, out_dtype),
+             "an operand exceeds 2 GiB (32-bit buffer offsets)");
   MG_REQUIRE(!(ep && ep->atomic) || out_dtype == MG_F32, "atomic epilogue requires fp32 output");
   if (B == 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

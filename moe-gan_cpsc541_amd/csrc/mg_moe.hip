@@ -21,10 +21,10 @@ MG_DEV float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 __global__ void k_reparam(const float* __restrict__ mu, const float* __restrict__ rho, const float* __restrict__ eps,
                           int64_t n, float* __restrict__ W) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float m = fminf(fmaxf(mu[i], -10.f), 10.f);
-    float r = fminf(fmaxf(rho[i], -8.f), 4.f);
-    float sg = fminf(fmaxf(softplusf(r), 1e-6f), 10.f);
-    float e = fminf(fmaxf(eps[i], -2.f), 2.f);
+    float m = clampf(mu[i], -10.f, 10.f);
+    float r = clampf(rho[i], -8.f, 4.f);
+    float sg = clampf(softplusf(r), 1e-6f, 10.f);
+    float e = clampf(eps[i], -2.f, 2.f);
     W[i] = m + sg * e;
   }
 }
@@ -82,7 +82,7 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     z[e] = (acc[e] + Lt[(int64_t)b * E + e]) / te;
-    float l = fminf(fmaxf(z[e], -20.f), 20.f);
+    float l = clampf(z[e], -20.f, 20.f);
     p[e] = l;
     mx = fmaxf(mx, l);
   }
@@ -95,7 +95,7 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
   float s2 = 0.f;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    p[e] = fminf(fmaxf(p[e] / s, 1e-6f), 1.f);
+    p[e] = clampf(p[e] / s, 1e-6f, 1.f);
     s2 += p[e];
   }
 #pragma unroll
@@ -693,10 +693,13 @@ __global__ void k_router_kl(const float* __restrict__ mf, const float* __restric
 }
 
 // gmu += gW*[|mu|<=10] + c*mu ; grho += gW*clamp(eps)*dsigma/drho + c*sig(rho)*(sigma - 1/sigma)
+// (flags & mask: the generator loss was replaced by 0, t2i_moe_gan.py:1396-1399 -- only the KL term remains)
 __global__ void k_router_param_bwd(const float* __restrict__ mu, const float* __restrict__ rho,
                                    const float* __restrict__ eps, const float* __restrict__ gW, int64_t n,
-                                   const float* __restrict__ klc, float* __restrict__ gmu, float* __restrict__ grho) {
+                                   const float* __restrict__ klc, float* __restrict__ gmu, float* __restrict__ grho,
+                                   const int32_t* __restrict__ flags, int32_t mask) {
   float c = klc ? klc[0] : 0.f;
+  if (flags && (flags[0] & mask)) gW = nullptr;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float m = mu[i], r = rho[i];
     float gm = c * m, gr = 0.f;
@@ -753,9 +756,11 @@ __global__ void k_kl_coefs(const float* __restrict__ kl2, int R, float eff_w, fl
   if (threadIdx.x != 0) return;
   float t = 0.f;
   for (int r = 0; r < R; ++r) t += kl2[2 * r];
-  bool live = !(t > 50.f);
+  // kl > 50 -> clamp (no gradient); NaN / Inf -> the constant 0 (no gradient), :1369-1376
+  const bool finite = isfinite(t);
+  const bool live = finite && t <= 50.f;
   for (int r = 0; r < R; ++r) coef[r] = live ? eff_w * kl2[2 * r + 1] : 0.f;
-  total[0] = live ? t : 50.f;
+  total[0] = live ? t : (finite ? 50.f : 0.f);
 }
 
 inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
@@ -942,11 +947,9 @@ extern "C" int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t n = (int64_t)nf + nt + nc;
   int nparts = (int)std::min<int64_t>(64, std::max<int64_t>(1, cdiv(n, 2048)));
-  static float* s_part = nullptr;  // 64 partials; reuse is ordered by the stream
-  if (!s_part && hipMalloc(&s_part, 64 * sizeof(float)) != hipSuccess) {
-    mg_set_error("mg_router_kl: scratch allocation failed");
-    return MG_ERR_LAUNCH;
-  }
+  // 64 partials in this stream's workspace block (reuse is ordered by the stream)
+  float* s_part = reinterpret_cast<float*>(mg_workspace(64 * sizeof(float), st));
+  MG_REQUIRE(s_part, "no workspace");
   hipLaunchKernelGGL(k_router_kl_part, dim3(nparts), dim3(256), 0, st, mu_f, rho_f, nf, mu_t, rho_t, nt, mu_c, rho_c,
                      nc, s_part);
   hipLaunchKernelGGL(k_router_kl_fin, dim3(1), dim3(64), 0, st, s_part, nparts, out);
@@ -954,9 +957,12 @@ extern "C" int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const
 }
 
 extern "C" int mg_router_param_bwd(const float* mu, const float* rho, const float* eps, const float* gW, int64_t n,
-                                   const float* kl_coef, float* gmu, float* grho, void* stream) {
+                                   const float* kl_coef, float* gmu, float* grho, const int32_t* flags, int32_t mask,
+                                   void* stream) {
+  MG_REQUIRE(!gW || eps, "eps required with gW");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_router_param_bwd, dim3(nblk(n)), dim3(256), 0, st, mu, rho, eps, gW, n, kl_coef, gmu, grho);
+  hipLaunchKernelGGL(k_router_param_bwd, dim3(nblk(n)), dim3(256), 0, st, mu, rho, eps, gW, n, kl_coef, gmu, grho,
+                     flags, mask);
   return mg_check_launch("mg_router_param_bwd");
 }
 

@@ -231,9 +231,10 @@ __global__ void k_wn_bwd(const float* __restrict__ v, const float* __restrict__ 
   }
 }
 
-// sum of squares of n floats, accumulated into out[0]
-// (<= 256 blocks: every block ends in one same-address atomic, and those serialise at the memory side)
-__global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+// sum of squares of n floats, accumulated into out[0] -- deterministically: <= 256 blocks write one partial
+// each, and k_sumsq_fin folds them in a fixed order (the clip coefficient then comes out bit-identical on
+// every data-parallel rank that holds the same all-reduced gradient; float atomics would not)
+__global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restrict__ part) {
   __shared__ float red[16];
   float s = 0.f;
   const int64_t nv = mg_al16(x) ? n / 4 : 0;
@@ -253,8 +254,18 @@ __global__ void k_sumsq(const float* __restrict__ x, int64_t n, float* __restric
   if (threadIdx.x == 0) {
     float t = 0.f;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
-    atomicAdd(out, t);
+    part[blockIdx.x] = t;
   }
+}
+
+__global__ __launch_bounds__(256) void k_sumsq_fin(const float* __restrict__ part, int nparts,
+                                                   float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = threadIdx.x < nparts ? part[threadIdx.x] : 0.f;
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] += (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // One AdamW element update (torch.optim.AdamW single-tensor math, t2i_moe_gan.py:1101-1102), with every
@@ -291,10 +302,21 @@ __global__ void k_adamw(float* __restrict__ p, const float* __restrict__ g, floa
   }
 }
 
-__global__ void k_opt_prologue(float* __restrict__ sumsq, int32_t* __restrict__ step) {
+// Whether a gated optimizer launch runs (loss guards, mg_guard.hip): not when the step's flag word has a
+// skip bit (a NaN/Inf discriminator loss skips the batch, t2i_moe_gan.py:1315-1320), and only when the
+// accumulation-window word says the parameter group received a gradient (torch's AdamW skips a parameter
+// whose .grad is None).  NULL words = always run.
+MG_DEV bool opt_runs(const int32_t* flags, int32_t skip_mask, const int32_t* win, int32_t run_mask) {
+  if (flags && (flags[0] & skip_mask)) return false;
+  if (win && run_mask && !(win[0] & run_mask)) return false;
+  return true;
+}
+
+__global__ void k_opt_prologue(float* __restrict__ sumsq, int32_t* __restrict__ step, const int32_t* flags,
+                               int32_t skip_mask, const int32_t* win, int32_t run_mask) {
   if (threadIdx.x == 0) {
-    sumsq[0] = 0.f;
-    step[0] += 1;
+    if (sumsq) sumsq[0] = 0.f;
+    if (step && opt_runs(flags, skip_mask, win, run_mask)) step[0] += 1;
   }
 }
 
@@ -327,7 +349,9 @@ __global__ __launch_bounds__(256) void k_adamw_dev_v(float* __restrict__ p, cons
                                                      float lr, float b1, float b2, float eps, float wd,
                                                      const int32_t* __restrict__ step,
                                                      const float* __restrict__ sumsq, float max_norm,
-                                                     bf16_t* __restrict__ shadow) {
+                                                     bf16_t* __restrict__ shadow, const int32_t* flags,
+                                                     int32_t skip_mask, const int32_t* win, int32_t run_mask) {
+  if (!opt_runs(flags, skip_mask, win, run_mask)) return;
   const float t = (float)step[0];
   const float bc1 = 1.f - powf(b1, t);
   const float bc2_sqrt = sqrtf(1.f - powf(b2, t));
@@ -532,7 +556,11 @@ extern "C" int mg_weight_norm_bwd(const float* v, const float* g, const float* n
 extern "C" int mg_sumsq(const float* x, int64_t n, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (n == 0) return MG_OK;
-  hipLaunchKernelGGL(k_sumsq, dim3(std::min(nblk(n / 4 + 1), 256)), dim3(256), 0, st, x, n, out);
+  const int blocks = std::min(nblk(n / 4 + 1), 256);
+  float* part = reinterpret_cast<float*>(mg_workspace(256 * sizeof(float), st));
+  MG_REQUIRE(part, "no workspace");
+  hipLaunchKernelGGL(k_sumsq, dim3(blocks), dim3(256), 0, st, x, n, part);
+  hipLaunchKernelGGL(k_sumsq_fin, dim3(1), dim3(256), 0, st, part, blocks, out);
   return mg_check_launch("mg_sumsq");
 }
 
@@ -548,10 +576,11 @@ extern "C" int mg_adamw(float* p, const float* g, float* m, float* v, int64_t n,
   return mg_check_launch("mg_adamw");
 }
 
-extern "C" int mg_opt_prologue(float* sumsq, int32_t* step, void* stream) {
-  MG_REQUIRE(sumsq && step, "null pointer");
+extern "C" int mg_opt_prologue(float* sumsq, int32_t* step, const int32_t* flags, int32_t skip_mask,
+                               const int32_t* win, int32_t run_mask, void* stream) {
+  MG_REQUIRE(sumsq || step, "null pointers");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_opt_prologue, dim3(1), dim3(64), 0, st, sumsq, step);
+  hipLaunchKernelGGL(k_opt_prologue, dim3(1), dim3(64), 0, st, sumsq, step, flags, skip_mask, win, run_mask);
   return mg_check_launch("mg_opt_prologue");
 }
 
@@ -568,14 +597,15 @@ extern "C" int mg_adamw_dev(float* p, const float* g, float* m, float* v, int64_
 
 extern "C" int mg_adamw_dev_shadow(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                                    float beta2, float eps, float weight_decay, const int32_t* step,
-                                   const float* sumsq, float max_norm, void* shadow_bf16, void* stream) {
+                                   const float* sumsq, float max_norm, void* shadow_bf16, const int32_t* flags,
+                                   int32_t skip_mask, const int32_t* win, int32_t run_mask, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (n == 0) return MG_OK;
   MG_REQUIRE(mg_al16(p) && mg_al16(g) && mg_al16(m) && mg_al16(v) &&
              (!shadow_bf16 || (reinterpret_cast<uintptr_t>(shadow_bf16) & 7) == 0), "16-B aligned p/g/m/v, 8-B shadow");
   hipLaunchKernelGGL(k_adamw_dev_v, dim3(std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4 + 1, 256), 4096))),
                      dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, sumsq, max_norm,
-                     reinterpret_cast<bf16_t*>(shadow_bf16));
+                     reinterpret_cast<bf16_t*>(shadow_bf16), flags, skip_mask, win, run_mask);
   return mg_check_launch("mg_adamw_dev_shadow");
 }
 

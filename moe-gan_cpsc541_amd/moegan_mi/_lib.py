@@ -37,16 +37,19 @@ class GemmDesc(ctypes.Structure):
 # Argument types are derived from include/moegan_hip.h itself, so the binding
 # cannot drift from the C ABI (the header travels with the library).
 _HEADER = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "moegan_hip.h"))
-_CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "float": _f32, "void": _c_void_p,
-          "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc)}
+_CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "size_t": ctypes.c_size_t, "float": _f32,
+          "void": _c_void_p, "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc)}
+_RESTYPE = {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "const char*": ctypes.c_char_p}
+SIG_RE = r"\b(int|int64_t|const char\*)\s+(mg_\w+)\(([^)]*)\);"
 
 
 def _parse_header(path=_HEADER):
+    """{name: (restype, [argtypes])} for every entry point declared in the C-ABI header."""
     import re
     txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     sigs = {}
-    for name, args in re.findall(r"\b(?:int|const char\*)\s+(mg_\w+)\(([^)]*)\);", txt, flags=re.S):
+    for ret, name, args in re.findall(SIG_RE, txt, flags=re.S):
         types = []
         for a in args.split(","):
             a = " ".join(a.split())
@@ -57,7 +60,7 @@ def _parse_header(path=_HEADER):
                 types.append(_CTYPE[base] if base in ("mg_epilogue", "mg_gemm_desc") else _c_void_p)
             else:
                 types.append(_CTYPE[base])
-        sigs[name] = types
+        sigs[name] = (_RESTYPE[ret], types)
     return sigs
 
 
@@ -77,16 +80,31 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise MGError(f"libmoegan_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
         h = ctypes.CDLL(LIB_PATH)
-        for name, args in _SIGS.items():
-            if name == "mg_last_error":
-                continue
+        for name, (res, args) in _SIGS.items():
             fn = getattr(h, name)
             fn.argtypes = list(args)
-            fn.restype = ctypes.c_int32
-        h.mg_last_error.restype = ctypes.c_char_p
-        h.mg_last_error.argtypes = []
+            fn.restype = res
         _lib = h
     return _lib
+
+
+def source_hash_expected():
+    """Hash of the HIP sources shipped next to the library (csrc/srchash.py)."""
+    import importlib.util
+    path = os.path.join(_HERE, "..", "csrc", "srchash.py")
+    spec = importlib.util.spec_from_file_location("_mg_srchash", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_hash()
+
+
+def check_source_hash():
+    """Raise unless the loaded library was built from the sources in this tree."""
+    got = lib().mg_source_hash().decode()
+    want = source_hash_expected()
+    if got != want:
+        raise MGError(f"libmoegan_hip.so was built from other sources (hash {got}, tree {want}): rebuild it")
+    return got
 
 
 def exported_symbols():

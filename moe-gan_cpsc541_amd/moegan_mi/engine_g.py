@@ -53,6 +53,7 @@ class GeneratorEngine:
         self._mean_latent = None
         self._want_kl = True
         self._bv = None  # per-block vectors of the running forward (_block_vectors)
+        self.guard_flags = None  # the training step's loss-guard word (step.py), read by the router backward
         # weight gradients run on a side stream, overlapping the data-gradient chain (joined in backward)
         self.side = graphs.SideStream(self.dev, enabled=graphs.side_streams_enabled(self.dev))
 
@@ -421,7 +422,8 @@ class GeneratorEngine:
             r = q["r"]
             for nm, gWx, epi in (("feature", q["gWf"], 0), ("text", q["gWt"], 1), ("combined", q["gWc"], 2)):
                 ops.router_param_bwd(self.P(r + nm + "_mu"), self.P(r + nm + "_rho"), q["eps"][epi], gWx,
-                                     q["kl_coef"], self.G(r + nm + "_mu"), self.G(r + nm + "_rho"))
+                                     q["kl_coef"], self.G(r + nm + "_mu"), self.G(r + nm + "_rho"),
+                                     flags=self.guard_flags, mask=ops.FLAG_G_BAD)
 
     def _cbuf(self):
         return self.st.shadow if self.st.shadow is not None else self.st.data

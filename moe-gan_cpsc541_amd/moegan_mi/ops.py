@@ -299,16 +299,51 @@ def adamw(p, g, m, v, lr, beta1, beta2, eps, wd, step, sumsq_buf=None, max_norm=
          max_norm, S())
 
 
-def opt_prologue(sumsq_buf, step_dev):
-    """sumsq_buf[0] = 0; step_dev[0] += 1 (device-side AdamW step counter, graph-replayable)."""
-    call("mg_opt_prologue", ptr(sumsq_buf), ptr(step_dev), S())
+def opt_prologue(sumsq_buf, step_dev, gate=None):
+    """sumsq_buf[0] = 0 (if given); step_dev[0] += 1 (device-side AdamW step counter, graph-replayable) unless
+    the gate ``(flags, skip_mask, win, run_mask)`` says the optimizer does not run this step."""
+    fl, skip, win, run = gate if gate is not None else (None, 0, None, 0)
+    call("mg_opt_prologue", ptr(sumsq_buf), ptr(step_dev), ptr(fl), skip, ptr(win), run, S())
 
 
-def adamw_dev(p, g, m, v, lr, beta1, beta2, eps, wd, step_dev, sumsq_buf=None, max_norm=0.0, shadow=None):
+def adamw_dev(p, g, m, v, lr, beta1, beta2, eps, wd, step_dev, sumsq_buf=None, max_norm=0.0, shadow=None,
+              gate=None):
     """AdamW with the device step counter and clip coefficient; ``shadow`` (bf16, same length) also receives the
-    updated parameters (mg_adamw_dev_shadow)."""
+    updated parameters (mg_adamw_dev_shadow); ``gate`` as in opt_prologue."""
+    fl, skip, win, run = gate if gate is not None else (None, 0, None, 0)
     call("mg_adamw_dev_shadow", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps, wd, ptr(step_dev),
-         ptr(sumsq_buf), max_norm, ptr(shadow), S())
+         ptr(sumsq_buf), max_norm, ptr(shadow), ptr(fl), skip, ptr(win), run, S())
+
+
+# ---------------------------------------------------------------------------
+# loss guards (mg_guard.hip): device flag words, no host sync
+# ---------------------------------------------------------------------------
+FLAG_D_BAD, FLAG_G_BAD = 1, 2
+WIN_D, WIN_G_MAIN, WIN_G_KL = 1, 2, 4
+
+
+def finite_flag(x, bit, flags):
+    call("mg_finite_flag", ptr(x), x.numel(), bit, ptr(flags), S())
+
+
+def flag_window(flags, win, *, reset_bits=0, keep_mask=0, bad_mask=0, set_bits=0):
+    """win &= ~reset_bits unless flags & keep_mask; win |= set_bits unless flags & bad_mask."""
+    call("mg_flag_window", ptr(flags), reset_bits, keep_mask, bad_mask, set_bits, ptr(win), S())
+
+
+def zero_if(x, flags, mask, when_set=True):
+    """x = 0 when (flags & mask) != 0 equals ``when_set``."""
+    call("mg_zero_if", ptr(x), x.numel() * x.element_size(), ptr(flags), mask, int(bool(when_set)), S())
+
+
+def gated_axpy(acc, g, flags, mask):
+    call("mg_gated_axpy", ptr(acc), ptr(g), acc.numel(), ptr(flags), mask, S())
+
+
+def select_if(src, flags, mask, out=None):
+    out = torch.empty_like(src) if out is None else out
+    call("mg_select_if", ptr(src), src.numel(), ptr(flags), mask, ptr(out), S())
+    return out
 
 
 def const_fwd(cst, B, dtype):
@@ -482,9 +517,9 @@ def kl_coefs(kl2, R, eff_w, coef, total):
     call("mg_kl_coefs", ptr(kl2), R, eff_w, ptr(coef), ptr(total), S())
 
 
-def router_param_bwd(mu, rho, eps, gW, kl_coef, gmu, grho):
+def router_param_bwd(mu, rho, eps, gW, kl_coef, gmu, grho, flags=None, mask=0):
     call("mg_router_param_bwd", ptr(mu), ptr(rho), ptr(eps), ptr(gW), mu.numel(), ptr(kl_coef), ptr(gmu),
-         ptr(grho), S())
+         ptr(grho), ptr(flags), mask, S())
 
 
 def balance(load, E_, T, weight, grad_scale, out, coef):

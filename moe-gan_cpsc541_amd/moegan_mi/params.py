@@ -21,13 +21,18 @@ from . import ops
 from .layout import is_buffer
 
 _EXPERT = re.compile(r"^(.*\.moe\.)experts\.(\d+)\.net\.(\d)\.(weight|bias)$")
+# the routers' KL parameters (BayesianRouter mu / rho, t2i_moe_gan.py:280-300, :405-423)
+_KL = re.compile(r"^.*\.router\.(feature|text|combined)_(mu|rho)$")
 ALIGN = 8  # elements: keeps every view 16-byte aligned for fp32 and bf16 vector loads
 
 
 def flat_order(shapes, frozen_prefixes=()):
     """Reference names reordered: the modulated convs' style weights and then their biases first (one
     [sum Cin, 512] matrix and one [sum Cin] vector: every style of a forward is ONE GEMM), experts grouped
-    per (block, layer, kind); frozen names last."""
+    per (block, layer, kind), the routers' KL parameters (mu / rho) at the end of the optimised range, frozen
+    names last.  The KL group is the only part of the generator that still receives a gradient when the
+    loop's guard replaces a non-finite generator loss by 0 (t2i_moe_gan.py:1396-1404), so it is stepped by
+    its own (gated) optimizer launch with its own step counter."""
     names = [n for n in shapes if not is_buffer(n)]
     groups = OrderedDict()
     order, frozen = [], []
@@ -38,12 +43,15 @@ def flat_order(shapes, frozen_prefixes=()):
         style_w, style_b = [], []
     lead = set(style_w) | set(style_b)
     order.extend(style_w + style_b)
+    kl_tail = []
     for n in names:
         m = _EXPERT.match(n)
         if n in lead:
             continue
         if is_frozen(n):
             frozen.append(n)
+        elif _KL.match(n):
+            kl_tail.append(n)
         elif m:
             key = (m.group(1), m.group(3), m.group(4))
             if key not in groups:
@@ -58,7 +66,7 @@ def flat_order(shapes, frozen_prefixes=()):
             out.extend(n for _, n in sorted(groups[o]))
         else:
             out.append(o)
-    return out, frozen
+    return out + kl_tail, frozen
 
 
 class ParamStore:
@@ -82,6 +90,9 @@ class ParamStore:
                 off = off  # experts stay packed (each expert tensor is a multiple of 8 elements)
         if not frozen:
             self.n_opt = off
+        # [0, n_main): parameters stepped by the main optimizer launch; [n_main, n_opt): router KL parameters
+        kl = [n for n in order if _KL.match(n)]
+        self.n_main = self.offsets[kl[0]][0] if kl else self.n_opt
         self.total = (off + ALIGN - 1) // ALIGN * ALIGN
         self.data = torch.zeros(self.total, device=self.device, dtype=torch.float32)
         self.grad = torch.zeros(self.total, device=self.device, dtype=torch.float32)
@@ -89,6 +100,8 @@ class ParamStore:
         self.v = torch.zeros(self.total, device=self.device, dtype=torch.float32)
         self.step_count = 0  # host mirror (eager steps); the optimizer reads the device counter below
         self.step_dev = torch.zeros(1, device=self.device, dtype=torch.int32)
+        self.step_dev_kl = torch.zeros(1, device=self.device, dtype=torch.int32)  # AdamW step of [n_main, n_opt)
+        self.acc = None  # gradient accumulated over a window (gradient_accumulation_steps > 1), ensure_acc()
         self.buffers = OrderedDict((n, torch.zeros(s, device=self.device)) for n, s in self.shapes.items()
                                    if is_buffer(n))
         self.shadow_dtype = shadow_dtype
@@ -127,6 +140,9 @@ class ParamStore:
             self.m = self.m.to(dev)
             self.v = self.v.to(dev)
             self.step_dev = self.step_dev.to(dev)
+            self.step_dev_kl = self.step_dev_kl.to(dev)
+            if self.acc is not None:
+                self.acc = self.acc.to(dev)
             self.buffers = OrderedDict((n, b.to(dev)) for n, b in self.buffers.items())
             if self.shadow is not None:
                 self.shadow = torch.zeros(self.total, device=dev, dtype=self.shadow_dtype)
@@ -172,6 +188,13 @@ class ParamStore:
 
     def zero_grad(self):
         self.grad.zero_()
+
+    def ensure_acc(self):
+        """The window accumulator: with gradient accumulation each batch's gradient is formed in ``grad`` and
+        added here only if the loop's guards keep that batch (t2i_moe_gan.py:1315-1320)."""
+        if self.acc is None or self.acc.device != self.data.device:
+            self.acc = torch.zeros(self.total, device=self.device, dtype=torch.float32)
+        return self.acc
 
     # ---- state dict (reference layout) ----
     def state_dict(self, cpu=True):

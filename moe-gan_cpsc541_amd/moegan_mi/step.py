@@ -1,6 +1,6 @@
 """One G+D training step of train_aurora_gan (t2i_moe_gan.py:1262-1421) on the HIP engines.
 
-The step keeps the reference's order and semantics with gradient_accumulation_steps=1:
+The step keeps the reference's order and semantics:
   D phase: D(real) + R1, G forward under no_grad (fresh router noise), D(fake), D(real, text[perm]),
            D backward, clip_grad_norm_(D, 0.7), AdamW(D)
   G phase: G forward (fresh router noise), KL clamp at 50, D(fake) with the UPDATED D, G adversarial
@@ -10,17 +10,31 @@ Parameters with no gradient in the reference (to_rgb_8: only feeds the gradient-
 sit in the store's frozen tail and are never updated -- exactly as torch's AdamW skips a
 parameter whose .grad is None.
 
-Nothing here synchronises with the host: every loss value stays on the device until the
-caller reads it, and all randomness is passed in.  Data parallelism (one process per GPU,
-RCCL) all-reduces the flat D and G gradient buffers and the [E] expert-load vector.
+Loss guards (t2i_moe_gan.py:1315-1320, :1367-1376, :1396-1404) run on the device: a flag word per step
+(``out["flags"]``) records a non-finite discriminator loss (the whole batch is skipped: no gradient is
+kept, no optimizer steps, no step counters advance) or a non-finite generator loss (replaced by 0: only
+the routers' KL term keeps a gradient).  A second word per accumulation window records which parameter
+groups received a gradient, so the gated optimizer launches skip a group whose gradient the reference
+would leave as None.  Everything stays one captured hipGraph; the host reads the flags at most once per
+step.
+
+Gradient accumulation (gradient_accumulation_steps > 1): each batch's gradients are formed in
+``store.grad`` and added to the window accumulator ``store.acc`` only if the guards keep the batch.
+
+Nothing here synchronises with the host: every loss value stays on the device until the caller reads it,
+and all randomness is passed in.  Data parallelism (one process per GPU, RCCL) all-reduces the flat D and
+G gradient buffers, the [E] expert-load vector and the guard word.
 """
 import torch
+import torch.nn.functional as F
 
 from . import graphs, ops
 from .engine_d import DiscriminatorEngine
 from .engine_g import GeneratorEngine
 from .layout import discriminator_shapes, generator_shapes
 from .params import ParamStore
+
+FD, FG = ops.FLAG_D_BAD, ops.FLAG_G_BAD
 
 
 class StepConfig:
@@ -35,6 +49,20 @@ class StepConfig:
         self.beta1, self.beta2, self.weight_decay, self.eps = beta1, beta2, weight_decay, eps
         self.d_clip, self.g_clip = d_clip, g_clip
         self.psi = psi
+
+
+def clip_loss(images_nchw, text, encode_image):
+    """CLIPLoss.forward (t2i_moe_gan.py:75-119): 1 - mean cos(CLIP(image), text), forward only (no gradient,
+    :98-101).  Logging / validation only; values are parity-unpinned (CLIP weights are not available here)."""
+    with torch.no_grad():
+        im = torch.clamp(images_nchw.float(), -1, 1)
+        if im.shape[-1] != 224 or im.shape[-2] != 224:
+            im = F.interpolate(im, size=(224, 224), mode="bilinear", align_corners=False)
+        f = encode_image(im).float()
+        f = f / f.norm(dim=-1, keepdim=True)
+        t = text.float() / text.float().norm(dim=-1, keepdim=True)
+        sim = torch.nan_to_num((f * t).sum(dim=1))
+        return (1.0 - sim.mean()).reshape(1)
 
 
 class TrainStep:
@@ -52,7 +80,9 @@ class TrainStep:
         if process_group is not None:
             import torch.distributed as dist
             self.world = dist.get_world_size(process_group)
-        self.clip_encoder = None  # optional image encoder for the (gradient-free) CLIP loss
+        # optional image encoder for the (gradient-free) CLIP loss terms; images are [B,3,H,W] in [-1, 1]
+        self.clip_encoder = None
+        self.win = torch.zeros(1, device=self.dev, dtype=torch.int32)  # accumulation-window word (mg_flag_window)
 
     # ---- data-parallel reductions ----
     # (collectives stay eager segments when the step is replayed as hipGraphs, graphs.py)
@@ -72,20 +102,40 @@ class TrainStep:
         import torch.distributed as dist
         graphs.eager(lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg))
 
+    def _allreduce_flags(self, flags):
+        """Every rank takes the same guard decision: a bit set on any rank is set on all (MAX per bit)."""
+        if self.pg is None:
+            return
+        import torch.distributed as dist
+
+        def run():
+            bits = torch.stack([(flags & FD), (flags & FG)]).view(-1)
+            dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=self.pg)
+            flags.copy_(bits[0:1] | bits[1:2])
+        graphs.eager(run)
+
     # ---- optimizer ----
-    def _adamw(self, store, lr, max_norm, n=None, grad_scale=1.0):
-        n = store.n_opt if n is None else n
+    def _adamw(self, store, grad, lr, max_norm, flags, ranges, grad_scale=1.0):
+        """clip_grad_norm_ + AdamW over ``grad[:n_opt]`` (torch semantics, :1333-1337 / :1417-1421).  ``ranges``:
+        [(lo, hi, step counter, window bit)] -- each range is one gated launch with its own step counter."""
+        n = store.n_opt
         store.step_count += 1
         if grad_scale != 1.0:  # (loss / accumulation_steps) of the reference == scaling the summed gradient
-            store.grad[:n].mul_(grad_scale)
+            grad[:n].mul_(grad_scale)
         ss = torch.empty(1, device=self.dev)
-        ops.opt_prologue(ss, store.step_dev)  # ss = 0, device step counter += 1 (graph-replayable)
-        ops.sumsq(store.grad[:n], ss)
+        ops.opt_prologue(ss, None)
+        ops.sumsq(grad[:n], ss)
         c = self.cfg
-        shadow = store.shadow[:n] if (store.shadow is not None and store.shadow.dtype == torch.bfloat16) else None
-        ops.adamw_dev(store.data[:n], store.grad[:n], store.m[:n], store.v[:n], lr, c.beta1, c.beta2, c.eps,
-                      c.weight_decay, store.step_dev, ss, max_norm, shadow=shadow)
-        if shadow is not None:
+        bf16_shadow = store.shadow is not None and store.shadow.dtype == torch.bfloat16
+        for lo, hi, step_dev, wbit in ranges:
+            if hi <= lo:
+                continue
+            gate = (flags, FD, self.win, wbit)
+            ops.opt_prologue(None, step_dev, gate=gate)  # device step counter += 1 (graph-replayable), gated
+            ops.adamw_dev(store.data[lo:hi], grad[lo:hi], store.m[lo:hi], store.v[lo:hi], lr, c.beta1, c.beta2,
+                          c.eps, c.weight_decay, step_dev, ss, max_norm,
+                          shadow=store.shadow[lo:hi] if bf16_shadow else None, gate=gate)
+        if bf16_shadow:
             store.mark_shadow_written()
         return ss
 
@@ -99,44 +149,67 @@ class TrainStep:
         a window, ``step_optim`` at its last; gradients are summed and scaled by 1/acc before clipping.  As in
         the reference, the generator step's loss also accumulates into the discriminator's gradients, which
         matters only when the D optimizer has not stepped yet in the window (acc > 1)."""
-        c = self.cfg
-        B = real.shape[0]
         ops.ARENA.begin(self.dev)
         try:
             return self._step(real, text, z, eps_d, eps_g, perm, anneal, lr_g, lr_d, eff_kl_weight, prep, acc,
                               zero_grads, step_optim)
         finally:
             ops.ARENA.end()
+            self.ge.guard_flags = None
 
     def _step(self, real, text, z, eps_d, eps_g, perm, anneal, lr_g, lr_d, eff_kl_weight, prep, acc, zero_grads,
               step_optim):
         c = self.cfg
-        B = real.shape[0]
+        accum = acc > 1
+        gs, ds = self.gs, self.ds
+        flags = ops.zeros(1, device=self.dev, dtype=torch.int32)  # the step's guard word (zero arena)
+        self.ge.guard_flags = flags
         if prep:
             self.ge.prep()
             self.de.prep()
+        if accum:
+            gs.ensure_acc()
+            ds.ensure_acc()
+            if zero_grads:
+                ds.acc.zero_()
         # ------------------------- D phase -------------------------
-        if zero_grads:
-            self.ds.zero_grad()
+        if zero_grads or accum:
+            ds.zero_grad()
         # the router-independent prefix of this forward (mapping, styles, gen_block_4's convolution block) is
         # kept with its saved activations and reused by the G-phase forward: same z / text, G not yet updated
-        f16, _, _, _, _, _ = self.ge.forward(z, text, eps_d, anneal, c.psi, train=True, save=False, want_kl=False,
-                                             keep_prefix=True)
+        f16, _, _, probs_d, topi_d, _ = self.ge.forward(z, text, eps_d, anneal, c.psi, train=True, save=False,
+                                                        want_kl=False, keep_prefix=True)
         prefix, self.ge.last_prefix = self.ge.last_prefix, None
         dres = self.de.d_phase(real, text, f16, ("nhwc", 8), perm, c.r1_gamma)
+        # guard: NaN / Inf d_loss skips the whole batch (t2i_moe_gan.py:1315-1320)
+        ops.finite_flag(dres["losses"][:1], FD, flags)
+        ops.finite_flag(dres["r1"], FD, flags)
+        self._allreduce_flags(flags)
+        ops.flag_window(flags, self.win, reset_bits=ops.WIN_D if zero_grads else 0, bad_mask=FD, set_bits=ops.WIN_D)
+        if accum:
+            ops.gated_axpy(ds.acc, ds.grad, flags, FD)
+        dgrad = ds.acc if accum else ds.grad
         d_sumsq = None
         if step_optim:
-            self._allreduce_mean(self.ds.grad)
-            d_sumsq = self._adamw(self.ds, lr_d, c.d_clip, grad_scale=1.0 / acc)
+            self._allreduce_mean(dgrad)
+            d_sumsq = self._adamw(ds, dgrad, lr_d, c.d_clip, flags, [(0, ds.n_opt, ds.step_dev, ops.WIN_D)],
+                                  grad_scale=1.0 / acc)
             self.de.prep()
         # ------------------------- G phase -------------------------
-        if zero_grads:
-            self.gs.zero_grad()
+        if accum:
+            gs.zero_grad()
+            if zero_grads:  # optimizer_g.zero_grad() (:1353) is never reached by a skipped batch
+                ops.zero_if(gs.acc, flags, FD, when_set=False)
+        elif zero_grads:
+            gs.zero_grad()
         want8 = self.clip_encoder is not None
-        img16, img8, kl2s, probs, _, ctx = self.ge.forward(z, text, eps_g, anneal, c.psi, train=True, save=True,
-                                                           want_img8=want8, prefix=prefix)
+        img16, img8, kl2s, probs, topi_g, ctx = self.ge.forward(z, text, eps_g, anneal, c.psi, train=True,
+                                                                save=True, want_img8=want8, prefix=prefix)
         prefix = None
-        g_gan, fake_pred, g_img = self.de.g_phase(img16, ("nhwc", 8), text, want_d_params=(acc > 1 and not step_optim))
+        leak = accum and not step_optim  # the G loss also reaches D's gradients while D has not stepped yet
+        if leak:
+            ds.zero_grad()
+        g_gan, fake_pred, g_img = self.de.g_phase(img16, ("nhwc", 8), text, want_d_params=leak)
         # balance loss on the last MoE layer, over the GLOBAL batch (t2i_moe_gan.py:951-1000)
         last = probs[-1]
         load = ops.zeros(c.E, device=self.dev)
@@ -145,18 +218,43 @@ class TrainStep:
         bal = torch.zeros(1, device=self.dev)
         coef = torch.empty(c.E, device=self.dev)
         ops.balance(load, c.E, last.shape[0] * self.world, c.balance_weight, float(self.world), bal, coef)
+        # CLIP terms (t2i_moe_gan.py:1385-1387): forward only, they enter g_loss's value but no gradient
+        clip16 = clip8 = None
+        if self.clip_encoder is not None:
+            clip16 = clip_loss(img16[..., :3].permute(0, 3, 1, 2), text, self.clip_encoder)
+            clip8 = clip_loss(img8[..., :3].permute(0, 3, 1, 2), text, self.clip_encoder)
         # KL (t2i_moe_gan.py:846, :1367-1376, :1402-1404)
         kl2 = torch.stack(kl2s)
         kl_coef = torch.empty(len(kl2s), device=self.dev)
         kl_total = torch.empty(1, device=self.dev)
         ops.kl_coefs(kl2, len(kl2s), eff_kl_weight, kl_coef, kl_total)
+        # guard: NaN / Inf (GAN + CLIP + balance) generator loss -> 0, the KL term stays (:1396-1404)
+        for t in (g_gan, bal, clip16, clip8):
+            if t is not None:
+                ops.finite_flag(t, FG, flags)
+        self._allreduce_flags(flags)
+        ops.flag_window(flags, self.win, reset_bits=(ops.WIN_G_MAIN | ops.WIN_G_KL) if zero_grads else 0,
+                        keep_mask=FD, bad_mask=FD, set_bits=ops.WIN_G_KL)
+        ops.flag_window(flags, self.win, bad_mask=FD | FG, set_bits=ops.WIN_G_MAIN)
         self.ge.backward(ctx, g_img, coef=coef, kl_coef=kl_coef)
+        if accum:
+            ops.gated_axpy(gs.acc[:gs.n_main], gs.grad[:gs.n_main], flags, FD | FG)
+            ops.gated_axpy(gs.acc[gs.n_main:gs.n_opt], gs.grad[gs.n_main:gs.n_opt], flags, FD)
+            if leak:
+                ops.gated_axpy(ds.acc, ds.grad, flags, FD | FG)
+        else:
+            ops.zero_if(gs.grad[:gs.n_main], flags, FG)  # the router KL range kept only its KL term
+        ggrad = gs.acc if accum else gs.grad
         g_sumsq = None
         if step_optim:
-            self._allreduce_mean(self.gs.grad)
-            g_sumsq = self._adamw(self.gs, lr_g, c.g_clip, grad_scale=1.0 / acc)
+            self._allreduce_mean(ggrad)
+            g_sumsq = self._adamw(gs, ggrad, lr_g, c.g_clip, flags,
+                                  [(0, gs.n_main, gs.step_dev, ops.WIN_G_MAIN),
+                                   (gs.n_main, gs.n_opt, gs.step_dev_kl, ops.WIN_G_KL)],
+                                  grad_scale=1.0 / acc)
         out = dict(d_losses=dres["losses"], r1=dres["r1"], g_gan=g_gan, balance=bal, kl=kl_total, kl_raw=kl2,
                    d_grad_sumsq=d_sumsq, g_grad_sumsq=g_sumsq, real_pred=dres["real_pred"],
                    fake_pred=dres["fake_pred"], mism_pred=dres["mism_pred"], r1_grad=dres["r1_grad"],
-                   img16=img16, img8=img8)
+                   img16=img16, img8=img8, probs=probs, topi=topi_g, probs_d=probs_d, topi_d=topi_d,
+                   fake_img_d=f16, flags=flags, clip16=clip16, clip8=clip8, d_grad=dgrad, g_grad=ggrad)
         return out

@@ -114,33 +114,39 @@ def expert_ffn(x, P, pre):
     return F.linear(h, P[pre + "net.2.weight"], P[pre + "net.2.bias"])
 
 
-def topk_route(probs, k):
+def topk_route(probs, k, idx=None):
     """Build extension: top-k (lowest index wins ties) with renormalised weights.
 
     For k == E this is exactly the reference's dense soft combine (weights = probs).
+    ``idx`` [T, k] replays a given selection instead of recomputing it (tests resolve near-ties -- tokens
+    whose top-k margin is within the device's rounding -- the way the device did, then compare the rest).
     """
     E = probs.shape[1]
     if k >= E:
         return probs
-    top = torch.topk(probs, k, dim=1, sorted=True)
-    wsel = top.values / top.values.sum(dim=1, keepdim=True)
-    return torch.zeros_like(probs).scatter(1, top.indices, wsel)
+    if idx is None:
+        idx = torch.topk(probs, k, dim=1, sorted=True).indices
+    vals = probs.gather(1, idx.long())
+    wsel = vals / vals.sum(dim=1, keepdim=True)
+    return torch.zeros_like(probs).scatter(1, idx.long(), wsel)
 
 
-def sparse_moe(x, w, P, pre, E, eps=None, training=True, anneal=1.0, topk=None):
+def sparse_moe(x, w, P, pre, E, eps=None, training=True, anneal=1.0, topk=None, route=None):
     B, C, H, W = x.shape
     tok = x.permute(0, 2, 3, 1).reshape(-1, C)  # :455
     wtok = w[:, None, None, :].expand(B, H, W, w.shape[1]).reshape(-1, w.shape[1])  # :456
     probs, _ = router(tok, wtok, P, pre + "router.", eps, training, anneal)
     out = torch.zeros_like(tok)
     if training:
-        gate = probs if topk is None else topk_route(probs, topk)
+        gate = probs if topk is None else topk_route(probs, topk, route)
         for e in range(E):  # :467-470 (dense soft combine)
             if topk is not None and topk < E:
-                sel = gate[:, e] > 0
-                if sel.any():
-                    out = out.index_put((sel.nonzero().squeeze(1),),
-                                        out[sel] + gate[sel, e:e + 1] * expert_ffn(tok[sel], P, f"{pre}experts.{e}."))
+                # an expert that no token selected still runs on its (empty) token set, so its parameters get
+                # a zero gradient rather than None -- the extension's defined semantics (the device's grouped
+                # GEMMs produce zero gradients for an empty group, and AdamW then applies its decay step)
+                idx = (gate[:, e] > 0).nonzero().squeeze(1)
+                y = expert_ffn(tok[idx], P, f"{pre}experts.{e}.")
+                out = out.index_add(0, idx, gate[idx, e:e + 1] * y)
             else:
                 out = out + gate[:, e:e + 1] * expert_ffn(tok, P, f"{pre}experts.{e}.")
     else:
@@ -174,7 +180,7 @@ def mha(q_in, kv_in, P, pre, heads=8):
     return F.linear(o, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
 
 
-def attention_block(x, w, text_seq, P, pre, E, eps=None, training=True, anneal=1.0, topk=None):
+def attention_block(x, w, text_seq, P, pre, E, eps=None, training=True, anneal=1.0, topk=None, route=None):
     B, C, H, W = x.shape
     xin = modconv(x, w, P, pre + "proj_in.")  # :539
     xf = xin.permute(0, 2, 3, 1).reshape(B, H * W, C)
@@ -185,7 +191,7 @@ def attention_block(x, w, text_seq, P, pre, E, eps=None, training=True, anneal=1
     xf = xf + mha(ln(xf, "norm2"), tp, P, pre + "cross_attn.")  # :553-555
     xs = xf.reshape(B, H, W, C).permute(0, 3, 1, 2)
     xn3 = ln(xf, "norm3").reshape(B, H, W, C).permute(0, 3, 1, 2)  # :561
-    mo, kl, probs = sparse_moe(xn3, w, P, pre + "moe.", E, eps, training, anneal, topk)  # :564
+    mo, kl, probs = sparse_moe(xn3, w, P, pre + "moe.", E, eps, training, anneal, topk, route)  # :564
     return modconv(xs + mo, w, P, pre + "proj_out."), kl, probs  # :571-574
 
 
@@ -199,11 +205,11 @@ def conv_block(x, w, P, pre):
     return out + skip
 
 
-def gen_block(x, w, text_seq, P, pre, upsample, E, eps=None, training=True, anneal=1.0, topk=None):
+def gen_block(x, w, text_seq, P, pre, upsample, E, eps=None, training=True, anneal=1.0, topk=None, route=None):
     if upsample:  # :657-658
         x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
     x = conv_block(x, w, P, pre + "conv_block.")
-    return attention_block(x, w, text_seq, P, pre + "attn_block.", E, eps, training, anneal, topk)
+    return attention_block(x, w, text_seq, P, pre + "attn_block.", E, eps, training, anneal, topk, route)
 
 
 BLOCKS = (("gen_block_4", False), ("gen_block_8", True), ("gen_block_16", True))
@@ -223,8 +229,9 @@ def mapping(zt, P):
     return F.linear(h, P["mapping.6.weight"], P["mapping.6.bias"])
 
 
-def generator(z, text, P, eps=None, training=True, anneal=1.0, psi=0.7, topk=None):
-    """:762-855.  ``eps`` = list of 3 (eps_f, eps_t, eps_c) tuples, one per MoE block."""
+def generator(z, text, P, eps=None, training=True, anneal=1.0, psi=0.7, topk=None, routes=None):
+    """:762-855.  ``eps`` = list of 3 (eps_f, eps_t, eps_c) tuples, one per MoE block; ``routes`` = optional
+    list of 3 top-k index tensors to replay (topk_route)."""
     B = z.shape[0]
     E = num_experts(P)
     if text.shape[0] != B and text.shape[0] == 1:  # :781-787
@@ -243,7 +250,7 @@ def generator(z, text, P, eps=None, training=True, anneal=1.0, psi=0.7, topk=Non
     img8 = None
     for i, (name, up) in enumerate(BLOCKS):
         x, kl, p = gen_block(x, w, text_seq, P, name + ".", up, E, None if eps is None else eps[i],
-                             training, anneal, topk)
+                             training, anneal, topk, None if routes is None else routes[i])
         kls.append(kl)
         probs.append(p)
         if name == "gen_block_8":
@@ -262,12 +269,21 @@ def wn(PD, pre):
     return v * (g / norm)
 
 
-def discriminator(img, text, PD):
-    h = F.leaky_relu(F.conv2d(img, wn(PD, "conv_layers.0."), PD["conv_layers.0.bias"], stride=2, padding=1), 0.2)
-    h = F.leaky_relu(F.conv2d(h, wn(PD, "conv_layers.2."), PD["conv_layers.2.bias"], stride=2, padding=1), 0.2)
-    t = F.leaky_relu(F.linear(text, wn(PD, "text_projection.0."), PD["text_projection.0.bias"]), 0.2)
+def round_bf16_st(t):
+    """Straight-through bf16 rounding: the value is rounded, the gradient passes unchanged.  Used only to MEASURE
+    the bf16 sensitivity floor of a quantity (tests/steputil.py), never in a parity reference."""
+    return t + (t.detach().bfloat16().float() - t.detach())
+
+
+def discriminator(img, text, PD, rnd=None):
+    """``rnd`` (floor measurements only): applied to the image and to every effective weight."""
+    r = rnd or (lambda t: t)
+    h = F.leaky_relu(F.conv2d(r(img), r(wn(PD, "conv_layers.0.")), PD["conv_layers.0.bias"], stride=2, padding=1),
+                     0.2)
+    h = F.leaky_relu(F.conv2d(h, r(wn(PD, "conv_layers.2.")), PD["conv_layers.2.bias"], stride=2, padding=1), 0.2)
+    t = F.leaky_relu(F.linear(text, r(wn(PD, "text_projection.0.")), PD["text_projection.0.bias"]), 0.2)
     t = t[:, :, None, None].expand(-1, -1, h.shape[2], h.shape[3])  # :898-899
-    out = F.conv2d(torch.cat([h, t], dim=1), wn(PD, "output_layer.0."), PD["output_layer.0.bias"])
+    out = F.conv2d(torch.cat([h, t], dim=1), r(wn(PD, "output_layer.0.")), PD["output_layer.0.bias"])
     return out.reshape(-1)  # :907
 
 
@@ -310,29 +326,36 @@ def clip_loss(images, text, encode_image):
 def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, *, r1_gamma=10.0,
                clip_w16=0.1, clip_w8=0.05, kl_weight_eff=1e-8, balance_weight=0.01, anneal=3.0,
                psi=0.7, topk=None, encode_image=None, d_clip=0.7, g_clip=0.8, acc=1, zero_grads=True,
-               step_optim=True):
+               step_optim=True, routes_d=None, routes_g=None, full=False, d_round=None):
     """Replays one batch of the reference loop with explicit randomness.
 
     ``PG``/``PD`` map reference state_dict keys to leaf tensors (requires_grad
     for parameters); ``optG``/``optD`` are torch AdamW instances over them (the
     reference's own optimizer).  Gradient accumulation (:1272, :1329, :1353, :1413): ``zero_grads`` at
-    the first batch of a window, ``step_optim`` at its last, losses divided by ``acc``.  Returns a dict
-    of logged scalars.
+    the first batch of a window, ``step_optim`` at its last, losses divided by ``acc``.  The loop's loss
+    guards are kept (:1315-1320 skip the batch on a NaN/Inf D loss, :1367-1376 KL clamp / NaN -> 0,
+    :1396-1399 NaN/Inf G loss -> 0).  ``routes_d`` / ``routes_g``: top-k selections to replay in the
+    D-phase / G-phase generator forwards (topk_route).  Returns a dict of logged scalars (``full``: also
+    the images, logits and routing probabilities of the step).  ``d_round`` (floor measurements only) rounds
+    the discriminator's inputs and effective weights (discriminator(rnd=...)).
     """
+    D = lambda img, txt: discriminator(img, txt, PD, d_round)  # noqa: E731
     B = real.shape[0]
     if zero_grads:
         for p in PD.values():
             p.grad = None
     real = real.clone().requires_grad_(True)  # :1276
-    real_pred = discriminator(real, text, PD)  # :1279
+    real_pred = D(real, text)  # :1279
     g, = torch.autograd.grad(real_pred.sum(), real, create_graph=True)  # :1282-1284
     r1 = (r1_gamma / 2) * (g.reshape(B, -1).norm(2, dim=1) ** 2).mean()  # :1285-1286
     with torch.no_grad():  # :1289-1298
-        f16, f8, _, _ = generator(z, text, PG, eps_dphase, True, anneal, psi, topk)
-    fake_pred = discriminator(f16.detach(), text, PD)  # :1299
-    mism_pred = discriminator(real.detach(), text[perm], PD)  # :1303-1305
+        f16d, f8, _, probs_d = generator(z, text, PG, eps_dphase, True, anneal, psi, topk, routes_d)
+    fake_pred = D(f16d.detach(), text)  # :1299
+    mism_pred = D(real.detach(), text[perm])  # :1303-1305
     dgan = d_loss(real_pred, fake_pred, mism_pred)
     dl = dgan + r1
+    if not torch.isfinite(dl):  # :1315-1320 -- `continue`: no backward, no optimizer step, no G phase
+        return {"d_loss_gan": float(dgan.detach()), "r1": float(r1.detach()), "skipped": True}
     (dl / acc).backward()  # :1326
     if step_optim:
         torch.nn.utils.clip_grad_norm_([p for p in PD.values() if p.requires_grad], max_norm=d_clip)  # :1336
@@ -340,20 +363,33 @@ def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, 
     if zero_grads:
         for p in PG.values():
             p.grad = None
-    f16, f8, kl, probs = generator(z, text, PG, eps_gphase, True, anneal, psi, topk)  # :1358-1364
+    f16, f8, kl, probs = generator(z, text, PG, eps_gphase, True, anneal, psi, topk, routes_g)  # :1358-1364
     if kl > 50.0:  # :1369-1370
         kl = torch.clamp(kl, max=50.0)
-    gg = g_loss(discriminator(f16, text, PD))  # :1379-1382
+    if not torch.isfinite(kl):  # :1372-1376
+        kl = torch.tensor(0.0, requires_grad=True)
+    fake_pred_g = D(f16, text)
+    gg = g_loss(fake_pred_g)  # :1379-1382
     if encode_image is not None:
         c16, c8 = clip_loss(f16, text, encode_image), clip_loss(f8, text, encode_image)
     else:
         c16 = c8 = torch.tensor(0.0)
     bal = balance_loss(probs, balance_weight)
     gl = gg + (clip_w16 * c16 + clip_w8 * c8) + bal  # :1393
+    g_zeroed = not bool(torch.isfinite(gl))
+    if g_zeroed:  # :1396-1399
+        gl = torch.tensor(0.0, requires_grad=True)
     gl = gl + kl_weight_eff * kl  # :1402-1404
     (gl / acc).backward()  # :1410
     if step_optim:
         torch.nn.utils.clip_grad_norm_([p for p in PG.values() if p.requires_grad], max_norm=g_clip)  # :1420
         optG.step()
-    return {"d_loss_gan": float(dgan), "r1": float(r1), "g_loss_gan": float(gg), "kl": float(kl),
-            "balance": float(bal), "clip16": float(c16), "clip8": float(c8), "r1_grad": g.detach()}
+    out = {"d_loss_gan": float(dgan.detach()), "r1": float(r1.detach()), "g_loss_gan": float(gg.detach()),
+           "kl": float(kl.detach()), "balance": float(bal.detach()), "clip16": float(c16), "clip8": float(c8),
+           "r1_grad": g.detach(),
+           "skipped": False, "g_zeroed": g_zeroed}
+    if full:
+        out.update(img16=f16.detach(), img8=f8.detach(), img16_d=f16d, probs=[p.detach() for p in probs],
+                   probs_d=probs_d, real_pred=real_pred.detach(), fake_pred=fake_pred.detach(),
+                   mism_pred=mism_pred.detach(), fake_pred_g=fake_pred_g.detach())
+    return out

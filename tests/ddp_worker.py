@@ -1,0 +1,36 @@
+"""Worker of tests/test_ddp_gpu.py: one rank of the product TrainStep under torch.distributed (gloo, every rank on
+cuda:0).  Saves its losses and the averaged gradients the optimizer used to ``<out>/rank<r>.pt``."""
+import os
+import sys
+
+
+def run(rank, world, port, out_dir, B, E):
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (here, repo, os.path.join(repo, "moe-gan_cpsc541_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from steputil import gpu_step, make_inputs
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        real, text, z, eps_d, eps_g, perm = make_inputs(B * world, E, seed=7)
+        sl = slice(rank * B, (rank + 1) * B)
+        local_perm = torch.randperm(B, generator=torch.Generator().manual_seed(100 + rank))
+        ts = gpu_step(E, None, "fp32", "cuda:0")
+        ts.pg, ts.world = dist.group.WORLD, world
+        cu = lambda t: t.to("cuda:0")  # noqa: E731
+        out = ts.step(cu(real[sl].contiguous()), cu(text[sl].contiguous()), cu(z[sl].contiguous()),
+                      [tuple(map(cu, e)) for e in eps_d], [tuple(map(cu, e)) for e in eps_g], cu(local_perm.int()),
+                      anneal=3.0, eff_kl_weight=0.001 * 1e-5)
+        torch.cuda.synchronize()
+        res = {k: out[k].detach().cpu().clone() for k in ("d_losses", "r1", "g_gan", "balance", "d_grad", "g_grad",
+                                                          "d_grad_sumsq", "g_grad_sumsq", "flags")}
+        res["g_data"], res["d_data"] = ts.gs.data.cpu().clone(), ts.ds.data.cpu().clone()
+        res["local_perm"] = local_perm
+        torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,143 @@
+"""Shared set-up for the step-level parity tests: the same seeded weights, inputs and router noise for the
+HIP TrainStep and the CPU oracle (oracle/aurora_cpu.train_step), plus the comparison metrics."""
+import numpy as np
+import torch
+
+from oracle import aurora_cpu as O
+from oracle.recipe import fill_state
+
+EPS_DIMS = [(512, 512), (256, 512), (128, 512)]  # (C, text dim) per MoE block
+
+
+def make_inputs(B, E, seed=0):
+    """real U(-1,1) [B,3,64,64], text / z N(0,1) [B,512], 6 router-noise triples (D phase, G phase), perm."""
+    g = torch.Generator().manual_seed(seed)
+    real = torch.rand(B, 3, 64, 64, generator=g) * 2 - 1
+    text = torch.randn(B, 512, generator=g)
+    z = torch.randn(B, 512, generator=g)
+    eps = [tuple(torch.randn(s, generator=g) for s in ((c, 128), (t, 128), (256, E))) for c, t in EPS_DIMS * 2]
+    perm = torch.randperm(B, generator=g)
+    return real, text, z, eps[:3], eps[3:], perm
+
+
+def oracle_models(E, lr=2e-4, seed_g=0, seed_d=50):
+    """Reference-layout fp32 leaves + the reference's AdamW (betas 0.5/0.999, wd 0.01, :1100-1102), with the
+    clipped gradients captured right before each optimizer step."""
+    from moegan_mi.layout import discriminator_shapes, generator_shapes
+    PG = {n: torch.from_numpy(v) for n, v in fill_state(generator_shapes(E), seed_g).items()}
+    PD = {n: torch.from_numpy(v).requires_grad_(True) for n, v in fill_state(discriminator_shapes(), seed_d).items()}
+    for n, v in PG.items():
+        if not n.split(".")[-1].startswith("epsilon_"):
+            v.requires_grad_(True)
+    optG = torch.optim.AdamW([v for v in PG.values() if v.requires_grad], lr=lr, betas=(0.5, 0.999),
+                             weight_decay=0.01)
+    optD = torch.optim.AdamW(list(PD.values()), lr=lr, betas=(0.5, 0.999), weight_decay=0.01)
+    return PG, PD, optG, optD, _capture(optD, optG, PD, PG)
+
+
+def _capture(optD, optG, PD, PG):
+    grads = {}
+    for opt, which, P in ((optD, "D", PD), (optG, "G", PG)):
+        def pre(o, a, k, which=which, P=P):
+            grads[which] = {n: (None if t.grad is None else t.grad.clone()) for n, t in P.items() if t.requires_grad}
+        opt.register_step_pre_hook(pre)
+    return grads
+
+
+def oracle_clone(PG, PD, optG, optD, lr=2e-4):
+    """Independent copy of the oracle's current parameters and AdamW state (to run a second, perturbed step from
+    the same point), with gradient capture."""
+    PG2 = {n: v.detach().clone().requires_grad_(v.requires_grad) for n, v in PG.items()}
+    PD2 = {n: v.detach().clone().requires_grad_(True) for n, v in PD.items()}
+    optG2 = torch.optim.AdamW([v for v in PG2.values() if v.requires_grad], lr=lr, betas=(0.5, 0.999),
+                              weight_decay=0.01)
+    optD2 = torch.optim.AdamW(list(PD2.values()), lr=lr, betas=(0.5, 0.999), weight_decay=0.01)
+    optG2.load_state_dict(optG.state_dict())
+    optD2.load_state_dict(optD.state_dict())
+    return PG2, PD2, optG2, optD2, _capture(optD2, optG2, PD2, PG2)
+
+
+def gpu_step(E, topk, dtype, dev="cuda", seed_g=0, seed_d=50):
+    from moegan_mi.layout import discriminator_shapes, generator_shapes
+    from moegan_mi.step import StepConfig, TrainStep
+    ts = TrainStep(StepConfig(E=E, topk=topk, dtype=dtype), dev)
+    ts.gs.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(generator_shapes(E), seed_g).items()})
+    ts.ds.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(discriminator_shapes(), seed_d).items()})
+    return ts
+
+
+def cosine(a, b):
+    a = a.detach().double().reshape(-1).cpu()
+    b = b.detach().double().reshape(-1).cpu()
+    na, nb = float(a.norm()), float(b.norm())
+    if na == 0.0 and nb == 0.0:
+        return 1.0
+    if na == 0.0 or nb == 0.0:
+        return 0.0
+    return float((a @ b) / (na * nb))
+
+
+def rel_norm_diff(a, b):
+    a = a.detach().double().reshape(-1).cpu()
+    b = b.detach().double().reshape(-1).cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def topk_margin(probs, k):
+    """log(p_(k) / p_(k+1)): the logit-space gap deciding top-k membership ([T]; +inf when k == E)."""
+    E = probs.shape[1]
+    if k >= E:
+        return torch.full((probs.shape[0],), float("inf"))
+    v = torch.topk(probs.double(), k + 1, dim=1).values
+    return torch.log(v[:, k - 1]) - torch.log(v[:, k])
+
+
+def routing_agreement(topi_dev, probs_dev, probs_ref, k, delta):
+    """Device top-k sets vs the oracle's own top-k on its fp32 probabilities.
+
+    Returns a dict: n tokens; ``self_mismatch`` = tokens whose device selection is not the top-k of the device's
+    own probabilities (must be 0: kernel consistency); ``mismatch``; ``near`` = tokens whose oracle margin
+    log(p_(k)/p_(k+1)) is below ``delta``; ``bad`` = mismatches outside the near-ties; ``drift`` = the largest
+    change of that margin between oracle and device (logit units, measured on the oracle's k-th / (k+1)-th
+    experts) -- the quantity ``delta`` must bound."""
+    pd, pr = probs_dev.detach().float().cpu(), probs_ref.detach().float().cpu()
+    dev = topi_dev.long().cpu().sort(dim=1).values
+    # the device's selection must be a top-k of its own probabilities: min selected >= max unselected (value
+    # based, so exact ties may resolve either way)
+    sel = torch.zeros_like(pd, dtype=torch.bool).scatter_(1, topi_dev.long().cpu(), True)
+    own_ok = pd.masked_fill(~sel, float("inf")).min(dim=1).values >= pd.masked_fill(sel, float("-inf")).max(dim=1).values
+    ref_idx = torch.topk(pr.double(), min(k + 1, pr.shape[1]), dim=1).indices
+    ref = ref_idx[:, :k].sort(dim=1).values
+    mism = (ref != dev).any(dim=1)
+    margin = topk_margin(pr, k)
+    near = margin < delta
+    drift = 0.0
+    if k < pr.shape[1]:
+        a, b = ref_idx[:, k - 1:k], ref_idx[:, k:k + 1]
+        md = torch.log(pd.double().gather(1, a)) - torch.log(pd.double().gather(1, b))
+        drift = float((md.view(-1) - margin).abs().max())
+    return dict(n=int(mism.numel()), self_mismatch=int((~own_ok).sum()), mismatch=int(mism.sum()),
+                near=int(near.sum()), bad=int((mism & ~near).sum()), drift=drift)
+
+
+def nchw(img_nhwc_padded):
+    return img_nhwc_padded[..., :3].permute(0, 3, 1, 2).float().cpu()
+
+
+def np32(t):
+    return np.asarray(t.detach().cpu(), dtype=np.float32)
+
+
+def bf16_r1_floor(PD, real, text):
+    """How far bf16 rounding ALONE moves the R1 input gradient d sum D(real) / d real (t2i_moe_gan.py:1282): the
+    fp32 oracle fed the bf16-rounded image and bf16-rounded weights, vs the plain fp32 oracle (relative L2).  The
+    LeakyReLU masks make this gradient ill-conditioned (a rounded pre-activation near 0 flips its slope), so a
+    bf16 device cannot be held closer than this."""
+    def g_of(P, x):
+        x = x.clone().requires_grad_(True)
+        g, = torch.autograd.grad(O.discriminator(x, text, P).sum(), x)
+        return g
+    bf = lambda t: t.detach().bfloat16().float()  # noqa: E731
+    Pb = {k: (bf(v) if k.endswith("weight_v") else v.detach()) for k, v in PD.items()}
+    P0 = {k: v.detach() for k, v in PD.items()}
+    return rel_norm_diff(g_of(Pb, bf(real)), g_of(P0, real))

@@ -1,0 +1,81 @@
+"""The product's data-parallel path on the GPU: 2 ranks (torch.distributed gloo, both on cuda:0) each run the HIP
+TrainStep on half of a batch; the all-reduced (averaged) D / G gradients, the global balance loss (all-reduced
+[E] expert load) and the updated parameters must equal one process stepping the whole batch (fp32).
+
+The mismatched-text permutation stays per rank: the single-process reference uses the
+block-diagonal permutation the two ranks' local permutations form.  Also rehearses bench.py's multi-rank path
+(hipGraph capture with the collectives as eager segments) with 2 gloo ranks on the one GPU."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from steputil import cosine, gpu_step, make_inputs, rel_norm_diff
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_trainstep_matches_single_process(tmp_path):
+    import torch.multiprocessing as mp
+    from ddp_worker import run
+    world, B, E = 2, 2, 4
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=run, args=(r, world, port, str(tmp_path), B, E)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0, p.exitcode
+    res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    # single process, whole batch, block-diagonal permutation
+    real, text, z, eps_d, eps_g, _ = make_inputs(B * world, E, seed=7)
+    perm = torch.cat([res[r]["local_perm"] + r * B for r in range(world)])
+    ts = gpu_step(E, None, "fp32", "cuda")
+    cu = lambda t: t.to("cuda")  # noqa: E731
+    out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d], [tuple(map(cu, e)) for e in eps_g],
+                  cu(perm.int()), anneal=3.0, eff_kl_weight=0.001 * 1e-5)
+    torch.cuda.synchronize()
+    # the global balance loss is identical on every rank
+    for r in range(world):
+        assert abs(float(res[r]["balance"][0]) - float(out["balance"][0])) <= 1e-4 * float(out["balance"][0]) + 1e-7
+    # per-rank losses average to the whole-batch loss (equal shards)
+    for k in ("d_losses", "r1", "g_gan"):
+        avg = sum(float(res[r][k][0]) for r in range(world)) / world
+        assert abs(avg - float(out[k][0])) <= 1e-4 * abs(float(out[k][0])) + 1e-6, k
+    # averaged gradients == whole-batch gradients; identical updated parameters on every rank
+    for key, ref in (("d_grad", out["d_grad"]), ("g_grad", out["g_grad"])):
+        for r in range(world):
+            got = res[r][key]
+            assert cosine(got, ref) >= 0.99999 and rel_norm_diff(got, ref) <= 1e-3, (key, r)
+    for key, ref in (("d_data", ts.ds.data), ("g_data", ts.gs.data)):
+        assert torch.equal(res[0][key], res[1][key]), key
+        assert rel_norm_diff(res[0][key], ref) <= 1e-5, key
+
+
+def test_bench_two_rank_graph_replay():
+    """bench.py's N>1 path (captured hipGraph segments + eager all-reduces) with 2 gloo ranks on one GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "8", "--one-device", "--backend", "gloo",
+           "--no-cpu-baseline"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    import json
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    rec = json.loads(line)
+    assert rec["n_gpus"] == 2 and rec["finite"] and rec["value"] > 0

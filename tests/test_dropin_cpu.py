@@ -16,7 +16,7 @@ GOLD = os.path.join(REPO, "tests", "golden")
 def _header_symbols():
     txt = open(os.path.join(REPO, "include", "moegan_hip.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return re.findall(r"\b(?:int|const char\*)\s+(mg_\w+)\(", txt)
+    return re.findall(r"\b(?:int|int64_t|const char\*)\s+(mg_\w+)\(", txt)
 
 
 def test_library_exports_every_header_symbol():

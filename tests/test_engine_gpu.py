@@ -243,7 +243,8 @@ def _train_replay(name, cdt="fp32"):
         close(out["r1_grad"][..., :3].permute(0, 3, 1, 2), d["r1_grad" + sfx], rtol=1e-4, what="r1_grad")
     for which, store, before, ref_max in (("D", ts.ds, d_before, 0.7), ("G", ts.gs, g_before, 0.8)):
         n_opt = store.n_opt
-        gn = float(store.grad[:n_opt].double().norm())
+        gbuf = store.acc if acc > 1 else store.grad  # the buffer AdamW stepped with (window accumulator)
+        gn = float(gbuf[:n_opt].double().norm())
         coef = min(1.0, ref_max / (gn + 1e-6))
         for n, (off, numel) in store.offsets.items():
             shape = store.shapes[n]
@@ -251,7 +252,7 @@ def _train_replay(name, cdt="fp32"):
                 assert off >= n_opt, n
                 assert torch.equal(store.data[off:off + numel], before[off:off + numel]), n
                 continue
-            g = (store.grad[off:off + numel] * coef).view(shape).cpu()
+            g = (gbuf[off:off + numel] * coef).view(shape).cpu()
             check_packed(d, f"{which}/grad/{n}", g, rtol=2e-3, atol=1e-8)
             delta = (store.data[off:off + numel] - before[off:off + numel]).view(shape).cpu()
             check_packed(d, f"{which}/delta/{n}", delta, rtol=2e-2, atol=2e-6)
