@@ -36,6 +36,7 @@ from moegan_mi.init import init_discriminator, init_generator  # noqa: E402
 from moegan_mi.layout import discriminator_shapes, generator_shapes  # noqa: E402
 from moegan_mi.params import ParamStore  # noqa: E402
 from moegan_mi.step import StepConfig, TrainStep  # noqa: E402
+from moegan_mi.checkpoint import load_resume, save_resume  # noqa: E402,F401
 
 LATENT_DIM = 512
 TEXT_EMBEDDING_DIM = 512
@@ -62,15 +63,16 @@ def get_clip_model():
     return _clip_model, None
 
 
-def _eps_for(store, E, device):
-    """Fresh router noise for one generator forward (reference draws normal_() per router, :349-351)."""
+def _eps_for(store, generator=None):
+    """Fresh router noise for one generator forward (the reference draws normal_() into its epsilon buffers per
+    router, :349-351); ``generator`` = a torch.Generator (the rank-shared one under data parallelism)."""
     eps = []
     for name in ("gen_block_4", "gen_block_8", "gen_block_16"):
         r = f"{name}.attn_block.moe.router."
         trip = []
         for n in ("epsilon_f", "epsilon_t", "epsilon_c"):
             buf = store.buffers[r + n]
-            buf.normal_()
+            buf.normal_(generator=generator)
             trip.append(buf)
         eps.append(tuple(trip))
     return eps
@@ -196,7 +198,7 @@ class AuroraGenerator(_FlatModule):
             else:
                 raise ValueError(f"Batch size mismatch: z has batch size {B}, but text_embeddings has batch size "
                                  f"{text.shape[0]}")
-        eps = _eps_for(self._store, self.num_experts, z.device) if self.training else None
+        eps = _eps_for(self._store) if self.training else None
         outs = _GenFn.apply(self.flat, z, text, self, float(annealing_factor), float(truncation_psi), self.training,
                             bool(return_intermediate), eps)
         img16, img8, kl = outs[0], outs[1], outs[2]
@@ -333,10 +335,21 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
                      log_interval=10, save_interval=1000, metric_callback=None, use_amp=True,
                      gradient_accumulation_steps=8, checkpoint_activation=True, batch_memory_limit=20.0,
                      max_resolution=16, *, clip_weight_64=None, clip_weight_32=None, num_experts=NUM_EXPERTS,
-                     topk=None, dtype=None, process_group=None, seed=0):
+                     topk=None, dtype=None, process_group=None, seed=0, resume_from=None, save_every_epoch=False):
     """Reference :1029-1669.  ``clip_weight_64``/``clip_weight_32`` (the names train_model.py passes,
     SURVEY.md §0) map to the 16x16 / 8x8 CLIP weights.  ``use_amp`` selects bf16 (the MI355X mixed
-    precision; the reference's fp16 GradScaler is not needed) unless ``dtype`` is given."""
+    precision; the reference's fp16 GradScaler is not needed) unless ``dtype`` is given.
+
+    Data parallel (``process_group``, one process per GPU): z and the mismatch permutation come from a per-rank
+    generator, the router noise from a generator seeded identically on every rank (one weight sample per
+    forward for the whole global batch); a DistributedSampler is re-seeded every epoch
+    (``set_epoch``); validation runs on every rank's shard and its sums are all-reduced, and the early-stop
+    decision of ``metric_callback`` (called on rank 0) is broadcast so every rank leaves the loop together.
+
+    Loss guards (:1315-1320, :1367-1376, :1396-1399) run inside the step on the device; the loop reads the
+    step's flag word once per batch to print the reference's warnings and to not count a skipped batch.
+    ``resume_from``: a resume checkpoint (:1484-1491 layout, ours or the reference's) to start from;
+    ``save_every_epoch``: write that layout after every epoch (the reference's commented-out :1642-1652)."""
     os.makedirs(save_dir, exist_ok=True)
     if clip_weight_64 is not None:
         clip_weight_16 = clip_weight_64
@@ -345,86 +358,132 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
     device = torch.device(device)
     if dtype is None:
         dtype = "bf16" if use_amp else "fp32"
+    dist = None
+    rank, world = 0, 1
+    if process_group is not None:
+        import torch.distributed as dist
+        rank, world = dist.get_rank(process_group), dist.get_world_size(process_group)
     generator = AuroraGenerator(num_experts=num_experts, topk=topk, dtype=dtype, seed=seed).to(device)
     discriminator = AuroraDiscriminator(dtype=dtype, seed=seed + 1).to(device)
     if checkpoint_activation:
         generator.enable_checkpointing()
+    start_epoch, step = 0, 0
+    if resume_from is not None:
+        start_epoch, step = load_resume(resume_from, generator, discriminator)
+        print(f"Resumed from {resume_from}: epoch {start_epoch}, step {step}")
     cfg = StepConfig(E=num_experts, topk=topk, dtype=dtype, r1_gamma=r1_gamma, clip_weight_16=clip_weight_16,
                      clip_weight_8=clip_weight_8, balance_weight=balance_weight, beta1=beta1, beta2=beta2)
     ts = TrainStep(cfg, device, process_group=process_group, gstore=generator._store, dstore=discriminator._store)
-    print(f"Generator parameters: {generator._store.n_opt + (generator._store.total - generator._store.n_opt):,}")
+    if _clip_model is not None:  # CLIP terms of the generator loss (logging / guard only: no gradient, :98-101)
+        ts.clip_encoder = _clip_model.encode_image
+    if rank == 0:
+        print(f"Generator parameters: {generator._store.n_opt + (generator._store.total - generator._store.n_opt):,}")
     lrs = _lr_schedule(lr, num_epochs, lr_warmup_epochs)
     gan_loss = AuroraGANLoss(device)
     acc = max(1, int(gradient_accumulation_steps))
-    step = 0
+    # randomness: per-rank z / permutation, rank-shared router noise
+    g_local = torch.Generator(device=device).manual_seed(1_000_003 * (seed + 1) + 7919 * rank)
+    g_shared = torch.Generator(device=device).manual_seed(1_000_003 * (seed + 1) + 17)
     from tqdm import tqdm
-    for epoch in range(num_epochs):
+    for epoch in range(start_epoch, num_epochs):
         cur_lr = lrs[epoch]
         kl_warmup = min(1.0, (epoch / kl_annealing_epochs) ** 2)
         eff_kl = kl_weight * (1e-5 + (1.0 - 1e-5) * kl_warmup)
         temperature_factor = max(1.0, 3.0 - epoch * 0.1)
-        print(f"\n{'=' * 20} Epoch {epoch + 1}/{num_epochs} {'=' * 20}")
-        print(f"  LR: {cur_lr:.6f}  Temperature factor: {temperature_factor:.2f}  Effective KL weight: {eff_kl:.8f}")
-        pbar = tqdm(dataloader, desc=f"Epoch {epoch + 1}/{num_epochs}")
+        sampler = getattr(dataloader, "sampler", None)
+        if hasattr(sampler, "set_epoch"):
+            sampler.set_epoch(epoch)
+        if rank == 0:
+            print(f"\n{'=' * 20} Epoch {epoch + 1}/{num_epochs} {'=' * 20}")
+            print(f"  LR: {cur_lr:.6f}  Temperature factor: {temperature_factor:.2f}  "
+                  f"Effective KL weight: {eff_kl:.8f}")
+        pbar = tqdm(dataloader, desc=f"Epoch {epoch + 1}/{num_epochs}", disable=rank != 0)
         n_batches = len(dataloader)
         for batch_idx, (real, text) in enumerate(pbar):
             real = real.to(device, non_blocking=True).float()
             text = text.to(device, non_blocking=True).float()
             B = real.shape[0]
-            z = torch.randn(B, LATENT_DIM, device=device)
-            eps_d = _eps_for(generator._store, num_experts, device)
-            eps_d = [tuple(t.clone() for t in trip) for trip in eps_d]
-            eps_g = _eps_for(generator._store, num_experts, device)
-            perm = torch.randperm(B, device=device).int()
+            z = torch.randn(B, LATENT_DIM, device=device, generator=g_local)
+            eps_d = [tuple(t.clone() for t in trip) for trip in _eps_for(generator._store, g_shared)]
+            eps_g = _eps_for(generator._store, g_shared)
+            perm = torch.randperm(B, device=device, generator=g_local).int()
             zero = batch_idx % acc == 0
             stp = (batch_idx + 1) % acc == 0 or (batch_idx + 1) == n_batches
             out = ts.step(real, text, z, eps_d, eps_g, perm, anneal=temperature_factor, lr_g=cur_lr, lr_d=cur_lr,
                           eff_kl_weight=eff_kl, acc=acc, zero_grads=zero, step_optim=stp)
-            if step % log_interval == 0:
+            flags = int(out["flags"][0])  # the step's guard word: one read per batch
+            if flags & 1:
+                print("⚠️ NaN/Inf detected in discriminator loss! Skipping this batch.")
+                continue
+            if flags & 2:
+                print("⚠️ NaN or Inf detected in generator loss! Resetting to zero.")
+            if step % log_interval == 0 and rank == 0:
                 d_gan, r1 = float(out["d_losses"][0]), float(out["r1"][0])
                 g_gan, bal, kl = float(out["g_gan"][0]), float(out["balance"][0]), float(out["kl"][0])
-                if not (math.isfinite(d_gan) and math.isfinite(g_gan)):
-                    print("⚠️ NaN/Inf detected in losses")
+                c16 = float(out["clip16"][0]) if out["clip16"] is not None else 0.0
+                c8 = float(out["clip8"][0]) if out["clip8"] is not None else 0.0
+                g_loss = 0.0 if flags & 2 else g_gan + clip_weight_16 * c16 + clip_weight_8 * c8 + bal
+                g_loss += eff_kl * kl
                 logger.info(f"\nStep [{step}] Epoch [{epoch + 1}] Batch [{batch_idx}/{n_batches}] "
-                            f"D_loss: {d_gan + r1:.4f} (GAN: {d_gan:.4f}, R1: {r1:.4f}), G_loss: "
-                            f"{g_gan + bal + eff_kl * kl:.4f} (GAN: {g_gan:.4f}, KL: {kl:.4f}, Balance: {bal:.4f})")
+                            f"D_loss: {d_gan + r1:.4f} (GAN: {d_gan:.4f}, R1: {r1:.4f}), "
+                            f"G_loss: {g_loss:.4f} (GAN: {g_gan:.4f}, Clip16: {c16:.4f}, Clip8: {c8:.4f}, "
+                            f"KL: {kl:.4f}, Balance: {bal:.4f})")
                 pbar.set_postfix({"D_loss": f"{d_gan:.3f}", "R1": f"{r1:.3f}", "G_loss": f"{g_gan:.3f}",
-                                  "KL": f"{kl:.4f}", "Balance": f"{bal:.4f}"})
+                                  "KL": f"{kl:.4f}", "Balance": f"{bal:.4f}", "Clip16": f"{c16:.3f}",
+                                  "Clip8": f"{c8:.3f}"})
             step += 1
         pbar.close()
+        if save_every_epoch and rank == 0:
+            save_resume(os.path.join(save_dir, f"aurora_checkpoint_epoch_{epoch + 1}.pt"), generator, discriminator,
+                        epoch + 1, step, cur_lr, cur_lr, (beta1, beta2))
         if val_dataloader is not None:
-            vm = _validate(generator, discriminator, val_dataloader, gan_loss, temperature_factor, eff_kl, device)
-            print(f"Validation Results - D_loss: {vm['val_d_loss']:.4f}, G_loss: {vm['val_g_loss']:.4f}, "
-                  f"Clip_Loss_16: {vm['val_clip_loss_16']:.4f}, Clip_Loss_8: {vm['val_clip_loss_8']:.4f}")
-            if metric_callback and not metric_callback(epoch, vm):
-                print("Early stopping triggered by metric callback")
+            vm = _validate(generator, discriminator, val_dataloader, gan_loss, temperature_factor, eff_kl, device,
+                           process_group, g_local)
+            stop = False
+            if rank == 0:
+                print(f"Validation Results - D_loss: {vm['val_d_loss']:.4f}, G_loss: {vm['val_g_loss']:.4f}, "
+                      f"Clip_Loss_16: {vm['val_clip_loss_16']:.4f}, Clip_Loss_8: {vm['val_clip_loss_8']:.4f}")
+                stop = bool(metric_callback and not metric_callback(epoch, vm))
+            if dist is not None:  # every rank leaves together (the next all-reduce would otherwise hang)
+                flag = torch.tensor([1 if stop else 0], device=device, dtype=torch.int32)
+                dist.broadcast(flag, src=dist.get_global_rank(process_group, 0), group=process_group)
+                stop = bool(flag.item())
+            if stop:
+                if rank == 0:
+                    print("Early stopping triggered by metric callback")
                 break
     return generator, discriminator
 
 
-def _validate(generator, discriminator, loader, gan_loss, temperature_factor, eff_kl, device):
-    """Reference validation loop :1519-1639 (eval-mode generator: mean router weights, hard top-1)."""
+def _validate(generator, discriminator, loader, gan_loss, temperature_factor, eff_kl, device, process_group=None,
+              gen=None):
+    """Reference validation loop :1519-1639 (eval-mode generator: mean router weights, hard top-1).  Under data
+    parallelism each rank evaluates its shard and the per-sample sums are all-reduced."""
     generator.eval()
     discriminator.eval()
-    tot = {"val_d_loss": 0.0, "val_g_loss": 0.0, "val_clip_loss_16": 0.0, "val_clip_loss_8": 0.0}
-    n = 0
+    keys = ("val_d_loss", "val_g_loss", "val_clip_loss_16", "val_clip_loss_8")
+    tot = torch.zeros(len(keys) + 1, dtype=torch.float64)
     with torch.no_grad():
         for real, text in loader:
             real, text = real.to(device).float(), text.to(device).float()
             B = real.shape[0]
-            z = torch.randn(B, LATENT_DIM, device=device)
+            z = torch.randn(B, LATENT_DIM, device=device, generator=gen)
             f16, f8, kl = generator(z, text, return_intermediate=True, annealing_factor=temperature_factor)
             rp = discriminator(real, text)
             fp = discriminator(f16, text)
-            mp = discriminator(real, text[torch.randperm(B, device=device)])
-            tot["val_d_loss"] += float(gan_loss.discriminator_loss(rp, fp, mp)) * B
-            tot["val_g_loss"] += float(gan_loss.generator_loss(fp, kl, kl_weight=eff_kl)) * B
-            tot["val_clip_loss_16"] += float(gan_loss.compute_clip_loss(f16, text)) * B
-            tot["val_clip_loss_8"] += float(gan_loss.compute_clip_loss(f8, text)) * B
-            n += B
+            mp = discriminator(real, text[torch.randperm(B, device=device, generator=gen)])
+            vals = (gan_loss.discriminator_loss(rp, fp, mp), gan_loss.generator_loss(fp, kl, kl_weight=eff_kl),
+                    gan_loss.compute_clip_loss(f16, text), gan_loss.compute_clip_loss(f8, text))
+            tot += torch.tensor([float(v) * B for v in vals] + [B], dtype=torch.float64)
+    if process_group is not None:
+        import torch.distributed as dist
+        t = tot.to(device)
+        dist.all_reduce(t, group=process_group)
+        tot = t.cpu()
     generator.train()
     discriminator.train()
-    vm = {k: v / max(n, 1) for k, v in tot.items()}
+    n = max(float(tot[-1]), 1.0)
+    vm = {k: float(tot[i]) / n for i, k in enumerate(keys)}
     vm["val_clip_loss"] = vm["val_clip_loss_16"]
     return vm
 

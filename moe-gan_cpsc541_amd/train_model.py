@@ -67,6 +67,11 @@ def parse_args(argv=None):
     p.add_argument("--topk", type=int, default=None, help="sparse top-k routing (default: dense soft combine)")
     p.add_argument("--dtype", choices=["fp32", "bf16"], default="bf16")
     p.add_argument("--gradient_accumulation_steps", type=int, default=8)
+    p.add_argument("--resume", type=str, default=None, help="resume checkpoint (t2i_moe_gan.py:1484-1491 layout)")
+    p.add_argument("--save_every_epoch", action="store_true", help="write a resume checkpoint after every epoch")
+    p.add_argument("--hyperparameters", type=str, default=None,
+                   help="SageMaker-style hyperparameters.json (string values, sagemaker_train.py:85-102); its keys "
+                        "override the flags above")
     return p.parse_args(argv)
 
 
@@ -105,16 +110,24 @@ def main(argv=None):
     workers = max(1, min(8, (os.cpu_count() or 2) // 2))
     train_dl = DataLoader(train_ds, batch_size=args.batch_size, shuffle=sampler is None, sampler=sampler,
                           num_workers=workers, pin_memory=True, drop_last=True)
-    val_dl = DataLoader(val_ds, batch_size=args.batch_size, shuffle=False, num_workers=workers,
-                        pin_memory=True) if val_ds is not None and rank == 0 else None
-    G, D = M.train_aurora_gan(train_dl, val_dataloader=val_dl, num_epochs=args.epochs, lr=args.lr,
-                              beta1=args.beta1, beta2=args.beta2, r1_gamma=args.r1_gamma,
-                              clip_weight_64=args.clip_weight_64, clip_weight_32=args.clip_weight_32,
-                              kl_weight=args.kl_weight, balance_weight=args.balance_weight, device=device,
-                              save_dir=args.save_dir, log_interval=args.log_interval,
-                              save_interval=args.save_interval, num_experts=args.num_experts, topk=args.topk,
-                              dtype=args.dtype, gradient_accumulation_steps=args.gradient_accumulation_steps,
-                              process_group=pg)
+    val_dl = None
+    if val_ds is not None:  # every rank validates its shard; the sums are all-reduced inside the loop
+        vs = None
+        if world > 1:
+            from torch.utils.data.distributed import DistributedSampler
+            vs = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False, drop_last=False)
+        val_dl = DataLoader(val_ds, batch_size=args.batch_size, shuffle=False, sampler=vs, num_workers=workers,
+                            pin_memory=True)
+    kw = dict(num_epochs=args.epochs, lr=args.lr, beta1=args.beta1, beta2=args.beta2, r1_gamma=args.r1_gamma,
+              clip_weight_16=args.clip_weight_64, clip_weight_8=args.clip_weight_32, kl_weight=args.kl_weight,
+              balance_weight=args.balance_weight, log_interval=args.log_interval, save_interval=args.save_interval,
+              gradient_accumulation_steps=args.gradient_accumulation_steps)
+    if args.hyperparameters:
+        from moegan_mi.hparams import given_train_kwargs, load_sagemaker_hyperparameters
+        kw.update(given_train_kwargs(load_sagemaker_hyperparameters(args.hyperparameters)))
+    G, D = M.train_aurora_gan(train_dl, val_dataloader=val_dl, device=device, save_dir=args.save_dir,
+                              num_experts=args.num_experts, topk=args.topk, dtype=args.dtype, process_group=pg,
+                              resume_from=args.resume, save_every_epoch=args.save_every_epoch, **kw)
     if rank == 0:
         torch.save({"generator": G.state_dict(), "discriminator": D.state_dict()},
                    os.path.join(args.save_dir, "aurora_final.pt"))

@@ -326,7 +326,7 @@ def clip_loss(images, text, encode_image):
 def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, *, r1_gamma=10.0,
                clip_w16=0.1, clip_w8=0.05, kl_weight_eff=1e-8, balance_weight=0.01, anneal=3.0,
                psi=0.7, topk=None, encode_image=None, d_clip=0.7, g_clip=0.8, acc=1, zero_grads=True,
-               step_optim=True, routes_d=None, routes_g=None, full=False, d_round=None):
+               step_optim=True, routes_d=None, routes_g=None, full=False, d_round=None, after_d_step=None):
     """Replays one batch of the reference loop with explicit randomness.
 
     ``PG``/``PD`` map reference state_dict keys to leaf tensors (requires_grad
@@ -337,7 +337,8 @@ def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, 
     :1396-1399 NaN/Inf G loss -> 0).  ``routes_d`` / ``routes_g``: top-k selections to replay in the
     D-phase / G-phase generator forwards (topk_route).  Returns a dict of logged scalars (``full``: also
     the images, logits and routing probabilities of the step).  ``d_round`` (floor measurements only) rounds
-    the discriminator's inputs and effective weights (discriminator(rnd=...)).
+    the discriminator's inputs and effective weights (discriminator(rnd=...)).  ``after_d_step(PD)`` is called
+    right after the discriminator's optimizer step (tests use it to continue the G phase from a given D).
     """
     D = lambda img, txt: discriminator(img, txt, PD, d_round)  # noqa: E731
     B = real.shape[0]
@@ -360,6 +361,8 @@ def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, 
     if step_optim:
         torch.nn.utils.clip_grad_norm_([p for p in PD.values() if p.requires_grad], max_norm=d_clip)  # :1336
         optD.step()
+        if after_d_step is not None:
+            after_d_step(PD)
     if zero_grads:
         for p in PG.values():
             p.grad = None

@@ -141,3 +141,44 @@ def bf16_r1_floor(PD, real, text):
     Pb = {k: (bf(v) if k.endswith("weight_v") else v.detach()) for k, v in PD.items()}
     P0 = {k: v.detach() for k, v in PD.items()}
     return rel_norm_diff(g_of(Pb, bf(real)), g_of(P0, real))
+
+
+class _RoundBoth(torch.autograd.Function):
+    """bf16 rounding of a value and of the gradient flowing back through it."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.bfloat16().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+class bf16_module_rounding:
+    """Context manager: the oracle's module outputs (modulated convs, MTMs, convolution / attention blocks,
+    expert FFNs) and the gradients flowing back through them are rounded to bf16 -- a coarse model of a bf16
+    device (which also rounds many more intermediates and its weights).  With ``d_round=oracle.round_bf16_st``
+    on the discriminator this gives the bf16 FLOOR of a whole step's gradients: how far bf16 storage alone,
+    in otherwise exact fp32 arithmetic, moves them."""
+    NAMES = ("modconv", "mtm", "attention_block", "expert_ffn", "conv_block")
+
+    def __enter__(self):
+        self.orig = {n: getattr(O, n) for n in self.NAMES}
+        for n, f in self.orig.items():
+            def wrap(*a, f=f, **k):
+                r = f(*a, **k)
+                return (_RoundBoth.apply(r[0]),) + tuple(r[1:]) if isinstance(r, tuple) else _RoundBoth.apply(r)
+            setattr(O, n, wrap)
+        return self
+
+    def __exit__(self, *exc):
+        for n, f in self.orig.items():
+            setattr(O, n, f)
+        return False
+
+
+def whole(grads, names=None):
+    """One vector of every gradient in ``grads`` (dict name -> tensor or None), in a fixed name order."""
+    names = sorted(n for n, v in grads.items() if v is not None) if names is None else names
+    return torch.cat([grads[n].reshape(-1) for n in names]), names

@@ -36,7 +36,7 @@ def test_generator_module_train_vs_F7(monkeypatch):
     d, _ = load("F7_generator")
     G = _gen(M)
     eps = [[T(d[f"eps{i}/{n}"]).to(DEV) for n in ("epsilon_f", "epsilon_t", "epsilon_c")] for i in range(3)]
-    monkeypatch.setattr(M, "_eps_for", lambda store, E, device: eps)
+    monkeypatch.setattr(M, "_eps_for", lambda store, generator=None: eps)
     z = T(d["z"]).to(DEV).requires_grad_(True)
     text = T(d["text"]).to(DEV).requires_grad_(True)
     img16, img8, kl, probs = G(z, text, return_routing=True, return_intermediate=True, annealing_factor=3.0)
