@@ -336,6 +336,7 @@ template <int E>
 __global__ void k_router_bwd(const float* __restrict__ probs, const float* __restrict__ zlog,
                              const int* __restrict__ topi, const float* __restrict__ gate,
                              const float* __restrict__ g_gate, const float* __restrict__ g_probs,
+                             const float* __restrict__ g_logits,
                              const float* __restrict__ coef, int Tn, int k, int lgHW, const float* __restrict__ temp,
                              float anneal, float* __restrict__ g_raw, float* __restrict__ gsum,
                              float* __restrict__ g_temp) {
@@ -419,11 +420,13 @@ __global__ void k_router_bwd(const float* __restrict__ probs, const float* __res
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       float gl = s[e] * (gs_[e] - d2);
+      if (g_logits) gl += g_logits[(int64_t)t * E + e];  // the router's second output, logits (:378-381)
       gl = (z[e] >= -20.f && z[e] <= 20.f) ? gl : 0.f;
       gt_part += -gl * z[e] / te;
       float gr = gl / te;
       g_raw[(int64_t)t * E + e] = gr;
-      atomicAdd(&red[bl * E + e], gr);
+      if (lgHW >= 4) atomicAdd(&red[bl * E + e], gr);
+      else atomicAdd(&gsum[(int64_t)(t >> lgHW) * E + e], gr);  // < 16 tokens per image: > 18 images per block
     }
   }
   gt_part = wave_sum(gt_part);
@@ -431,7 +434,8 @@ __global__ void k_router_bwd(const float* __restrict__ probs, const float* __res
   __syncthreads();
   int tl = min(Tn, t0 + (int)blockDim.x) - 1;
   int nimg = (tl >> lgHW) - b0 + 1;
-  for (int i = threadIdx.x; i < nimg * E; i += blockDim.x) atomicAdd(&gsum[(int64_t)b0 * E + i], red[i]);
+  if (lgHW >= 4)
+    for (int i = threadIdx.x; i < nimg * E; i += blockDim.x) atomicAdd(&gsum[(int64_t)b0 * E + i], red[i]);
   if (threadIdx.x == 0 && g_temp) {
     float tt = 0.f;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tt += tred[i];
@@ -855,16 +859,17 @@ extern "C" int mg_moe_gate_grad(int dtype, int gout_dtype, const void* gout, int
 }
 
 extern "C" int mg_router_bwd(const float* probs, const float* zlog, const int32_t* topi, const float* gate,
-                             const float* g_gate, const float* g_probs, const float* coef, int T, int E, int k, int HW,
+                             const float* g_gate, const float* g_probs, const float* g_logits, const float* coef, int T,
+                             int E, int k, int HW,
                              const float* temperature, float anneal, float* g_raw, float* gsum, float* g_temp,
                              void* stream) {
   MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
-  MG_REQUIRE(HW >= 16 && (HW & (HW - 1)) == 0, "HW must be a power of two >= 16");
+  MG_REQUIRE(HW >= 1 && (HW & (HW - 1)) == 0, "HW must be a power of two");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int lg = 0;
   while ((1 << lg) < HW) ++lg;
   dim3 grid(cdiv(T, 256));
-#define L_(EE) hipLaunchKernelGGL((k_router_bwd<EE>), grid, dim3(256), 0, st, probs, zlog, topi, gate, g_gate, g_probs, coef, T, k, lg, \
+#define L_(EE) hipLaunchKernelGGL((k_router_bwd<EE>), grid, dim3(256), 0, st, probs, zlog, topi, gate, g_gate, g_probs, g_logits, coef, T, k, lg, \
                                   temperature, anneal, g_raw, gsum, g_temp)
   if (E == 4) L_(4); else if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
 #undef L_

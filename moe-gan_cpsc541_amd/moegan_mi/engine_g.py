@@ -35,9 +35,17 @@ def _modconv_prefixes(E=None):
     return out
 
 
+def _offset_prefixes():
+    return [f"{name}.conv_block.{m}.offset_net.0." for name, *_ in GEN_BLOCKS for m in ("mtm1", "mtm2")]
+
+
 class GeneratorEngine:
-    def __init__(self, store, E, topk=None, cdt=torch.float32):
+    def __init__(self, store, E, topk=None, cdt=torch.float32, modconvs=None, offset_nets=None):
+        """``modconvs`` [(prefix, k)] / ``offset_nets`` [prefix]: the modulated convs and MTM offset heads prep()
+        packs -- the whole generator's by default; the sub-module API (modules.py) passes its own."""
         self.st = store
+        self.mc_list = _modconv_prefixes() if modconvs is None else list(modconvs)
+        self.off_list = _offset_prefixes() if offset_nets is None else list(offset_nets)
         self.E = E
         self.k = topk or E
         self.cdt = cdt
@@ -90,7 +98,7 @@ class GeneratorEngine:
             self.style_gb = self.st.grad[b0:b0 + nrows]
         self._mean_latent = None  # truncation centre: mapping of zeros, a function of the weights only
         pk = {}
-        for pre, k in _modconv_prefixes():
+        for pre, k in self.mc_list:
             W = self.P(pre + "weight")
             Cout = W.shape[0]
             rows = max(Cout, 8)
@@ -103,11 +111,9 @@ class GeneratorEngine:
             else:
                 ent["w"] = self.Pc(pre + "weight").view(Cout, -1)
             pk[pre] = ent
-        for name, _, _, _, _ in GEN_BLOCKS:
-            for m in ("mtm1", "mtm2"):
-                pre = f"{name}.conv_block.{m}.offset_net.0."
-                W = self.P(pre + "weight")
-                pk[pre] = {"w": ops.pack_conv(W, self.cdt), "wflip": ops.pack_conv(W, self.cdt, flip=True)}
+        for pre in self.off_list:
+            W = self.P(pre + "weight")
+            pk[pre] = {"w": ops.pack_conv(W, self.cdt), "wflip": ops.pack_conv(W, self.cdt, flip=True)}
         self.packs = pk
 
     # ------------------------------------------------------------------
@@ -428,7 +434,7 @@ class GeneratorEngine:
     def _cbuf(self):
         return self.st.shadow if self.st.shadow is not None else self.st.data
 
-    def moe_bwd(self, pre, sv, g_out, g_tok, gw, coef=None, kl_coef=None, g_probs=None):
+    def moe_bwd(self, pre, sv, g_out, g_tok, gw, coef=None, kl_coef=None, g_probs=None, g_logits=None):
         """g_out: grad of (resid + moe) [T, C]; writes g_tok (grad of the LN3 tokens); accumulates gw."""
         r = pre + "router."
         tok, w, Y, Pre = sv["tok"], sv["w"], sv["Y"], sv["Pre"]
@@ -460,7 +466,8 @@ class GeneratorEngine:
                                ops.grouped_colsum(gP, row_off, Hd, n, gb1)), gP)
         # router
         g_raw, gsum = ops.router_bwd(sv["probs"], sv["zlog"], sv["topi"], sv["gate"], g_gate, g_probs, coef,
-                                     sv["HW"], self.P(r + "temperature"), sv["anneal"], self.G(r + "temperature"), B)
+                                     sv["HW"], self.P(r + "temperature"), sv["anneal"], self.G(r + "temperature"), B,
+                                     g_logits=g_logits)
         ops.moe_token_grad(gX, sv["pos_of"], g_raw, sv["Wfc"], g_tok, k)
         G1 = ops.zeros(C, E, device=self.dev)
         ops.router_feat_grad(tok, g_raw, G1)

@@ -477,13 +477,13 @@ def moe_gate_grad(gout, Y, pos_of, T, k):
     return g
 
 
-def router_bwd(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, anneal, g_temp, B):
+def router_bwd(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, anneal, g_temp, B, g_logits=None):
     T, E_ = probs.shape
     k = topi.shape[1]
     g_raw = torch.empty(T, E_, device=probs.device, dtype=torch.float32)
     gsum = zeros(B, E_, device=probs.device)
-    call("mg_router_bwd", ptr(probs), ptr(zlog), ptr(topi), ptr(gate), ptr(g_gate), ptr(g_probs), ptr(coef), T, E_,
-         k, HW, ptr(temperature), anneal, ptr(g_raw), ptr(gsum), ptr(g_temp), S())
+    call("mg_router_bwd", ptr(probs), ptr(zlog), ptr(topi), ptr(gate), ptr(g_gate), ptr(g_probs), ptr(g_logits),
+         ptr(coef), T, E_, k, HW, ptr(temperature), anneal, ptr(g_raw), ptr(gsum), ptr(g_temp), S())
     return g_raw, gsum
 
 

@@ -1,7 +1,10 @@
 """Drop-in replacement for the reference module ``t2i_moe_gan`` (moegan/t2i_moe_gan.py) on MI355X.
 
 Same public names and signatures -- ``train_aurora_gan``, ``AuroraGenerator``,
-``AuroraDiscriminator``, ``AuroraGANLoss``, ``sample_aurora_gan``, the module constants -- and
+``AuroraDiscriminator``, ``AuroraGANLoss``, ``sample_aurora_gan``, the sub-module classes
+(``ModulatedConv``, ``ModulatedTransformationModule``, ``SparseExpertFFN``, ``BayesianRouter``,
+``SparseMoE``, ``AttentionBlock``, ``ConvolutionBlock``, ``GenerativeBlock``, moegan_mi/modules.py),
+``create_optimizer_for_active_blocks``, the module constants -- and
 the same ``state_dict`` keys/shapes, so the reference's entry points (train_model.py,
 sagemaker_train.py, inference.py, generate_images.py) work by pointing ``sys.path`` here.
 
@@ -37,6 +40,9 @@ from moegan_mi.layout import discriminator_shapes, generator_shapes  # noqa: E40
 from moegan_mi.params import ParamStore  # noqa: E402
 from moegan_mi.step import StepConfig, TrainStep  # noqa: E402
 from moegan_mi.checkpoint import load_resume, save_resume  # noqa: E402,F401
+from moegan_mi.modules import (AttentionBlock, BayesianRouter, ConvolutionBlock, GenerativeBlock,  # noqa: E402,F401
+                               ModulatedConv, ModulatedTransformationModule, SparseExpertFFN, SparseMoE,
+                               create_optimizer_for_active_blocks)
 
 LATENT_DIM = 512
 TEXT_EMBEDDING_DIM = 512
