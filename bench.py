@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the captured hipGraphs")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N>1 (nccl = RCCL)")
+    ap.add_argument("--no-families", action="store_true",
+                    help="skip the per-family roofline attribution step (one extra eager step after the timed region)")
     ap.add_argument("--one-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box, with --backend gloo)")
     return ap.parse_args()
@@ -209,6 +211,57 @@ def main():
         elapsed = float(t)
     finite = bool(torch.isfinite(out["d_losses"]).all() and torch.isfinite(out["g_gan"]).all())
 
+    families = fam_meta = None
+    if not args.no_families and rank == 0 and world == 1:
+        # per-family roofline: one more eager step (outside the timed region) with every C-ABI call bracketed
+        # by HIP events and its algorithmic work computed from its shape arguments (moegan_mi/roofline.py)
+        from moegan_mi.roofline import Attribution
+        refill()
+        with Attribution() as at:
+            if graph is not None:
+                graph.run_eager(run_step)
+            else:
+                run_step()
+        families = at.summary(steps=1, peak_tflops=MFMA_PEAK_TFLOPS[args.dtype], peak_gbs=HBM_PEAK_GBS)
+        fam_total = sum(f["ms_per_step"] for f in families)
+        if rank == 0:
+            print(f"[bench] family attribution: {fam_total:.3f} ms of call time in the attributed step "
+                  f"(host_bound={at.host_bound})", file=sys.stderr, flush=True)
+
+        def _prof(name):  # committed rocprofv3 records of this same workload (tools/gpu_families.sh)
+            path = os.path.join(REPO, "profiles", name)
+            if not os.path.exists(path):
+                return None
+            rec = json.load(open(path))
+            ok = rec.get("batch") == B and rec.get("dtype") == args.dtype and rec.get("experts") == E
+            return rec if ok else None
+
+        ftime, ftraf = _prof("family_time.json"), _prof("family_traffic.json")
+        for f in families:
+            f["event_ms_per_step"] = f.pop("ms_per_step")  # live, includes ~3 us of event overhead per call
+            t = ftime["families"].get(f["family"]) if ftime else None
+            if t is not None:  # achieved rate over the rocprof kernel time (the event pairs inflate small calls)
+                f["rocprof_ms_per_step"] = t["ms_per_step"]
+                ms_k = t["ms_per_step"]
+                work = f.get("gflop_per_step", 0) * 1e9 if f["bound"] == "mfma" else f.get("mb_per_step", 0) * 1e6
+                if f["bound"] == "mfma" and ms_k > 0:
+                    f["achieved"] = round(work / (ms_k * 1e-3) / 1e12, 1)
+                    f["frac"] = round(f["achieved"] / f["peak"], 4)
+                elif f["bound"] == "hbm" and ms_k > 0:
+                    f["achieved"] = round(work / (ms_k * 1e-3) / 1e9, 1)
+                    f["frac"] = round(f["achieved"] / f["peak"], 4)
+                f["time_source"] = "rocprof"
+            elif f["bound"] is not None:
+                f["time_source"] = "hip events (live)"
+            tr = ftraf["families"].get(f["family"]) if ftraf else None
+            if tr is not None:
+                f["traffic_mb_per_step"] = tr["mb_per_step"]
+        fam_meta = {"work": "live: algorithmic FLOPs / bytes from each C-ABI call's shape arguments "
+                            "(moe-gan_cpsc541_amd/moegan_mi/roofline.py)",
+                    "time": ftime["source"] if ftime else "live HIP events per call",
+                    "profile_busy_ms_per_step": ftime["busy_ms_per_step"] if ftime else None,
+                    "traffic": ftraf["source"] if ftraf else None}
+
     if rank == 0:
         imgs = B * world * args.steps
         value = imgs / elapsed
@@ -246,7 +299,8 @@ def main():
                            "launch": "eager" if args.eager else "hipGraph replay"},
                 "step_tflops_algorithmic": round(step_tflops, 2),
                 "step_mfma_frac": round(step_tflops / peak, 4), "finite": finite,
-                "roofline": roof, "cpu_baseline": cpu}
+                "roofline": roof, "roofline_families": families,
+                "roofline_families_sources": fam_meta, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if pg is not None:
         torch.distributed.destroy_process_group()

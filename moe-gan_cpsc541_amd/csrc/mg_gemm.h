@@ -833,7 +833,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 }
 
 
-template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
+// TAG only names the instantiation (1 = MoE expert GEMMs) so profiles can attribute its dispatches.
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP, int TAG = 0>
 __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M, int N, int K, int kchunk, Grouping grp) {
   constexpr int TBK = Tile<T>::BK;
   // ---- resolve tile / group ----
@@ -911,7 +912,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_batch_kernel(BatchArgs<TO, AL, 
 }
 
 // launch helper: picks the grid; grouped-M launches an upper bound of tiles.
-template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, int TAG = 0, class AL, class BL, class EP>
 inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, int K, int splits, Grouping grp,
                         int max_tiles_m, hipStream_t st) {
   constexpr int TBK = Tile<T>::BK;
@@ -925,7 +926,7 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   EP e2 = ep;
   e2.vec_ok = e2.host_vec_ok() ? 1 : 0;
   if (grp.mode == 0) grp.swz = g_mg_tune[MG_TUNE_XCD] == 1 ? 1 : 0;  // measured: no gain at these shapes
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP, TAG>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
                      K, kchunk, grp);
 }
 

@@ -574,20 +574,20 @@ void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_o
     if (g_mg_tune[MG_TUNE_GEMM_TILE] == 257 && N >= 256) {
       if constexpr (BKc) {
         LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
-        launch_gemm<T, 128, 256, true, true>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+        launch_gemm<T, 128, 256, true, true, 1>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
       } else {
         LdMCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
-        launch_gemm<T, 128, 256, true, false>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+        launch_gemm<T, 128, 256, true, false, 1>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
       }
       return;
     }
   }
   if constexpr (BKc) {
     LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
-    launch_gemm<T, 128, 128, true, true>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+    launch_gemm<T, 128, 128, true, true, 1>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
   } else {
     LdMCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
-    launch_gemm<T, 128, 128, true, false>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+    launch_gemm<T, 128, 128, true, false, 1>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
   }
 }
 
@@ -606,9 +606,9 @@ void run_grouped_wgrad(int M, int N, int ngroups, const int32_t* row_off, int to
   ep.gstride_c = (int64_t)M * N;
   Grouping grp{2, ngroups, row_off, nullptr, 0};
   if (sizeof(T) == 2 && M >= 128 && N >= 128 && g_mg_tune[MG_TUNE_GWGRAD_TILE] != 64)
-    launch_gemm<T, 128, 128, false, false>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
+    launch_gemm<T, 128, 128, false, false, 1>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
   else
-    launch_gemm<T, 64, 64, false, false>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
+    launch_gemm<T, 64, 64, false, false, 1>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
 }
 }  // namespace
 

@@ -50,7 +50,7 @@ def _parse_header(path=_HEADER):
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     sigs = {}
     for ret, name, args in re.findall(SIG_RE, txt, flags=re.S):
-        types = []
+        types, names = [], []
         for a in args.split(","):
             a = " ".join(a.split())
             if not a or a == "void":
@@ -60,10 +60,13 @@ def _parse_header(path=_HEADER):
                 types.append(_CTYPE[base] if base in ("mg_epilogue", "mg_gemm_desc") else _c_void_p)
             else:
                 types.append(_CTYPE[base])
+            names.append(a.replace("*", " ").split()[-1])
         sigs[name] = (_RESTYPE[ret], types)
+        ARGNAMES[name] = names
     return sigs
 
 
+ARGNAMES = {}  # entry point -> parameter names, in order (the roofline attribution reads shapes by name)
 _SIGS = _parse_header()
 EP = ctypes.POINTER(Epilogue)
 
@@ -111,8 +114,13 @@ def exported_symbols():
     return list(_SIGS)
 
 
+# Optional observer of every C-ABI call (moegan_mi/roofline.py): HOOK(name, args, run) must call run() once.
+HOOK = None
+
+
 def call(name, *args):
-    rc = getattr(lib(), name)(*args)
+    fn = getattr(lib(), name)
+    rc = fn(*args) if HOOK is None else HOOK(name, args, lambda: fn(*args))
     if rc != 0:
         raise MGError(f"{name} failed ({rc}): {lib().mg_last_error().decode()}")
 

@@ -1,0 +1,227 @@
+"""Per-family roofline attribution of the training step (bench.py).
+
+Every C-ABI call of one eager step is observed through ``_lib.HOOK``: its algorithmic work is computed from
+the call's own shape arguments (FLOPs for the MFMA families, bytes for the HBM-bound ones: each operand
+read once, each output written once -- the SURVEY.md §8(d) formulas) and the call is bracketed by HIP events
+on the stream it is enqueued on.  A family's achieved rate is its total work over its total event time.
+
+A call's event time includes every kernel that entry point launches (e.g. ``mg_conv2d_wgrad`` = GEMM +
+``k_wgrad_fold`` / split-K reduce), so the wgrad family carries its fold.  ``KERNELS`` maps the rocprofv3
+kernel names to the same families so the PMC traffic of a ``--pmc`` pass (tools/family_pmc.py) can be
+attributed per family too.
+"""
+import re
+
+import torch
+
+from . import _lib as L
+
+ELT = {0: 4, 1: 2}  # MG_F32, MG_BF16
+
+# family -> (bound, entry points)
+FAMILIES = {
+    "conv_fwd": ("mfma", ("mg_conv2d_fwd",)),
+    "conv_dgrad_s2": ("mfma", ("mg_conv2d_dgrad_s2",)),
+    "conv_wgrad+fold": ("mfma", ("mg_conv2d_wgrad",)),
+    "expert_gemm": ("mfma", ("mg_gemm_grouped", "mg_gemm_grouped_wgrad")),
+    "gemm": ("mfma", ("mg_gemm", "mg_gemm_batch")),
+    "attention": ("mfma", ("mg_attn_fwd", "mg_attn_bwd")),
+    "router_fwd": ("hbm", ("mg_router_fwd",)),
+    "dispatch_combine": ("hbm", ("mg_gather_rows", "mg_moe_combine")),
+    "warp_fwd": ("hbm", ("mg_warp_fwd", "mg_warp_fwd_scaled")),
+    "mtm_bwd": ("hbm", ("mg_mtm_bwd_fused",)),
+    "modconv_bwd_io": ("hbm", ("mg_modconv_bwd_in", "mg_modconv_bwd_out", "mg_scale_bc")),
+    "r1": ("hbm", ("mg_r1",)),
+    "sumsq": ("hbm", ("mg_sumsq",)),
+    "adamw": ("hbm", ("mg_adamw_dev", "mg_adamw_dev_shadow", "mg_adamw")),
+    "bias_colsum": ("hbm", ("mg_colsum", "mg_grouped_colsum")),
+    "weight_prep": ("hbm", ("mg_pack_conv", "mg_pack_conv_flip", "mg_pack_dgrad_s2", "mg_wsq", "mg_wsq_bwd",
+                            "mg_router_reparam", "mg_weight_norm_fwd", "mg_weight_norm_bwd")),
+}
+_FAMILY_OF = {e: f for f, (_, es) in FAMILIES.items() for e in es}
+
+# rocprofv3 kernel name (regex, first match wins) -> family, for PMC attribution
+KERNELS = [
+    (r"k_wgrad_fold|splitk_reduce_kernel<mg::Epi<float>", "conv_wgrad+fold"),
+    (r"gemm_kernel<.*, 1>\(", "expert_gemm"),  # TAG = 1 instantiations (mg_gemm.h)
+    (r"gemm_kernel<[^>]*LdKCConvT", "conv_dgrad_s2"),
+    (r"gemm_kernel<.*LdMCConv", "conv_wgrad+fold"),
+    (r"gemm_kernel<.*LdKCConv", "conv_fwd"),
+    (r"gemm_kernel<|gemm_batch_kernel<|splitk_reduce_kernel", "gemm"),
+    (r"k_attn_", "attention"),
+    (r"k_router_fwd", "router_fwd"),
+    (r"k_gather_rows|k_combine", "dispatch_combine"),
+    (r"k_warp_fwd", "warp_fwd"),
+    (r"k_mtm_bwd", "mtm_bwd"),
+    (r"k_bwd_in|k_bwd_out|k_scale_bc", "modconv_bwd_io"),
+    (r"k_r1", "r1"),
+    (r"k_sumsq", "sumsq"),
+    (r"k_adamw", "adamw"),
+    (r"k_colsum|k_grouped_colsum", "bias_colsum"),
+    (r"k_pack_|k_wsq|k_reparam|k_wn_", "weight_prep"),
+]
+
+
+def kernel_family(kernel_name):
+    for pat, fam in KERNELS:
+        if re.search(pat, kernel_name):
+            return fam
+    return "other"
+
+
+def _conv_out(H, W, KH, KW, s, p):
+    return (H + 2 * p - KH) // s + 1, (W + 2 * p - KW) // s + 1
+
+
+def work(name, a):
+    """Algorithmic work of one call: FLOPs (MFMA families) or bytes (HBM families); None = not modelled."""
+    if name == "mg_conv2d_fwd" or name == "mg_conv2d_wgrad":
+        OH, OW = _conv_out(a["H"], a["W"], a["KH"], a["KW"], a["stride"], a["pad"])
+        return 2.0 * a["B"] * OH * OW * a["Cout"] * a["KH"] * a["KW"] * a["Cin"]
+    if name == "mg_conv2d_dgrad_s2":  # 4x4 stride-2 transpose: every input pixel takes 4 of the 16 taps
+        return 2.0 * a["B"] * (2 * a["OH"]) * (2 * a["OW"]) * a["Cin"] * a["Cg"] * 4
+    if name == "mg_gemm":
+        return 2.0 * a["M"] * a["N"] * a["K"]
+    if name == "mg_gemm_batch":
+        d = a["descs"]
+        return sum(2.0 * d[i].M * d[i].N * d[i].K for i in range(a["n"]))
+    if name == "mg_gemm_grouped":
+        return 2.0 * a["total_rows"] * a["N"] * a["K"]
+    if name == "mg_gemm_grouped_wgrad":
+        return 2.0 * a["M"] * a["N"] * a["total_rows"]
+    if name == "mg_attn_fwd":  # S = QK^T, O = PV
+        return 4.0 * a["B"] * a["L"] * a["L"] * a["C"]
+    if name == "mg_attn_bwd":  # dV, dP, dQ, dK (the S recompute is not algorithmic work)
+        return 8.0 * a["B"] * a["L"] * a["L"] * a["C"]
+    if name == "mg_router_fwd":
+        T, C, E, k = a["T"], a["C"], a["E"], a["k"]
+        return T * C * ELT[a["dtype"]] + E * C * 4 + T * E * 8 + T * k * 8
+    if name == "mg_gather_rows":
+        return 2.0 * a["n"] * a["C"] * ELT[a["dtype"]]
+    if name == "mg_moe_combine":
+        e = ELT[a["dtype"]]
+        return (a["T"] * a["k"] + 2 * a["T"]) * a["C"] * e
+    if name in ("mg_warp_fwd", "mg_warp_fwd_scaled"):
+        P, C, e = a["B"] * a["H"] * a["W"], a["C"], ELT[a["dtype"]]
+        outs = 2 if name == "mg_warp_fwd_scaled" else 1
+        return P * (C * e * (1 + outs) + 32 * e + 16)
+    if name == "mg_mtm_bwd_fused":
+        P, C, e = a["B"] * a["H"] * a["W"], a["C"], ELT[a["dtype"]]
+        gx = C * ELT[a["gx_dtype"]] * (2 if a["accumulate"] else 1)
+        return P * (C * ELT[a["gout_dtype"]] + C * e + 16 + 32 * e * 2 + gx)
+    if name == "mg_scale_bc":
+        return 2.0 * a["B"] * a["HW"] * a["C"] * ELT[a["dtype"]]
+    if name == "mg_modconv_bwd_in":
+        n = a["B"] * a["HW"] * a["Cin"]
+        gx = ELT[a["gx_dtype"]] * (2 if a["accumulate"] else 1)
+        return n * (ELT[a["gxt_dtype"]] + ELT[a["dtype"]] + gx)
+    if name == "mg_modconv_bwd_out":
+        n = a["B"] * a["HW"] * a["Cout"]
+        e = ELT[a["dtype"]]
+        return n * (ELT[a["gz_dtype"]] + e + (e if a["zsub"] else 0) + e)
+    if name == "mg_r1":
+        return a["B"] * a["per"] * (ELT[a["dtype"]] + ELT[a["u_dtype"]])
+    if name == "mg_sumsq":
+        return 4.0 * a["n"]
+    if name in ("mg_adamw_dev", "mg_adamw"):
+        return 28.0 * a["n"]
+    if name == "mg_adamw_dev_shadow":
+        return (28.0 + (2 if a["shadow_bf16"] else 0)) * a["n"]
+    if name in ("mg_pack_conv", "mg_pack_conv_flip"):
+        K = a["KH"] * a["KW"]
+        return a["Cout"] * a["Cin"] * K * 4 + (a["rows"] * a["Cin"] if name == "mg_pack_conv" else
+                                                a["rows"] * a["Cout"]) * K * ELT[a["dtype"]]
+    if name == "mg_pack_dgrad_s2":
+        return a["Cg"] * a["Cin"] * 16 * 4 + 16 * a["rows"] * a["Cg"] * ELT[a["dtype"]]
+    if name == "mg_wsq":
+        return a["Cout"] * a["Cin"] * a["taps"] * 4 + a["rows"] * a["Cin"] * 4
+    if name == "mg_wsq_bwd":
+        return a["Cout"] * a["Cin"] * (a["taps"] * 12 + 4)
+    if name == "mg_router_reparam":
+        return 16.0 * a["n"]
+    if name == "mg_weight_norm_fwd":
+        return 8.0 * a["O"] * a["K"]
+    if name == "mg_weight_norm_bwd":
+        return 16.0 * a["O"] * a["K"]
+    if name == "mg_colsum":
+        return a["R"] * a["C"] * ELT[a["dtype"]]
+    return None
+
+
+class Attribution:
+    """Install with ``with Attribution() as at: run_step()``; then ``at.summary(steps=1)``.
+
+    The eager step is host-bound (Python enqueues each call), so events around a call would also time the
+    host's launch latency.  ``__enter__`` therefore first parks the stream on a spin kernel of ``lead_ms``
+    (longer than the host needs to enqueue the whole step): the calls then run back to back behind it and each
+    event pair brackets only its own kernels.  ``host_bound`` reports whether the GPU caught up with the host
+    anyway (the lead was too short), which would inflate the small families."""
+
+    def __init__(self, lead_ms=150.0):
+        self.calls = []  # (entry point, family, work, start event, end event)
+        self.lead_ms = lead_ms
+        self.host_bound = None
+
+    def _hook(self, name, args, run):
+        names = L.ARGNAMES.get(name)
+        a = {}
+        if names:
+            for n, v in zip(names, args):
+                a[n] = v.value if hasattr(v, "value") and not isinstance(v, L.ctypes.Array) else v
+        try:
+            w = work(name, a)
+        except (KeyError, TypeError, AttributeError):
+            w = None
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = run()
+        e.record()
+        self.calls.append((name, _FAMILY_OF.get(name, "other"), w, s, e))
+        return rc
+
+    def __enter__(self):
+        assert L.HOOK is None, "nested attribution"
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        torch.cuda._sleep(2_000_000)
+        e.record()
+        e.synchronize()
+        cyc_per_ms = 2_000_000 / max(s.elapsed_time(e), 1e-3)
+        torch.cuda._sleep(int(self.lead_ms * cyc_per_ms))
+        L.HOOK = self._hook
+        return self
+
+    def __exit__(self, *exc):
+        L.HOOK = None
+        if self.calls:
+            self.host_bound = bool(self.calls[0][3].query())  # first call already ran: the GPU caught up
+
+    def summary(self, steps=1, peak_tflops=2500.0, peak_gbs=8000.0):
+        torch.cuda.synchronize()
+        if self.host_bound:
+            import warnings
+            warnings.warn("roofline attribution: the GPU caught up with the host; small families are inflated")
+        fam = {}
+        for name, f, w, s, e in self.calls:
+            r = fam.setdefault(f, {"calls": 0, "ms": 0.0, "work": 0.0, "entry_points": set()})
+            r["calls"] += 1
+            r["ms"] += s.elapsed_time(e)
+            r["work"] += w or 0.0
+            r["entry_points"].add(name)
+        out = []
+        for f, r in sorted(fam.items(), key=lambda kv: -kv[1]["ms"]):
+            bound = FAMILIES[f][0] if f in FAMILIES else None
+            ms = r["ms"] / steps
+            rec = {"family": f, "bound": bound, "launches_per_step": r["calls"] / steps, "ms_per_step": round(ms, 4)}
+            if bound == "mfma":
+                tf = r["work"] / steps / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+                rec.update({"gflop_per_step": round(r["work"] / steps / 1e9, 3), "achieved": round(tf, 1),
+                            "unit": "TFLOP/s", "peak": peak_tflops, "frac": round(tf / peak_tflops, 4)})
+            elif bound == "hbm":
+                gbs = r["work"] / steps / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+                rec.update({"mb_per_step": round(r["work"] / steps / 1e6, 3), "achieved": round(gbs, 1),
+                            "unit": "GB/s", "peak": peak_gbs, "frac": round(gbs / peak_gbs, 4)})
+            else:
+                rec["entry_points"] = sorted(r["entry_points"])[:12]
+            out.append(rec)
+        return out

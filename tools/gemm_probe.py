@@ -110,6 +110,12 @@ def main():
     gwm = torch.zeros(512, 512, device=dev)
     cases.append(("style_wgrad_fp32", 2.0 * B * 512 * 512, lambda: ops.linear_wgrad(gs, w, gwm)))
     cases.append(("style_dgrad_fp32", 2.0 * B * 512 * 512, lambda: ops.linear_dgrad(gs, Wm)))
+    # hipBLASLt (torch.matmul) on the plain-GEMM equivalents of the conv shapes: the library ceiling
+    for tag, (M, N, K) in {"conv8": (B * 64, 256, 2304), "conv4": (B * 16, 512, 4608),
+                           "conv16": (B * 256, 128, 1152), "dconv1": (B * 256, 256, 2048),
+                           "fc1": (8 * 16384, 512, 128), "sq4096": (4096, 4096, 4096)}.items():
+        At, Bt = rn(M, K, dt=bf), rn(N, K, dt=bf)
+        cases.append((f"torch_{tag}", 2.0 * M * N * K, lambda At=At, Bt=Bt: torch.matmul(At, Bt.t())))
 
     only = set(a.only.split(",")) if a.only else None
     variants = [("", {})]
