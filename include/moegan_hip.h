@@ -197,6 +197,13 @@ int mg_d_text_bwd(const float* g_tb, const float* t, const float* w2sum, int B, 
 /* im2col for the discriminator's first conv (3->128, 4x4/s2/p1), any input strides, K padded to Kp. */
 int mg_im2col_4x4s2(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H, int W, int C, int Kp, int out_dtype, void* out, void* stream);
 
+/* Data gradient of a 4x4 / stride-2 / pad-1 conv with few (C <= 4) input channels, second half: Y [B*OH*OW, ldy]
+   = g @ wpack (wpack as mg_pack_conv, [Cg][16*C]) holds every (tap, channel) contribution of an output pixel;
+   out[b, y, x, c] (pitch ldo, written for c < C) = sum over the <= 4 (oy, ox, kh, kw) with y = 2oy-1+kh,
+   x = 2ox-1+kw of Y[b, oy, ox, (kh*4+kw)*C + c].  Replaces the padded-channel mg_conv2d_dgrad_s2 for the
+   discriminator's first conv (image gradient of R1, t2i_moe_gan.py:1281-1286, and the G phase). */
+int mg_col2im_4x4s2(int in_dtype, const void* Y, int64_t ldy, int B, int OH, int OW, int C, int out_dtype, void* out, int64_t ldo, void* stream);
+
 /* Discriminator output_layer, image channels: out[b,o] = sum h1[b,o+tap,c] W2[c,tap] (t2i_moe_gan.py:885-907). */
 int mg_disc_head_fwd(int dtype, const void* h1, const float* W2, int B, int Hf, int Cf, float* out, void* stream);
 
@@ -323,6 +330,43 @@ int mg_wsq(const float* W, int Cout, int Cin, int taps, int rows, float* out, vo
 
 /* gW[o][ci][t] += 2 W[o][ci][t] gwsq[o][ci]  (demodulation backward). */
 int mg_wsq_bwd(const float* W, const float* gwsq, int Cout, int Cin, int taps, float* gW, void* stream);
+
+/* Multi-tensor weight preparation: every descriptor's element map in ONE launch (tables of more than 32
+   descriptors take one launch per 32).  Kinds and fields (W = fp32 source; out in the launch dtype for the
+   packs, fp32 otherwise):
+     MG_PREP_PACK          = mg_pack_conv       (Cout, Cin, KH, KW, rows)
+     MG_PREP_PACK_FLIP     = mg_pack_conv_flip  (Cout, Cin, KH, KW, rows)
+     MG_PREP_PACK_DGRAD_S2 = mg_pack_dgrad_s2   (Cout = Cg, Cin, rows)
+     MG_PREP_WSQ           = mg_wsq             (Cout, Cin, KH*KW = taps, rows)
+     MG_PREP_WSQ_BWD       = mg_wsq_bwd         (Cout, Cin, KH*KW = taps; aux = gwsq; out = gW, +=)
+     MG_PREP_REPARAM       = mg_router_reparam  (W = mu, aux = rho, aux2 = eps, n; out = W)
+   n is derived from the shape fields except for MG_PREP_REPARAM. */
+#define MG_PREP_PACK 1
+#define MG_PREP_PACK_FLIP 2
+#define MG_PREP_PACK_DGRAD_S2 3
+#define MG_PREP_WSQ 4
+#define MG_PREP_WSQ_BWD 5
+#define MG_PREP_REPARAM 6
+typedef struct mg_prep_desc {
+  int32_t kind;
+  int32_t Cout, Cin, KH, KW, rows;
+  int64_t n;
+  const float* W;
+  const float* aux;
+  const float* aux2;
+  void* out;
+} mg_prep_desc;
+int mg_prep_batch(int dtype, int n, const mg_prep_desc* descs, void* stream);
+
+/* Multi-tensor column sums (bias gradients of a whole backward in one launch): out[c] += sum_r X[r*ld+c]
+   for every descriptor; fp32 atomics across row blocks (at most 32 descriptors per launch). */
+typedef struct mg_colsum_desc {
+  int32_t dtype, R, C;
+  int64_t ld;
+  const void* X;
+  float* out;
+} mg_colsum_desc;
+int mg_colsum_batch(int n, const mg_colsum_desc* descs, void* stream);
 
 /* out = (alpha*in)[^2 if square] with dtype conversion. */
 int mg_cast(int in_dtype, const void* in, int out_dtype, void* out, int64_t n, float alpha, int square, void* stream);

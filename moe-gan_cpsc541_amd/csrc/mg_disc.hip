@@ -18,21 +18,64 @@ namespace {
 template <typename TI, typename TO>
 __global__ void k_im2col(const TI* __restrict__ x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H,
                          int W, int C, int Kp, TO* __restrict__ out) {
-  int OH = H / 2, OW = W / 2;
-  int64_t n = (int64_t)B * OH * OW * Kp;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int k = (int)(i % Kp);
-    int64_t r = i / Kp;
-    float v = 0.f;
+  // one thread per (output pixel, 8-column group): consecutive threads write one pixel's row contiguously
+  // (16-B stores when bf16 and Kp % 8 == 0), and each thread's 8 gathers are independent loads
+  const int OH = H / 2, OW = W / 2;
+  const int G = (Kp + 7) >> 3;
+  const int np = B * OH * OW;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np * G) return;
+  const int r = i / G, k0 = (i - r * G) * 8;
+  const int ow = r % OW, oh = (r / OW) % OH, b = r / (OW * OH);
+  const TI* xb = x + (int64_t)b * sb;
+  TO* o = out + (int64_t)r * Kp;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    v[j] = 0.f;
     if (k < 16 * C) {
-      int tap = k / C, c = k - (k / C) * C;
-      int kh = tap >> 2, kw = tap & 3;
-      int ow = (int)(r % OW), oh = (int)((r / OW) % OH), b = (int)(r / ((int64_t)OW * OH));
-      int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
-      if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = ldf(x, b * sb + ih * sh + iw * sw + c * sc);
+      const int tap = k / C, c = k - tap * C;
+      const int ih = 2 * oh - 1 + (tap >> 2), iw = 2 * ow - 1 + (tap & 3);
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W) v[j] = ldf(xb, ih * sh + iw * sw + c * sc);
     }
-    stf(out, i, v);
   }
+  if (sizeof(TO) == 2 && (Kp & 7) == 0 && mg_al16(out)) {
+    st8(reinterpret_cast<bf16_t*>(o) + k0, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (k0 + j < Kp) stf(o, k0 + j, v[j]);
+  }
+}
+
+// col2im of a 4x4 / stride-2 / pad-1 conv's data gradient (few input channels): Y[b, oy, ox, (kh*4+kw)*C + c] =
+// sum_co g[b, oy, ox, co] W[co, c, kh, kw] (one small GEMM), summed here into out[b, y, x, c] over the <= 4
+// (oy, ox, kh, kw) with y = 2 oy - 1 + kh, x = 2 ox - 1 + kw.  One thread per input pixel.
+template <typename TI, typename TO>
+__global__ void k_col2im_4x4s2(const TI* __restrict__ Y, int64_t ldy, int B, int OH, int OW, int C,
+                               TO* __restrict__ out, int64_t ldo) {
+  const int H = 2 * OH, W = 2 * OW;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * H * W) return;
+  const int x = i % W, y = (i / W) % H, b = i / (W * H);
+  // kh has the parity of y + 1: kh0 = (y + 1) & 1, the two candidates kh0 and kh0 + 2
+  const int kh0 = (y + 1) & 1, kw0 = (x + 1) & 1;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int kh = kh0 + 2 * a, oy = (y + 1 - kh) >> 1;
+    if (oy < 0 || oy >= OH) continue;
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) {
+      const int kw = kw0 + 2 * c2, ox = (x + 1 - kw) >> 1;
+      if (ox < 0 || ox >= OW) continue;
+      const TI* row = Y + ((int64_t)(b * OH + oy) * OW + ox) * ldy + (kh * 4 + kw) * C;
+      for (int c = 0; c < C && c < 4; ++c) acc[c] += ldf(row, c);
+    }
+  }
+  TO* o = out + (int64_t)i * ldo;
+  for (int c = 0; c < C && c < 4; ++c) stf(o, c, acc[c]);
 }
 
 // head, image channels: out[b, o] = sum_{c<256, kh, kw} h1[b, oy+kh, ox+kw, c] * W2[c, kh, kw]
@@ -325,12 +368,28 @@ extern "C" int mg_im2col_4x4s2(int in_dtype, const void* x, int64_t sb, int64_t 
                                int H, int W, int C, int Kp, int out_dtype, void* out, void* stream) {
   MG_REQUIRE(Kp >= 16 * C, "Kp too small");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  int64_t n = (int64_t)B * (H / 2) * (W / 2) * Kp;
-#define L_(TI, TO) hipLaunchKernelGGL((k_im2col<TI, TO>), dim3(nblk(n)), dim3(256), 0, st, (const TI*)x, sb, sh, sw, sc, B, H, W, C, Kp, (TO*)out)
+  const int64_t nt = (int64_t)B * (H / 2) * (W / 2) * ((Kp + 7) / 8);
+  MG_REQUIRE(nt < (1LL << 31), "too many pixels");
+#define L_(TI, TO) hipLaunchKernelGGL((k_im2col<TI, TO>), dim3(cdiv(nt, 256)), dim3(256), 0, st, (const TI*)x, sb, sh, sw, sc, B, H, W, C, Kp, (TO*)out)
   if (in_dtype == MG_F32) { if (out_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
   else { if (out_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
 #undef L_
   return mg_check_launch("mg_im2col_4x4s2");
+}
+
+extern "C" int mg_col2im_4x4s2(int in_dtype, const void* Y, int64_t ldy, int B, int OH, int OW, int C,
+                               int out_dtype, void* out, int64_t ldo, void* stream) {
+  MG_REQUIRE(C >= 1 && C <= 4, "1 <= C <= 4");
+  MG_REQUIRE(ldy >= 16 * C && ldo >= C, "bad pitches");
+  const int64_t n = (int64_t)B * 4 * OH * OW;
+  MG_REQUIRE(n < (1LL << 31), "too many pixels");
+  if (n == 0) return MG_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define L_(TI, TO) hipLaunchKernelGGL((k_col2im_4x4s2<TI, TO>), dim3(cdiv(n, 256)), dim3(256), 0, st, (const TI*)Y, ldy, B, OH, OW, C, (TO*)out, ldo)
+  if (in_dtype == MG_F32) { if (out_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
+  else { if (out_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
+#undef L_
+  return mg_check_launch("mg_col2im_4x4s2");
 }
 
 extern "C" int mg_disc_head_fwd(int dtype, const void* h1, const float* W2, int B, int Hf, int Cf, float* out,

@@ -935,6 +935,22 @@ template <class EP>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
                                                             EP ep) {
   const int64_t MN = (int64_t)M * N;
+  if (ep.vec_ok && (N & 7) == 0) {  // 8 columns per thread: 16-B slab loads, the vector epilogue
+    const int64_t n8 = MN >> 3;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n8; q += (int64_t)gridDim.x * 256) {
+      const int64_t i = q << 3;
+      float v[8], t[8];
+      ld8(ws + i, v);
+      for (int s = 1; s < splits; ++s) {
+        ld8(ws + s * MN + i, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += t[j];
+      }
+      const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+      ep.vec8(m, n, v);
+    }
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
     float v = 0.f;
     for (int s = 0; s < splits; ++s) v += ws[s * MN + i];

@@ -164,6 +164,7 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
     else go(la, LdMC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, FF{}, FF{});
   }
   auto ep = make_epi<TO>(C, ldc, e);
+  ep.vec_ok = ep.host_vec_ok() ? 1 : 0;
   int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
   hipLaunchKernelGGL((splitk_reduce_kernel<Epi<TO>>), dim3(blocks), dim3(256), 0, st, ws, splits, M, N, ep);
   return true;
@@ -298,17 +299,20 @@ void run_conv(const void* x, int B, int H, int W, int Cin, const void* wpack, in
   auto ep = make_epi<TO>(y, ldy, e);
   launch_gemm<T, BM, BN, true, true>(la, lb, ep, M, Cout, K, 1, kNoGroup, 0, st);
 }
-// Implicit conv with few output tiles (offset heads: Cout = 32 at 4x4 / 8x8) walks K = 9*Cin serially in
-// ~100 blocks; split K into fp32 slabs over ~512 blocks and apply the epilogue in the reduction.
-template <typename T, typename TO, bool SC>
-bool conv_slabs(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW, int stride,
-                int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
+// Implicit conv with few output tiles for its K (the MTM offset heads, Cout = 32, K = 9*Cin up to 4608; the 4x4
+// 512 -> 512 convs, 512 tiles of 72 K steps) walks K serially in too few blocks to hide load latency: split K into
+// fp32 slabs over ~1024 blocks of >= 8 K steps each and apply the epilogue in the reduction.  Narrow outputs
+// (Cout <= 32) use 128 x 32 tiles (no MFMA columns wasted).
+template <typename T, typename TO, bool SC, int BM, int BN>
+bool conv_slabs_t(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW,
+                  int stride, int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
   constexpr int TBK = Tile<T>::BK;
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int M = B * OH * OW, K = KH * KW * Cin;
-  int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(Cout, 64);
-  if (tiles >= 256 || K < 8 * TBK || (e && e->atomic) || sc || g_mg_tune[MG_TUNE_NO_SLABS]) return false;
-  int splits = (int)std::min<int64_t>(cdiv(512, tiles), K / (4 * TBK));
+  int64_t tiles = (int64_t)cdiv(M, BM) * cdiv(Cout, BN);
+  const int ksteps = K / TBK;
+  if (tiles >= 1024 || ksteps < 16 || (e && e->atomic) || sc || g_mg_tune[MG_TUNE_NO_SLABS]) return false;
+  int splits = (int)std::min<int64_t>(cdiv(1024, tiles), ksteps / 8);
   if (splits < 2) return false;
   int kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
   splits = (K + kchunk - 1) / kchunk;
@@ -323,13 +327,24 @@ bool conv_slabs(const void* x, int B, int H, int W, int Cin, const void* wpack, 
   LdKCConv<T, false, SC> la{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), M,
                             KW, stride, pad, K, sc, kwinv(KW)};
   LdKC<T> lb{reinterpret_cast<const T*>(wpack), K, Cout, K, nullptr, 1, nullptr, 0};
-  dim3 grid(cdiv(M, 64), cdiv(Cout, 64), splits);
-  hipLaunchKernelGGL((gemm_kernel<T, 64, 64, true, true, LdKCConv<T, false, SC>, LdKC<T>, Epi<float>>), grid, dim3(NTHREADS), 0,
-                     st, la, lb, slab, M, Cout, K, kchunk, kNoGroup);
+  dim3 grid(cdiv(M, BM), cdiv(Cout, BN), splits);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, true, LdKCConv<T, false, SC>, LdKC<T>, Epi<float>>), grid,
+                     dim3(NTHREADS), 0, st, la, lb, slab, M, Cout, K, kchunk, kNoGroup);
   auto ep = make_epi<TO>(y, ldy, e);
+  ep.vec_ok = ep.host_vec_ok() ? 1 : 0;
   int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
   hipLaunchKernelGGL((splitk_reduce_kernel<Epi<TO>>), dim3(blocks), dim3(256), 0, st, ws, splits, M, Cout, ep);
   return true;
+}
+
+template <typename T, typename TO, bool SC>
+bool conv_slabs(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW, int stride,
+                int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (Cout <= 32)
+      return conv_slabs_t<T, TO, SC, 128, 32>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
+  }
+  return conv_slabs_t<T, TO, SC, 64, 64>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
 }
 
 template <typename T, typename TO>
@@ -511,7 +526,9 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
     // D conv1 / modconv 8x8 / modconv 16x16 weight gradients 1.36x / 1.2x / 1.6x over ~512 blocks)
     const int64_t want = slabs ? (big ? 1024 : 2048) : (big ? 288 : 576);
     int64_t t = std::max<int64_t>(tiles, 1);
-    const int64_t cap = (!big && tiles < 64) ? 32 : 16;  // few 64^2 tiles: up to 32 slabs (modconv 16x16 wgrad 65 -> 58 us)
+    // few 64^2 tiles: up to 32 slabs (modconv 16x16 wgrad 65 -> 58 us); a handful (to_rgb, Cout 3 -> 8 rows):
+    // up to 128, so the reduction over B*H*W pixels still spreads over >= 128 blocks
+    const int64_t cap = (!big && tiles < 8) ? 128 : (!big && tiles < 64) ? 32 : 16;
     splits = (int)std::max<int64_t>(1, std::min<int64_t>((want + t / 2) / t, slabs ? std::min<int64_t>(cap, P / 1024)
                                                                                       : P / 2048));
   }

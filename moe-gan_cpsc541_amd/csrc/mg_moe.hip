@@ -184,45 +184,59 @@ __global__ void k_disp_scatter(const int* __restrict__ topi, const float* __rest
                                const int* __restrict__ blk_base, const int* __restrict__ row_off,
                                int* __restrict__ perm, int* __restrict__ pos_of, float* __restrict__ gate_pos) {
   constexpr int PER = DCH / 256;
-  __shared__ int pre[256 * E];
+  __shared__ int wtot[4][E];
   int a0 = blockIdx.x * DCH + threadIdx.x * PER;
+  // the thread's PER assignments into registers first: independent loads in flight (a dependent chain of PER
+  // global loads per loop would cost PER round trips)
+  int ex_r[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) ex_r[i] = a0 + i < n ? topi[a0 + i] : -1;
   int loc[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) loc[e] = 0;
+#pragma unroll
   for (int i = 0; i < PER; ++i) {
-    int a = a0 + i;
-    if (a < n) {
-      int ex = topi[a];
 #pragma unroll
-      for (int e = 0; e < E; ++e) loc[e] += (ex == e);
-    }
+    for (int e = 0; e < E; ++e) loc[e] += (ex_r[i] == e);
   }
+  // exclusive prefix of loc[e] over the block's 256 threads (thread order = assignment order): inclusive wave
+  // scans, then the preceding waves' totals
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int incl[E];
 #pragma unroll
-  for (int e = 0; e < E; ++e) pre[e * 256 + threadIdx.x] = loc[e];
-  __syncthreads();
-  if (threadIdx.x < E) {  // exclusive scan per expert across threads
-    int e = threadIdx.x, s = 0;
-    for (int i = 0; i < 256; ++i) {
-      int c = pre[e * 256 + i];
-      pre[e * 256 + i] = s;
-      s += c;
+  for (int e = 0; e < E; ++e) {
+    int v = loc[e];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int u = __shfl_up(v, d, 64);
+      if (lane >= d) v += u;
     }
+    incl[e] = v;
+    if (lane == 63) wtot[wid][e] = v;
   }
   __syncthreads();
   int off[E];
 #pragma unroll
-  for (int e = 0; e < E; ++e) off[e] = row_off[e] + blk_base[blockIdx.x * E + e] + pre[e * 256 + threadIdx.x];
+  for (int e = 0; e < E; ++e) {
+    int base = 0;
+    for (int w = 0; w < wid; ++w) base += wtot[w][e];
+    off[e] = row_off[e] + blk_base[blockIdx.x * E + e] + base + incl[e] - loc[e];
+  }
+  float g_r[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) g_r[i] = a0 + i < n ? gate[a0 + i] : 0.f;
+#pragma unroll
   for (int i = 0; i < PER; ++i) {
-    int a = a0 + i;
+    const int a = a0 + i;
     if (a < n) {
-      int ex = topi[a];
+      const int ex = ex_r[i];
       int pos = 0;
 #pragma unroll
       for (int e = 0; e < E; ++e)
         if (ex == e) pos = off[e]++;
       perm[pos] = a;
       pos_of[a] = pos;
-      gate_pos[pos] = gate[a];
+      gate_pos[pos] = g_r[i];
     }
   }
 }

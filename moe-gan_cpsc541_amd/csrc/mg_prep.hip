@@ -409,13 +409,21 @@ __global__ void k_const_fwd(const float* __restrict__ cst, int C, int HW, int B,
 }
 // gconst[c][p] += sum_b g[b][p][c]
 template <typename T>
-__global__ void k_const_bwd(const T* __restrict__ g, int C, int HW, int B, float* __restrict__ gc) {
+__global__ void k_const_bwd(const T* __restrict__ g, int C, int HW, int B, int bchunk, float* __restrict__ gc) {
+  // grid.y splits the batch (the [C, HW] map alone is too few threads to fill the chip); partial sums meet
+  // in fp32 atomics
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= C * HW) return;
   int p = i / C, c = i - p * C;
-  float s = 0.f;
-  for (int b = 0; b < B; ++b) s += ldf(g, ((int64_t)b * HW + p) * C + c);
-  gc[(int64_t)c * HW + p] += s;
+  const int b0 = blockIdx.y * bchunk, b1 = min(B, b0 + bchunk);
+  float s0 = 0.f, s1 = 0.f;
+  int b = b0;
+  for (; b + 1 < b1; b += 2) {
+    s0 += ldf(g, ((int64_t)b * HW + p) * C + c);
+    s1 += ldf(g, ((int64_t)(b + 1) * HW + p) * C + c);
+  }
+  if (b < b1) s0 += ldf(g, ((int64_t)b * HW + p) * C + c);
+  atomicAdd(gc + (int64_t)c * HW + p, s0 + s1);
 }
 
 inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
@@ -619,7 +627,8 @@ extern "C" int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, v
 
 extern "C" int mg_const_bwd(int dtype, const void* g, int C, int HW, int B, float* gc, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(k_const_bwd<T>, dim3(cdiv(C * HW, 256)), dim3(256), 0, st,
-                                       reinterpret_cast<const T*>(g), C, HW, B, gc));
+  const int bchunk = std::max(8, cdiv(B, 16));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(k_const_bwd<T>, dim3(cdiv(C * HW, 256), cdiv(B, bchunk)), dim3(256), 0, st,
+                                       reinterpret_cast<const T*>(g), C, HW, B, bchunk, gc));
   return mg_check_launch("mg_const_bwd");
 }

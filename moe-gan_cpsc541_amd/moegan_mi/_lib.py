@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MOEGAN_HIP_LIB") or os.path.join(_HERE, "libmoegan_hip.so")  # override: A/B builds
 
 MG_F32, MG_BF16 = 0, 1
+PREP_PACK, PREP_PACK_FLIP, PREP_PACK_DGRAD_S2, PREP_WSQ, PREP_WSQ_BWD, PREP_REPARAM = 1, 2, 3, 4, 5, 6
 ACT_NONE, ACT_LRELU, ACT_GELU, ACT_MUL_GELU_GRAD, ACT_MUL_LRELU_GRAD, ACT_RSQRT_EPS = 0, 1, 2, 3, 4, 5
 
 _c_void_p, _i32, _i64, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
@@ -34,11 +35,23 @@ class GemmDesc(ctypes.Structure):
                 ("ldb", _i64), ("C", _c_void_p), ("ldc", _i64), ("ep", ctypes.POINTER(Epilogue))]
 
 
+class PrepDesc(ctypes.Structure):
+    """Mirror of ``mg_prep_desc``."""
+    _fields_ = [("kind", _i32), ("Cout", _i32), ("Cin", _i32), ("KH", _i32), ("KW", _i32), ("rows", _i32),
+                ("n", _i64), ("W", _c_void_p), ("aux", _c_void_p), ("aux2", _c_void_p), ("out", _c_void_p)]
+
+
+class ColsumDesc(ctypes.Structure):
+    """Mirror of ``mg_colsum_desc``."""
+    _fields_ = [("dtype", _i32), ("R", _i32), ("C", _i32), ("ld", _i64), ("X", _c_void_p), ("out", _c_void_p)]
+
+
 # Argument types are derived from include/moegan_hip.h itself, so the binding
 # cannot drift from the C ABI (the header travels with the library).
 _HEADER = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "moegan_hip.h"))
 _CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "size_t": ctypes.c_size_t, "float": _f32,
-          "void": _c_void_p, "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc)}
+          "void": _c_void_p, "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc),
+          "mg_prep_desc": ctypes.POINTER(PrepDesc), "mg_colsum_desc": ctypes.POINTER(ColsumDesc)}
 _RESTYPE = {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "const char*": ctypes.c_char_p}
 SIG_RE = r"\b(int|int64_t|const char\*)\s+(mg_\w+)\(([^)]*)\);"
 
@@ -57,7 +70,8 @@ def _parse_header(path=_HEADER):
                 continue
             base = a.replace("const ", "").split()[0].rstrip("*")
             if "*" in a:
-                types.append(_CTYPE[base] if base in ("mg_epilogue", "mg_gemm_desc") else _c_void_p)
+                types.append(_CTYPE[base] if base in ("mg_epilogue", "mg_gemm_desc", "mg_prep_desc", "mg_colsum_desc")
+                             else _c_void_p)
             else:
                 types.append(_CTYPE[base])
             names.append(a.replace("*", " ").split()[-1])

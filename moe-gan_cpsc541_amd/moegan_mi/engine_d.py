@@ -56,10 +56,11 @@ class DiscriminatorEngine:
             W[pre], norm[pre] = ops.weight_norm_fwd(self.P(pre + "weight_v"), self.P(pre + "weight_g"))
         self.W, self.norm = W, norm
         cdt = self.cdt
-        self.W0p = ops.pack_conv(W["conv_layers.0."], cdt)  # [128, 48] (k = tap*3 + c)
-        self.W0cls = ops.pack_dgrad_s2(W["conv_layers.0."], cdt, rows=3)  # [4, 3, 4*128]
-        self.W1p = ops.pack_conv(W["conv_layers.2."], cdt)  # [256, 16*128]
-        self.W1cls = ops.pack_dgrad_s2(W["conv_layers.2."], cdt)  # [4, 128, 4*256]
+        pb = ops.PrepBatch(cdt)  # the packs in one launch
+        self.W0p = pb.pack(W["conv_layers.0."])  # [128, 48] (k = tap*3 + c)
+        self.W1p = pb.pack(W["conv_layers.2."])  # [256, 16*128]
+        self.W1cls = pb.pack_dgrad_s2(W["conv_layers.2."])  # [4, 128, 4*256]
+        pb.run()
         W2 = W["output_layer.0."].view(384, 16)
         self.W2img = W2[:256]
         # head as GEMMs: P = h1 @ W2img ([pix, 16 taps]) and g_a1 = G @ W2img^T
@@ -104,16 +105,16 @@ class DiscriminatorEngine:
         if want_params:
             dW1, gb1 = self.dW["conv_layers.2."], self.G("conv_layers.2.bias")
             self.side.run(lambda: (ops.conv2d_wgrad(g_a1, f["h0"], 256, 4, 4, 2, 1, dW1),
-                                   ops.colsum(g_a1.view(-1, 256), gb1)), g_a1, f["h0"])
+                                   ops.colsum(g_a1.view(-1, 256), gb1, defer=True)), g_a1, f["h0"])
         g_a0 = torch.empty(B, H // 2, H // 2, 128, device=self.dev, dtype=self.cdt)
         ops.dgrad_s2(g_a1, self.W1cls, 128, g_a0, ep=E_(act=MUL_LRELU_GRAD, aux=f["h0"], ld_aux=128))
         if want_params:
             dW0, gb0 = self.dW["conv_layers.0."].view(128, 48), self.G("conv_layers.0.bias")
             self.side.run(lambda: (ops.gemm(g_a0.view(-1, 128), f["cols"], 128, 48, g_a0.numel() // 128, a_kc=False,
                                             b_kc=False, out=dW0, ep=E_(atomic=1), splits=0),
-                                   ops.colsum(g_a0.view(-1, 128), gb0)), g_a0, f["cols"])
+                                   ops.colsum(g_a0.view(-1, 128), gb0, defer=True)), g_a0, f["cols"])
         if g_input is not None:
-            ops.dgrad_s2(g_a0, self.W0cls, 3, g_input)
+            ops.dgrad_s2_small(g_a0, self.W0p, 3, g_input)
         return g_a1, g_a0
 
     def _head_bwd(self, g, g_bstride, h1, B, Hf, want_w, wgrad_input=None):
@@ -176,7 +177,7 @@ class DiscriminatorEngine:
         gA0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
         ops.dgrad_s2(gA1, self.W1cls, 128, gA0, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
         gx = ops.zeros(B, Hr, Hr, 4, device=dev)
-        ops.dgrad_s2(gA0, self.W0cls, 3, gx)  # d sum(real_pred) / d real  (NHWC, channel-padded)
+        ops.dgrad_s2_small(gA0, self.W0p, 3, gx)  # d sum(real_pred) / d real  (NHWC, channel-padded)
         r1 = torch.zeros(1, device=dev)
         u = torch.empty(B, Hr, Hr, 4, device=dev, dtype=self.cdt)
         ops.r1(gx, B, r1_gamma, r1, u)
@@ -235,9 +236,9 @@ class DiscriminatorEngine:
         B = t.shape[0]
         g_tpre = torch.empty(B, 128, device=self.dev)
         ops.d_text_bwd(g_tb, t, self.w2sum, 256, g_tpre, self.dW["output_layer.0."].view(384, 16))
-        ops.colsum(g_tb.view(B, 1), self.G("output_layer.0.bias"))
+        ops.colsum(g_tb.view(B, 1), self.G("output_layer.0.bias"), defer=True)
         ops.linear_wgrad(g_tpre, text, self.dW["text_projection.0."])
-        ops.colsum(g_tpre, self.G("text_projection.0.bias"))
+        ops.colsum(g_tpre, self.G("text_projection.0.bias"), defer=True)
 
     # ------------------------------------------------------------------
     # generic forward / backward for the module API (AuroraDiscriminator.forward)

@@ -98,22 +98,24 @@ class GeneratorEngine:
             self.style_gb = self.st.grad[b0:b0 + nrows]
         self._mean_latent = None  # truncation centre: mapping of zeros, a function of the weights only
         pk = {}
+        pb = ops.PrepBatch(self.cdt)  # every pack / demodulation sum of the generator in one launch
         for pre, k in self.mc_list:
             W = self.P(pre + "weight")
             Cout = W.shape[0]
             rows = max(Cout, 8)
-            ent = {"rows": rows, "wsq": ops.wsq(W, rows=rows)}
+            ent = {"rows": rows, "wsq": pb.wsq(W, rows=rows)}
             if k == 3:
-                ent["w"] = ops.pack_conv(W, self.cdt)
-                ent["wflip"] = ops.pack_conv(W, self.cdt, flip=True)
+                ent["w"] = pb.pack(W)
+                ent["wflip"] = pb.pack(W, flip=True)
             elif rows != Cout:
-                ent["w"] = ops.pack_conv(W, self.cdt, rows=rows)
+                ent["w"] = pb.pack(W, rows=rows)
             else:
                 ent["w"] = self.Pc(pre + "weight").view(Cout, -1)
             pk[pre] = ent
         for pre in self.off_list:
             W = self.P(pre + "weight")
-            pk[pre] = {"w": ops.pack_conv(W, self.cdt), "wflip": ops.pack_conv(W, self.cdt, flip=True)}
+            pk[pre] = {"w": pb.pack(W), "wflip": pb.pack(W, flip=True)}
+        pb.run()
         self.packs = pk
 
     # ------------------------------------------------------------------
@@ -193,7 +195,7 @@ class GeneratorEngine:
         ops.gemm(gdd, pk["wsq"], B, Cin, rows, b_kc=False, out=gs,
                  ep=E_(alpha=2.0, scale=s, scale_ld=s.stride(0), accumulate=1))  # gs += 2 s (gdd @ wsq)
         ops.linear_wgrad(gs, w, self.G(pre + "modulation.weight"))
-        ops.colsum(gs, self.G(pre + "modulation.bias"))
+        ops.colsum(gs, self.G(pre + "modulation.bias"), defer=True)
         ops.gemm(gs, self.P(pre + "modulation.weight"), B, w.shape[1], Cin, b_kc=False, out=gw,
                  ep=E_(accumulate=1))
 
@@ -223,7 +225,7 @@ class GeneratorEngine:
                               self.G(pre + "offset_net.2.weight"), self.G(pre + "offset_net.2.bias"), accumulate)
             ops.conv2d(ga1, opk["wflip"], Cin, 3, 3, 1, 1, out=gx.view(B, H, W, Cin), ep=E_(accumulate=1))
             ops.conv2d_wgrad(ga1, x, 32, 3, 3, 1, 1, self.G(pre + "offset_net.0.weight"))
-            ops.colsum(ga1.view(P, 32), self.G(pre + "offset_net.0.bias"))
+            ops.colsum(ga1.view(P, 32), self.G(pre + "offset_net.0.bias"), defer=True)
             return
         gx32 = ops.zeros(B, H, W, Cin, device=self.dev)
         goff = torch.empty(P, 2, device=self.dev, dtype=torch.float32)
@@ -233,7 +235,7 @@ class GeneratorEngine:
                             self.G(pre + "offset_net.2.weight"), self.G(pre + "offset_net.2.bias"))
         ops.conv2d(ga1, opk["wflip"], Cin, 3, 3, 1, 1, out=gx32, ep=E_(accumulate=1))
         ops.conv2d_wgrad(ga1, x, 32, 3, 3, 1, 1, self.G(pre + "offset_net.0.weight"))
-        ops.colsum(ga1.view(P, 32), self.G(pre + "offset_net.0.bias"))
+        ops.colsum(ga1.view(P, 32), self.G(pre + "offset_net.0.bias"), defer=True)
         ops.copy2d(gx32.view(P, Cin), gx.view(P, Cin), P, Cin, accumulate=accumulate)
 
     # ------------------------------------------------------------------
@@ -311,12 +313,14 @@ class GeneratorEngine:
                       gate_pos=gate_pos, Pre=Pre, Hid=Hid, Xg=Xg, Y=Y, W1=W1, W2=W2, max_tiles=max_tiles)
         return out, probs, kl2, topi, sv
 
-    def _router_weights(self, r, eps, train):
-        """Reparameterised router weights (t2i_moe_gan.py:302-333) in train mode, the means in eval mode."""
+    def _router_weights(self, r, eps, train, pb=None):
+        """Reparameterised router weights (t2i_moe_gan.py:302-333) in train mode, the means in eval mode.
+        With a PrepBatch ``pb`` the three reparameterisations join its launch (the caller runs it)."""
         if train:
-            return (ops.reparam(self.P(r + "feature_mu"), self.P(r + "feature_rho"), eps[0]),
-                    ops.reparam(self.P(r + "text_mu"), self.P(r + "text_rho"), eps[1]),
-                    ops.reparam(self.P(r + "combined_mu"), self.P(r + "combined_rho"), eps[2]))
+            rp = pb.reparam if pb is not None else ops.reparam
+            return (rp(self.P(r + "feature_mu"), self.P(r + "feature_rho"), eps[0]),
+                    rp(self.P(r + "text_mu"), self.P(r + "text_rho"), eps[1]),
+                    rp(self.P(r + "combined_mu"), self.P(r + "combined_rho"), eps[2]))
         return self.P(r + "feature_mu"), self.P(r + "text_mu"), self.P(r + "combined_mu")
 
     def _block_vectors(self, w, text_seq, eps, train):
@@ -346,14 +350,16 @@ class GeneratorEngine:
             src = outs
         E = self.E
         probs1, probs2 = [], []
+        pb = ops.PrepBatch(torch.float32)  # the routers' reparameterisations: one launch
         for i, (p, C) in enumerate(zip(pres, Cs)):
             d = bv[p + "moe."]
-            Wf, Wt, Wc = self._router_weights(p + "moe.router.", None if eps is None else eps[i], train)
+            Wf, Wt, Wc = self._router_weights(p + "moe.router.", None if eps is None else eps[i], train, pb)
             d.update(Wf=Wf, Wt=Wt, Wc=Wc, Wfc=torch.empty(C, E, device=dev), u=torch.empty(B, 128, device=dev),
                      Lt=torch.empty(B, E, device=dev))
             probs1.append(dict(A=Wf, B=Wc[:128], M=C, N=E, K=128, out=d["Wfc"]))  # Wf @ Wc1
             probs1.append(dict(A=w, B=Wt, M=B, N=128, K=w.shape[1], out=d["u"]))  # w @ Wt
             probs2.append(dict(A=d["u"], B=Wc[128:], M=B, N=E, K=128, out=d["Lt"]))  # u @ Wc2
+        pb.run()
         ops.gemm_batch(probs1, b_kc=False)
         ops.gemm_batch(probs2, b_kc=False)
         for i, p in enumerate(pres):
@@ -394,7 +400,7 @@ class GeneratorEngine:
                 else:
                     q[gout] = torch.empty(M, Wm.shape[1], device=dev)
                     dg.append(dict(A=g, B=Wm, M=M, N=Wm.shape[1], K=N, out=q[gout]))
-                ops.colsum(g, q[gbk])
+                ops.colsum(g, q[gbk], defer=True)
             ops.gemm_batch(wg, a_kc=False, b_kc=False)
             ops.gemm_batch(dg, a_kc=True, b_kc=False)
 
@@ -535,7 +541,7 @@ class GeneratorEngine:
         g_qkv = ops.attn_bwd(sv["qkv"], sv["att"], g_att, sv["lse"], B, L_, C)
         g_n1 = ops.linear_dgrad(g_qkv, self.Pc(pre + "self_attn.in_proj_weight"))
         gWqkv, gbqkv = self.G(pre + "self_attn.in_proj_weight"), self.G(pre + "self_attn.in_proj_bias")
-        self.side.run(lambda: (ops.linear_wgrad(g_qkv, sv["n1"], gWqkv), ops.colsum(g_qkv, gbqkv)), g_qkv)
+        self.side.run(lambda: (ops.linear_wgrad(g_qkv, sv["n1"], gWqkv), ops.colsum(g_qkv, gbqkv, defer=True)), g_qkv)
         g_xf0 = g_xf1
         ops.layernorm_bwd(g_n1, sv["xf0"], sv["mu1"], sv["rs1"], self.P(pre + "norm1.weight"), g_xf0,
                           self.G(pre + "norm1.weight"), self.G(pre + "norm1.bias"), accumulate=1)
@@ -710,39 +716,41 @@ class GeneratorEngine:
                                ep=E_(alpha=2.0, scale=s, scale_ld=s.stride(0), accumulate=1)))  # gs += 2 s (gdd@wsq)
             ops.gemm_batch(pw, a_kc=False, b_kc=False)
             ops.gemm_batch(pg, a_kc=True, b_kc=False)
+            pb = ops.PrepBatch(torch.float32)
             for (pre, _, _, _, _, Cin, rows, Cout), q in zip(self._demod_bwd, pw):
-                ops.wsq_bwd(self.P(pre + "weight"), q["out"][:Cout], self.G(pre + "weight"))
+                pb.wsq_bwd(self.P(pre + "weight"), q["out"][:Cout], self.G(pre + "weight"))
+            pb.run()
             self._demod_bwd = []
             GS, self._GS = self._GS, None
             GSc = self._c(GS)
             ops.linear_wgrad(GSc, ctx["w_c"], self.style_gW)
-            ops.colsum(GS, self.style_gb)
+            ops.colsum(GS, self.style_gb, defer=True)
             ops.gemm(GSc, self.style_Wc, B, gw.shape[1], self.style_n, b_kc=False, out=gw, ep=E_(accumulate=1))
         # truncation: w = mean + psi (w_full - mean), mean under no_grad
         psi = ctx["psi"]
         g6 = ops.cast(gw, self.cdt, alpha=psi if psi < 1.0 else 1.0)
         hs = ctx["hs"]
         ops.linear_wgrad(g6, hs[3], self.G("mapping.6.weight"))
-        ops.colsum(g6, self.G("mapping.6.bias"))
+        ops.colsum(g6, self.G("mapping.6.bias"), defer=True)
         g = ops.linear_dgrad(g6, self.Pc("mapping.6.weight"))
         for j, i in enumerate((4, 2, 0)):
             ops.lrelu_mask_mul(g, hs[3 - j], g)
             ops.linear_wgrad(g, hs[2 - j], self.G(f"mapping.{i}.weight"))
-            ops.colsum(g, self.G(f"mapping.{i}.bias"))
+            ops.colsum(g, self.G(f"mapping.{i}.bias"), defer=True)
             if i != 0 or want_input_grads:
                 g = ops.linear_dgrad(g, self.Pc(f"mapping.{i}.weight"))
         g_zt = g if want_input_grads else None
         # text projection backward
         g_tsc = self._c(g_ts)
         ops.linear_wgrad(g_tsc, ctx["t1c"], self.G("text_projection.3.weight"))
-        ops.colsum(g_ts, self.G("text_projection.3.bias"))
+        ops.colsum(g_ts, self.G("text_projection.3.bias"), defer=True)
         g_t1 = ops.linear_dgrad(g_tsc, self.Pc("text_projection.3.weight"), out_dtype=torch.float32)
         ops.lrelu_mask_mul(g_t1, ctx["t1"], g_t1)
         g_t0 = torch.empty_like(g_t1)
         ops.layernorm_bwd(g_t1, ctx["t0"], ctx["tmu"], ctx["trs"], self.P("text_projection.1.weight"), g_t0,
                           self.G("text_projection.1.weight"), self.G("text_projection.1.bias"))
         ops.linear_wgrad(self._c(g_t0), ctx["text_c"], self.G("text_projection.0.weight"))
-        ops.colsum(g_t0, self.G("text_projection.0.bias"))
+        ops.colsum(g_t0, self.G("text_projection.0.bias"), defer=True)
         if not want_input_grads:
             return None, None
         gtext = ops.linear_dgrad(g_t0, self.P("text_projection.0.weight"))

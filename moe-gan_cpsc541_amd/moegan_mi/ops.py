@@ -196,6 +196,15 @@ def dgrad_s2(g, wcls, Cin, out, ep=None):
     return out
 
 
+def dgrad_s2_small(g, wpack, Cin, out):
+    """4x4/s2/p1 conv data gradient for few input channels (Cin <= 4): Y = g @ wpack ([Cg, 16*Cin] pack_conv
+    layout; fp32), then mg_col2im_4x4s2 into out [B, 2OH, 2OW, ldo] (channels < Cin written)."""
+    B, OH, OW, Cg = g.shape
+    Y = gemm(g.view(-1, Cg), wpack, B * OH * OW, 16 * Cin, Cg, b_kc=False, out_dtype=torch.float32)
+    call("mg_col2im_4x4s2", L.MG_F32, ptr(Y), 16 * Cin, B, OH, OW, Cin, dt(out), ptr(out), out.shape[-1], S())
+    return out
+
+
 def gemm_grouped(A, B, row_off, tile_off, max_tiles, N, K, *, b_kc=True, b_gstride, out, ep=None, lda=None,
                  ldb=None, ldc=None):
     _timed("gemm_grouped", (out.shape[0], N, K),
@@ -246,6 +255,62 @@ def wsq(W, rows=None):
     return out
 
 
+class PrepBatch:
+    """Weight-preparation jobs (packs, demodulation sums and their backward, router reparameterisation)
+    collected and launched as one mg_prep_batch call; the outputs are allocated when a job is added."""
+
+    def __init__(self, dtype):
+        self.dtype = dtype
+        self.descs, self.keep = [], []
+
+    def _add(self, kind, W, out, Cout=0, Cin=0, KH=0, KW=0, rows=0, n=0, aux=None, aux2=None):
+        assert W.is_contiguous() and out.is_contiguous()
+        self.descs.append(L.PrepDesc(kind, Cout, Cin, KH, KW, rows, n, W.data_ptr(),
+                                     None if aux is None else aux.data_ptr(),
+                                     None if aux2 is None else aux2.data_ptr(), out.data_ptr()))
+        self.keep += [W, out, aux, aux2]
+        return out
+
+    def pack(self, W, rows=None, flip=False):
+        Cout, Cin, KH, KW = W.shape
+        if flip:
+            rows = rows or Cin
+            out = torch.empty(rows, KH * KW * Cout, device=W.device, dtype=self.dtype)
+            return self._add(L.PREP_PACK_FLIP, W, out, Cout, Cin, KH, KW, rows)
+        rows = rows or Cout
+        out = torch.empty(rows, KH * KW * Cin, device=W.device, dtype=self.dtype)
+        return self._add(L.PREP_PACK, W, out, Cout, Cin, KH, KW, rows)
+
+    def pack_dgrad_s2(self, W, rows=None):
+        Cg, Cin = W.shape[:2]
+        rows = rows or Cin
+        out = torch.empty(4, rows, 4 * Cg, device=W.device, dtype=self.dtype)
+        return self._add(L.PREP_PACK_DGRAD_S2, W, out, Cg, Cin, 4, 4, rows)
+
+    def wsq(self, W, rows=None):
+        Cout, Cin = W.shape[:2]
+        taps = W[0, 0].numel()
+        rows = rows or Cout
+        out = torch.empty(rows, Cin, device=W.device, dtype=torch.float32)
+        return self._add(L.PREP_WSQ, W, out, Cout, Cin, taps, 1, rows)
+
+    def wsq_bwd(self, W, gwsq, gW):
+        Cout, Cin = W.shape[:2]
+        assert gwsq.is_contiguous()
+        return self._add(L.PREP_WSQ_BWD, W, gW, Cout, Cin, W[0, 0].numel(), 1, aux=gwsq)
+
+    def reparam(self, mu, rho, eps):
+        W = torch.empty_like(mu)
+        return self._add(L.PREP_REPARAM, mu, W, n=mu.numel(), aux=rho, aux2=eps)
+
+    def run(self):
+        if self.descs:
+            n = len(self.descs)
+            arr = (L.PrepDesc * n)(*self.descs)
+            call("mg_prep_batch", L.MG_BF16 if self.dtype == torch.bfloat16 else L.MG_F32, n, arr, S())
+        self.descs, self.keep = [], []
+
+
 def wsq_bwd(W, gwsq, gW):
     Cout, Cin = W.shape[:2]
     call("mg_wsq_bwd", ptr(W), ptr(gwsq), Cout, Cin, W[0, 0].numel(), ptr(gW), S())
@@ -263,10 +328,39 @@ def copy2d(x, out, R, C, alpha=1.0, accumulate=0, ldi=None, ldo=None):
     return out
 
 
-def colsum(X, out, R=None, C=None, ld=None):
+class ColsumQueue:
+    """Bias-gradient column sums deferred to one mg_colsum_batch launch.  Only active inside a training step
+    (TrainStep sets ``active`` and flushes before the gradients are read); everywhere else ``colsum(...,
+    defer=True)`` runs at once.  A deferred source must not be written again before the flush."""
+
+    def __init__(self):
+        self.active = False
+        self.items = []  # (ColsumDesc, X, out)
+
+    def add(self, X, out, R, C, ld):
+        self.items.append((L.ColsumDesc(dt(X), R, C, ld, X.data_ptr(), out.data_ptr()), X, out))
+
+    def flush(self):
+        if not self.items:
+            return
+        n = len(self.items)
+        arr = (L.ColsumDesc * n)(*[d for d, _, _ in self.items])
+        call("mg_colsum_batch", n, arr, S())
+        self.items = []
+
+
+COLSUMS = ColsumQueue()
+
+
+def colsum(X, out, R=None, C=None, ld=None, defer=False):
+    """out += column sums of X (mg_colsum); ``defer`` queues it on COLSUMS while a step is running."""
     R = R if R is not None else X.shape[0]
     C = C if C is not None else X.shape[-1]
-    call("mg_colsum", dt(X), ptr(X), ld or X.shape[-1], R, C, ptr(out), S())
+    ld = ld or X.shape[-1]
+    if defer and COLSUMS.active:
+        COLSUMS.add(X, out, R, C, ld)
+        return out
+    call("mg_colsum", dt(X), ptr(X), ld, R, C, ptr(out), S())
     return out
 
 

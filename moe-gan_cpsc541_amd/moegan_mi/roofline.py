@@ -157,8 +157,10 @@ class Attribution:
     event pair brackets only its own kernels.  ``host_bound`` reports whether the GPU caught up with the host
     anyway (the lead was too short), which would inflate the small families."""
 
-    def __init__(self, lead_ms=150.0):
+    def __init__(self, lead_ms=150.0, keep_args=False):
         self.calls = []  # (entry point, family, work, start event, end event)
+        self.keep_args = keep_args
+        self.args = []  # scalar arguments per call (keep_args)
         self.lead_ms = lead_ms
         self.host_bound = None
 
@@ -177,6 +179,8 @@ class Attribution:
         rc = run()
         e.record()
         self.calls.append((name, _FAMILY_OF.get(name, "other"), w, s, e))
+        if self.keep_args:
+            self.args.append({k: v for k, v in a.items() if isinstance(v, (int, float))})
         return rc
 
     def __enter__(self):
@@ -195,6 +199,16 @@ class Attribution:
         L.HOOK = None
         if self.calls:
             self.host_bound = bool(self.calls[0][3].query())  # first call already ran: the GPU caught up
+
+    def top_calls(self, family=None, n=30):
+        """The n slowest calls (of one family), with their scalar shape arguments (needs keep_args)."""
+        torch.cuda.synchronize()
+        rows = []
+        for i, (name, f, w, s, e) in enumerate(self.calls):
+            if family is None or f == family:
+                ms = s.elapsed_time(e)
+                rows.append((ms, name, w, self.args[i] if self.keep_args else {}))
+        return sorted(rows, key=lambda r: -r[0])[:n]
 
     def summary(self, steps=1, peak_tflops=2500.0, peak_gbs=8000.0):
         torch.cuda.synchronize()

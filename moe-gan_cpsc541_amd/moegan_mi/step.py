@@ -150,11 +150,14 @@ class TrainStep:
         the reference, the generator step's loss also accumulates into the discriminator's gradients, which
         matters only when the D optimizer has not stepped yet in the window (acc > 1)."""
         ops.ARENA.begin(self.dev)
+        ops.COLSUMS.active = True  # bias-gradient column sums batched per backward (flushed below)
         try:
             return self._step(real, text, z, eps_d, eps_g, perm, anneal, lr_g, lr_d, eff_kl_weight, prep, acc,
                               zero_grads, step_optim)
         finally:
             ops.ARENA.end()
+            ops.COLSUMS.active = False
+            ops.COLSUMS.items = []
             self.ge.guard_flags = None
 
     def _step(self, real, text, z, eps_d, eps_g, perm, anneal, lr_g, lr_d, eff_kl_weight, prep, acc, zero_grads,
@@ -181,6 +184,7 @@ class TrainStep:
                                                         want_kl=False, keep_prefix=True)
         prefix, self.ge.last_prefix = self.ge.last_prefix, None
         dres = self.de.d_phase(real, text, f16, ("nhwc", 8), perm, c.r1_gamma)
+        ops.COLSUMS.flush()
         # guard: NaN / Inf d_loss skips the whole batch (t2i_moe_gan.py:1315-1320)
         ops.finite_flag(dres["losses"][:1], FD, flags)
         ops.finite_flag(dres["r1"], FD, flags)
@@ -210,6 +214,7 @@ class TrainStep:
         if leak:
             ds.zero_grad()
         g_gan, fake_pred, g_img = self.de.g_phase(img16, ("nhwc", 8), text, want_d_params=leak)
+        ops.COLSUMS.flush()
         # balance loss on the last MoE layer, over the GLOBAL batch (t2i_moe_gan.py:951-1000)
         last = probs[-1]
         load = ops.zeros(c.E, device=self.dev)
@@ -237,6 +242,7 @@ class TrainStep:
                         keep_mask=FD, bad_mask=FD, set_bits=ops.WIN_G_KL)
         ops.flag_window(flags, self.win, bad_mask=FD | FG, set_bits=ops.WIN_G_MAIN)
         self.ge.backward(ctx, g_img, coef=coef, kl_coef=kl_coef)
+        ops.COLSUMS.flush()
         if accum:
             ops.gated_axpy(gs.acc[:gs.n_main], gs.grad[:gs.n_main], flags, FD | FG)
             ops.gated_axpy(gs.acc[gs.n_main:gs.n_opt], gs.grad[gs.n_main:gs.n_opt], flags, FD)
