@@ -177,6 +177,16 @@ int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const int32_t* r
                           const void* A, int64_t lda, const void* B, int64_t ldb, const int32_t* b_idx,
                           int b_idx_div, int b_gelu, float* C, int splits, const mg_epilogue* ep, void* stream);
 
+/* Fused expert FFN forward (t2i_moe_gan.py:257-263 for every expert of a SparseMoE at once): for the rows of
+   group g (row_off / tile_off as mg_moe_dispatch builds them with bm = 128),
+     Y[r] = GELU(X[r] W1[g]^T + b1[g]) W2[g]^T + b2[g]
+   with W1 [G][Hd][C], W2 [G][C][Hd] (bf16), b1 [G][Hd], b2 [G][C] (fp32), Y [rows][C].  The hidden activation
+   stays on chip; pre (the pre-activation) and hid (the GELU output) [rows][Hd] are written only when non-NULL
+   (the backward's saved tensors); total_rows = row_off[G].  X row r is X[x_idx[r] / x_idx_div] when x_idx is given (the dispatch gather),
+   else X[r].  Same arithmetic as mg_gemm_grouped with the GELU / bias epilogues.  bf16, C in {128, 256},
+   Hd % 64 == 0; grid = max_tiles blocks. */
+int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off, int max_tiles, const void* X, int64_t ldx, const int32_t* x_idx, int x_idx_div, const void* W1, const float* b1, const void* W2, const float* b2, void* pre, void* hid, void* Y, void* stream);
+
 /* ---- op-level entry points ---- */
 
 /* LayerNorm over C (128/256/512) per row (+ optional LeakyReLU), saving mean/rstd. t2i_moe_gan.py:505-507, :684. */

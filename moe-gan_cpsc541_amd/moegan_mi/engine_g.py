@@ -289,16 +289,30 @@ class GeneratorEngine:
         W2 = self.st.group_view(ex + "0.net.2.weight", f"{ex}{E-1}.net.2.weight", self._cbuf())
         b2 = self.st.group_view(ex + "0.net.2.bias", f"{ex}{E-1}.net.2.bias")
         Hd = 4 * C
-        # tokens in dispatch order (k copies per token), shared by the expert GEMM and its weight gradient
-        Xg = ops.gather_rows(tok, perm, k)
-        # the pre-activation is kept only for the backward's GELU' (a no-grad forward skips that store)
-        Pre = torch.empty(n, Hd, device=self.dev, dtype=self.cdt) if save else None
-        Hid = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
-        ops.gemm_grouped(Xg, W1, row_off, tile_off, max_tiles, Hd, C, b_gstride=Hd * C, out=Hid, ldb=C,
-                         ep=E_(bias=b1, act=GELU, out_pre=Pre, ld_pre=Hd if save else 0))
         Y = torch.empty(n, C, device=self.dev, dtype=self.cdt)
-        ops.gemm_grouped(Hid, W2, row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y, ldb=Hd,
-                         ep=E_(bias=b2))
+        if ops.ffn_fusable(self.cdt, C):
+            # fused expert FFN: the hidden activation stays on chip; saved (pre-activation for GELU', GELU output
+            # for dW2, gathered tokens for dW1) only when the backward will run
+            if save:
+                Xg = ops.gather_rows(tok, perm, k)
+                Pre = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+                Hid = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+                ops.moe_ffn_fwd(Xg, W1.view(E, Hd, C), b1, W2.view(E, C, Hd), b2, row_off, tile_off, max_tiles, Y,
+                                pre=Pre, hid=Hid)
+            else:
+                Xg = Pre = Hid = None
+                ops.moe_ffn_fwd(tok, W1.view(E, Hd, C), b1, W2.view(E, C, Hd), b2, row_off, tile_off, max_tiles, Y,
+                                x_idx=perm, x_idx_div=k)
+        else:
+            # tokens in dispatch order (k copies per token), shared by the expert GEMM and its weight gradient
+            Xg = ops.gather_rows(tok, perm, k)
+            # the pre-activation is kept only for the backward's GELU' (a no-grad forward skips that store)
+            Pre = torch.empty(n, Hd, device=self.dev, dtype=self.cdt) if save else None
+            Hid = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+            ops.gemm_grouped(Xg, W1, row_off, tile_off, max_tiles, Hd, C, b_gstride=Hd * C, out=Hid, ldb=C,
+                             ep=E_(bias=b1, act=GELU, out_pre=Pre, ld_pre=Hd if save else 0))
+            ops.gemm_grouped(Hid, W2, row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y, ldb=Hd,
+                             ep=E_(bias=b2))
         out = torch.empty(T, C, device=self.dev, dtype=self.cdt)
         ops.moe_combine(Y, pos_of, gate, resid, out)  # x_spatial + moe_out (:571)
         kl2 = None

@@ -23,7 +23,7 @@ FAMILIES = {
     "conv_fwd": ("mfma", ("mg_conv2d_fwd",)),
     "conv_dgrad_s2": ("mfma", ("mg_conv2d_dgrad_s2",)),
     "conv_wgrad+fold": ("mfma", ("mg_conv2d_wgrad",)),
-    "expert_gemm": ("mfma", ("mg_gemm_grouped", "mg_gemm_grouped_wgrad")),
+    "expert_gemm": ("mfma", ("mg_gemm_grouped", "mg_gemm_grouped_wgrad", "mg_moe_ffn_fwd")),
     "gemm": ("mfma", ("mg_gemm", "mg_gemm_batch")),
     "attention": ("mfma", ("mg_attn_fwd", "mg_attn_bwd")),
     "router_fwd": ("hbm", ("mg_router_fwd",)),
@@ -43,7 +43,7 @@ _FAMILY_OF = {e: f for f, (_, es) in FAMILIES.items() for e in es}
 # rocprofv3 kernel name (regex, first match wins) -> family, for PMC attribution
 KERNELS = [
     (r"k_wgrad_fold|splitk_reduce_kernel<mg::Epi<float>", "conv_wgrad+fold"),
-    (r"gemm_kernel<.*, 1>\(", "expert_gemm"),  # TAG = 1 instantiations (mg_gemm.h)
+    (r"gemm_kernel<.*, 1>\(|k_moe_ffn_fwd", "expert_gemm"),  # TAG = 1 instantiations (mg_gemm.h), fused FFN
     (r"gemm_kernel<[^>]*LdKCConvT", "conv_dgrad_s2"),
     (r"gemm_kernel<.*LdMCConv", "conv_wgrad+fold"),
     (r"gemm_kernel<.*LdKCConv", "conv_fwd"),
@@ -89,6 +89,8 @@ def work(name, a):
         return 2.0 * a["total_rows"] * a["N"] * a["K"]
     if name == "mg_gemm_grouped_wgrad":
         return 2.0 * a["M"] * a["N"] * a["total_rows"]
+    if name == "mg_moe_ffn_fwd":  # two GEMMs per routed row
+        return 4.0 * a["total_rows"] * a["C"] * a["Hd"]
     if name == "mg_attn_fwd":  # S = QK^T, O = PV
         return 4.0 * a["B"] * a["L"] * a["L"] * a["C"]
     if name == "mg_attn_bwd":  # dV, dP, dQ, dK (the S recompute is not algorithmic work)

@@ -1,0 +1,69 @@
+"""Fused expert FFN forward (mg_moe_ffn_fwd) against the two grouped GEMMs it replaces (mg_gemm_grouped with the
+bias + GELU (pre-activation saved) and bias epilogues): bit-identical Y, pre-activation and GELU output, with the
+dispatch gather inside the kernel or from pre-gathered rows; skewed and empty experts, ragged last tiles."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from moegan_mi import _lib as L  # noqa: E402
+from moegan_mi import ops  # noqa: E402
+
+DEV = "cuda"
+bf = torch.bfloat16
+
+
+def _case(T, C, E, k, seed, empty_expert=False):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    tok = (torch.randn(T, C, device=DEV, generator=g)).to(bf)
+    Hd = 4 * C
+    W1 = (torch.randn(E, Hd, C, device=DEV, generator=g) * C ** -0.5).to(bf)
+    b1 = torch.randn(E * Hd, device=DEV, generator=g) * 0.1
+    W2 = (torch.randn(E, C, Hd, device=DEV, generator=g) * Hd ** -0.5).to(bf)
+    b2 = torch.randn(E * C, device=DEV, generator=g) * 0.1
+    topi = torch.randint(0, E, (T, k), device=DEV, generator=g, dtype=torch.int32)
+    topi[: T // 3, 0] = 2  # skew
+    if empty_expert:
+        topi[topi == E - 1] = 0
+    gate = torch.rand(T, k, device=DEV, generator=g)
+    return tok, W1, b1, W2, b2, topi, gate
+
+
+@pytest.mark.parametrize("T,C,E,k", [(65536, 128, 8, 2), (16384, 256, 8, 2), (1000, 128, 8, 2), (300, 256, 4, 1),
+                                     (2048, 128, 32, 4)])
+def test_fused_ffn_matches_grouped_gemms(T, C, E, k):
+    tok, W1, b1, W2, b2, topi, gate = _case(T, C, E, k, T + C, empty_expert=(T == 1000))
+    Hd = 4 * C
+    row_off, tile_off, perm, pos_of, gate_pos = ops.moe_dispatch(topi, gate, E)
+    n = T * k
+    max_tiles = (n + 127) // 128 + E
+    Xg = ops.gather_rows(tok, perm, k)
+    # reference: the unfused path of engine_g.moe_fwd
+    Pre_r = torch.empty(n, Hd, device=DEV, dtype=bf)
+    Hid_r = torch.empty(n, Hd, device=DEV, dtype=bf)
+    ops.gemm_grouped(Xg, W1.view(-1), row_off, tile_off, max_tiles, Hd, C, b_gstride=Hd * C, out=Hid_r, ldb=C,
+                     ep=ops.E(bias=b1, act=L.ACT_GELU, out_pre=Pre_r, ld_pre=Hd))
+    Y_r = torch.empty(n, C, device=DEV, dtype=bf)
+    ops.gemm_grouped(Hid_r, W2.view(-1), row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y_r, ldb=Hd,
+                     ep=ops.E(bias=b2))
+    # fused, saved tensors
+    Pre = torch.empty(n, Hd, device=DEV, dtype=bf)
+    Hid = torch.empty(n, Hd, device=DEV, dtype=bf)
+    Y = torch.empty(n, C, device=DEV, dtype=bf)
+    ops.moe_ffn_fwd(Xg, W1, b1, W2, b2, row_off, tile_off, max_tiles, Y, pre=Pre, hid=Hid)
+    # fused, gather inside, nothing saved
+    Y2 = torch.empty(n, C, device=DEV, dtype=bf)
+    ops.moe_ffn_fwd(tok, W1, b1, W2, b2, row_off, tile_off, max_tiles, Y2, x_idx=perm, x_idx_div=k)
+    torch.cuda.synchronize()
+    assert torch.equal(Pre, Pre_r)
+    assert torch.equal(Hid, Hid_r)
+    assert torch.equal(Y, Y_r)
+    assert torch.equal(Y2, Y_r)
+    # and against float64 math on the same bf16 operands (sampled rows)
+    rows = torch.randperm(n, device=DEV)[:64]
+    e_of = torch.bucketize(rows.int(), row_off[1:].contiguous(), right=True)
+    x = Xg[rows].double()
+    h = torch.einsum("rc,rhc->rh", x, W1[e_of].double()) + b1.view(E, Hd)[e_of].double()
+    hg = torch.nn.functional.gelu(h).to(bf).double()
+    y = torch.einsum("rh,rch->rc", hg, W2[e_of].double()) + b2.view(E, C)[e_of].double()
+    assert (Y[rows].double() - y).abs().max() <= 2e-2 * y.abs().max() + 1e-3

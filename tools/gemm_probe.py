@@ -87,6 +87,18 @@ def main():
     cases.append(("expert_fc1", 2.0 * E_ * rows * 512 * 128,
                   lambda: ops.gemm_grouped(Ae, We, row_off, tile_off, E_ * rows // 128, 512, 128, b_gstride=512 * 128,
                                            out=oute, ep=ops.E(act=L.ACT_GELU))))
+    # fused expert FFN (fc1 + GELU + fc2 on chip), no-grad and saved forms
+    We1 = rn(E_, 512, 128, dt=bf, sc=0.08)
+    We2 = rn(E_, 128, 512, dt=bf, sc=0.04)
+    be1, be2 = rn(E_ * 512), rn(E_ * 128)
+    Yf = torch.empty(E_ * rows, 128, device=dev, dtype=bf)
+    Pf = torch.empty(E_ * rows, 512, device=dev, dtype=bf)
+    Hf = torch.empty(E_ * rows, 512, device=dev, dtype=bf)
+    mt = E_ * rows // 128 + E_
+    cases.append(("ffn128_nosave", 4.0 * E_ * rows * 512 * 128,
+                  lambda: ops.moe_ffn_fwd(Ae, We1, be1, We2, be2, row_off, tile_off, mt, Yf)))
+    cases.append(("ffn128_save", 4.0 * E_ * rows * 512 * 128,
+                  lambda: ops.moe_ffn_fwd(Ae, We1, be1, We2, be2, row_off, tile_off, mt, Yf, pre=Pf, hid=Hf)))
     # expert weight gradient (grouped over rows, plain operands)
     gG = rn(E_ * rows, 128, dt=bf)
     Hid = rn(E_ * rows, 512, dt=bf)
