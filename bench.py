@@ -38,6 +38,10 @@ def parse():
     ap.add_argument("--experts", type=int, default=8)
     ap.add_argument("--topk", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--config", default="C2", choices=["C2", "C5"],
+                    help="C2 = BASELINE configs[1] (the headline line); C5 = the single-GPU slice of configs[4]: "
+                         "32 experts top-4, MX-fp8 3x3 modulated convs")
+    ap.add_argument("--fp8", action="store_true", help="MX-fp8 3x3 modulated convs (implied by --config C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU-oracle steps (B=8; ~10-20 s of CPU work)")
     ap.add_argument("--time-kernel", default="d_conv1",
@@ -49,7 +53,11 @@ def parse():
                     help="skip the per-family roofline attribution step (one extra eager step after the timed region)")
     ap.add_argument("--one-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box, with --backend gloo)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.config == "C5":  # BASELINE configs[4]: 64x64, 32 experts top-4, fp8 MFMA conv path, KL + balance
+        args.experts, args.topk, args.fp8 = 32, 4, True
+    assert not args.fp8 or args.dtype == "bf16", "the MX-fp8 convs run inside the bf16 mode"
+    return args
 
 
 EPS_DIMS = [(512, 512), (256, 512), (128, 512)]  # (C, text) per MoE block: eps_f [C,128], eps_t [512,128], eps_c
@@ -130,7 +138,7 @@ def main():
     from moegan_mi.step import StepConfig, TrainStep
 
     E, k, B = args.experts, args.topk, args.batch
-    ts = TrainStep(StepConfig(E=E, topk=k, dtype=args.dtype), dev, process_group=pg)
+    ts = TrainStep(StepConfig(E=E, topk=k, dtype=args.dtype, fp8=args.fp8), dev, process_group=pg)
     init_generator(ts.gs, seed=0)
     init_discriminator(ts.ds, seed=1)
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -233,7 +241,8 @@ def main():
             if not os.path.exists(path):
                 return None
             rec = json.load(open(path))
-            ok = rec.get("batch") == B and rec.get("dtype") == args.dtype and rec.get("experts") == E
+            ok = (rec.get("batch") == B and rec.get("dtype") == args.dtype and rec.get("experts") == E and
+                  bool(rec.get("fp8", False)) == args.fp8)
             return rec if ok else None
 
         ftime, ftraf = _prof("family_time.json"), _prof("family_traffic.json")
@@ -276,7 +285,7 @@ def main():
         pmc = os.path.join(REPO, "profiles", "pmc_roofline_kernel.json")
         if os.path.exists(pmc):  # HBM bytes per launch from the committed rocprofv3 --pmc passes
             rec = json.load(open(pmc))
-            if rec.get("batch") == B and args.dtype == "bf16":
+            if rec.get("batch") == B and args.dtype == "bf16" and not args.fp8:
                 traffic = rec["traffic_bytes_per_launch"]
         roof = {"bound": "mfma", "kernel": "mg_conv2d_fwd D conv_layers.2 (64x64 real), implicit GEMM "
                                           f"M={M} N={N} K={K}", "achieved": round(achieved, 2) if achieved else None,
@@ -293,8 +302,12 @@ def main():
         line = {"metric": "images/sec (G+D step, 64x64 MS-COCO layout)", "value": round(value, 2),
                 "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                "dtype": args.dtype, "data": "synthetic (U(-1,1) images, N(0,1) 512-d captions, random init)",
-                "config": {"workload": f"C2: 64x64, {E} experts top-{k}, batch {B}/GPU, {args.dtype}, R1 on",
+                "dtype": args.dtype + ("+mx8" if args.fp8 else ""),
+                "data": "synthetic (U(-1,1) images, N(0,1) 512-d captions, random init)",
+                "config": {"workload": (f"C5 single-GPU slice: 64x64, {E} experts top-{k}, batch {B}/GPU, bf16 with "
+                                        "MX-fp8 (e4m3) 3x3 modulated-conv GEMMs, KL + balance, R1 on") if args.config == "C5"
+                           else f"C2: 64x64, {E} experts top-{k}, batch {B}/GPU, {args.dtype}"
+                                + (" + MX-fp8 3x3 convs" if args.fp8 else "") + ", R1 on",
                            "global_batch": B * world, "experts": E, "topk": k, "parallelism": f"dp{world}",
                            "launch": "eager" if args.eager else "hipGraph replay"},
                 "step_tflops_algorithmic": round(step_tflops, 2),

@@ -143,6 +143,22 @@ int mg_conv2d_fwd(int dtype, const void* x, int B, int H, int W, int Cin, const 
                   int KW, int stride, int pad, const float* in_scale, void* y, int64_t ldy, int y_dtype,
                   const mg_epilogue* ep, void* stream);
 
+/* MX-fp8 form of mg_conv2d_fwd (BASELINE config C5, "fp8 MFMA conv path"; same math as :169-180):
+ *   y[b,oh,ow,o] = epilogue( sum_{kh,kw,ci} Q(x)[b,ih,iw,ci] * Q(W)[o][(kh*KW+kw)*Cin+ci] )
+ * Q = OCP MX quantization: e4m3 elements with one E8M0 scale per 32 consecutive channels, multiplied by
+ * v_mfma_scale_f32_16x16x128_f8f6f4 (fp32 accumulation).  x / xscale = mg_quant_mx8 of the NHWC
+ * activation rows ([B*H*W][Cin] e4m3, [B*H*W][Cin/32] E8M0); wq / wscale = mg_quant_mx8 of the packed
+ * [Cout][KH*KW*Cin] bf16 weights.  Cin a power of two >= 128; in_scale is not supported (quantize x * s).
+ * Replaces the 3x3 modulated-conv forward and data-gradient GEMMs under fp8 (engine_g.mc_fwd / mc_bwd). */
+int mg_conv2d_fwd_mx8(const void* x, const void* xscale, int B, int H, int W, int Cin, const void* wq,
+                      const void* wscale, int Cout, int KH, int KW, int stride, int pad, void* y, int64_t ldy, int y_dtype, const mg_epilogue* ep,
+                      void* stream);
+
+/* MX-fp8 quantization of bf16 rows: x [rows][K] (pitch ldx) -> q [rows][K] e4m3 bytes and
+ * scale [rows][K/32] E8M0 bytes; per 32-element block e = ceil(log2(amax / 448)) + 127 (nothing saturates),
+ * round-to-nearest-even.  K % 32 == 0.  Used per optimizer step for the fp8 conv weights. */
+int mg_quant_mx8(const void* x, int64_t ldx, int64_t rows, int K, void* q, void* scale, void* stream);
+
 /* Weight gradient of the convolution above, accumulated (fp32 atomics) into
  * gw in the reference layout [Cout][Cin][KH][KW]:
  *   gw[o,ci,kh,kw] += sum_{b,oh,ow} gy[b,oh,ow,o] * x[b,ih,iw,ci] * in_scale[b,ci] */

@@ -29,6 +29,8 @@ MG_DEV void stf(bf16_t* p, int64_t i, float v) { p[i] = f2bf(v); }
 template <typename T> struct VecOf;  // 16-byte vectors
 template <> struct VecOf<float> { static constexpr int N = 4; typedef f32x4_t type; };
 template <> struct VecOf<bf16_t> { static constexpr int N = 8; typedef u16x8_t type; };
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+template <> struct VecOf<uint8_t> { static constexpr int N = 16; typedef u32x4_t type; };  // e4m3 bytes
 
 // 8 consecutive elements <-> float[8] (16-B aligned bf16, or 2 x 16-B fp32)
 MG_DEV void ld8(const float* p, float* t) {

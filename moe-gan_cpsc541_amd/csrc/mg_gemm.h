@@ -557,6 +557,63 @@ MG_DEV bf16x8_t mc_frag_bf16(const bf16_t* img, int ld, int kr0, int c0, int lan
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// Epilogue of one output tile: stage one 16-row band of each wave's accumulators through LDS (`smem`, at
+// least 4 * 16 * (BN/2 + 4) floats), then a plain (non-unrolled) loop applies the fused epilogue with
+// consecutive lanes on consecutive columns.  Static indexing keeps acc in registers; the loop keeps the
+// inlined epilogue code small.  Waves are arranged 2x2, each owning a (BM/2)x(BN/2) block of 16x16 fragments
+// in the MFMA C/D layout (dtype-independent on gfx950).
+template <int BM, int BN, class EP>
+MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const EP& ep, int m0, int n0, int Mloc,
+                     int N, int mrow_base) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  constexpr int CSP = WN + 4;  // staging pitch in floats (16-B aligned rows)
+  float* cs = reinterpret_cast<float*>(smem) + wid * 16 * CSP;
+  // each wave stages through its own LDS band: one block barrier retires the K loop's reads of the
+  // tiles, after that a wave only orders its own LDS writes and reads (wave-scope fence)
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    if (MG_EPI_BLOCK_SYNC) __syncthreads();
+    else { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[(fq * 4 + r) * CSP + j * 16 + fr] = acc[i][j][r];
+    if (MG_EPI_BLOCK_SYNC) __syncthreads();
+    else { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
+    const int mb = m0 + wm * WM + i * 16, nb = n0 + wn * WN;
+    if (ep.vec_ok) {
+      // 8 consecutive columns per lane: vector loads of the epilogue operands, one 16-B store (bf16)
+#pragma unroll 1
+      for (int e = lane; e < 2 * WN; e += 64) {
+        int rr = e / (WN / 8), cc = (e - (e / (WN / 8)) * (WN / 8)) * 8;
+        int m = mb + rr, n = nb + cc;
+        if (m >= Mloc) continue;
+        const float* src = cs + rr * CSP + cc;
+        if (n + 8 <= N) {
+          float v[8];
+          f32x4_t a = *reinterpret_cast<const f32x4_t*>(src), b = *reinterpret_cast<const f32x4_t*>(src + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+          ep.vec8(mrow_base + m, n, v);
+        } else {
+          for (int j = 0; j < 8 && n + j < N; ++j) ep(mrow_base + m, n + j, src[j]);
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int e = lane; e < 16 * WN; e += 64) {
+        int rr = e / WN, cc = e - (e / WN) * WN;
+        int m = mb + rr, n = nb + cc;
+        if (m < Mloc && n < N) ep(mrow_base + m, n, cs[rr * CSP + cc]);
+      }
+    }
+  }
+}
+
 // One output tile: C[m0.., n0..] of rows [mrow_base, mrow_base + Mloc) over k in [kbeg, kend).
 template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
 MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, int Mloc, int N, int kbeg, int kend,
@@ -784,52 +841,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     }
   }
 
-  // ---- epilogue: stage one 16-row band of each wave's accumulators through LDS, then a plain
-  // (non-unrolled) loop applies the fused epilogue with consecutive lanes on consecutive columns.
-  // Static indexing keeps acc in registers; the loop keeps the inlined epilogue code small.
-  constexpr int CSP = WN + 4;  // staging pitch in floats (16-B aligned rows)
-  float* cs = reinterpret_cast<float*>(smem) + wid * 16 * CSP;
-  // each wave stages through its own LDS band: one block barrier retires the K loop's reads of the
-  // tiles, after that a wave only orders its own LDS writes and reads (wave-scope fence)
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    if (MG_EPI_BLOCK_SYNC) __syncthreads();
-    else { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cs[(fq * 4 + r) * CSP + j * 16 + fr] = acc[i][j][r];
-    if (MG_EPI_BLOCK_SYNC) __syncthreads();
-    else { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
-    const int mb = m0 + wm * WM + i * 16, nb = n0 + wn * WN;
-    if (ep.vec_ok) {
-      // 8 consecutive columns per lane: vector loads of the epilogue operands, one 16-B store (bf16)
-#pragma unroll 1
-      for (int e = lane; e < 2 * WN; e += 64) {
-        int rr = e / (WN / 8), cc = (e - (e / (WN / 8)) * (WN / 8)) * 8;
-        int m = mb + rr, n = nb + cc;
-        if (m >= Mloc) continue;
-        const float* src = cs + rr * CSP + cc;
-        if (n + 8 <= N) {
-          float v[8];
-          f32x4_t a = *reinterpret_cast<const f32x4_t*>(src), b = *reinterpret_cast<const f32x4_t*>(src + 4);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
-          ep.vec8(mrow_base + m, n, v);
-        } else {
-          for (int j = 0; j < 8 && n + j < N; ++j) ep(mrow_base + m, n + j, src[j]);
-        }
-      }
-    } else {
-#pragma unroll 1
-      for (int e = lane; e < 16 * WN; e += 64) {
-        int rr = e / WN, cc = e - (e / WN) * WN;
-        int m = mb + rr, n = nb + cc;
-        if (m < Mloc && n < N) ep(mrow_base + m, n, cs[rr * CSP + cc]);
-      }
-    }
-  }
+  epi_tile<BM, BN>(acc, smem, ep, m0, n0, Mloc, N, mrow_base);
 }
 
 

@@ -40,7 +40,7 @@ def _offset_prefixes():
 
 
 class GeneratorEngine:
-    def __init__(self, store, E, topk=None, cdt=torch.float32, modconvs=None, offset_nets=None):
+    def __init__(self, store, E, topk=None, cdt=torch.float32, modconvs=None, offset_nets=None, fp8=False):
         """``modconvs`` [(prefix, k)] / ``offset_nets`` [prefix]: the modulated convs and MTM offset heads prep()
         packs -- the whole generator's by default; the sub-module API (modules.py) passes its own."""
         self.st = store
@@ -49,6 +49,10 @@ class GeneratorEngine:
         self.E = E
         self.k = topk or E
         self.cdt = cdt
+        # MX-fp8 (e4m3 + per-32-channel E8M0 scales) for the 3x3 modulated-conv forward and data-gradient GEMMs
+        # (BASELINE config C5); needs the bf16 compute dtype and >= 128 channels on the reduction side
+        self.fp8 = bool(fp8)
+        assert not self.fp8 or cdt == torch.bfloat16, "fp8 modulated convs run inside the bf16 mode"
         self.dev = store.device
         self.packs = {}
         self._ones = None
@@ -116,7 +120,19 @@ class GeneratorEngine:
             W = self.P(pre + "weight")
             pk[pre] = {"w": pb.pack(W), "wflip": pb.pack(W, flip=True)}
         pb.run()
+        if self.fp8:  # per-step MX-fp8 copies of the packed 3x3 weights (forward and flipped data-gradient form)
+            for pre, k in self.mc_list:
+                ent = pk[pre]
+                if k == 3 and self._mx8_ok(self.P(pre + "weight").shape[1]):
+                    ent["wq"] = ops.quant_mx8(ent["w"])
+                if k == 3 and self._mx8_ok(ent["rows"]):
+                    ent["wflipq"] = ops.quant_mx8(ent["wflip"])
         self.packs = pk
+
+    @staticmethod
+    def _mx8_ok(cin):
+        """The MX-fp8 conv reduces over 128-channel steps inside one tap."""
+        return cin >= 128 and cin % 128 == 0 and (cin & (cin - 1)) == 0
 
     # ------------------------------------------------------------------
     # ModulatedConv  (t2i_moe_gan.py:154-186), fused form
@@ -144,7 +160,11 @@ class GeneratorEngine:
                 ld_res=resid.shape[-1] if resid is not None else 0)
         if xs is None:  # x * style, shared by the conv and its weight gradient (the MTM warp writes it itself)
             xs = ops.scale_bc(x, s)
-        y = ops.conv2d(xs, pk["w"], rows, k, k, 1, k // 2, ep=ep, out_dtype=self.cdt)
+        if "wq" in pk:  # MX-fp8: quantize x * s per 32 channels, e4m3 x e4m3 scaled MFMA
+            xq, xsc = ops.quant_mx8(xs.view(-1, Cin))
+            y = ops.conv2d_mx8(xq.view(B, H, W, Cin), xsc, *pk["wq"], rows, k, k, 1, k // 2, ep=ep, out_dtype=self.cdt)
+        else:
+            y = ops.conv2d(xs, pk["w"], rows, k, k, 1, k // 2, ep=ep, out_dtype=self.cdt)
         sv = (x, xs, w, s, s2, d, y, resid, act) if save else None
         return y, sv
 
@@ -163,7 +183,10 @@ class GeneratorEngine:
         ops.modconv_bwd_out(gz.view(P, -1), z.view(P, -1), d, B, HW, rows, act, gyt, gdd,
                             zsub=None if zsub is None else zsub.view(P, -1))
         # data gradient of the shared-weight conv
-        if k == 3:
+        if k == 3 and "wflipq" in pk:  # MX-fp8 data gradient (gradient rows quantized per 32 channels)
+            gq, gsc = ops.quant_mx8(gyt)
+            gxt = ops.conv2d_mx8(gq.view(B, H, W, rows), gsc, *pk["wflipq"], Cin, 3, 3, 1, 1, out_dtype=self.cdt)
+        elif k == 3:
             gxt = ops.conv2d(gyt.view(B, H, W, rows), pk["wflip"], Cin, 3, 3, 1, 1)
         else:
             gxt = ops.gemm(gyt, pk["w"], P, Cin, rows, b_kc=False)

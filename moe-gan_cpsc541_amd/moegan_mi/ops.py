@@ -180,6 +180,33 @@ def conv2d(x, wpack, Cout, KH, KW, stride=1, pad=0, in_scale=None, out=None, out
     return out
 
 
+def quant_mx8(x, K=None):
+    """MX-fp8 quantization of bf16 rows (mg_quant_mx8): x [rows, K] -> (q uint8 e4m3 [rows, K], scale uint8
+    E8M0 [rows, K/32])."""
+    x2 = x.reshape(-1, x.shape[-1]) if K is None else x.reshape(-1, K)
+    rows, K = x2.shape
+    q = torch.empty(rows, K, device=x.device, dtype=torch.uint8)
+    sc = torch.empty(rows, K // 32, device=x.device, dtype=torch.uint8)
+    call("mg_quant_mx8", ptr(x2), x2.stride(0), rows, K, ptr(q), ptr(sc), S())
+    return q, sc
+
+
+def conv2d_mx8(xq, xsc, wq, wsc, Cout, KH, KW, stride=1, pad=0, out=None, out_dtype=torch.bfloat16, ep=None,
+               ldy=None, tag=None):
+    """MX-fp8 NHWC implicit-GEMM conv (mg_conv2d_fwd_mx8): xq [B,H,W,Cin] e4m3 / xsc [B*H*W, Cin/32] and
+    wq / wsc from quant_mx8 (activation rows, packed [Cout, KH*KW*Cin] weights)."""
+    B, H, W, Cin = xq.shape
+    x = xq
+    OH = (H + 2 * pad - KH) // stride + 1
+    OW = (W + 2 * pad - KW) // stride + 1
+    if out is None:
+        out = torch.empty(B, OH, OW, ldy or Cout, device=x.device, dtype=out_dtype)
+    _timed("conv2d_mx8" if tag is None else "conv2d_mx8:" + tag, (B * OH * OW, Cout, KH * KW * Cin),
+           lambda: call("mg_conv2d_fwd_mx8", ptr(x), ptr(xsc), B, H, W, Cin, ptr(wq), ptr(wsc), Cout, KH, KW, stride, pad,
+                        ptr(out), ldy or out.shape[-1], dt(out), ep, S()))
+    return out
+
+
 def conv2d_wgrad(gy, x, Cout, KH, KW, stride, pad, gw, in_scale=None, ldg=None, splits=0):
     """gw [Cout,Cin,KH,KW] fp32 += weight gradient (mg_conv2d_wgrad)."""
     B, H, W, Cin = x.shape

@@ -17,10 +17,12 @@ import torch
 from . import _lib as L
 
 ELT = {0: 4, 1: 2}  # MG_F32, MG_BF16
+MX8_PEAK_TFLOPS = 5000.0  # dense MX-fp8 MFMA peak (MI355X_MICROARCH.md: 2x the bf16 rate per clock)
 
 # family -> (bound, entry points)
 FAMILIES = {
     "conv_fwd": ("mfma", ("mg_conv2d_fwd",)),
+    "conv_fwd_mx8": ("mfma8", ("mg_conv2d_fwd_mx8",)),  # MX-fp8 (C5): priced against the fp8 MFMA peak
     "conv_dgrad_s2": ("mfma", ("mg_conv2d_dgrad_s2",)),
     "conv_wgrad+fold": ("mfma", ("mg_conv2d_wgrad",)),
     "expert_gemm": ("mfma", ("mg_gemm_grouped", "mg_gemm_grouped_wgrad", "mg_moe_ffn_fwd")),
@@ -36,13 +38,14 @@ FAMILIES = {
     "adamw": ("hbm", ("mg_adamw_dev", "mg_adamw_dev_shadow", "mg_adamw")),
     "bias_colsum": ("hbm", ("mg_colsum", "mg_grouped_colsum")),
     "weight_prep": ("hbm", ("mg_pack_conv", "mg_pack_conv_flip", "mg_pack_dgrad_s2", "mg_wsq", "mg_wsq_bwd",
-                            "mg_router_reparam", "mg_weight_norm_fwd", "mg_weight_norm_bwd")),
+                            "mg_router_reparam", "mg_weight_norm_fwd", "mg_weight_norm_bwd", "mg_quant_mx8")),
 }
 _FAMILY_OF = {e: f for f, (_, es) in FAMILIES.items() for e in es}
 
 # rocprofv3 kernel name (regex, first match wins) -> family, for PMC attribution
 KERNELS = [
     (r"k_wgrad_fold|splitk_reduce_kernel<mg::Epi<float>", "conv_wgrad+fold"),
+    (r"k_mx8_conv", "conv_fwd_mx8"),
     (r"gemm_kernel<.*, 1>\(|k_moe_ffn_fwd", "expert_gemm"),  # TAG = 1 instantiations (mg_gemm.h), fused FFN
     (r"gemm_kernel<[^>]*LdKCConvT", "conv_dgrad_s2"),
     (r"gemm_kernel<.*LdMCConv", "conv_wgrad+fold"),
@@ -58,7 +61,7 @@ KERNELS = [
     (r"k_sumsq", "sumsq"),
     (r"k_adamw", "adamw"),
     (r"k_colsum|k_grouped_colsum", "bias_colsum"),
-    (r"k_pack_|k_wsq|k_reparam|k_wn_", "weight_prep"),
+    (r"k_pack_|k_wsq|k_reparam|k_wn_|k_quant_mx8", "weight_prep"),
 ]
 
 
@@ -75,7 +78,7 @@ def _conv_out(H, W, KH, KW, s, p):
 
 def work(name, a):
     """Algorithmic work of one call: FLOPs (MFMA families) or bytes (HBM families); None = not modelled."""
-    if name == "mg_conv2d_fwd" or name == "mg_conv2d_wgrad":
+    if name in ("mg_conv2d_fwd", "mg_conv2d_wgrad", "mg_conv2d_fwd_mx8"):
         OH, OW = _conv_out(a["H"], a["W"], a["KH"], a["KW"], a["stride"], a["pad"])
         return 2.0 * a["B"] * OH * OW * a["Cout"] * a["KH"] * a["KW"] * a["Cin"]
     if name == "mg_conv2d_dgrad_s2":  # 4x4 stride-2 transpose: every input pixel takes 4 of the 16 taps
@@ -147,6 +150,8 @@ def work(name, a):
         return 16.0 * a["O"] * a["K"]
     if name == "mg_colsum":
         return a["R"] * a["C"] * ELT[a["dtype"]]
+    if name == "mg_quant_mx8":  # bf16 in, e4m3 + one E8M0 byte per 32 out
+        return a["rows"] * a["K"] * (2 + 1 + 1 / 32)
     return None
 
 
@@ -229,10 +234,11 @@ class Attribution:
             bound = FAMILIES[f][0] if f in FAMILIES else None
             ms = r["ms"] / steps
             rec = {"family": f, "bound": bound, "launches_per_step": r["calls"] / steps, "ms_per_step": round(ms, 4)}
-            if bound == "mfma":
+            if bound in ("mfma", "mfma8"):
+                pk = MX8_PEAK_TFLOPS if bound == "mfma8" else peak_tflops
                 tf = r["work"] / steps / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-                rec.update({"gflop_per_step": round(r["work"] / steps / 1e9, 3), "achieved": round(tf, 1),
-                            "unit": "TFLOP/s", "peak": peak_tflops, "frac": round(tf / peak_tflops, 4)})
+                rec.update({"bound": "mfma", "gflop_per_step": round(r["work"] / steps / 1e9, 3),
+                            "achieved": round(tf, 1), "unit": "TFLOP/s", "peak": pk, "frac": round(tf / pk, 4)})
             elif bound == "hbm":
                 gbs = r["work"] / steps / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
                 rec.update({"mb_per_step": round(r["work"] / steps / 1e6, 3), "achieved": round(gbs, 1),

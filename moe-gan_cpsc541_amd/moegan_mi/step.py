@@ -40,9 +40,10 @@ FD, FG = ops.FLAG_D_BAD, ops.FLAG_G_BAD
 class StepConfig:
     def __init__(self, E=4, topk=None, dtype="fp32", r1_gamma=10.0, clip_weight_16=0.1, clip_weight_8=0.05,
                  balance_weight=0.01, beta1=0.5, beta2=0.999, weight_decay=0.01, eps=1e-8, d_clip=0.7, g_clip=0.8,
-                 psi=0.7):
+                 psi=0.7, fp8=False):
         self.E, self.topk = E, topk
         self.dtype = dtype
+        self.fp8 = fp8  # MX-fp8 3x3 modulated convs (BASELINE config C5), inside the bf16 mode
         self.r1_gamma = r1_gamma
         self.clip_weight_16, self.clip_weight_8 = clip_weight_16, clip_weight_8
         self.balance_weight = balance_weight
@@ -73,7 +74,7 @@ class TrainStep:
         self.gs = gstore if gstore is not None else ParamStore(
             generator_shapes(cfg.E), self.dev, frozen_prefixes=("to_rgb_8.",), shadow_dtype=self.cdt)
         self.ds = dstore if dstore is not None else ParamStore(discriminator_shapes(), self.dev)
-        self.ge = GeneratorEngine(self.gs, cfg.E, cfg.topk, self.cdt)
+        self.ge = GeneratorEngine(self.gs, cfg.E, cfg.topk, self.cdt, fp8=getattr(cfg, "fp8", False))
         self.de = DiscriminatorEngine(self.ds, self.cdt)
         self.pg = process_group
         self.world = 1

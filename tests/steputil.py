@@ -57,10 +57,10 @@ def oracle_clone(PG, PD, optG, optD, lr=2e-4):
     return PG2, PD2, optG2, optD2, _capture(optD2, optG2, PD2, PG2)
 
 
-def gpu_step(E, topk, dtype, dev="cuda", seed_g=0, seed_d=50):
+def gpu_step(E, topk, dtype, dev="cuda", seed_g=0, seed_d=50, fp8=False):
     from moegan_mi.layout import discriminator_shapes, generator_shapes
     from moegan_mi.step import StepConfig, TrainStep
-    ts = TrainStep(StepConfig(E=E, topk=topk, dtype=dtype), dev)
+    ts = TrainStep(StepConfig(E=E, topk=topk, dtype=dtype, fp8=fp8), dev)
     ts.gs.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(generator_shapes(E), seed_g).items()})
     ts.ds.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(discriminator_shapes(), seed_d).items()})
     return ts

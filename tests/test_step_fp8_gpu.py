@@ -1,0 +1,100 @@
+"""Step-level parity of the MX-fp8 mode (BASELINE config C5: 32 experts top-4, the 3x3 modulated-conv forward and
+data-gradient GEMMs in OCP MX-fp8, everything else bf16) against the fp32 CPU oracle, one full G+D step.
+
+The device's top-k selection is replayed into the oracle (topk_route(idx=...)), so everything after the routers is
+compared like for like; the selection itself is reported (fp8 moves the router features, so near-ties flip) and
+bounded.  Bars (stated per check; measured values printed with pytest -s):
+  * discriminator-only quantities (real / mismatched logits, R1, the D gradient) carry no fp8 operand: the bf16
+    bar, 2e-2 relative L2 / whole-model gradient cosine >= 0.999;
+  * generator outputs (images, routing probabilities, the generator loss): relative L2 <= REL8 (measured at
+    E=32 top-4, B=4: images 2.3e-2, probabilities <= 2.3e-2, g_gan 3e-3);
+  * the generator's whole-model clipped gradient: cosine >= COS8 with the oracle's (measured 0.981: the image
+    gradient passes six MX-fp8 data-gradient convs, each ~3.8 % relative RMS, test_fp8_gpu.py); every tensor
+    >= COS8_TENSOR (measured minimum 0.886, the MTM offset heads' biases, whose gradient is a sum over all
+    pixels of small warp-gradient terms that largely cancel; a wrong sign, transpose or missing term sits far
+    below that).  The bf16 mode's bars (test_step_bf16_gpu.py) are the tighter reference.
+The kernel-level exactness of the MX-fp8 conv (vs the dequantized operands) is test_fp8_gpu.py's job.
+"""
+import pytest
+import torch
+
+from oracle import aurora_cpu as O
+from steputil import cosine, gpu_step, make_inputs, nchw, oracle_models, rel_norm_diff
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+REL8 = 0.12      # fp8-touched outputs, relative L2
+COS8 = 0.97      # generator whole-model gradient cosine
+COS8_TENSOR = 0.85
+EFF_KL = 0.001 * 1e-5
+torch.set_num_threads(8)
+
+
+@pytest.mark.parametrize("E,topk,B", [(32, 4, 4), (8, 2, 4)])
+def test_fp8_step_vs_oracle(E, topk, B):
+    real, text, z, eps_d, eps_g, perm = make_inputs(B, E, seed=300 + E)
+    ts = gpu_step(E, topk, "bf16", DEV, fp8=True)
+    PG, PD, optG, optD, rgrads = oracle_models(E)
+    cu = lambda t: t.to(DEV)  # noqa: E731
+    out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d], [tuple(map(cu, e)) for e in eps_g],
+                  cu(perm.int()), anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=EFF_KL)
+    torch.cuda.synchronize()
+    assert sum("wq" in p for p in ts.ge.packs.values()) == 6  # every 3x3 modulated conv ran in MX-fp8
+    assert int(out["flags"][0]) == 0
+    routes_d = [t.cpu().long() for t in out["topi_d"]]
+    routes_g = [t.cpu().long() for t in out["topi"]]
+    d_after = {n: ts.ds.view(n).detach().cpu().clone() for n in ts.ds.offsets}
+
+    def use_device_d(P):
+        with torch.no_grad():
+            for n, t in P.items():
+                t.copy_(d_after[n].view(t.shape))
+    ref = O.train_step(PG, PD, optG, optD, real, text, z, eps_d, eps_g, perm.long(), topk=topk, kl_weight_eff=EFF_KL,
+                       routes_d=routes_d, routes_g=routes_g, full=True, after_d_step=use_device_d)
+    report, fails = [], []
+
+    def check(ok, what):
+        report.append(what)
+        if not ok:
+            fails.append(what)
+    # routing: the device's own selection vs the oracle's fp32 top-k of its probabilities (reported, bounded)
+    for tag, dev_t, ref_p in (("D", out["topi_d"], ref["probs_d"]), ("G", out["topi"], ref["probs"])):
+        for li in range(3):
+            rt = torch.topk(ref_p[li].float(), topk, dim=1).indices.sort(1).values
+            dt = dev_t[li].cpu().long().sort(1).values
+            mism = int((rt != dt).any(1).sum())
+            check(mism <= max(4, dt.shape[0] // 4), f"{tag}-phase layer{li}: {mism}/{dt.shape[0]} top-{topk} sets differ")
+    for li in range(3):
+        r = rel_norm_diff(out["probs"][li], ref["probs"][li])
+        check(r <= REL8, f"probs layer{li}: rel {r:.3e}")
+    for name, dv, rv, bar in (("real_pred", out["real_pred"], ref["real_pred"], 2e-2),
+                              ("mism_pred", out["mism_pred"], ref["mism_pred"], 2e-2),
+                              ("img16", nchw(out["img16"]), ref["img16"], REL8),
+                              ("img16_d", nchw(out["fake_img_d"]), ref["img16_d"], REL8)):
+        r = rel_norm_diff(dv, rv)
+        check(r <= bar, f"{name}: rel {r:.3e} (bar {bar})")
+    for name, dv, rv, bar in (("r1", float(out["r1"][0]), ref["r1"], 2e-2),
+                              ("g_gan", float(out["g_gan"][0]), ref["g_loss_gan"], REL8),
+                              ("balance", float(out["balance"][0]), ref["balance"], REL8)):
+        r = abs(dv - rv) / max(abs(rv), 1e-6)
+        check(r <= bar, f"{name}: {dv:.6f} vs {rv:.6f} rel {r:.3e} (bar {bar})")
+    for which, store, gbuf, ss, max_norm, bar in (("D", ts.ds, out["d_grad"], out["d_grad_sumsq"], 0.7, 0.999),
+                                                  ("G", ts.gs, out["g_grad"], out["g_grad_sumsq"], 0.8, COS8)):
+        coef = min(1.0, max_norm / (float(ss[0]) ** 0.5 + 1e-6))
+        a, b, worst = [], [], []
+        for n, (off, numel) in store.offsets.items():
+            rg = rgrads[which].get(n)
+            if rg is None:
+                continue
+            g = (gbuf[off:off + numel] * coef).cpu()
+            a.append(g.reshape(-1))
+            b.append(rg.reshape(-1))
+            worst.append((cosine(g, rg), n))
+        cg = cosine(torch.cat(a), torch.cat(b))
+        worst.sort()
+        check(cg >= bar, f"{which}: whole-model gradient cosine {cg:.6f} (bar {bar}); worst tensors " +
+              ", ".join(f"{n} {c:.4f}" for c, n in worst[:3]))
+        tb = 0.9 if which == "D" else COS8_TENSOR
+        check(worst[0][0] >= tb, f"{which}: every tensor cosine >= {tb} (min {worst[0][0]:.4f} {worst[0][1]})")
+    print("\n".join(report))
+    assert not fails, fails
