@@ -66,6 +66,9 @@ class GeneratorEngine:
         self._want_kl = True
         self._bv = None  # per-block vectors of the running forward (_block_vectors)
         self.guard_flags = None  # the training step's loss-guard word (step.py), read by the router backward
+        # called with (lo, hi) when a contiguous range of the flat gradient is final during backward (a block's
+        # expert weights / biases): the data-parallel step starts that range's all-reduce right away (step.py)
+        self.on_grad_final = None
         # weight gradients run on a side stream, overlapping the data-gradient chain (joined in backward)
         self.side = graphs.SideStream(self.dev, enabled=graphs.side_streams_enabled(self.dev))
 
@@ -507,6 +510,10 @@ class GeneratorEngine:
         gb1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias", self.st.grad)
         self.side.run(lambda: (ops.gemm_grouped_wgrad(gP, sv["Xg"], row_off, n, Hd, C, gW1),
                                ops.grouped_colsum(gP, row_off, Hd, n, gb1)), gP)
+        if self.on_grad_final is not None:  # this block's expert parameters receive no further gradient
+            lo = self.st.offsets[ex + "0.net.0.weight"][0]
+            o, nl = self.st.offsets[f"{ex}{E-1}.net.2.bias"]
+            self.on_grad_final(lo, o + nl)
         # router
         g_raw, gsum = ops.router_bwd(sv["probs"], sv["zlog"], sv["topi"], sv["gate"], g_gate, g_probs, coef,
                                      sv["HW"], self.P(r + "temperature"), sv["anneal"], self.G(r + "temperature"), B,
