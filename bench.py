@@ -38,9 +38,10 @@ def parse():
     ap.add_argument("--experts", type=int, default=8)
     ap.add_argument("--topk", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--config", default="C2", choices=["C2", "C5"],
-                    help="C2 = BASELINE configs[1] (the headline line); C5 = the single-GPU slice of configs[4]: "
-                         "32 experts top-4, MX-fp8 3x3 modulated convs")
+    ap.add_argument("--config", default="C2", choices=["C2", "C4", "C5"],
+                    help="C2 = BASELINE configs[1] (the headline line); C4 = the per-GPU slice of configs[3]: the "
+                         "128x128 progressive generator, 16 experts top-2, CLIP loss on; C5 = the per-GPU slice of "
+                         "configs[4]: 32 experts top-4, MX-fp8 3x3 modulated convs")
     ap.add_argument("--fp8", action="store_true", help="MX-fp8 3x3 modulated convs (implied by --config C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU-oracle steps (B=8; ~10-20 s of CPU work)")
@@ -54,8 +55,11 @@ def parse():
     ap.add_argument("--one-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box, with --backend gloo)")
     args = ap.parse_args()
+    args.res, args.max_res = 64, 16
     if args.config == "C5":  # BASELINE configs[4]: 64x64, 32 experts top-4, fp8 MFMA conv path, KL + balance
         args.experts, args.topk, args.fp8 = 32, 4, True
+    if args.config == "C4":  # BASELINE configs[3]: 128x128 progressive stage, 16 experts top-2, CLIP loss on
+        args.experts, args.topk, args.res, args.max_res = 16, 2, 128, 128
     assert not args.fp8 or args.dtype == "bf16", "the MX-fp8 convs run inside the bf16 mode"
     return args
 
@@ -138,11 +142,15 @@ def main():
     from moegan_mi.step import StepConfig, TrainStep
 
     E, k, B = args.experts, args.topk, args.batch
-    ts = TrainStep(StepConfig(E=E, topk=k, dtype=args.dtype, fp8=args.fp8), dev, process_group=pg)
+    ts = TrainStep(StepConfig(E=E, topk=k, dtype=args.dtype, fp8=args.fp8, max_res=args.max_res), dev,
+                   process_group=pg)
     init_generator(ts.gs, seed=0)
     init_discriminator(ts.ds, seed=1)
+    if args.config == "C4":  # CLIP loss on: the forward-only ViT-B/32 image tower (random weights: no download)
+        from moegan_mi.clip_vit import ClipImageEncoder
+        ts.clip_encoder = ClipImageEncoder(device=dev).encode_image
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    real = torch.rand(B, 3, 64, 64, device=dev, generator=gen) * 2 - 1
+    real = torch.rand(B, 3, args.res, args.res, device=dev, generator=gen) * 2 - 1
     text = torch.randn(B, 512, device=dev, generator=gen)
     z = torch.randn(B, 512, device=dev, generator=gen)
     eps_gen = torch.Generator(device=dev).manual_seed(3)  # identical router noise on every rank
@@ -161,7 +169,7 @@ def main():
 
     # live timing of the roofline kernel: D conv_layers.2 forward on the 64x64 real batch
     # (implicit GEMM M = B*16*16, N = 256, K = 4*4*128); inactive until the timed region
-    want_dims = (B * 256, 256, 2048)
+    want_dims = (B * (args.res // 4) ** 2, 256, 2048)
     ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "conv2d:d_conv1" and dims == want_dims, active=False)
 
     graph = None
@@ -242,7 +250,7 @@ def main():
                 return None
             rec = json.load(open(path))
             ok = (rec.get("batch") == B and rec.get("dtype") == args.dtype and rec.get("experts") == E and
-                  bool(rec.get("fp8", False)) == args.fp8)
+                  bool(rec.get("fp8", False)) == args.fp8 and rec.get("max_res", 16) == args.max_res)
             return rec if ok else None
 
         ftime, ftraf = _prof("family_time.json"), _prof("family_traffic.json")
@@ -285,27 +293,36 @@ def main():
         pmc = os.path.join(REPO, "profiles", "pmc_roofline_kernel.json")
         if os.path.exists(pmc):  # HBM bytes per launch from the committed rocprofv3 --pmc passes
             rec = json.load(open(pmc))
-            if rec.get("batch") == B and args.dtype == "bf16" and not args.fp8:
+            if rec.get("batch") == B and args.dtype == "bf16" and not args.fp8 and args.res == 64:
                 traffic = rec["traffic_bytes_per_launch"]
-        roof = {"bound": "mfma", "kernel": "mg_conv2d_fwd D conv_layers.2 (64x64 real), implicit GEMM "
+        roof = {"bound": "mfma", "kernel": f"mg_conv2d_fwd D conv_layers.2 ({args.res}x{args.res} real), implicit GEMM "
                                           f"M={M} N={N} K={K}", "achieved": round(achieved, 2) if achieved else None,
                 "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                 "traffic": traffic, "traffic_unit": "bytes per launch (HBM, PMC)",
                 "algorithmic_flop_per_launch": flop, "launches_timed": len(kms), "avg_launch_ms": round(avg_ms, 4)}
-        step_tflops = gflop_per_image(k) * B * world / (ms * 1e-3) / 1e3
+        if args.config == "C4":  # extension: no reference FLOP formula; the executed MFMA work (roofline.py)
+            gf_step = sum(f.get("gflop_per_step", 0.0) for f in (families or []) if f["bound"] == "mfma")
+            step_tflops = gf_step * world / (ms * 1e-3) / 1e3 if gf_step else 0.0
+        else:
+            step_tflops = gflop_per_image(k) * B * world / (ms * 1e-3) / 1e3
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.config != "C4":
             try:
                 cpu = cpu_baseline(args, E, k)
             except Exception as e:  # the baseline is a report, never the measured value
                 cpu = {"error": repr(e)}
-        line = {"metric": "images/sec (G+D step, 64x64 MS-COCO layout)", "value": round(value, 2),
+        metric = ("images/sec (G+D step, 64x64 MS-COCO layout)" if args.res == 64 else
+                  f"images/sec (G+D step, {args.res}x{args.res} progressive stage)")
+        line = {"metric": metric, "value": round(value, 2),
                 "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                 "dtype": args.dtype + ("+mx8" if args.fp8 else ""),
                 "data": "synthetic (U(-1,1) images, N(0,1) 512-d captions, random init)",
                 "config": {"workload": (f"C5 single-GPU slice: 64x64, {E} experts top-{k}, batch {B}/GPU, bf16 with "
                                         "MX-fp8 (e4m3) 3x3 modulated-conv GEMMs, KL + balance, R1 on") if args.config == "C5"
+                           else (f"C4 single-GPU slice: 128x128 progressive generator (extension blocks 32/64/128), "
+                                 f"{E} experts top-{k}, batch {B}/GPU, {args.dtype}, CLIP loss on (ViT-B/32 image "
+                                 "tower, random weights), R1 on") if args.config == "C4"
                            else f"C2: 64x64, {E} experts top-{k}, batch {B}/GPU, {args.dtype}"
                                 + (" + MX-fp8 3x3 convs" if args.fp8 else "") + ", R1 on",
                            "global_batch": B * world, "experts": E, "topk": k, "parallelism": f"dp{world}",

@@ -50,6 +50,7 @@ extern "C" {
 #define MG_ACT_MUL_GELU_GRAD 3  /* v *= GELU'(aux[m,n]) */
 #define MG_ACT_MUL_LRELU_GRAD 4 /* v *= LReLU'(aux[m,n]) */
 #define MG_ACT_RSQRT_EPS 5      /* v = rsqrt(v + 1e-8)  (demodulation, t2i_moe_gan.py:165) */
+#define MG_ACT_QUICK_GELU 6     /* v * sigmoid(1.702 v)  (CLIP ViT MLP, forward-only CLIP loss :66-119) */
 
 /* Fused GEMM epilogue / prologue options (all pointers optional = NULL).
  *   v = alpha * acc
@@ -246,8 +247,9 @@ int mg_disc_head_bwd_data(int dtype, const float* g, int64_t g_bstride, const fl
 /* Head weight gradient (image channels) dW2[c,tap] += sum_b,o g h1. */
 int mg_disc_head_bwd_w(int dtype, const float* g, int64_t g_bstride, const void* h1, int B, int Hf, int Cf, float* dW2, void* stream);
 
-/* Discriminator loss (t2i_moe_gan.py:940-949) for real (64x64 patch logits), fake and mismatched-text logits + gradients. */
-int mg_d_loss(const float* img_real, const float* img_fake, const float* tb, const int32_t* perm, int B, int No, float* out, float* g_img, float* g_fake, float* g_tb, float* real_out, float* mism_out, float* fake_out, void* stream);
+/* Discriminator loss (t2i_moe_gan.py:940-949) for real (No patch logits per image), fake (Nf per image: 1 for the
+   reference's 16x16 fakes, (R/4-3)^2 for the progressive extension's RxR fakes) and mismatched-text logits + gradients. */
+int mg_d_loss(const float* img_real, const float* img_fake, const float* tb, const int32_t* perm, int B, int No, int Nf, float* out, float* g_img, float* g_fake, float* g_tb, float* real_out, float* mism_out, float* fake_out, void* stream);
 
 /* Generator adversarial loss softplus(-f).mean() and its gradient (t2i_moe_gan.py:917-924). */
 int mg_g_loss(const float* fake, int B, float scale, float* out, float* g, void* stream);

@@ -367,10 +367,11 @@ __global__ __launch_bounds__(256) void k_ln_bwd_v(const TG* __restrict__ gy, int
 extern "C" int mg_layernorm_fwd(int dtype, const void* x, int64_t ldx, int R, int C, const float* gamma,
                                 const float* beta, float eps, void* y, int64_t ldy, float* mean, float* rstd, int act,
                                 void* stream) {
-  MG_REQUIRE(C == 128 || C == 256 || C == 512, "C must be 128, 256 or 512");
+  // 128 / 256 / 512: the generator's widths; 768: the CLIP image tower (forward only, clip_vit.py)
+  MG_REQUIRE(C == 128 || C == 256 || C == 512 || C == 768, "C must be 128, 256, 512 or 768");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (R == 0) return MG_OK;
-  if (ldx % 8 == 0 && ldy % 8 == 0 && mg_al16(x) && mg_al16(y) && mg_al16(gamma) && mg_al16(beta)) {
+  if (C <= 512 && ldx % 8 == 0 && ldy % 8 == 0 && mg_al16(x) && mg_al16(y) && mg_al16(gamma) && mg_al16(beta)) {
     const int lpr = C / 8, rpw = 64 / lpr;
     dim3 g2(std::min(cdiv(R, 4 * rpw), 2048)), b2(256);
 #define LV_(T, P) hipLaunchKernelGGL((k_ln_fwd_v<T, P>), g2, b2, 0, st, (const T*)x, ldx, R, gamma, beta, eps, (T*)y, ldy, mean, rstd, act)
@@ -385,9 +386,9 @@ extern "C" int mg_layernorm_fwd(int dtype, const void* x, int64_t ldx, int R, in
   dim3 grid(cdiv(R, 4)), blk(256);
 #define L_(T, N) hipLaunchKernelGGL((k_ln_fwd<T, N>), grid, blk, 0, st, (const T*)x, ldx, R, gamma, beta, eps, (T*)y, ldy, mean, rstd, act)
   if (dtype == MG_F32) {
-    if (C == 128) L_(float, 2); else if (C == 256) L_(float, 4); else L_(float, 8);
+    if (C == 128) L_(float, 2); else if (C == 256) L_(float, 4); else if (C == 512) L_(float, 8); else L_(float, 12);
   } else {
-    if (C == 128) L_(bf16_t, 2); else if (C == 256) L_(bf16_t, 4); else L_(bf16_t, 8);
+    if (C == 128) L_(bf16_t, 2); else if (C == 256) L_(bf16_t, 4); else if (C == 512) L_(bf16_t, 8); else L_(bf16_t, 12);
   }
 #undef L_
   return mg_check_launch("mg_layernorm_fwd");

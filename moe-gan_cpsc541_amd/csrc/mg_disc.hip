@@ -197,7 +197,7 @@ __global__ void k_head_bwd_w(const float* __restrict__ g, int64_t g_bstride, con
 // out (zeroed by caller): [0] d_loss_gan, [1] mean softplus(-real), [2] mean softplus(fake), [3] mean softplus(mism)
 // g_img_real / g_img_fake: d loss / d image-part logits; g_tb (zeroed): d loss / d tb.
 __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict__ img_fake,
-                         const float* __restrict__ tb, const int* __restrict__ perm, int B, int No,
+                         const float* __restrict__ tb, const int* __restrict__ perm, int B, int No, int Nf,
                          float* __restrict__ out, float* __restrict__ g_img, float* __restrict__ g_fake,
                          float* __restrict__ g_tb, float* __restrict__ real_out, float* __restrict__ mism_out,
                          float* __restrict__ fake_out) {
@@ -205,6 +205,32 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
   int b = blockIdx.x;
   float sr = 0.f, sm = 0.f, gr = 0.f, gm = 0.f;
   float inv = 1.f / ((float)B * No);
+  if (b > B) {
+    // fake logits with Nf > 1 per image (progressive generator, images >= 32x32): one block per image
+    int i = b - B - 1;
+    float tf = tb[i], invf = 1.f / ((float)B * Nf), sf = 0.f, gs = 0.f;
+    for (int o = threadIdx.x; o < Nf; o += blockDim.x) {
+      int64_t e = (int64_t)i * Nf + o;
+      float f = img_fake[e] + tf;
+      if (fake_out) fake_out[e] = f;
+      sf += (f > 20.f) ? f : log1pf(expf(f));
+      float gf = 1.f / (1.f + expf(-f)) * invf;
+      g_fake[e] = gf;
+      gs += gf;
+    }
+    sf = wave_sum(sf); gs = wave_sum(gs);
+    int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = sf; red[1][w] = gs; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float a = 0, c = 0;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { a += red[0][k]; c += red[1][k]; }
+      atomicAdd(&out[2], a * invf);
+      atomicAdd(&out[0], a * invf);
+      atomicAdd(&g_tb[i], c);
+    }
+    return;
+  }
   if (b < B) {
     float tr = tb[b], tm = tb[perm[b]];
     for (int o = threadIdx.x; o < No; o += blockDim.x) {
@@ -235,7 +261,7 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
       atomicAdd(&g_tb[b], d);
       atomicAdd(&g_tb[perm[b]], e);
     }
-  } else {
+  } else if (Nf == 1) {
     float sf = 0.f;
     for (int i = threadIdx.x; i < B; i += blockDim.x) {
       float f = img_fake[i] + tb[i];
@@ -446,11 +472,14 @@ extern "C" int mg_disc_head_bwd_w(int dtype, const float* g, int64_t g_bstride, 
 }
 
 extern "C" int mg_d_loss(const float* img_real, const float* img_fake, const float* tb, const int32_t* perm, int B,
-                         int No, float* out, float* g_img, float* g_fake, float* g_tb, float* real_out,
+                         int No, int Nf, float* out, float* g_img, float* g_fake, float* g_tb, float* real_out,
                          float* mism_out, float* fake_out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_d_loss, dim3(B + 1), dim3(256), 0, st, img_real, img_fake, tb, perm, B, No, out, g_img, g_fake,
-                     g_tb, real_out, mism_out, fake_out);
+  MG_REQUIRE(B > 0 && No > 0 && Nf > 0, "mg_d_loss: B, No, Nf must be positive");
+  // block B (one logit per fake, the reference's 16x16 fakes) or blocks B+1..2B (Nf logits per fake image)
+  int grid = Nf == 1 ? B + 1 : 2 * B + 1;
+  hipLaunchKernelGGL(k_d_loss, dim3(grid), dim3(256), 0, st, img_real, img_fake, tb, perm, B, No, Nf, out, g_img,
+                     g_fake, g_tb, real_out, mism_out, fake_out);
   return mg_check_launch("mg_d_loss");
 }
 

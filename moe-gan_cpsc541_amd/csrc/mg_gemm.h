@@ -382,7 +382,11 @@ struct LdMCGroupW {
 // ---------------------------------------------------------------------------
 // Epilogue
 // ---------------------------------------------------------------------------
-enum { ACT_NONE = 0, ACT_LRELU = 1, ACT_GELU = 2, ACT_MUL_GELU_GRAD = 3, ACT_MUL_LRELU_GRAD = 4, ACT_RSQRT_EPS = 5 };
+enum { ACT_NONE = 0, ACT_LRELU = 1, ACT_GELU = 2, ACT_MUL_GELU_GRAD = 3, ACT_MUL_LRELU_GRAD = 4, ACT_RSQRT_EPS = 5,
+       ACT_QUICK_GELU = 6 };
+
+// QuickGELU x * sigmoid(1.702 x) (the CLIP image tower's MLP activation)
+MG_DEV float quick_gelu(float x) { return x / (1.f + __expf(-1.702f * x)); }
 
 template <typename TO>
 struct Epi {
@@ -456,6 +460,9 @@ struct Epi {
     } else if (act == ACT_RSQRT_EPS) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = rsqrtf(v[j] + 1e-8f);
+    } else if (act == ACT_QUICK_GELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = quick_gelu(v[j]);
     }
     if (rowscale) {
       float r = rowscale[m];
@@ -494,6 +501,7 @@ struct Epi {
     }
     else if (act == ACT_MUL_LRELU_GRAD) v *= lrelu_grad(ldf(aux, (int64_t)m * ld_aux + n));
     else if (act == ACT_RSQRT_EPS) v = rsqrtf(v + 1e-8f);
+    else if (act == ACT_QUICK_GELU) v = quick_gelu(v);
     if (rowscale) v *= rowscale[m];
     if (addvec) v += addvec[(int64_t)(m >> add_shift) * add_ld + n];
     if (resid) v += ldf(resid, (int64_t)m * ld_res + n);

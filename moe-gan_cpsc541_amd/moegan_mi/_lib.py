@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("MOEGAN_HIP_LIB") or os.path.join(_HERE, "libmoegan_hi
 
 MG_F32, MG_BF16 = 0, 1
 PREP_PACK, PREP_PACK_FLIP, PREP_PACK_DGRAD_S2, PREP_WSQ, PREP_WSQ_BWD, PREP_REPARAM = 1, 2, 3, 4, 5, 6
-ACT_NONE, ACT_LRELU, ACT_GELU, ACT_MUL_GELU_GRAD, ACT_MUL_LRELU_GRAD, ACT_RSQRT_EPS = 0, 1, 2, 3, 4, 5
+ACT_NONE, ACT_LRELU, ACT_GELU, ACT_MUL_GELU_GRAD, ACT_MUL_LRELU_GRAD, ACT_RSQRT_EPS, ACT_QUICK_GELU = range(7)
 
 _c_void_p, _i32, _i64, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
 

@@ -145,7 +145,7 @@ class DiscriminatorEngine:
     # ------------------------------------------------------------------
     def d_phase(self, real_nchw, text, fake_img, fake_layout, perm, r1_gamma):
         """D loss + R1 and all D parameter gradients (t2i_moe_gan.py:1276-1326).
-        real_nchw [B,3,64,64] fp32; fake_img: generator output (NHWC padded [B,16,16,ld]).
+        real_nchw [B,3,H,H] fp32; fake_img: generator output (NHWC padded [B,R,R,ld]; R = 16 in the reference).
         Returns device scalars [d_loss_gan, sp_real, sp_fake, sp_mism] and r1, plus logits."""
         B = real_nchw.shape[0]
         Hr = real_nchw.shape[-1]
@@ -161,9 +161,9 @@ class DiscriminatorEngine:
         g_tb = ops.zeros(B, device=dev)
         real_pred = torch.empty(B, No, device=dev)
         mism_pred = torch.empty(B, No, device=dev)
-        fake_pred = torch.empty(B, device=dev)
-        ops.d_loss(fr["img_part"], ff["img_part"].view(-1), tb, perm, out, g_img, g_fake.view(-1), g_tb,
-                   real_pred, mism_pred, fake_pred)
+        fake_pred = torch.empty(B, ff["img_part"].shape[1], device=dev)
+        ops.d_loss(fr["img_part"], ff["img_part"], tb, perm, out, g_img, g_fake, g_tb, real_pred, mism_pred,
+                   fake_pred)
         # ordinary first-order backward (real + mismatched share the image features)
         self.stack_backward(fr, g_img)
         self.stack_backward(ff, g_fake)
@@ -199,6 +199,8 @@ class DiscriminatorEngine:
         self.side.join()
         self._remap_w0()
         self.finish_grads()
+        if fake_pred.shape[1] == 1:  # [B] as the reference's 16x16 fakes give
+            fake_pred = fake_pred.view(-1)
         return dict(losses=out, r1=r1, real_pred=real_pred, mism_pred=mism_pred, fake_pred=fake_pred, r1_grad=gx)
 
     def _remap_w0(self):
@@ -215,22 +217,29 @@ class DiscriminatorEngine:
         Hs = fake_img.shape[1]
         t, tb = self.text_branch(text)
         f = self.forward(fake_img, fake_layout, text, B, Hs)
-        fake_pred = torch.empty(B, device=self.dev)
-        ops.copy2d(f["img_part"], fake_pred.view(B, 1), B, 1)
-        ops.copy2d(tb.view(B, 1), fake_pred.view(B, 1), B, 1, accumulate=1)
+        No = f["img_part"].shape[1]  # 1 for the reference's 16x16 fakes, (Hs/4-3)^2 for larger ones
+        fake_pred = torch.empty(B, No, device=self.dev)
+        ops.copy2d(f["img_part"], fake_pred, B, No)
+        ops.copy2d(tb.view(B, 1).expand(B, No).contiguous() if No > 1 else tb.view(B, 1), fake_pred, B, No,
+                   accumulate=1)
         loss = torch.zeros(1, device=self.dev)
-        g = torch.empty(B, 1, device=self.dev)
-        ops.g_loss(fake_pred, loss, g.view(-1), scale)
+        g = torch.empty(B, No, device=self.dev)
+        ops.g_loss(fake_pred.view(-1), loss, g.view(-1), scale)
         g_img = ops.zeros(*fake_img.shape, device=self.dev, dtype=self.cdt)
         if want_d_params:
             self.begin_grads()
         self.stack_backward(f, g, want_params=want_d_params, g_input=g_img)
         if want_d_params:
-            self._text_head_bwd(g.view(-1), t, text)
+            if No > 1:
+                g_tb = ops.zeros(B, device=self.dev)
+                ops.segsum(g, B, No, 1, g_tb.view(B, 1), ld=1)
+            else:
+                g_tb = g.view(-1)
+            self._text_head_bwd(g_tb, t, text)
             self.side.join()
             self._remap_w0()
             self.finish_grads()
-        return loss, fake_pred, g_img
+        return loss, (fake_pred.view(-1) if No == 1 else fake_pred), g_img
 
     def _text_head_bwd(self, g_tb, t, text):
         B = t.shape[0]

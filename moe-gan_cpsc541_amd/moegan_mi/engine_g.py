@@ -16,27 +16,29 @@ import torch
 
 from . import _lib as L
 from . import graphs, ops
-from .layout import GEN_BLOCKS
+from .layout import gen_blocks, max_res_of, rgb_layers
 
 E_ = ops.E
 LRELU, GELU, RSQRT = L.ACT_LRELU, L.ACT_GELU, L.ACT_RSQRT_EPS
 MUL_GELU_GRAD, MUL_LRELU_GRAD = L.ACT_MUL_GELU_GRAD, L.ACT_MUL_LRELU_GRAD
 
 
-def _modconv_prefixes(E=None):
+def _modconv_prefixes(max_res=16):
     out = []
-    for name, cin, cout, _, _ in GEN_BLOCKS:
+    for name, cin, cout, _, _, attn in gen_blocks(max_res):
         cb = name + ".conv_block."
         out += [(cb + "mtm1.modulated_conv.", 3), (cb + "mtm2.modulated_conv.", 3)]
         if cin != cout:
             out.append((cb + "skip_proj.", 1))
-        out += [(name + ".attn_block.proj_in.", 1), (name + ".attn_block.proj_out.", 1)]
-    out += [("to_rgb_8.", 1), ("to_rgb_16.", 1)]
+        if attn:
+            out += [(name + ".attn_block.proj_in.", 1), (name + ".attn_block.proj_out.", 1)]
+    out += [(n + ".", 1) for n, _ in rgb_layers(max_res)[-2:]]  # intermediate + final image
     return out
 
 
-def _offset_prefixes():
-    return [f"{name}.conv_block.{m}.offset_net.0." for name, *_ in GEN_BLOCKS for m in ("mtm1", "mtm2")]
+def _offset_prefixes(max_res=16):
+    return [f"{name}.conv_block.{m}.offset_net.0." for name, _, _, res, _, _ in gen_blocks(max_res) if res <= 16
+            for m in ("mtm1", "mtm2")]
 
 
 class GeneratorEngine:
@@ -44,8 +46,15 @@ class GeneratorEngine:
         """``modconvs`` [(prefix, k)] / ``offset_nets`` [prefix]: the modulated convs and MTM offset heads prep()
         packs -- the whole generator's by default; the sub-module API (modules.py) passes its own."""
         self.st = store
-        self.mc_list = _modconv_prefixes() if modconvs is None else list(modconvs)
-        self.off_list = _offset_prefixes() if offset_nets is None else list(offset_nets)
+        # block list: the reference's three blocks, or the progressive extension when the store holds it
+        self.max_res = max_res_of(store.offsets)
+        self.blocks = gen_blocks(self.max_res)
+        self.attn_blocks = [b[0] for b in self.blocks if b[5]]
+        rgb = rgb_layers(self.max_res)
+        self.rgb_final, self.rgb_half = rgb[-1][0] + ".", rgb[-2][0] + "."
+        self.half_block = "gen_block_%d" % (self.max_res // 2)
+        self.mc_list = _modconv_prefixes(self.max_res) if modconvs is None else list(modconvs)
+        self.off_list = _offset_prefixes(self.max_res) if offset_nets is None else list(offset_nets)
         self.E = E
         self.k = topk or E
         self.cdt = cdt
@@ -229,6 +238,9 @@ class GeneratorEngine:
     # Modulated Transformation Module  (t2i_moe_gan.py:218-247)
     # ------------------------------------------------------------------
     def mtm_fwd(self, pre, x, w, resid=None, save=True):
+        if (pre + "offset_net.0.") not in self.packs:  # no offset head above 16x16 (:199): modconv + LReLU
+            y, msv = self.mc_fwd(pre + "modulated_conv.", x, w, act=1, resid=resid, save=save)
+            return y, ((x, None, None, None, msv) if save else None)
         opk = self.packs[pre + "offset_net.0."]
         o1 = ops.conv2d(x, opk["w"], 32, 3, 3, 1, 1, out_dtype=self.cdt,
                         ep=E_(bias=self.P(pre + "offset_net.0.bias"), act=LRELU))
@@ -240,6 +252,9 @@ class GeneratorEngine:
 
     def mtm_bwd(self, pre, sv, gz, gx, gw, accumulate=0):
         x, o1, samp, xw, msv = sv
+        if o1 is None:  # no offset head
+            self.mc_bwd(pre + "modulated_conv.", msv, gz, gx, gw, accumulate=accumulate)
+            return
         B, H, W, Cin = x.shape
         P = B * H * W
         g_xw = torch.empty(P, Cin, device=self.dev, dtype=self.cdt)
@@ -369,7 +384,7 @@ class GeneratorEngine:
         matrix (:364-389) -- for all blocks at once: five batched launches instead of eighteen GEMMs."""
         B = w.shape[0]
         dev = self.dev
-        pres = [name + ".attn_block." for name, *_ in GEN_BLOCKS]
+        pres = [name + ".attn_block." for name in self.attn_blocks]
         Cs = [self.P(p + "text_proj.weight").shape[0] for p in pres]
         bv = {p + "moe.": {} for p in pres}
         chain = {}
@@ -658,7 +673,7 @@ class GeneratorEngine:
             ops.gemm_batch(probs)
         self._S, self._S2, self._D = S, S2, D
         x = ops.const_fwd(self.P("constant"), B, self.cdt)
-        name0, _, _, _, up0 = GEN_BLOCKS[0]
+        name0, _, _, _, up0, _ = self.blocks[0]
         assert not up0
         x0, cbsv0 = self.cb_fwd(name0 + ".conv_block.", x, w, save=save)
         return dict(B=B, text=text, text_c=text_c, t0=t0, t1=t1, t1c=t1c, tmu=tmu, trs=trs, text_seq=text_seq,
@@ -666,7 +681,8 @@ class GeneratorEngine:
 
     def forward(self, z, text, eps, anneal=1.0, psi=0.7, train=True, save=True, want_img8=False, want_kl=True,
                 keep_prefix=False, prefix=None):
-        """Returns (img16 [B,16,16,8] padded NHWC, img8 or None, kl2 list, probs list, ctx).
+        """Returns (img [B,R,R,8] padded NHWC, the intermediate R/2 image or None, kl2 list, probs list, ctx);
+        R = max_res (16: the reference generator, img16 / img8).  kl2 / probs / eps: one per attention block.
         ``want_kl=False`` skips the routers' KL terms (their kl2 entries are None).
         ``keep_prefix=True`` computes the router-independent prefix (``_prefix_fwd``) with its saved
         activations and returns it as ``self.last_prefix``; ``prefix=`` reuses such a prefix (same z, text,
@@ -684,22 +700,26 @@ class GeneratorEngine:
         probs, kl2s, topis, blocks = [], [], [], []
         img8, rgb8sv = None, None
         x = None
-        for i, (name, cin, cout, res, up) in enumerate(GEN_BLOCKS):
+        ai = 0
+        for i, (name, cin, cout, res, up, attn) in enumerate(self.blocks):
             if i == 0:
                 x, cbsv = prefix["x0"], (prefix["cbsv0"] if save else None)
             else:
                 if up:
                     x = ops.upsample2x(x)
                 x, cbsv = self.cb_fwd(name + ".conv_block.", x, w, save=save)
-            x, p, kl2, topi, asv = self.attn_fwd(name + ".attn_block.", x, w, text_seq,
-                                                 None if eps is None else eps[i], anneal, train, save)
-            probs.append(p)
-            kl2s.append(kl2)
-            topis.append(topi)
+            asv = None
+            if attn:
+                x, p, kl2, topi, asv = self.attn_fwd(name + ".attn_block.", x, w, text_seq,
+                                                     None if eps is None else eps[ai], anneal, train, save)
+                ai += 1
+                probs.append(p)
+                kl2s.append(kl2)
+                topis.append(topi)
             blocks.append((cbsv, asv, up))
-            if name == "gen_block_8" and want_img8:
-                img8, rgb8sv = self.mc_fwd("to_rgb_8.", x, w, save=save)
-        img16, rgbsv = self.mc_fwd("to_rgb_16.", x, w, save=save)
+            if name == self.half_block and want_img8:
+                img8, rgb8sv = self.mc_fwd(self.rgb_half, x, w, save=save)
+        img16, rgbsv = self.mc_fwd(self.rgb_final, x, w, save=save)
         self._S = self._S2 = self._D = None
         self._bv = None
         ctx = None
@@ -725,17 +745,22 @@ class GeneratorEngine:
         sv = ctx["rgbsv"]
         x_last = sv[0]
         gx = torch.empty(x_last.shape, device=dev, dtype=self.cdt)
-        self.mc_bwd("to_rgb_16.", sv, g_img16, gx, gw)
-        nb = len(GEN_BLOCKS)
-        for i in reversed(range(nb)):
-            name, cin, cout, res, up = GEN_BLOCKS[i]
+        self.mc_bwd(self.rgb_final, sv, g_img16, gx, gw)
+        na = len(self.attn_blocks)
+        ai = na
+        for i in reversed(range(len(self.blocks))):
+            name = self.blocks[i][0]
             cbsv, asv, up = ctx["blocks"][i]
-            g_cb = torch.empty(gx.shape, device=dev, dtype=self.cdt)
-            kc = None if kl_coef is None else kl_coef[i:i + 1]
-            if name == "gen_block_8" and g_img8 is not None:
-                self.mc_bwd("to_rgb_8.", ctx["rgb8sv"], g_img8, gx, gw, accumulate=1)
-            self.attn_bwd(name + ".attn_block.", asv, gx, g_cb, gw, g_ts, coef=coef if i == nb - 1 else None,
-                          kl_coef=kc, g_probs=None if g_probs is None else g_probs[i])
+            if name == self.half_block and g_img8 is not None:
+                self.mc_bwd(self.rgb_half, ctx["rgb8sv"], g_img8, gx, gw, accumulate=1)
+            if asv is not None:
+                ai -= 1
+                g_cb = torch.empty(gx.shape, device=dev, dtype=self.cdt)
+                kc = None if kl_coef is None else kl_coef[ai:ai + 1]
+                self.attn_bwd(name + ".attn_block.", asv, gx, g_cb, gw, g_ts, coef=coef if ai == na - 1 else None,
+                              kl_coef=kc, g_probs=None if g_probs is None else g_probs[ai])
+            else:
+                g_cb = gx
             x_in = cbsv[0][0]  # input of mtm1
             g_in = torch.empty(x_in.shape, device=dev, dtype=self.cdt)
             self.cb_bwd(name + ".conv_block.", cbsv, g_cb, g_in, gw)

@@ -770,7 +770,8 @@ def d_text_bwd(g_tb, t, w2sum, cofs, g_tpre, dW2):
 
 def d_loss(img_real, img_fake, tb, perm, out, g_img, g_fake, g_tb, real_out=None, mism_out=None, fake_out=None):
     B, No = img_real.shape
-    call("mg_d_loss", ptr(img_real), ptr(img_fake), ptr(tb), ptr(perm), B, No, ptr(out), ptr(g_img), ptr(g_fake),
+    Nf = img_fake.numel() // B
+    call("mg_d_loss", ptr(img_real), ptr(img_fake), ptr(tb), ptr(perm), B, No, Nf, ptr(out), ptr(g_img), ptr(g_fake),
          ptr(g_tb), ptr(real_out), ptr(mism_out), ptr(fake_out), S())
 
 

@@ -6,7 +6,8 @@ The step keeps the reference's order and semantics:
   G phase: G forward (fresh router noise), KL clamp at 50, D(fake) with the UPDATED D, G adversarial
            loss + CLIP terms (no gradient, :98-101) + balance loss (last layer) + annealed KL,
            G backward, clip_grad_norm_(G, 0.8), AdamW(G)
-Parameters with no gradient in the reference (to_rgb_8: only feeds the gradient-free CLIP loss)
+Parameters with no gradient in the reference (to_rgb_8: only feeds the gradient-free CLIP loss; with the
+progressive extension every to_rgb but the final one)
 sit in the store's frozen tail and are never updated -- exactly as torch's AdamW skips a
 parameter whose .grad is None.
 
@@ -31,7 +32,7 @@ import torch.nn.functional as F
 from . import graphs, ops
 from .engine_d import DiscriminatorEngine
 from .engine_g import GeneratorEngine
-from .layout import discriminator_shapes, generator_shapes
+from .layout import discriminator_shapes, frozen_rgb_prefixes, generator_shapes
 from .params import ParamStore
 
 FD, FG = ops.FLAG_D_BAD, ops.FLAG_G_BAD
@@ -40,8 +41,10 @@ FD, FG = ops.FLAG_D_BAD, ops.FLAG_G_BAD
 class StepConfig:
     def __init__(self, E=4, topk=None, dtype="fp32", r1_gamma=10.0, clip_weight_16=0.1, clip_weight_8=0.05,
                  balance_weight=0.01, beta1=0.5, beta2=0.999, weight_decay=0.01, eps=1e-8, d_clip=0.7, g_clip=0.8,
-                 psi=0.7, fp8=False):
+                 psi=0.7, fp8=False, max_res=16):
         self.E, self.topk = E, topk
+        # generator output resolution: 16 = the reference; 32 / 64 / 128 = the progressive extension (layout.py)
+        self.max_res = max_res
         self.dtype = dtype
         self.fp8 = fp8  # MX-fp8 3x3 modulated convs (BASELINE config C5), inside the bf16 mode
         self.r1_gamma = r1_gamma
@@ -72,7 +75,8 @@ class TrainStep:
         self.dev = torch.device(device)
         self.cdt = torch.bfloat16 if cfg.dtype == "bf16" else torch.float32
         self.gs = gstore if gstore is not None else ParamStore(
-            generator_shapes(cfg.E), self.dev, frozen_prefixes=("to_rgb_8.",), shadow_dtype=self.cdt)
+            generator_shapes(cfg.E, getattr(cfg, "max_res", 16)), self.dev,
+            frozen_prefixes=frozen_rgb_prefixes(getattr(cfg, "max_res", 16)), shadow_dtype=self.cdt)
         self.ds = dstore if dstore is not None else ParamStore(discriminator_shapes(), self.dev)
         self.ge = GeneratorEngine(self.gs, cfg.E, cfg.topk, self.cdt, fp8=getattr(cfg, "fp8", False))
         self.de = DiscriminatorEngine(self.ds, self.cdt)

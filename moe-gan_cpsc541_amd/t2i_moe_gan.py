@@ -36,8 +36,10 @@ if _HERE not in sys.path:
 from moegan_mi.engine_d import DiscriminatorEngine  # noqa: E402
 from moegan_mi.engine_g import GeneratorEngine  # noqa: E402
 from moegan_mi.init import init_discriminator, init_generator  # noqa: E402
-from moegan_mi.layout import discriminator_shapes, generator_shapes  # noqa: E402
+from moegan_mi.layout import (MAX_RESOLUTIONS, discriminator_shapes, frozen_rgb_prefixes,  # noqa: E402
+                             generator_shapes)
 from moegan_mi.params import ParamStore  # noqa: E402
+from moegan_mi.prefetch import DevicePrefetcher  # noqa: E402
 from moegan_mi.step import StepConfig, TrainStep  # noqa: E402
 from moegan_mi.checkpoint import load_resume, save_resume  # noqa: E402,F401
 from moegan_mi.modules import (AttentionBlock, BayesianRouter, ConvolutionBlock, GenerativeBlock,  # noqa: E402,F401
@@ -62,6 +64,15 @@ def set_clip_model(model):
     _clip_model = model
 
 
+def load_clip_weights(path, device=None):
+    """Register the forward-only CLIP image tower (moegan_mi/clip_vit.py) built from a local OpenAI CLIP
+    state_dict / safetensors file; the CLIP loss terms (:66-119) then use it.  Returns the encoder."""
+    from moegan_mi.clip_vit import ClipImageEncoder
+    enc = ClipImageEncoder.from_file(path, device=device or DEVICE)
+    set_clip_model(enc)
+    return enc
+
+
 def get_clip_model():
     """Reference :32-47.  CLIP weights cannot be downloaded here; use set_clip_model()."""
     if _clip_model is None:
@@ -73,7 +84,7 @@ def _eps_for(store, generator=None):
     """Fresh router noise for one generator forward (the reference draws normal_() into its epsilon buffers per
     router, :349-351); ``generator`` = a torch.Generator (the rank-shared one under data parallelism)."""
     eps = []
-    for name in ("gen_block_4", "gen_block_8", "gen_block_16"):
+    for name in ("gen_block_4", "gen_block_8", "gen_block_16"):  # the attention (MoE) blocks at every max_res
         r = f"{name}.attn_block.moe.router."
         trip = []
         for n in ("epsilon_f", "epsilon_t", "epsilon_c"):
@@ -143,12 +154,13 @@ class _GenFn(torch.autograd.Function):
         st = mod._store
         st.zero_grad()
         B, dev = ctx.gctx["B"], eng.dev
-        gi16 = torch.zeros(B, 16, 16, 8, device=dev, dtype=eng.cdt)
+        R = eng.max_res
+        gi16 = torch.zeros(B, R, R, 8, device=dev, dtype=eng.cdt)
         if g16 is not None:
             gi16[..., :3] = g16.permute(0, 2, 3, 1)
         gi8 = None
         if ctx.want8 and g8 is not None and g8.numel():
-            gi8 = torch.zeros(B, 8, 8, 8, device=dev, dtype=eng.cdt)
+            gi8 = torch.zeros(B, R // 2, R // 2, 8, device=dev, dtype=eng.cdt)
             gi8[..., :3] = g8.permute(0, 2, 3, 1)
         kl_coef = None
         if ctx.kl2 is not None and gkl is not None:
@@ -160,13 +172,17 @@ class _GenFn(torch.autograd.Function):
 
 class AuroraGenerator(_FlatModule):
     """Reference :668-855.  Extra keyword args: num_experts (default 4, as NUM_EXPERTS), topk (None = dense
-    soft combine over all experts, as the reference trains), dtype ("fp32" | "bf16")."""
+    soft combine over all experts, as the reference trains), dtype ("fp32" | "bf16").  ``max_resolution`` 16 is
+    the reference; 32 / 64 / 128 select the progressive extension (moegan_mi/layout.py gen_blocks: the output is
+    R x R and ``return_intermediate`` gives the R/2 image)."""
 
     def __init__(self, latent_dim=LATENT_DIM, text_embedding_dim=512, max_resolution=16, num_experts=NUM_EXPERTS,
                  topk=None, dtype="fp32", seed=0):
-        if latent_dim != 512 or text_embedding_dim != 512 or max_resolution != 16:
-            raise ValueError("the reference architecture is fixed at latent 512, text 512, 16x16 output")
-        super().__init__(generator_shapes(num_experts), frozen=("to_rgb_8.",), dtype=dtype)
+        if latent_dim != 512 or text_embedding_dim != 512 or max_resolution not in MAX_RESOLUTIONS:
+            raise ValueError("the architecture is fixed at latent 512, text 512 and a 16x16 output (the reference) "
+                             f"or one of the progressive resolutions {MAX_RESOLUTIONS[1:]}")
+        super().__init__(generator_shapes(num_experts, max_resolution), frozen=frozen_rgb_prefixes(max_resolution),
+                         dtype=dtype)
         self.latent_dim, self.text_embedding_dim, self.max_resolution = latent_dim, text_embedding_dim, max_resolution
         self.num_experts, self.topk = num_experts, topk
         self._use_checkpointing = False
@@ -369,7 +385,9 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
     if process_group is not None:
         import torch.distributed as dist
         rank, world = dist.get_rank(process_group), dist.get_world_size(process_group)
-    generator = AuroraGenerator(num_experts=num_experts, topk=topk, dtype=dtype, seed=seed).to(device)
+    # max_resolution 16 is the reference generator; 32 / 64 / 128 train the progressive extension (layout.py)
+    generator = AuroraGenerator(num_experts=num_experts, topk=topk, dtype=dtype, seed=seed,
+                                max_resolution=max_resolution).to(device)
     discriminator = AuroraDiscriminator(dtype=dtype, seed=seed + 1).to(device)
     if checkpoint_activation:
         generator.enable_checkpointing()
@@ -378,7 +396,8 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
         start_epoch, step = load_resume(resume_from, generator, discriminator)
         print(f"Resumed from {resume_from}: epoch {start_epoch}, step {step}")
     cfg = StepConfig(E=num_experts, topk=topk, dtype=dtype, r1_gamma=r1_gamma, clip_weight_16=clip_weight_16,
-                     clip_weight_8=clip_weight_8, balance_weight=balance_weight, beta1=beta1, beta2=beta2)
+                     clip_weight_8=clip_weight_8, balance_weight=balance_weight, beta1=beta1, beta2=beta2,
+                     max_res=max_resolution)
     ts = TrainStep(cfg, device, process_group=process_group, gstore=generator._store, dstore=discriminator._store)
     if _clip_model is not None:  # CLIP terms of the generator loss (logging / guard only: no gradient, :98-101)
         ts.clip_encoder = _clip_model.encode_image
@@ -403,7 +422,8 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
             print(f"\n{'=' * 20} Epoch {epoch + 1}/{num_epochs} {'=' * 20}")
             print(f"  LR: {cur_lr:.6f}  Temperature factor: {temperature_factor:.2f}  "
                   f"Effective KL weight: {eff_kl:.8f}")
-        pbar = tqdm(dataloader, desc=f"Epoch {epoch + 1}/{num_epochs}", disable=rank != 0)
+        # batch i+1's host -> HBM copy overlaps batch i's step (moegan_mi/prefetch.py)
+        pbar = tqdm(DevicePrefetcher(dataloader, device), desc=f"Epoch {epoch + 1}/{num_epochs}", disable=rank != 0)
         n_batches = len(dataloader)
         for batch_idx, (real, text) in enumerate(pbar):
             real = real.to(device, non_blocking=True).float()

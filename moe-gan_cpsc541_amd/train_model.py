@@ -69,6 +69,10 @@ def parse_args(argv=None):
     p.add_argument("--gradient_accumulation_steps", type=int, default=8)
     p.add_argument("--resume", type=str, default=None, help="resume checkpoint (t2i_moe_gan.py:1484-1491 layout)")
     p.add_argument("--save_every_epoch", action="store_true", help="write a resume checkpoint after every epoch")
+    p.add_argument("--max_resolution", type=int, default=16, choices=[16, 32, 64, 128],
+                   help="generator output size: 16 = the reference; 32/64/128 = the progressive extension")
+    p.add_argument("--clip_weights", type=str, default=None,
+                   help="local OpenAI CLIP state_dict / safetensors: enables the (gradient-free) CLIP loss terms")
     p.add_argument("--hyperparameters", type=str, default=None,
                    help="SageMaker-style hyperparameters.json (string values, sagemaker_train.py:85-102); its keys "
                         "override the flags above")
@@ -125,6 +129,9 @@ def main(argv=None):
     if args.hyperparameters:
         from moegan_mi.hparams import given_train_kwargs, load_sagemaker_hyperparameters
         kw.update(given_train_kwargs(load_sagemaker_hyperparameters(args.hyperparameters)))
+    if args.clip_weights:
+        M.load_clip_weights(args.clip_weights, device)
+    kw.setdefault("max_resolution", args.max_resolution)
     G, D = M.train_aurora_gan(train_dl, val_dataloader=val_dl, device=device, save_dir=args.save_dir,
                               num_experts=args.num_experts, topk=args.topk, dtype=args.dtype, process_group=pg,
                               resume_from=args.resume, save_every_epoch=args.save_every_epoch, **kw)

@@ -199,8 +199,9 @@ def attention_block(x, w, text_seq, P, pre, E, eps=None, training=True, anneal=1
 # Conv / generative blocks + generator  (t2i_moe_gan.py:579-855)
 # ---------------------------------------------------------------------------
 def conv_block(x, w, P, pre):
-    out = mtm(x, w, P, pre + "mtm1.")
-    out = mtm(out, w, P, pre + "mtm2.")
+    off = (pre + "mtm1.offset_net.0.weight") in P  # offset heads only at resolution <= 16 (:199)
+    out = mtm(x, w, P, pre + "mtm1.", off)
+    out = mtm(out, w, P, pre + "mtm2.", off)
     skip = modconv(x, w, P, pre + "skip_proj.") if (pre + "skip_proj.weight") in P else x  # :615-616
     return out + skip
 
@@ -213,6 +214,14 @@ def gen_block(x, w, text_seq, P, pre, upsample, E, eps=None, training=True, anne
 
 
 BLOCKS = (("gen_block_4", False), ("gen_block_8", True), ("gen_block_16", True))
+# progressive extension (BASELINE C4; no reference definition, t2i_moe_gan.py:1005-1026 names gen_block_32 / _64
+# only): upsample + ConvolutionBlock without offset heads, no attention block.  The composition of reference
+# functions is restated here; the block list itself is the build's (moegan_mi/layout.py) -- parity unpinned.
+EXT_BLOCKS = (("gen_block_32", 32), ("gen_block_64", 64), ("gen_block_128", 128))
+
+
+def max_resolution(P):
+    return max([16] + [r for n, r in EXT_BLOCKS if f"to_rgb_{r}.weight" in P])
 
 
 def num_experts(P):
@@ -247,15 +256,33 @@ def generator(z, text, P, eps=None, training=True, anneal=1.0, psi=0.7, topk=Non
         w = mean + psi * (w - mean)
     x = P["constant"].repeat(B, 1, 1, 1)
     kls, probs = [], []
-    img8 = None
+    feats = {}
     for i, (name, up) in enumerate(BLOCKS):
         x, kl, p = gen_block(x, w, text_seq, P, name + ".", up, E, None if eps is None else eps[i],
                              training, anneal, topk, None if routes is None else routes[i])
         kls.append(kl)
         probs.append(p)
-        if name == "gen_block_8":
-            img8 = modconv(x, w, P, "to_rgb_8.")  # :831
-    img16 = modconv(x, w, P, "to_rgb_16.")  # :839
+        feats[4 << i] = x
+    R = max_resolution(P)
+    for name, r in EXT_BLOCKS:  # progressive extension only (R > 16)
+        if r > R:
+            break
+        x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+        x = conv_block(x, w, P, name + ".conv_block.")
+        feats[r] = x
+    img8 = modconv(feats[R // 2], w, P, f"to_rgb_{R // 2}.")  # reference (R = 16): to_rgb_8, :831
+    img16 = modconv(feats[R], w, P, f"to_rgb_{R}.")  # to_rgb_16, :839
+    return img16, img8, sum(kls), probs
+    for name, r in EXT_BLOCKS:  # progressive extension: returns (R x R image, R/2 x R/2 image, ...)
+        if r > R:
+            break
+        x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+        x = conv_block(x, w, P, name + ".conv_block.")
+        if r == R // 2:
+            img8 = modconv(x, w, P, f"to_rgb_{r}.")
+        elif R == 32:
+            img8 = modconv(x_prev, w, P, "to_rgb_16.")
+    img16 = modconv(x, w, P, f"to_rgb_{R}.")
     return img16, img8, sum(kls), probs
 
 

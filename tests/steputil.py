@@ -9,10 +9,10 @@ from oracle.recipe import fill_state
 EPS_DIMS = [(512, 512), (256, 512), (128, 512)]  # (C, text dim) per MoE block
 
 
-def make_inputs(B, E, seed=0):
-    """real U(-1,1) [B,3,64,64], text / z N(0,1) [B,512], 6 router-noise triples (D phase, G phase), perm."""
+def make_inputs(B, E, seed=0, res=64):
+    """real U(-1,1) [B,3,res,res], text / z N(0,1) [B,512], 6 router-noise triples (D phase, G phase), perm."""
     g = torch.Generator().manual_seed(seed)
-    real = torch.rand(B, 3, 64, 64, generator=g) * 2 - 1
+    real = torch.rand(B, 3, res, res, generator=g) * 2 - 1
     text = torch.randn(B, 512, generator=g)
     z = torch.randn(B, 512, generator=g)
     eps = [tuple(torch.randn(s, generator=g) for s in ((c, 128), (t, 128), (256, E))) for c, t in EPS_DIMS * 2]
@@ -20,14 +20,17 @@ def make_inputs(B, E, seed=0):
     return real, text, z, eps[:3], eps[3:], perm
 
 
-def oracle_models(E, lr=2e-4, seed_g=0, seed_d=50):
+def oracle_models(E, lr=2e-4, seed_g=0, seed_d=50, max_res=16):
     """Reference-layout fp32 leaves + the reference's AdamW (betas 0.5/0.999, wd 0.01, :1100-1102), with the
-    clipped gradients captured right before each optimizer step."""
-    from moegan_mi.layout import discriminator_shapes, generator_shapes
-    PG = {n: torch.from_numpy(v) for n, v in fill_state(generator_shapes(E), seed_g).items()}
+    clipped gradients captured right before each optimizer step.  ``max_res`` > 16: progressive extension."""
+    from moegan_mi.layout import discriminator_shapes, frozen_rgb_prefixes, generator_shapes
+    PG = {n: torch.from_numpy(v) for n, v in fill_state(generator_shapes(E, max_res), seed_g).items()}
+    frozen = frozen_rgb_prefixes(max_res)
     PD = {n: torch.from_numpy(v).requires_grad_(True) for n, v in fill_state(discriminator_shapes(), seed_d).items()}
     for n, v in PG.items():
-        if not n.split(".")[-1].startswith("epsilon_"):
+        # (the reference's to_rgb_8 is a leaf whose .grad stays None; the progressive extension's unused lower
+        # to_rgb layers do not reach the loss at all, so they stay out of the optimizer there)
+        if not n.split(".")[-1].startswith("epsilon_") and (max_res == 16 or not n.startswith(frozen)):
             v.requires_grad_(True)
     optG = torch.optim.AdamW([v for v in PG.values() if v.requires_grad], lr=lr, betas=(0.5, 0.999),
                              weight_decay=0.01)
@@ -57,11 +60,12 @@ def oracle_clone(PG, PD, optG, optD, lr=2e-4):
     return PG2, PD2, optG2, optD2, _capture(optD2, optG2, PD2, PG2)
 
 
-def gpu_step(E, topk, dtype, dev="cuda", seed_g=0, seed_d=50, fp8=False):
+def gpu_step(E, topk, dtype, dev="cuda", seed_g=0, seed_d=50, fp8=False, max_res=16):
     from moegan_mi.layout import discriminator_shapes, generator_shapes
     from moegan_mi.step import StepConfig, TrainStep
-    ts = TrainStep(StepConfig(E=E, topk=topk, dtype=dtype, fp8=fp8), dev)
-    ts.gs.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(generator_shapes(E), seed_g).items()})
+    ts = TrainStep(StepConfig(E=E, topk=topk, dtype=dtype, fp8=fp8, max_res=max_res), dev)
+    ts.gs.load_state_dict({k: torch.from_numpy(v) for k, v in
+                           fill_state(generator_shapes(E, max_res), seed_g).items()})
     ts.ds.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(discriminator_shapes(), seed_d).items()})
     return ts
 

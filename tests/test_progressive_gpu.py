@@ -1,0 +1,131 @@
+"""Progressive generator extension (BASELINE config C4) on the GPU, fp32 parity mode.
+
+The reference defines no block above 16x16 (gen_block_32 / _64 appear only in the dead
+create_optimizer_for_active_blocks, t2i_moe_gan.py:1005-1026), so the block list is the build's
+(moegan_mi/layout.py gen_blocks) and this parity is "unpinned" against the reference: both sides compose the
+same pinned reference functions (upsample :657, ConvolutionBlock :604-621 with MTMs that have no offset head
+above 16x16, :199, ModulatedConv to_rgb :154-186), the oracle in plain fp32 PyTorch autograd
+(oracle/aurora_cpu.generator), the device through the HIP engines.  Bars are the fp32 ones of F7 / F8:
+1e-4 relative on values, 1e-3 on gradients, 2e-2 on AdamW deltas.
+"""
+import pytest
+import torch
+
+from goldens import close
+from oracle import aurora_cpu as O
+from oracle.recipe import fill_state
+from steputil import gpu_step, make_inputs, nchw, oracle_models
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+torch.set_num_threads(8)
+
+
+def _tensor_close(actual, expected, rtol, atol, what):
+    """The full-step bar of F8 (test_engine_gpu._train_replay): max-abs error within rtol of the tensor's scale,
+    plus relative L2 error <= rtol over the whole tensor.  (Per-element bars do not hold for the modulation-weight
+    gradients after a full step: they are sums over the batch of cancelling terms, so an element at 1/3 of the
+    tensor's RMS can carry a few % fp32 reordering error while the tensor as a whole agrees to 1e-4.)"""
+    a = actual.detach().double().cpu().reshape(-1)
+    e = expected.detach().double().cpu().reshape(-1)
+    err = float((a - e).abs().max())
+    scale = float(e.abs().max())
+    assert err <= atol + rtol * scale, f"{what}: max abs err {err:.3e} (scale {scale:.3e})"
+    rel = float((a - e).norm() / max(float(e.norm()), 1e-30))
+    assert rel <= rtol or err <= atol, f"{what}: relative L2 error {rel:.3e}"
+
+
+def _nhwc_pad(x):
+    B, C, H, W = x.shape
+    out = torch.zeros(B, H, W, 8, device=DEV)
+    out[..., :C] = x.permute(0, 2, 3, 1).to(DEV)
+    return out
+
+
+@pytest.mark.parametrize("R", [32, 64])
+def test_progressive_generator_fwd_bwd(R):
+    from moegan_mi.engine_g import GeneratorEngine
+    from moegan_mi.layout import frozen_rgb_prefixes, generator_shapes
+    from moegan_mi.params import ParamStore
+    E, B = 4, 2
+    shapes = generator_shapes(E, R)
+    vals = fill_state(shapes, 0)
+    st = ParamStore(shapes, DEV, frozen_prefixes=frozen_rgb_prefixes(R))
+    st.load_state_dict({k: torch.from_numpy(v) for k, v in vals.items()})
+    ge = GeneratorEngine(st, E)
+    assert ge.max_res == R and ge.attn_blocks == ["gen_block_4", "gen_block_8", "gen_block_16"]
+    ge.prep()
+    g = torch.Generator().manual_seed(R)
+    z, text = torch.randn(B, 512, generator=g), torch.randn(B, 512, generator=g)
+    eps = [tuple(torch.randn(s, generator=g) for s in ((c, 128), (512, 128), (256, E))) for c in (512, 256, 128)]
+    P = {n: torch.from_numpy(v).requires_grad_(not n.split(".")[-1].startswith("epsilon_")) for n, v in vals.items()}
+    img, img_half, kl, probs = O.generator(z, text, P, eps, True, 3.0, 0.7)
+    assert img.shape == (B, 3, R, R) and img_half.shape == (B, 3, R // 2, R // 2)
+    R_img = torch.randn(img.shape, generator=g)
+    R_half = torch.randn(img_half.shape, generator=g)
+    Rp = [torch.randn(p.shape, generator=g) * 1e-2 for p in probs]
+    loss = (img * R_img).sum() + (img_half * R_half).sum() + 0.37 * kl + sum((p * r).sum() for p, r in zip(probs, Rp))
+    loss.backward()
+
+    epsd = [tuple(t.to(DEV) for t in trip) for trip in eps]
+    im, ih, kl2s, pr, _, ctx = ge.forward(z.to(DEV), text.to(DEV), epsd, 3.0, 0.7, train=True, save=True,
+                                          want_img8=True)
+    close(nchw(im), img.detach(), rtol=1e-4, what="img")
+    close(nchw(ih), img_half.detach(), rtol=1e-4, what="img_half")
+    kl2 = torch.stack(kl2s)
+    close(kl2[:, 0].sum(), kl.detach(), rtol=1e-5, what="kl")
+    for i in range(3):
+        close(pr[i], probs[i].detach(), rtol=1e-4, what=f"probs{i}")
+    ge.backward(ctx, _nhwc_pad(R_img), kl_coef=(0.37 * kl2[:, 1]).contiguous(), g_probs=[r.to(DEV) for r in Rp],
+                g_img8=_nhwc_pad(R_half))
+    torch.cuda.synchronize()
+    n_checked = 0
+    for n, t in P.items():
+        if not t.requires_grad:
+            continue
+        if t.grad is None:  # the unused lower to_rgb layers: frozen tail, gradient stays zero
+            assert n.startswith(frozen_rgb_prefixes(R)), n
+            assert float(st.gview(n).abs().max()) == 0.0, n
+            continue
+        close(st.gview(n), t.grad, rtol=1e-3, atol=1e-7, what=n)
+        n_checked += 1
+    assert n_checked > 200
+
+
+def test_progressive_train_step_r32():
+    """One full G+D step at 32x32 (real and fake images 32x32: multi-logit fakes in the D and G losses) vs the
+    oracle's train_step: losses, clipped gradients and AdamW deltas of every tensor."""
+    E, B, R = 4, 2, 32
+    real, text, z, eps_d, eps_g, perm = make_inputs(B, E, seed=7, res=R)
+    PG, PD, optG, optD, grads = oracle_models(E, max_res=R)
+    gb = {n: v.detach().clone() for n, v in PG.items()}
+    db = {n: v.detach().clone() for n, v in PD.items()}
+    ref = O.train_step(PG, PD, optG, optD, real, text, z, eps_d, eps_g, perm, kl_weight_eff=1e-8)
+    assert not ref["skipped"]
+    ts = gpu_step(E, None, "fp32", max_res=R)
+    g0, d0 = ts.gs.data.clone(), ts.ds.data.clone()
+    dv = lambda trips: [tuple(t.to(DEV) for t in trip) for trip in trips]  # noqa: E731
+    out = ts.step(real.to(DEV), text.to(DEV), z.to(DEV), dv(eps_d), dv(eps_g), perm.int().to(DEV), anneal=3.0,
+                  eff_kl_weight=1e-8)
+    torch.cuda.synchronize()
+    assert abs(float(out["d_losses"][0]) - ref["d_loss_gan"]) < 1e-4 * abs(ref["d_loss_gan"])
+    assert abs(float(out["r1"][0]) - ref["r1"]) < 1e-4 * abs(ref["r1"]) + 1e-7
+    assert abs(float(out["g_gan"][0]) - ref["g_loss_gan"]) < 1e-4 * abs(ref["g_loss_gan"])
+    assert abs(float(out["balance"][0]) - ref["balance"]) < 1e-3 * ref["balance"] + 1e-7
+    assert out["fake_pred"].shape == (B, (R // 4 - 3) ** 2)
+    for which, store, before, P, P0, max_norm in (("D", ts.ds, d0, PD, db, 0.7), ("G", ts.gs, g0, PG, gb, 0.8)):
+        gn = float(store.grad[:store.n_opt].double().norm())
+        coef = min(1.0, max_norm / (gn + 1e-6))
+        for n, (off, numel) in store.offsets.items():
+            if n.split(".")[-1].startswith("epsilon_"):
+                continue
+            shape = store.shapes[n]
+            gref = grads[which].get(n)
+            if gref is None:
+                assert off >= store.n_opt, n  # frozen tail: never stepped
+                assert torch.equal(store.data[off:off + numel], before[off:off + numel]), n
+                continue
+            _tensor_close((store.grad[off:off + numel] * coef).view(shape), gref, 2e-3, 1e-8, f"{which} grad {n}")
+            delta = (store.data[off:off + numel] - before[off:off + numel]).view(shape)
+            _tensor_close(delta, (P[n].detach() - P0[n]), 2e-2, 2e-6, f"{which} delta {n}")
+    assert out["img16"].shape[1] == R
