@@ -397,24 +397,40 @@ void run_wgrad(const void* gy, int64_t ldg, const void* x, int B, int H, int W, 
 }
 
 // gw[o][ci][tap] += sum_s ws[s][o][tap * Cin + ci]: split-K slabs of a weight gradient folded and moved to the
-// reference [Cout][Cin][KH][KW] layout in one pass (threads walk gw in order: coalesced accumulate).
+// reference [Cout][Cin][KH][KW] layout in one pass.  Block (o, chunk) owns output channel o and input channels
+// [c0, c0 + CC): it reads the `taps` slab segments of CC floats as 16-B vectors with four slabs in flight per
+// step (a fixed summation order: deterministic), stages the sums in LDS and read-modify-writes the contiguous
+// reference-layout range gw[o][c0 .. c0+CC)[*] (the element-per-thread form wrote gw at a stride of `taps`).
 __global__ __launch_bounds__(256) void k_wgrad_fold(const float* __restrict__ ws, int splits, int Cout, int lgCin,
-                                                    int taps, float* __restrict__ gw) {
-  // threads walk the slabs in their own order (o, tap, ci): the split reads are coalesced; the reference
-  // layout write gw[o][ci][tap] is strided by taps (one read-modify-write per element)
-  const int Cin = 1 << lgCin, N = taps << lgCin;
+                                                    int taps, int lgCC, float* __restrict__ gw) {
+  extern __shared__ float seg[];  // [taps][CC]
+  const int Cin = 1 << lgCin, N = taps << lgCin, CC = 1 << lgCC;
   const int64_t MN = (int64_t)Cout * N;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
-    const int ci = (int)(i & (Cin - 1));
-    const int64_t t = i >> lgCin;  // o * taps + tap
-    const int tap = (int)(t % taps);
-    const int64_t o = t / taps;
-    float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += ws[s * MN + i];
-    gw[((o << lgCin) + ci) * taps + tap] += v;
+  const int o = blockIdx.x, c0 = blockIdx.y << lgCC;
+  const float* src = ws + (int64_t)o * N + c0;
+  const int nv = (taps << lgCC) >> 2;  // 16-B vectors of this block
+  for (int q = threadIdx.x; q < nv; q += 256) {
+    const int tap = (4 * q) >> lgCC, ci = (4 * q) & (CC - 1);
+    const float* p = src + ((int64_t)tap << lgCin) + ci;
+    f32x4_t v = *reinterpret_cast<const f32x4_t*>(p);
+    int s = 1;
+    for (; s + 3 < splits; s += 4) {
+      const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p + s * MN);
+      const f32x4_t b = *reinterpret_cast<const f32x4_t*>(p + (s + 1) * MN);
+      const f32x4_t c = *reinterpret_cast<const f32x4_t*>(p + (s + 2) * MN);
+      const f32x4_t d = *reinterpret_cast<const f32x4_t*>(p + (s + 3) * MN);
+      v += ((a + b) + (c + d));
+    }
+    for (; s < splits; ++s) v += *reinterpret_cast<const f32x4_t*>(p + s * MN);
+    *reinterpret_cast<f32x4_t*>(seg + 4 * q) = v;
+  }
+  __syncthreads();
+  float* dst = gw + ((int64_t)o * Cin + c0) * taps;
+  for (int j = threadIdx.x; j < (taps << lgCC); j += 256) {  // j = ci_local * taps + tap (reference order)
+    const int ci = j / taps, tap = j - ci * taps;
+    dst[j] += seg[(tap << lgCC) + ci];
   }
 }
-
 
 // Weight gradient with split-K into fp32 slabs written by the 8-column vector epilogue (coalesced, no atomics),
 // then k_wgrad_fold.  Returns false when the workspace cannot be had (caller falls back to atomics).
@@ -440,8 +456,11 @@ bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, i
   dim3 grid(cdiv(Cout, BM), cdiv(N, BN), splits);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, false, LdMC<T>, LdMCConv<T, XF>, Epi<float>>), grid, dim3(NTHREADS),
                      0, st, la, lb, slab, Cout, N, P, kchunk, kNoGroup);
-  int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 4096);
-  hipLaunchKernelGGL(k_wgrad_fold, dim3(blocks), dim3(256), 0, st, ws, splits, Cout, ilog2(Cin), KH * KW, gw);
+  // (Cout x Cin / CC) blocks: enough to spread the slab reads over the chip, >= 8 channels per segment
+  int lgCC = ilog2(Cin);
+  while (lgCC > 3 && (int64_t)Cout * (Cin >> lgCC) < 1024) --lgCC;
+  hipLaunchKernelGGL(k_wgrad_fold, dim3(Cout, Cin >> lgCC), dim3(256), (size_t)(KH * KW) * sizeof(float) << lgCC, st,
+                     ws, splits, Cout, ilog2(Cin), KH * KW, lgCC, gw);
   return true;
 }
 }  // namespace

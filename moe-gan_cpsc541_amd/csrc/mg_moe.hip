@@ -74,67 +74,110 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
     acc[e] += __shfl_xor(acc[e], 2, 64);
     acc[e] += __shfl_xor(acc[e], 4, 64);
   }
-  if (ok && tl == 0) {
-  int b = t >> lgHW;
-  float te = teff_of(temp, anneal);
-  float z[E], p[E];
+  // softmax / top-k spread over the team: after the butterfly every lane holds all E logits; lane tl owns
+  // experts tl, tl + 8, ... and the team reduces max / sums / arg-max with shuffles, so probs and zlog leave as
+  // 32-byte runs per token instead of one lane's scalar stores (the team-serial epilogue ran at ~9 % of HBM)
+  constexpr int NE = E >= TEAM ? E / TEAM : 1;
+  const int b = (ok ? t : 0) >> lgHW;
+  const float te = teff_of(temp, anneal);
+  float z[NE], p[NE];
   float mx = -INFINITY;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    z[e] = (acc[e] + Lt[(int64_t)b * E + e]) / te;
-    float l = clampf(z[e], -20.f, 20.f);
-    p[e] = l;
-    mx = fmaxf(mx, l);
-  }
-  float s = 0.f;
+  for (int j = 0; j < NE; ++j) {
+    const int e = tl + TEAM * j;
+    const bool own = e < E;
+    float a = 0.f;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    p[e] = expf(p[e] - mx);
-    s += p[e];
+    for (int q = 0; q < E; ++q)
+      if (q == e) a = acc[q];
+    z[j] = own && ok ? (a + Lt[(int64_t)b * E + e]) / te : 0.f;
+    p[j] = own ? clampf(z[j], -20.f, 20.f) : -INFINITY;
+    mx = fmaxf(mx, p[j]);
   }
+  mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+  float sm = 0.f;
+#pragma unroll
+  for (int j = 0; j < NE; ++j) {
+    p[j] = tl + TEAM * j < E ? expf(p[j] - mx) : 0.f;
+    sm += p[j];
+  }
+  sm += __shfl_xor(sm, 1, 64);
+  sm += __shfl_xor(sm, 2, 64);
+  sm += __shfl_xor(sm, 4, 64);
   float s2 = 0.f;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    p[e] = clampf(p[e] / s, 1e-6f, 1.f);
-    s2 += p[e];
+  for (int j = 0; j < NE; ++j) {
+    p[j] = tl + TEAM * j < E ? clampf(p[j] / sm, 1e-6f, 1.f) : 0.f;
+    s2 += p[j];
+  }
+  s2 += __shfl_xor(s2, 1, 64);
+  s2 += __shfl_xor(s2, 2, 64);
+  s2 += __shfl_xor(s2, 4, 64);
+#pragma unroll
+  for (int j = 0; j < NE; ++j) p[j] = p[j] / s2;
+  // top-k, lowest index first among equals: team arg-max k times (rounds unrolled over E so every lane keeps
+  // the picks it will store in registers: pick r goes to lane r % TEAM)
+  constexpr int NK = (E + TEAM - 1) / TEAM;
+  unsigned used = 0u;  // bit j: this lane's j-th expert taken
+  float gsum = 0.f, mg[NK];
+  int g0 = 0, mt[NK];
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+    mg[j] = 0.f;
+    mt[j] = 0;
   }
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    p[e] = p[e] / s2;
-    zlog[(int64_t)t * E + e] = z[e];
-  }
-  // top-k, lowest index first among equals
-  unsigned long long used = 0ull;
-  float gsum = 0.f;
-  float gv[E];
-  int gi[E];
-  for (int j = 0; j < k; ++j) {
-    int best = -1;
-    float bv = -INFINITY;
+  for (int r = 0; r < E; ++r) {
+    if (r < k) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-      if (!((used >> e) & 1ull) && (best < 0 || p[e] > bv)) {
-        best = e;
-        bv = p[e];
+      for (int j = 0; j < NE; ++j) {
+        const int e = tl + TEAM * j;
+        const float pv = p[j] == p[j] ? p[j] : -INFINITY;  // NaN ranks lowest: the pick is always an expert
+        if (e < E && !((used >> j) & 1u) && (pv > bv || (pv == bv && e < bi))) {
+          bv = pv;
+          bi = e;
+        }
       }
-    used |= 1ull << best;
-    gi[j] = best;
-    gv[j] = bv;
-    gsum += bv;
-  }
-  for (int j = 0; j < k; ++j) {
-    topi[(int64_t)t * k + j] = gi[j];
-    float g = eval_mode ? 1.f : (k == E ? gv[j] : gv[j] / gsum);
-    gate[(int64_t)t * k + j] = g;
-  }
-  if (eval_mode) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) probs[(int64_t)t * E + e] = (e == gi[0]) ? 1.f : 0.f;
-  } else {
-#pragma unroll
-    for (int e = 0; e < E; ++e) probs[(int64_t)t * E + e] = p[e];
+      for (int o = 1; o < TEAM; o <<= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (bi < E && (bi & (TEAM - 1)) == tl) used |= 1u << (bi / TEAM);
+      if (r == 0) g0 = bi;
+      if ((r & (TEAM - 1)) == tl) {
+        mt[r / TEAM] = bi < E ? bi : 0;
+        mg[r / TEAM] = bv;
+      }
+      gsum += bv;
+    }
   }
-  }  // ok && tl == 0
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int e = tl + TEAM * j;
+      if (e < E) {
+        zlog[(int64_t)t * E + e] = z[j];
+        probs[(int64_t)t * E + e] = eval_mode ? (e == g0 ? 1.f : 0.f) : p[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      const int r = tl + TEAM * j;
+      if (r < k) {
+        topi[(int64_t)t * k + r] = mt[j];
+        gate[(int64_t)t * k + r] = eval_mode ? 1.f : (k == E ? mg[j] : mg[j] / gsum);
+      }
+    }
+  }
   }  // token loop
 }
 

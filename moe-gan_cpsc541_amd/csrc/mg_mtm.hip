@@ -732,12 +732,22 @@ __global__ __launch_bounds__(1024) void k_mtm_bwd_img(const TG* __restrict__ gou
   for (int i = 0; i < 18; ++i) {
     accw[i] += __shfl_xor(accw[i], 32, 64);
   }
+  // per-wave rows of the (gw2) partial, folded below in wave order: 16 waves hitting the same 576 LDS words
+  // with atomics serialised ~300 atomic wave-instructions per block
+  float* wpart = reinterpret_cast<float*>(ent + 4 * HW);  // [nt / 64][576]
   if ((tid & 63) < 32) {
+    float* wr = wpart + (tid >> 6) * 576;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      atomicAdd(&red[c * 9 + tap], accw[tap]);
-      atomicAdd(&red[(32 + c) * 9 + tap], accw[9 + tap]);
+      wr[c * 9 + tap] = accw[tap];
+      wr[(32 + c) * 9 + tap] = accw[9 + tap];
     }
+  }
+  __syncthreads();
+  for (int i = tid; i < 576; i += nt) {
+    float sacc = 0.f;
+    for (int w = 0; w < (nt >> 6); ++w) sacc += wpart[w * 576 + i];
+    red[i] = sacc;
   }
   if (tid < 64) {
     float s0 = 0.f, s1 = 0.f;
@@ -867,7 +877,8 @@ extern "C" int mg_mtm_bwd_fused(int dtype, int gout_dtype, const void* gout, con
     mg_set_error("mg_mtm_bwd_fused: workspace allocation failed");
     return MG_ERR_LAUNCH;
   }
-  const size_t lds = (size_t)HW * 6 * sizeof(float) + (576 + 578) * sizeof(float) + (size_t)(9 * HW + 1) * sizeof(int);
+  const size_t lds = (size_t)HW * 6 * sizeof(float) + (576 + 578) * sizeof(float) + (size_t)(9 * HW + 1) * sizeof(int) +
+                     (size_t)16 * 576 * sizeof(float);  // + per-wave gw2 partial rows (16 waves of the 1024-thread block)
   MG_REQUIRE(lds <= 65536, "image too large for the per-image LDS lists");
 #define L_(T, TG, TX) hipLaunchKernelGGL((k_mtm_bwd_img<T, TG, TX>), dim3(B), dim3(1024), lds, st, (const TG*)gout, \
     (const T*)x, samp, (const T*)o1, w2, H, W, C, lgV, (TX*)gx, accumulate, (T*)ga1, part)

@@ -21,7 +21,7 @@ DEV = "cuda"
 torch.set_num_threads(8)
 
 
-def _tensor_close(actual, expected, rtol, atol, what):
+def _tensor_close(actual, expected, rtol, atol, what, maxabs=True):
     """The full-step bar of F8 (test_engine_gpu._train_replay): max-abs error within rtol of the tensor's scale,
     plus relative L2 error <= rtol over the whole tensor.  (Per-element bars do not hold for the modulation-weight
     gradients after a full step: they are sums over the batch of cancelling terms, so an element at 1/3 of the
@@ -30,7 +30,7 @@ def _tensor_close(actual, expected, rtol, atol, what):
     e = expected.detach().double().cpu().reshape(-1)
     err = float((a - e).abs().max())
     scale = float(e.abs().max())
-    assert err <= atol + rtol * scale, f"{what}: max abs err {err:.3e} (scale {scale:.3e})"
+    assert not maxabs or err <= atol + rtol * scale, f"{what}: max abs err {err:.3e} (scale {scale:.3e})"
     rel = float((a - e).norm() / max(float(e.norm()), 1e-30))
     assert rel <= rtol or err <= atol, f"{what}: relative L2 error {rel:.3e}"
 
@@ -127,5 +127,10 @@ def test_progressive_train_step_r32():
                 continue
             _tensor_close((store.grad[off:off + numel] * coef).view(shape), gref, 2e-3, 1e-8, f"{which} grad {n}")
             delta = (store.data[off:off + numel] - before[off:off + numel]).view(shape)
-            _tensor_close(delta, (P[n].detach() - P0[n]), 2e-2, 2e-6, f"{which} delta {n}")
+            # first AdamW step: ~lr * sign(g) per element, so elements whose gradient is ~0 flip freely (|err| 2 lr,
+            # e.g. the batch-summed modulation-weight gradients at B=2): the delta error is weighted by the oracle's
+            # |g|, as the bf16 step test does (test_step_bf16_gpu.py)
+            wgt = gref.detach().double().abs().reshape(shape)
+            _tensor_close(delta.double() * wgt.to(delta.device), (P[n].detach() - P0[n]).double() * wgt, 2e-2, 0.0,
+                          f"{which} |g|-weighted delta {n}", maxabs=False)
     assert out["img16"].shape[1] == R
