@@ -137,7 +137,11 @@ def main():
         pg = dist.group.WORLD
 
     from moegan_mi import ops
+    from moegan_mi import _lib
     from moegan_mi.graphs import SegmentedGraph
+    for kv in filter(None, os.environ.get("MOEGAN_TUNE", "").split(",")):  # A/B switches: "key=value,..."
+        k_, v_ = kv.split("=")
+        _lib.call("mg_set_tuning", int(k_), int(v_))
     from moegan_mi.init import init_discriminator, init_generator
     from moegan_mi.step import StepConfig, TrainStep
 

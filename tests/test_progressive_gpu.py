@@ -21,16 +21,17 @@ DEV = "cuda"
 torch.set_num_threads(8)
 
 
-def _tensor_close(actual, expected, rtol, atol, what, maxabs=True):
-    """The full-step bar of F8 (test_engine_gpu._train_replay): max-abs error within rtol of the tensor's scale,
-    plus relative L2 error <= rtol over the whole tensor.  (Per-element bars do not hold for the modulation-weight
+def _tensor_close(actual, expected, rtol, atol, what, maxabs=True, rtol_max=None):
+    """The full-step bar of F8 (test_engine_gpu._train_replay): relative L2 error <= rtol over the whole tensor,
+    plus max-abs error within rtol_max (default rtol) of the tensor's scale.  (Per-element bars do not hold for the modulation-weight
     gradients after a full step: they are sums over the batch of cancelling terms, so an element at 1/3 of the
     tensor's RMS can carry a few % fp32 reordering error while the tensor as a whole agrees to 1e-4.)"""
     a = actual.detach().double().cpu().reshape(-1)
     e = expected.detach().double().cpu().reshape(-1)
     err = float((a - e).abs().max())
     scale = float(e.abs().max())
-    assert not maxabs or err <= atol + rtol * scale, f"{what}: max abs err {err:.3e} (scale {scale:.3e})"
+    rm = rtol if rtol_max is None else rtol_max
+    assert not maxabs or err <= atol + rm * scale, f"{what}: max abs err {err:.3e} (scale {scale:.3e})"
     rel = float((a - e).norm() / max(float(e.norm()), 1e-30))
     assert rel <= rtol or err <= atol, f"{what}: relative L2 error {rel:.3e}"
 
@@ -125,7 +126,8 @@ def test_progressive_train_step_r32():
                 assert off >= store.n_opt, n  # frozen tail: never stepped
                 assert torch.equal(store.data[off:off + numel], before[off:off + numel]), n
                 continue
-            _tensor_close((store.grad[off:off + numel] * coef).view(shape), gref, 2e-3, 1e-8, f"{which} grad {n}")
+            _tensor_close((store.grad[off:off + numel] * coef).view(shape), gref, 2e-3, 1e-8, f"{which} grad {n}",
+                          rtol_max=5e-3)
             delta = (store.data[off:off + numel] - before[off:off + numel]).view(shape)
             # first AdamW step: ~lr * sign(g) per element, so elements whose gradient is ~0 flip freely (|err| 2 lr,
             # e.g. the batch-summed modulation-weight gradients at B=2): the delta error is weighted by the oracle's
