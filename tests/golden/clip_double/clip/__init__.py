@@ -9,7 +9,7 @@ logged CLIP loss so that fixtures are reproducible.
 
 The double is a fixed random projection of a 4x4 average-pooled image
 (encode_image) and of a hashed token histogram (encode_text).  The same double
-is used by the build's tests (tests/test_losses.py) so the plumbing of the
+is used by the build's fixture generator (tests/golden/make_golden.py) so the plumbing of the
 CLIP-loss term is pinned; real CLIP values remain "parity unpinned".
 """
 import numpy as np
