@@ -1,0 +1,63 @@
+"""Step-level check of the C4 configuration's ingredients together, in the benchmarked precision: the progressive
+generator (here its 32x32 stage, so the CPU oracle stays cheap), 16 experts top-2, bf16, CLIP loss on, one full
+G+D step against the fp32 CPU oracle (oracle.train_step on the same blocks, same epsilon / z / permutation).
+
+The device's top-2 selections are replayed into the oracle (topk_route(idx=...)), as test_step_bf16_gpu.py does,
+and the CLIP terms use the same image-tower weights on both sides (the device's ClipImageEncoder, the oracle a
+plain fp32 torch ViT).  Bars (bf16; the bf16 C2 test measures why the generator's gradient
+cannot be held tighter than ~cosine 0.99 in bf16):
+  * discriminator / generator GAN losses, R1 and balance loss: relative error <= 2e-2;
+  * generated images (32x32 and the 16x16 intermediate): relative L2 <= 5e-2;
+  * CLIP loss values: |device - oracle| <= 1e-2 (a 1 - mean cosine in [0, 2]);
+  * discriminator whole-model clipped gradient cosine >= 0.999, generator >= 0.98.
+The progressive blocks themselves have no reference definition: this is parity against the oracle's composition of
+the reference's functions ("parity unpinned" against the reference).
+"""
+import pytest
+import torch
+
+from oracle import aurora_cpu as O
+from steputil import cosine, gpu_step, make_inputs, nchw, oracle_models, rel_norm_diff, whole
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+torch.set_num_threads(8)
+
+
+def test_c4_ingredients_bf16_step_vs_oracle():
+    from moegan_mi.clip_vit import ClipImageEncoder, random_state_dict
+    from test_clip_gpu import torch_vit
+    E, k, B, R = 16, 2, 4, 32
+    real, text, z, eps_d, eps_g, perm = make_inputs(B, E, seed=404, res=R)
+    sd = random_state_dict(768, 2, 32, 224, 512, seed=5)
+    ts = gpu_step(E, k, "bf16", DEV, max_res=R)
+    ts.clip_encoder = ClipImageEncoder(sd, device=DEV).encode_image
+    cu = lambda t: t.to(DEV)  # noqa: E731
+    out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d], [tuple(map(cu, e)) for e in eps_g],
+                  cu(perm.int()), anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8)
+    torch.cuda.synchronize()
+    assert int(out["flags"][0]) == 0
+    PG, PD, optG, optD, rgrads = oracle_models(E, max_res=R)
+    ref = O.train_step(PG, PD, optG, optD, real, text, z, eps_d, eps_g, perm, topk=k, kl_weight_eff=1e-8,
+                       encode_image=lambda im: torch_vit(sd, im, 12),
+                       routes_d=[t.cpu().long() for t in out["topi_d"]], routes_g=[t.cpu().long() for t in out["topi"]],
+                       full=True)
+    rel = lambda a, b: abs(a - b) / max(abs(b), 1e-6)  # noqa: E731
+    m = {"d_loss": rel(float(out["d_losses"][0]), ref["d_loss_gan"]), "r1": rel(float(out["r1"][0]), ref["r1"]),
+         "g_gan": rel(float(out["g_gan"][0]), ref["g_loss_gan"]),
+         "balance": rel(float(out["balance"][0]), ref["balance"]),
+         "img": rel_norm_diff(nchw(out["img16"]), ref["img16"]), "img_half": rel_norm_diff(nchw(out["img8"]), ref["img8"]),
+         "clip16": abs(float(out["clip16"][0]) - ref["clip16"]), "clip8": abs(float(out["clip8"][0]) - ref["clip8"])}
+    for which, store, max_norm in (("D", ts.ds, 0.7), ("G", ts.gs, 0.8)):
+        gn = float(store.grad[:store.n_opt].double().norm())
+        coef = min(1.0, max_norm / (gn + 1e-6))
+        names = sorted(n for n, g in rgrads[which].items() if g is not None)
+        dev_vec = torch.cat([(store.gview(n) * coef).reshape(-1).cpu() for n in names])
+        ref_vec, _ = whole(rgrads[which], names)
+        m[f"{which}_grad_cos"] = cosine(dev_vec, ref_vec)
+    print("C4 ingredients, bf16 step vs fp32 oracle:", {k_: round(v, 5) for k_, v in m.items()})
+    for key in ("d_loss", "r1", "g_gan", "balance"):
+        assert m[key] <= 2e-2, (key, m[key])
+    assert m["img"] <= 5e-2 and m["img_half"] <= 5e-2
+    assert m["clip16"] <= 1e-2 and m["clip8"] <= 1e-2
+    assert m["D_grad_cos"] >= 0.999 and m["G_grad_cos"] >= 0.98
