@@ -307,31 +307,45 @@ __global__ __launch_bounds__(256) void k_ln_bwd_v(const TG* __restrict__ gy, int
   for (int j = 0; j < 8; ++j) pg[j] = pb[j] = 0.f;
   const int w = blockIdx.x * (blockDim.x >> 6) + wv;
   const int rbeg = w * rows_per_wave, rend = min(R, rbeg + rows_per_wave);
-  for (int r0 = rbeg; r0 < rend; r0 += RPW) {
-    const int r = r0 + sl;
-    if (r < rend) {
-      const float mu = mean[r], rs = rstd[r];
-      float g[8], xh[8], gh[8];
-      ld8(gy + (int64_t)r * ldg + c, g);
-      ld8(x + (int64_t)r * ldx + c, xh);
-      float s1 = 0.f, s2 = 0.f;
+  // two row slots per lane group per iteration, both rows' loads issued before either is used (one wave per
+  // SIMD walked its rows load-to-use serially: ~30 us for 65536 rows of 128)
+  for (int r0 = rbeg; r0 < rend; r0 += 2 * RPW) {
+    float g[2][8], xh[2][8], o[2][8], mu[2], rs[2];
+    bool ok[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * RPW + sl;
+      ok[u] = r < rend;
+      mu[u] = rs[u] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[u][j] = xh[u][j] = o[u][j] = 0.f;
+      if (ok[u]) {
+        mu[u] = mean[r];
+        rs[u] = rstd[r];
+        ld8(gy + (int64_t)r * ldg + c, g[u]);
+        ld8(x + (int64_t)r * ldx + c, xh[u]);
+        if (gx && accumulate) ld8(gx + (int64_t)r * ldgx + c, o[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * RPW + sl;
+      float gh[8], s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        xh[j] = (xh[j] - mu) * rs;
-        gh[j] = g[j] * ga[j];
-        pg[j] += g[j] * xh[j];
-        pb[j] += g[j];
+        xh[u][j] = (xh[u][j] - mu[u]) * rs[u];
+        gh[j] = g[u][j] * ga[j];
+        pg[j] += g[u][j] * xh[u][j];
+        pb[j] += g[u][j];
         s1 += gh[j];
-        s2 += gh[j] * xh[j];
+        s2 += gh[j] * xh[u][j];
       }
-      s1 = row_sum<LPR>(s1) / C;
+      s1 = row_sum<LPR>(s1) / C;  // every lane of a row group takes part (row validity is uniform in it)
       s2 = row_sum<LPR>(s2) / C;
-      if (gx) {
-        float o[8];
-        if (accumulate) ld8(gx + (int64_t)r * ldgx + c, o);
+      if (gx && ok[u]) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rs * (gh[j] - s1 - xh[j] * s2) + (accumulate ? o[j] : 0.f);
-        st8(gx + (int64_t)r * ldgx + c, o);
+        for (int j = 0; j < 8; ++j) o[u][j] = rs[u] * (gh[j] - s1 - xh[u][j] * s2) + (accumulate ? o[u][j] : 0.f);
+        st8(gx + (int64_t)r * ldgx + c, o[u]);
       }
     }
   }
@@ -404,8 +418,10 @@ extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t
       mg_al16(gamma)) {
     // ~1024 waves; each walks a multiple of the rows it covers at once
     const int lpr = C / 8, rw = 64 / lpr;
-    int rows = std::max(rw, cdiv(R, 1024));
-    rows = cdiv(rows, rw) * rw;
+    // ~1024 waves (more blocks measured slower at C = 256 / 512: each adds 2C same-address atomics for
+    // ggamma / gbeta), two row slots per iteration
+    int rows = std::max(2 * rw, cdiv(R, 1024));
+    rows = cdiv(rows, 2 * rw) * 2 * rw;
     dim3 g2(cdiv(cdiv(R, rows), 4)), b2(256);
 #define LV_(T, TG, P) hipLaunchKernelGGL((k_ln_bwd_v<T, TG, P>), g2, b2, 0, st, (const TG*)gy, ldg, (const T*)x, ldx, R, \
                                          mean, rstd, gamma, (T*)gx, ldgx, accumulate, ggamma, gbeta, rows)

@@ -92,7 +92,44 @@ __global__ __launch_bounds__(256) void k_bwd_out_v(const TG* __restrict__ gz, in
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (live) ld8(d + (int64_t)b * Cout + o, dd);
-  for (int p = ty; live && p < HW; p += TY) {
+  // two pixels per iteration with both loads in flight (one block per image: latency-bound otherwise)
+  int p = ty;
+  for (; live && p + TY < HW; p += 2 * TY) {
+    const int64_t r0 = (int64_t)b * HW + p, r1 = r0 + TY;
+    float g1[8], z1[8], t1[8];
+    ld8(gz + r0 * ld_gz + o, g);
+    ld8(gz + r1 * ld_gz + o, g1);
+    ld8(z + r0 * ld_z + o, zz);
+    ld8(z + r1 * ld_z + o, z1);
+    if (zsub) {
+      ld8(zsub + r0 * ld_zsub + o, t);
+      ld8(zsub + r1 * ld_zsub + o, t1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        zz[j] -= t[j];
+        z1[j] -= t1[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float y = zz[j], y1 = z1[j];
+      if (act && zz[j] <= 0.f) {
+        y = zz[j] * 5.f;
+        g[j] *= 0.2f;
+      }
+      if (act && z1[j] <= 0.f) {
+        y1 = z1[j] * 5.f;
+        g1[j] *= 0.2f;
+      }
+      acc[j] += g[j] * y;
+      acc[j] += g1[j] * y1;
+      t[j] = g[j] * dd[j];
+      t1[j] = g1[j] * dd[j];
+    }
+    st8(gyt + r0 * ld_gyt + o, t);
+    st8(gyt + r1 * ld_gyt + o, t1);
+  }
+  for (; live && p < HW; p += TY) {
     int64_t row = (int64_t)b * HW + p;
     ld8(gz + row * ld_gz + o, g);
     ld8(z + row * ld_z + o, zz);
@@ -141,7 +178,35 @@ __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, in
   if (live) ld8(s + (int64_t)b * ld_s + c, sc);
   // pixels split over grid.z (more blocks in flight for few images x large maps)
   const int ppz = (HW + gridDim.z - 1) / gridDim.z, p1 = min(HW, ((int)blockIdx.z + 1) * ppz);
-  for (int p = blockIdx.z * ppz + ty; live && p < p1; p += TY) {
+  // two pixels per iteration, all their loads issued before either is used (latency, not bandwidth, bounded
+  // the one-pixel loop)
+  int p = blockIdx.z * ppz + ty;
+  for (; live && p + TY < p1; p += 2 * TY) {
+    const int64_t r0 = (int64_t)b * HW + p, r1 = r0 + TY;
+    float g1[8], x1[8], t1[8];
+    ld8(gxt + r0 * ld_gxt + c, g);
+    ld8(gxt + r1 * ld_gxt + c, g1);
+    ld8(x + r0 * ld_x + c, xx);
+    ld8(x + r1 * ld_x + c, x1);
+    if (gx && accumulate) {
+      ld8(gx + r0 * ld_gx + c, t);
+      ld8(gx + r1 * ld_gx + c, t1);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += g[j] * xx[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += g1[j] * x1[j];
+    if (gx) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        t[j] = g[j] * sc[j] + (accumulate ? t[j] : 0.f);
+        t1[j] = g1[j] * sc[j] + (accumulate ? t1[j] : 0.f);
+      }
+      st8(gx + r0 * ld_gx + c, t);
+      st8(gx + r1 * ld_gx + c, t1);
+    }
+  }
+  for (; live && p < p1; p += TY) {
     int64_t row = (int64_t)b * HW + p;
     ld8(gxt + row * ld_gxt + c, g);
     ld8(x + row * ld_x + c, xx);

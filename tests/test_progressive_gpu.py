@@ -6,8 +6,8 @@ create_optimizer_for_active_blocks, t2i_moe_gan.py:1005-1026), so the block list
 same pinned reference functions (upsample :657, ConvolutionBlock :604-621 with MTMs that have no offset head
 above 16x16, :199, ModulatedConv to_rgb :154-186), the oracle in plain fp32 PyTorch autograd
 (oracle/aurora_cpu.generator), the device through the HIP engines.  Bars are the fp32 ones of F7 / F8: 1e-4 relative on values, 1e-3 on the
-generator's gradients for a given upstream gradient; for the full step 5e-3 relative L2 per gradient tensor and
-2e-2 on |g|-weighted AdamW deltas.
+generator's gradients for a given upstream gradient; for the full step 2e-3 relative L2 per gradient tensor
+(1e-2 for the batch-summed style (modulation) parameters) and 2e-2 on |g|-weighted AdamW deltas.
 """
 import pytest
 import torch
@@ -127,10 +127,12 @@ def test_progressive_train_step_r32():
                 assert off >= store.n_opt, n  # frozen tail: never stepped
                 assert torch.equal(store.data[off:off + numel], before[off:off + numel]), n
                 continue
-            # 5e-3: the 32x32 step's batch-summed modulation-weight gradients carry the fp32 reordering noise of the
-            # whole backward (measured up to 3.2e-3 relative L2; every other tensor < 1e-3)
-            _tensor_close((store.grad[off:off + numel] * coef).view(shape), gref, 5e-3, 1e-8, f"{which} grad {n}",
-                          rtol_max=1e-2)
+            # the 32x32 step's batch-summed modulation-weight gradients (sums over images of per-image style
+            # gradients that largely cancel) carry the fp32 reordering noise of the whole backward: measured
+            # 3e-3 .. 5e-3 relative L2 as kernel summation orders change; every other tensor stays < 1e-3
+            tol = 1e-2 if ".modulation." in n else 2e-3
+            _tensor_close((store.grad[off:off + numel] * coef).view(shape), gref, tol, 1e-8, f"{which} grad {n}",
+                          rtol_max=2 * tol)
             delta = (store.data[off:off + numel] - before[off:off + numel]).view(shape)
             # first AdamW step: ~lr * sign(g) per element, so elements whose gradient is ~0 flip freely (|err| 2 lr,
             # e.g. the batch-summed modulation-weight gradients at B=2): the delta error is weighted by the oracle's
