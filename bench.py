@@ -44,6 +44,9 @@ def parse():
                          "configs[4]: 32 experts top-4, MX-fp8 3x3 modulated convs")
     ap.add_argument("--fp8", action="store_true", help="MX-fp8 3x3 modulated convs (implied by --config C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--secondary", default="C5,C4",
+                    help="comma-separated configs measured after the headline one, each in a child bench.py process "
+                         "(N=1 only), reported under 'secondary' in the same JSON line; '' to skip")
     ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU-oracle steps (B=8; ~10-20 s of CPU work)")
     ap.add_argument("--time-kernel", default="d_conv1",
                     help="kernel whose launches are timed with HIP events for the roofline field")
@@ -115,6 +118,27 @@ def cpu_baseline(args, E, k):
     return {"value": round(B * n / dt, 3), "unit": "images/sec", "cores": torch.get_num_threads(),
             "kind": "port", "sample": f"oracle/aurora_cpu.train_step, B={B}, E={E} top-{k}, fp32, "
                                       f"{n} timed steps after 1 warm-up"}
+
+
+def run_secondary(cfg, args):
+    """Measure another BASELINE config (e.g. C5's single-GPU slice) in a child process -- its own GPU context,
+    graphs and memory -- and return its JSON line (the headline line above stays C2)."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--config", cfg, "--steps", str(max(5, args.steps)),
+           "--warmup", str(args.warmup), "--no-cpu-baseline", "--secondary", ""]
+    if cfg != "C4":  # C4's FLOP count comes from the per-call attribution pass (no reference formula)
+        cmd.append("--no-families")
+    print(f"[bench] secondary config {cfg}: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"config": cfg, "error": f"rc={r.returncode}: {r.stderr[-400:]}"}
+        rec = json.loads(lines[-1])
+        return {k: rec.get(k) for k in ("metric", "value", "unit", "ms_per_step", "dtype", "config",
+                                         "step_tflops_algorithmic", "step_mfma_frac", "roofline")}
+    except Exception as e:  # a report, never the headline value
+        return {"config": cfg, "error": repr(e)}
 
 
 def main():
@@ -317,6 +341,10 @@ def main():
                 cpu = {"error": repr(e)}
         metric = ("images/sec (G+D step, 64x64 MS-COCO layout)" if args.res == 64 else
                   f"images/sec (G+D step, {args.res}x{args.res} progressive stage)")
+        secondary = []
+        if world == 1 and args.config == "C2" and args.secondary:
+            for cfg in [c for c in args.secondary.split(",") if c and c != args.config]:
+                secondary.append(run_secondary(cfg, args))
         line = {"metric": metric, "value": round(value, 2),
                 "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -334,7 +362,7 @@ def main():
                 "step_tflops_algorithmic": round(step_tflops, 2),
                 "step_mfma_frac": round(step_tflops / peak, 4), "finite": finite,
                 "roofline": roof, "roofline_families": families,
-                "roofline_families_sources": fam_meta, "cpu_baseline": cpu}
+                "roofline_families_sources": fam_meta, "cpu_baseline": cpu, "secondary": secondary or None}
         print(json.dumps(line), flush=True)
     if pg is not None:
         torch.distributed.destroy_process_group()
