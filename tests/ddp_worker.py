@@ -4,7 +4,7 @@ import os
 import sys
 
 
-def run(rank, world, port, out_dir, B, E):
+def run(rank, world, port, out_dir, B, E, R=16):
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
     for p in (here, repo, os.path.join(repo, "moe-gan_cpsc541_amd")):
@@ -17,10 +17,10 @@ def run(rank, world, port, out_dir, B, E):
     from steputil import gpu_step, make_inputs
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        real, text, z, eps_d, eps_g, perm = make_inputs(B * world, E, seed=7)
+        real, text, z, eps_d, eps_g, perm = make_inputs(B * world, E, seed=7, res=64 if R == 16 else R)
         sl = slice(rank * B, (rank + 1) * B)
         local_perm = torch.randperm(B, generator=torch.Generator().manual_seed(100 + rank))
-        ts = gpu_step(E, None, "fp32", "cuda:0")
+        ts = gpu_step(E, None, "fp32", "cuda:0", max_res=R)
         ts.pg, ts.world = dist.group.WORLD, world
         cu = lambda t: t.to("cuda:0")  # noqa: E731
         out = ts.step(cu(real[sl].contiguous()), cu(text[sl].contiguous()), cu(z[sl].contiguous()),

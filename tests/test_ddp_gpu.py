@@ -25,13 +25,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_two_rank_trainstep_matches_single_process(tmp_path):
+@pytest.mark.parametrize("R", [16, 32])
+def test_two_rank_trainstep_matches_single_process(tmp_path, R):
+    """R = 16: the reference generator; R = 32: the progressive extension (32x32 real and fake images, several
+    fake logits per image in the D / G losses)."""
     import torch.multiprocessing as mp
     from ddp_worker import run
     world, B, E = 2, 2, 4
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=run, args=(r, world, port, str(tmp_path), B, E)) for r in range(world)]
+    procs = [ctx.Process(target=run, args=(r, world, port, str(tmp_path), B, E, R)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -42,9 +45,9 @@ def test_two_rank_trainstep_matches_single_process(tmp_path):
         assert p.exitcode == 0, p.exitcode
     res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
     # single process, whole batch, block-diagonal permutation
-    real, text, z, eps_d, eps_g, _ = make_inputs(B * world, E, seed=7)
+    real, text, z, eps_d, eps_g, _ = make_inputs(B * world, E, seed=7, res=64 if R == 16 else R)
     perm = torch.cat([res[r]["local_perm"] + r * B for r in range(world)])
-    ts = gpu_step(E, None, "fp32", "cuda")
+    ts = gpu_step(E, None, "fp32", "cuda", max_res=R)
     cu = lambda t: t.to("cuda")  # noqa: E731
     out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d], [tuple(map(cu, e)) for e in eps_g],
                   cu(perm.int()), anneal=3.0, eff_kl_weight=0.001 * 1e-5)
