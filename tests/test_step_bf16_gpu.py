@@ -14,7 +14,8 @@ Bar, written per check below (SURVEY.md §8(c) asks 2e-2 on outputs and cosine >
     discriminator's input image and weights already moves it by ~5 % (cosine 0.9989), and the R1 input
     gradient by ~4 % (steputil.bf16_r1_floor) -- and the device sits at 1.5-2x that floor.  SURVEY §8(c)'s
     per-tensor 0.999 is therefore not reachable in bf16 at all; per-tensor parity at 1e-3 is the fp32 mode's
-    job (F7 / F8 / F10 in test_engine_gpu.py).  Each tensor's error and floor are printed;
+    job (F7 / F8 / F10 in test_engine_gpu.py).  Each tensor's error and floor are printed (a tensor whose own floor
+    is >= 20 % -- an expert few tokens reach at this batch -- is held to FLOOR_X x its floor instead of the cosine);
   * top-k expert selection: the device picks a top-k of its own probabilities; its sets equal the oracle's own
     fp32 top-k wherever the oracle margin log(p_(k)/p_(k+1)) exceeds DELTA, DELTA bounds the measured drift of
     that margin, flips stay below 10 % of tokens; the oracle then replays the device's selection
@@ -213,7 +214,10 @@ def _run(E, topk, inputs_per_step, lr=2e-4):
                 c, rn = cosine(g, rg), rel_norm_diff(g, rg)
                 fl = rel_norm_diff(fgrads[which][n], rg)
                 worst.append((c, rn, fl, which + ":" + n))
-                check(c >= COS_TENSOR, f"step{si} grad {which}:{n} cosine {c:.6f} rel {rn:.2e} (floor {fl:.2e})")
+                # direction bar per tensor; a tensor whose own bf16 floor is already >= 20 % (an expert that few
+                # tokens reach at a test-sized batch) is held to FLOOR_X x its floor instead
+                check(c >= COS_TENSOR or (fl >= 0.2 and rn <= FLOOR_X * fl),
+                      f"step{si} grad {which}:{n} cosine {c:.6f} rel {rn:.2e} (floor {fl:.2e})")
                 dd = (store.data[off:off + numel] - before[off:off + numel]).cpu()
                 rd = ((pd_stepped[n] if which == "D" else P[n].detach()) - pbefore[n]).reshape(-1)
                 w = rg.reshape(-1).abs()
