@@ -134,8 +134,10 @@ def test_progressive_train_step_r32():
             # (modulation, offset heads) relative L2 as kernel
             # summation orders change.  The generator's own fwd/bwd above is held at 1e-3 per element.
             tol = 2e-3 if which == "D" else (1e-2 if (".modulation." in n or ".offset_net." in n) else 5e-3)
+            # (a single flipped pre-activation moves the 9 x Cin weight entries it touches by up to ~1 % of the
+            # tensor's scale at B = 2: the max-abs bar is 4x the L2 one)
             _tensor_close((store.grad[off:off + numel] * coef).view(shape), gref, tol, 1e-8, f"{which} grad {n}",
-                          rtol_max=2 * tol)
+                          rtol_max=4 * tol)
             delta = (store.data[off:off + numel] - before[off:off + numel]).view(shape)
             # first AdamW step: ~lr * sign(g) per element, so elements whose gradient is ~0 flip freely (|err| 2 lr,
             # e.g. the batch-summed modulation-weight gradients at B=2): the delta error is weighted by the oracle's
