@@ -82,12 +82,46 @@ MG_DEV void prep_elem(const mg_prep_desc& q, int64_t i) {
   }
 }
 
+// Flipped pack through an LDS tile: (16 input channels x 32 output channels x taps) per block.  The item form
+// read W[o][ci][*] with o varying across lanes (a stride of Cin * taps floats: every lane its own cache line);
+// here each output channel's 16 x taps floats are read as one contiguous run and the flipped rows are written
+// 32 output channels (64 B of bf16) at a time.
+constexpr int kFlipTC = 16, kFlipTO = 32, kFlipMaxTaps = 9;
+__host__ __device__ inline bool flip_tiled(const mg_prep_desc& q) { return q.kind == MG_PREP_PACK_FLIP && q.KH * q.KW <= kFlipMaxTaps; }
+
+template <typename T>
+MG_DEV void flip_tile(const mg_prep_desc& q, int lb) {
+  __shared__ float sm[kFlipTC][kFlipMaxTaps][kFlipTO + 1];
+  const int taps = q.KH * q.KW;
+  const int nto = (q.Cout + kFlipTO - 1) / kFlipTO;
+  const int ci0 = (lb / nto) * kFlipTC, o0 = (lb % nto) * kFlipTO;
+  const int run = kFlipTC * taps;  // contiguous floats of W[o][ci0 ..][*]
+  for (int e = threadIdx.x; e < kFlipTO * run; e += kPrepThreads) {
+    const int oo = e / run, r = e - oo * run;
+    const int cc = r / taps, t = r - cc * taps;
+    const int o = o0 + oo, ci = ci0 + cc;
+    sm[cc][t][oo] = (o < q.Cout && ci < q.Cin) ? q.W[((int64_t)o * q.Cin + ci) * taps + t] : 0.f;
+  }
+  __syncthreads();
+  T* out = reinterpret_cast<T*>(q.out);
+  for (int e = threadIdx.x; e < kFlipTC * taps * kFlipTO; e += kPrepThreads) {
+    const int oo = e % kFlipTO, r = e / kFlipTO;
+    const int cc = r / taps, tt = r - cc * taps;  // tt = flipped tap position in the output
+    const int o = o0 + oo, ci = ci0 + cc;
+    if (o < q.Cout && ci < q.rows) stf(out, ((int64_t)ci * taps + tt) * q.Cout + o, sm[cc][taps - 1 - tt][oo]);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kPrepThreads) void k_prep_batch(PrepArgs a) {
   const int b = blockIdx.x;
   int p = 0;
   while (p + 1 < a.n && b >= a.block_off[p + 1]) ++p;
   const mg_prep_desc& q = a.d[p];
+  if (flip_tiled(q)) {
+    flip_tile<T>(q, b - a.block_off[p]);
+    return;
+  }
   const int64_t base = (int64_t)(b - a.block_off[p]) * kPrepThreads * kPrepIlp + threadIdx.x;
 #pragma unroll
   for (int j = 0; j < kPrepIlp; ++j) {
@@ -210,7 +244,8 @@ extern "C" int mg_prep_batch(int dtype, int n, const mg_prep_desc* descs, void* 
       if (cnt == 0) continue;
       a.d[a.n] = q;
       a.block_off[a.n] = blocks;
-      blocks += (int)((cnt + kPrepThreads * kPrepIlp - 1) / (kPrepThreads * kPrepIlp));
+      blocks += flip_tiled(q) ? ((q.rows + kFlipTC - 1) / kFlipTC) * ((q.Cout + kFlipTO - 1) / kFlipTO)
+                              : (int)((cnt + kPrepThreads * kPrepIlp - 1) / (kPrepThreads * kPrepIlp));
       ++a.n;
     }
     a.block_off[a.n] = blocks;
