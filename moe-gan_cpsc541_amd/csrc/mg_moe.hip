@@ -377,15 +377,26 @@ __global__ __launch_bounds__(256) void k_token_grad_v(const T* __restrict__ gX, 
 template <typename T, typename TG>
 __global__ void k_gate_grad(const TG* __restrict__ gout, int64_t ldg, const T* __restrict__ Y, int64_t ldy,
                             const int* __restrict__ pos_of, int n, int k, int C, float* __restrict__ g_gate) {
-  int a = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  int lane = threadIdx.x & 63;
-  if (a >= n) return;
-  int t = a / k;
-  int64_t pr = (int64_t)pos_of[a] * ldy;
+  // 8 lanes per assignment with 16-B vectors (one wave per assignment issued 2-byte loads and spent most of
+  // its time launching: 131072 waves for the 16x16 block)
+  const int a = blockIdx.x * (blockDim.x >> 3) + (threadIdx.x >> 3), tl = threadIdx.x & 7;
+  const bool ok = a < n;
   float s = 0.f;
-  for (int c = lane; c < C; c += 64) s += ldf(gout, (int64_t)t * ldg + c) * ldf(Y, pr + c);
-  s = wave_sum(s);
-  if (lane == 0) g_gate[a] = s;
+  if (ok) {
+    const int t = a / k;
+    const int64_t pr = (int64_t)pos_of[a] * ldy, pg = (int64_t)t * ldg;
+    for (int c = tl * 8; c < C; c += 64) {
+      float g[8], y[8];
+      ld8(gout + pg + c, g);
+      ld8(Y + pr + c, y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += g[j] * y[j];
+    }
+  }
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (ok && tl == 0) g_gate[a] = s;
 }
 
 // per-token router backward: (g_gate, balance coefficients) -> g_raw [T, E]
@@ -555,12 +566,85 @@ __global__ void k_router_feat_grad(const T* __restrict__ tok, int64_t ld, int Tn
   }
 }
 
-// out[i] += sum_r part[r * n + i]: 64 columns x 16 row lanes per block, LDS fold
-__global__ __launch_bounds__(1024) void k_feat_grad_fin(const float* __restrict__ part, int nparts, int n,
-                                                        float* __restrict__ out) {
-  __shared__ float red[16][64];
-  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + cx;
+// Vector form: a block is TX = C / CV channel lanes (CV channels each, 16-B loads for CV = 8 bf16) x TY = 256 / TX
+// token lanes walking its token chunk; the token lanes of a wave fold with shuffles and each wave-row group
+// writes one partial row [C * E] (k_feat_grad_fin folds them).  The thread-per-channel form issued 2-byte loads
+// one token at a time (35 us for 65536 tokens x 128 channels).
+template <typename T, int E, int CV>
+__global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict__ tok, int64_t ld, int Tn, int C,
+                                                            const float* __restrict__ g_raw, int chunk,
+                                                            float* __restrict__ part) {
+  const int TX = C / CV, TY = 256 / TX;
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  const int c = tx * CV;
+  const int t0 = blockIdx.x * chunk, t1 = min(Tn, t0 + chunk);
+  float acc[CV][E];
+#pragma unroll
+  for (int j = 0; j < CV; ++j)
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[j][e] = 0.f;
+  for (int t = t0 + ty; t < t1; t += TY) {
+    float x[CV];
+    if constexpr (CV == 8) {
+      ld8(tok + (int64_t)t * ld + c, x);
+    } else {
+#pragma unroll
+      for (int j = 0; j < CV; ++j) x[j] = ldf(tok, (int64_t)t * ld + c + j);
+    }
+    float gv[E];  // the token's E raw-logit gradients as 16-B loads (rows are 16-B aligned: E % 4 == 0)
+#pragma unroll
+    for (int e = 0; e < E; e += 4) {
+      const f32x4_t q = *reinterpret_cast<const f32x4_t*>(g_raw + (int64_t)t * E + e);
+      gv[e] = q[0];
+      gv[e + 1] = q[1];
+      gv[e + 2] = q[2];
+      gv[e + 3] = q[3];
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int j = 0; j < CV; ++j) acc[j][e] += x[j] * gv[e];
+  }
+  const int tyw = TX < 64 ? 64 / TX : 1;  // token lanes per wave
+  for (int o = TX; o < 64; o <<= 1)
+#pragma unroll
+    for (int j = 0; j < CV; ++j)
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[j][e] += __shfl_xor(acc[j][e], o, 64);
+  const int R = TY / tyw;  // partial rows of this block (one per wave-row group)
+  if (R > 1 && (int64_t)R * C * E <= 8192) {  // fold them in LDS (fixed order): one row per block
+    __shared__ float red[8192];
+    if (ty % tyw == 0) {
+#pragma unroll
+      for (int j = 0; j < CV; ++j)
+#pragma unroll
+        for (int e = 0; e < E; ++e) red[(ty / tyw) * C * E + (c + j) * E + e] = acc[j][e];
+    }
+    __syncthreads();
+    float* pr = part + (int64_t)blockIdx.x * C * E;
+    for (int i = threadIdx.x; i < C * E; i += 256) {
+      float v = 0.f;
+      for (int r = 0; r < R; ++r) v += red[r * C * E + i];
+      pr[i] = v;
+    }
+    return;
+  }
+  if (ty % tyw == 0) {
+    float* pr = part + ((int64_t)blockIdx.x * R + ty / tyw) * C * E + (int64_t)c * E;
+#pragma unroll
+    for (int j = 0; j < CV; ++j)
+#pragma unroll
+      for (int e = 0; e < E; ++e) pr[j * E + e] = acc[j][e];
+  }
+}
+
+// out[i] += sum_r part[r * n + i]: 16 columns x 16 row lanes per block (n / 16 blocks: the partial rows of a
+// few-column gradient still spread over the chip), LDS fold in row order
+__global__ __launch_bounds__(256) void k_feat_grad_fin(const float* __restrict__ part, int nparts, int n,
+                                                       float* __restrict__ out) {
+  __shared__ float red[16][16];
+  const int cx = threadIdx.x & 15, ry = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + cx;
   float s = 0.f;
   if (i < n)
     for (int r = ry; r < nparts; r += 16) s += part[(int64_t)r * n + i];
@@ -907,7 +991,9 @@ extern "C" int mg_moe_gate_grad(int dtype, int gout_dtype, const void* gout, int
                                 const int32_t* pos_of, int T, int k, int C, float* g_gate, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int n = T * k;
-  dim3 grid(cdiv(n, 4));
+  MG_REQUIRE(C % 8 == 0 && ldg % 8 == 0 && ldy % 8 == 0 && mg_al16(gout) && mg_al16(Y),
+             "mg_moe_gate_grad: C and row pitches multiples of 8, 16-B aligned rows");
+  dim3 grid(cdiv(n, 32));  // 32 assignments (8 lanes each) per block
 #define L_(TT, TG) hipLaunchKernelGGL((k_gate_grad<TT, TG>), grid, dim3(256), 0, st, (const TG*)gout, ldg, (const TT*)Y, ldy, pos_of, n, k, C, g_gate)
   if (dtype == MG_F32) { if (gout_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
   else { if (gout_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
@@ -963,6 +1049,29 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
   MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
   MG_REQUIRE(C <= 512, "C <= 512");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int CV = E <= 8 ? 8 : (E == 16 ? 4 : 2);
+  if (C % CV == 0 && C / CV <= 256 && (256 % (C / CV)) == 0 && ld % 8 == 0 && mg_al16(tok) && mg_al16(g_raw) &&
+      T > 0) {
+    const int TX = C / CV, TY = 256 / TX, R = TY / (TX < 64 ? 64 / TX : 1);
+    const int rows_per_block = (R > 1 && (int64_t)R * C * E <= 8192) ? 1 : R;  // in-block LDS fold (kernel)
+    int chunk = std::max(TY, (T / 256 + TY - 1) / TY * TY);  // ~256 blocks ...
+    const int64_t row = (int64_t)rows_per_block * C * E;      // ... with at most 1 M floats of partial rows
+    const int64_t min_chunk = ((int64_t)T * row / (1 << 20) + TY - 1) / TY * TY;
+    if (min_chunk > chunk) chunk = (int)min_chunk;
+    const int nb = cdiv(T, chunk);
+    float* part = reinterpret_cast<float*>(mg_workspace((size_t)nb * rows_per_block * C * E * sizeof(float), st));
+    MG_REQUIRE(part != nullptr, "mg_router_feat_grad: no workspace");
+#define LV_(TT, EE, CC) hipLaunchKernelGGL((k_router_feat_grad_v<TT, EE, CC>), dim3(nb), dim3(256), 0, st, (const TT*)tok, \
+                                           ld, T, C, g_raw, chunk, part)
+#define LVE_(TT) if (E == 4) LV_(TT, 4, 8); else if (E == 8) LV_(TT, 8, 8); else if (E == 16) LV_(TT, 16, 4); \
+                 else LV_(TT, 32, 2)
+    if (dtype == MG_F32) { LVE_(float); } else { LVE_(bf16_t); }
+#undef LVE_
+#undef LV_
+    hipLaunchKernelGGL(k_feat_grad_fin, dim3(cdiv(C * E, 16)), dim3(256), 0, st, part, nb * rows_per_block, C * E,
+                       G1);
+    return mg_check_launch("mg_router_feat_grad");
+  }
   // ~512 blocks (a 64-token step per LDS refill); per-block partial rows folded by k_feat_grad_fin
   int chunk = std::max(64, std::min(256, (T / 512) / 64 * 64));
   dim3 grid(cdiv(T, chunk));
@@ -973,7 +1082,7 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
   if (dtype == MG_F32) { LE_(float); } else { LE_(bf16_t); }
 #undef LE_
 #undef L_
-  if (part) hipLaunchKernelGGL(k_feat_grad_fin, dim3(cdiv(C * E, 64)), dim3(1024), 0, st, part, (int)grid.x, C * E, G1);
+  if (part) hipLaunchKernelGGL(k_feat_grad_fin, dim3(cdiv(C * E, 16)), dim3(256), 0, st, part, (int)grid.x, C * E, G1);
   return mg_check_launch("mg_router_feat_grad");
 }
 
