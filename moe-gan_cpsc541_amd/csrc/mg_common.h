@@ -104,7 +104,8 @@ int mg_check_launch(const char* what);
 // Tuning overrides (0 = automatic), set through mg_set_tuning for A/B measurements.
 enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, MG_TUNE_GEMM_TILE = 3,
        MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_XCD = 6, MG_TUNE_WGRAD_MODE = 7,
-       MG_TUNE_WARP_LDS = 8, MG_TUNE_SHORTK = 9, MG_TUNE_COUNT = 16 };
+       MG_TUNE_WARP_LDS = 8, MG_TUNE_SHORTK = 9, MG_TUNE_ATOMIC_BLOCKS = 10,
+       MG_TUNE_COUNT = 16 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 // Device scratch, one block per (device, stream): caller-owned (mg_set_workspace) or library-owned
 // (grown on demand, never shrunk).  NULL when it cannot be provided (mg_last_error says why).

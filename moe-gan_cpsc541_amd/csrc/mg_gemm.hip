@@ -147,7 +147,8 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
   if (splits < 1) {  // auto split-K (atomic fp32 epilogues only): ~512 blocks, >= 256 of K per split
     if (ep && ep->atomic) {
       int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
-      int64_t want = std::max<int64_t>(1, 512 / std::max<int64_t>(tiles, 1));
+      const int target = g_mg_tune[MG_TUNE_ATOMIC_BLOCKS] > 0 ? (int)g_mg_tune[MG_TUNE_ATOMIC_BLOCKS] : 512;
+      int64_t want = std::max<int64_t>(1, target / std::max<int64_t>(tiles, 1));
       splits = (int)std::max<int64_t>(1, std::min<int64_t>(want, K / 256));
     } else {
       splits = 1;
