@@ -131,31 +131,35 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
-        for (int fn = 0; fn < 2; ++fn)
-          acc1[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fm], b[fn], acc1[fm][fn], 0, 0, 0);
+        for (int fn = 0; fn < 2; ++fn)  // transposed product: lane holds 4 consecutive hidden units of one row
+          acc1[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[fn], a[fm], acc1[fm][fn], 0, 0, 0);
     }
     // ---- + b1, pre-activation / GELU out (when saved), bf16 GELU -> hs.  The previous chunk's GEMM2 finished
-    // reading hs before the barriers at the top of this chunk. ----
+    // reading hs before the barriers at the top of this chunk.  acc1[fm][fn][j] = hidden unit
+    // wn*32 + fn*16 + 4*(lane>>4) + j of row wm*32 + fm*16 + (lane&15): four consecutive hidden units per lane, so
+    // the bias is one 16-B load and every store (LDS image, saved tensors) is one 8-B run. ----
     // 32-bit element offsets from the tile's first row (128 rows x Hd fit easily)
     const int nrows = rend - r0;
 #pragma unroll
     for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
       for (int fn = 0; fn < 2; ++fn) {
-        const int col = wn * 32 + fn * 16 + fr;
-        const float bias = b1g[h0 + col];
+        const int row = wm * 32 + fm * 16 + fr;
+        const int col = wn * 32 + fn * 16 + 4 * (lane >> 4);
+        const f32x4_t bias = *reinterpret_cast<const f32x4_t*>(b1g + h0 + col);
+        u16x4_t pv, gv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int row = wm * 32 + fm * 16 + 4 * (lane >> 4) + j;
-          const float v = acc1[fm][fn][j] + bias;
-          const float gl = gelu_fast(v);
-          if (row < nrows) {
-            const int o = row * Hd + h0 + col;
-            if (Pre) preb[o] = f2bf(v);
-            if (Hid) hidb[o] = f2bf(gl);
-          }
-          sm.hs[kci<FBM>(row, col)] = f2bf(gl);
+          const float v = acc1[fm][fn][j] + bias[j];
+          pv[j] = __builtin_bit_cast(unsigned short, f2bf(v));
+          gv[j] = __builtin_bit_cast(unsigned short, f2bf(gelu_fast(v)));
         }
+        if (row < nrows) {
+          const int o = row * Hd + h0 + col;
+          if (Pre) *reinterpret_cast<u16x4_t*>(preb + o) = pv;
+          if (Hid) *reinterpret_cast<u16x4_t*>(hidb + o) = gv;
+        }
+        *reinterpret_cast<u16x4_t*>(sm.hs + kci<FBM>(row, col)) = gv;
       }
     __syncthreads();
     // ---- GEMM2: out[128 x C] += hs[128 x 64] . W2c[C x 64]^T; wave (wm, wn): rows wm*32, cols wn*C/2 ----
@@ -207,8 +211,9 @@ extern "C" int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngro
   MG_REQUIRE(C == 128 || C == 256, "C must be 128 or 256");
   MG_REQUIRE(Hd > 0 && Hd % FHC == 0, "Hd must be a multiple of 64");
   MG_REQUIRE(ngroups >= 1 && ngroups <= 64, "1 <= ngroups <= 64");
-  MG_REQUIRE(ldx % 8 == 0 && mg_al16(X) && mg_al16(W1) && mg_al16(W2) && mg_al16(Y) && mg_al16(pre) && mg_al16(hid),
-             "operands must be 16-byte aligned, ldx a multiple of 8");
+  MG_REQUIRE(ldx % 8 == 0 && mg_al16(X) && mg_al16(W1) && mg_al16(W2) && mg_al16(Y) && mg_al16(pre) && mg_al16(hid) &&
+                 mg_al16(b1),
+             "operands (and b1) must be 16-byte aligned, ldx a multiple of 8");
   MG_REQUIRE(x_idx_div >= 1, "x_idx_div >= 1");
   MG_REQUIRE(total_rows >= 0 && max_tiles >= (total_rows + FBM - 1) / FBM, "max_tiles below the row tiles");
   if (max_tiles <= 0 || total_rows == 0) return MG_OK;
