@@ -2,12 +2,15 @@
 // expert's dispatched tokens, Y = GELU(X W1^T + b1) W2^T + b2 with the hidden activation kept on chip.
 //
 // The hidden dimension (Hd = 4C) is walked in 64-unit chunks: GEMM1 (X tile [128 x C] from LDS, resident for the
-// whole block, times the chunk's W1 rows) -> + b1 and GELU in registers (the pre-activation / GELU output go to
-// HBM straight from the accumulator layout, only when the backward needs them; L2 merges the row pieces into
-// whole lines) -> bf16 GELU output to LDS -> GEMM2 accumulates the chunk's contribution into the [128 x C]
-// output held in registers.  The next chunk's W1 / W2 slices are prefetched into registers during the current
-// chunk.  LDS is 80 KiB at C = 128, so two blocks (16 waves) share a CU and hide each other's barriers.  The unfused path (two grouped GEMMs) writes and re-reads
-// the [rows x 4C] hidden activation; here a no-grad forward moves only X in and Y out.
+// whole block, times the chunk's W1 rows, issued as W1 . X^T so each lane's accumulator holds four consecutive
+// hidden units of one row) -> + b1 (one 16-B load) and GELU in registers (the pre-activation / GELU output go to
+// HBM as 8-B runs straight from the accumulator layout, only when the backward needs them) -> bf16 GELU output to
+// LDS (8-B stores) -> GEMM2 accumulates the chunk's contribution into the [128 x C] output held in registers.
+// The kernel is VALU-issue bound (GELU ~70 cycles per element vs 16 per 16x16x32 MFMA); a register prefetch of
+// the next chunk's weights measured slower (113 -> 121 us), so the other block on the CU covers those loads.
+// LDS is 80 KiB at C = 128, so two blocks (16 waves) share a CU and hide each other's barriers.  The unfused path
+// (two grouped GEMMs) writes and re-reads the [rows x 4C] hidden activation; here a no-grad forward moves only X
+// in and Y out.
 //
 // Arithmetic matches the grouped-GEMM path bit for bit: the same v_mfma_f32_16x16x32_bf16 sequence over k, the
 // same fp32 bias add and fast GELU (mg_common.h gelu_fast) before the bf16 rounding of the hidden activation.
