@@ -1,0 +1,26 @@
+"""Per-kernel issue profile of the step from one rocprofv3 --pmc pass (SQ counters): summed over dispatches,
+ranked by wave-cycles; VALU / MFMA instruction ratio and the parked (WAIT_ANY) share.
+    python tools/pmc_step_issue.py <counter_collection.csv> [steps]"""
+import collections
+import csv
+import sys
+
+tot = collections.defaultdict(lambda: collections.defaultdict(float))
+calls = collections.Counter()
+seen = set()
+for r in csv.DictReader(open(sys.argv[1])):
+    name = r["Kernel_Name"].replace("unsigned short", "bf16").replace("(anonymous namespace)::", "")[:80]
+    tot[name][r["Counter_Name"]] += float(r["Counter_Value"])
+    did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+    if (name, did) not in seen:
+        seen.add((name, did))
+        calls[name] += 1
+steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
+allwc = sum(c.get("SQ_WAVE_CYCLES", 0) for c in tot.values())
+print(f"{'share':>6} {'calls':>6} {'VALU/MFMA':>9} {'wait%':>6} {'active%':>7}  kernel")
+for name, c in sorted(tot.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:40]:
+    wc = c.get("SQ_WAVE_CYCLES", 0)
+    mf = c.get("SQ_INSTS_MFMA", 0)
+    ratio = c.get("SQ_INSTS_VALU", 0) / mf if mf else float("inf")
+    print(f"{100 * wc / allwc:5.1f}% {calls[name] / steps:6.1f} {ratio:9.1f} {100 * c.get('SQ_WAIT_ANY', 0) / max(wc, 1):5.0f}% "
+          f"{100 * c.get('SQ_ACTIVE_INST_ANY', 0) / max(wc, 1):6.0f}%  {name}")
