@@ -109,12 +109,14 @@ MG_DEV void stage(bf16_t* img, const bf16_t* src, int64_t ld, int L, int Lp, int
 // ---------------------------------------------------------------------------
 // forward: O = softmax(Q K^T / sqrt(D)) V, lse per query
 // ---------------------------------------------------------------------------
-template <int D, int L, int U>  // U units (image, head) per block, WPU waves per unit
-__global__ __launch_bounds__(256) void k_attn_fwd_mfma(const bf16_t* __restrict__ qkv, int B, int C, int heads,
+// LT: token tile length (a multiple of 16); the sequence length L <= LT is a runtime argument (L = LT for the
+// generator's blocks; CLIP's 50 tokens run on the 64-token tiles with rows >= L masked on load and store)
+template <int D, int LT, int U>  // U units (image, head) per block, WPU waves per unit
+__global__ __launch_bounds__(256) void k_attn_fwd_mfma(const bf16_t* __restrict__ qkv, int B, int L, int C, int heads,
                                                        bf16_t* __restrict__ out, float* __restrict__ lse) {
   constexpr int P = Pitch<D>::P;
-  constexpr int Lp = L < 32 ? 32 : L;
-  constexpr int WPU = L / 16 < 4 ? L / 16 : 4;
+  constexpr int Lp = LT < 32 ? 32 : LT;
+  constexpr int WPU = LT / 16 < 4 ? LT / 16 : 4;
   constexpr int NKB = Lp / 16;
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, fr = lane & 15;
@@ -133,11 +135,11 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(const bf16_t* __restrict_
   __syncthreads();
   if (!live) return;
   const float scale = rsqrtf((float)D);
-  for (int t = wu; t < L / 16; t += WPU) {
-    // Q fragment straight from HBM (rows t*16 + fr)
+  for (int t = wu; t < LT / 16; t += WPU) {
+    // Q fragment straight from HBM (rows t*16 + fr; rows past L read as the clamped last row, never stored)
     Frag<D> qf;
     {
-      const bf16_t* qr = base + (int64_t)(t * 16 + fr) * ld;
+      const bf16_t* qr = base + (int64_t)min(t * 16 + fr, L - 1) * ld;
       if constexpr (D == 16) qf.a = *reinterpret_cast<const s16x4_t*>(qr + 4 * g);
       else if constexpr (D == 32) qf.a = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(qr + 8 * g));
       else {
@@ -184,8 +186,8 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(const bf16_t* __restrict_
     for (int db = 0; db < D / 16; ++db)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        out[((int64_t)b * L + t * 16 + 4 * g + r) * C + h * D + db * 16 + fr] = f2bf(o[db][r]);
-    if (g == 0) lse[((int64_t)b * heads + h) * L + t * 16 + fr] = m + __logf(l);
+        if (t * 16 + 4 * g + r < L) out[((int64_t)b * L + t * 16 + 4 * g + r) * C + h * D + db * 16 + fr] = f2bf(o[db][r]);
+    if (g == 0 && t * 16 + fr < L) lse[((int64_t)b * heads + h) * L + t * 16 + fr] = m + __logf(l);
   }
 }
 
@@ -328,11 +330,11 @@ constexpr int units_bwd() {
   return u;
 }
 
-template <int D, int L>
-int launch_fwd(const bf16_t* qkv, int B, int C, int heads, bf16_t* out, float* lse, hipStream_t st) {
-  constexpr int P = Pitch<D>::P, Lp = L < 32 ? 32 : L, WPU = L / 16 < 4 ? L / 16 : 4, U = units_fwd<D, L>();
+template <int D, int LT>
+int launch_fwd(const bf16_t* qkv, int B, int C, int heads, bf16_t* out, float* lse, hipStream_t st, int L = LT) {
+  constexpr int P = Pitch<D>::P, Lp = LT < 32 ? 32 : LT, WPU = LT / 16 < 4 ? LT / 16 : 4, U = units_fwd<D, LT>();
   size_t sm = (size_t)U * 2 * Lp * P * sizeof(bf16_t);
-  hipLaunchKernelGGL((k_attn_fwd_mfma<D, L, U>), dim3(cdiv(B * heads, U)), dim3(64 * U * WPU), sm, st, qkv, B, C,
+  hipLaunchKernelGGL((k_attn_fwd_mfma<D, LT, U>), dim3(cdiv(B * heads, U)), dim3(64 * U * WPU), sm, st, qkv, B, L, C,
                      heads, out, lse);
   return mg_check_launch("mg_attn_fwd (mfma)");
 }
@@ -361,6 +363,7 @@ int mg_attn_fwd_mfma(const void* qkv, int B, int L, int C, int heads, void* out,
   if (D == 64 && L == 64) return launch_fwd<64, 64>(q, B, C, heads, o, lse, st);
   if (D == 32 && L == 16) return launch_fwd<32, 16>(q, B, C, heads, o, lse, st);
   if (D == 16 && L == 64) return launch_fwd<16, 64>(q, B, C, heads, o, lse, st);
+  if (D == 64 && L > 32 && L < 64) return launch_fwd<64, 64>(q, B, C, heads, o, lse, st, L);  // CLIP ViT-B/32: 50
   return 1;
 }
 

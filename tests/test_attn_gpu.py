@@ -37,3 +37,24 @@ def test_attention_bf16_mfma_vs_fp32(L, C):
     for part in range(3):
         sl = slice(part * C, (part + 1) * C)
         assert rel(g_qkv[:, sl], gref[:, sl]) < 3e-2, part
+
+
+@pytest.mark.parametrize("L", [50, 33, 63])
+def test_attention_ragged_tokens_forward(L):
+    """Forward-only ragged sequence (the CLIP ViT-B/32 image tower: 50 tokens, 12 heads of 64) on the 64-token MFMA
+    tiles: rows past L masked on load and store; the image after the last one is never touched."""
+    B, heads, C = 7, 12, 768
+    D = C // heads
+    g = torch.Generator(device=DEV).manual_seed(L)
+    qkv = (torch.randn(B * L, 3 * C, device=DEV, generator=g) * 1.5).bfloat16()
+    out = torch.full((B * L + 16, C), 7.0, device=DEV).bfloat16()  # guard rows after the last image
+    lse = torch.full((B * heads * L + 16,), 7.0, device=DEV)
+    ops.call("mg_attn_fwd", ops.dt(qkv), ops.ptr(qkv), B, L, C, heads, ops.ptr(out), ops.ptr(lse), ops.S())
+    torch.cuda.synchronize()
+    x = qkv.float().view(B, L, 3, heads, D).permute(2, 0, 3, 1, 4)
+    q, k, v = x[0], x[1], x[2]
+    s = q @ k.transpose(-1, -2) / D ** 0.5
+    ref = (torch.softmax(s, -1) @ v).permute(0, 2, 1, 3).reshape(B * L, C)
+    assert rel(out[:B * L], ref) < 2e-2
+    assert (lse[:B * heads * L].view(B, heads, L) - torch.logsumexp(s, -1)).abs().max().item() < 2e-2
+    assert bool((out[B * L:].float() == 7.0).all()) and bool((lse[B * heads * L:] == 7.0).all())
