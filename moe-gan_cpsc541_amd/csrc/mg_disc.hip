@@ -284,11 +284,14 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
 }
 
 // G adversarial loss softplus(-f).mean() (t2i_moe_gan.py:919) and its gradient
+// Grid-stride over the B logits; with one block the block writes the mean, with several each block writes its
+// partial sum and k_g_loss_fin folds them in block order (deterministic).  The progressive stages' multi-logit fakes
+// (B x 841 at 128^2) would take 500 us in one block.
 __global__ void k_g_loss(const float* __restrict__ fake, int B, float scale, float* __restrict__ out,
-                         float* __restrict__ g) {
+                         float* __restrict__ g, float* __restrict__ part) {
   __shared__ float red[16];
   float s = 0.f;
-  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B; i += gridDim.x * blockDim.x) {
     float f = fake[i];
     s += (-f > 20.f) ? -f : log1pf(expf(-f));
     g[i] = -1.f / (1.f + expf(f)) / B * scale;
@@ -299,8 +302,15 @@ __global__ void k_g_loss(const float* __restrict__ fake, int B, float scale, flo
   if (threadIdx.x == 0) {
     float a = 0;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) a += red[i];
-    out[0] = a / B;
+    if (part) part[blockIdx.x] = a;
+    else out[0] = a / B;
   }
+}
+__global__ void k_g_loss_fin(const float* __restrict__ part, int nb, int B, float* __restrict__ out) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 64) s += part[i];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) out[0] = s / B;
 }
 
 // R1 (t2i_moe_gan.py:1285-1286): r1 = gamma/2 * mean_b ||g_b||^2; u = gamma/B * g  (d r1 / d g)
@@ -485,7 +495,14 @@ extern "C" int mg_d_loss(const float* img_real, const float* img_fake, const flo
 
 extern "C" int mg_g_loss(const float* fake, int B, float scale, float* out, float* g, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_g_loss, dim3(1), dim3(256), 0, st, fake, B, scale, out, g);
+  const int nb = std::min(256, std::max(1, B / 4096));
+  float* part = nullptr;
+  if (nb > 1) {
+    part = reinterpret_cast<float*>(mg_workspace(nb * sizeof(float), st));
+    MG_REQUIRE(part, "mg_g_loss: no workspace");
+  }
+  hipLaunchKernelGGL(k_g_loss, dim3(nb), dim3(256), 0, st, fake, B, scale, out, g, part);
+  if (nb > 1) hipLaunchKernelGGL(k_g_loss_fin, dim3(1), dim3(64), 0, st, part, nb, B, out);
   return mg_check_launch("mg_g_loss");
 }
 

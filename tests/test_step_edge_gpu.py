@@ -71,3 +71,22 @@ def test_step_edge_batches_vs_oracle(B, E, k):
                           f"{which} |g|-weighted delta {n}", maxabs=False)
             n_checked += 1
     assert n_checked > 200
+
+
+@pytest.mark.parametrize("n", [1, 256, 4095, 215296, 1048577])
+def test_g_loss_sizes(n):
+    """mg_g_loss (softplus(-f).mean(), t2i_moe_gan.py:917-924, and its gradient) from one logit up to the multi-block
+    fold of the progressive stages' per-patch fakes (B x 841 at 128^2); two calls give the same bits."""
+    from moegan_mi import ops
+    f = torch.randn(n, generator=torch.Generator().manual_seed(n)) * 4
+    fd = f.to(DEV)
+    out, g = torch.zeros(1, device=DEV), torch.empty(n, device=DEV)
+    ops.g_loss(fd, out, g, 0.5)
+    out2, g2 = torch.zeros(1, device=DEV), torch.empty(n, device=DEV)
+    ops.g_loss(fd, out2, g2, 0.5)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.softplus(-f.double()).mean()
+    gref = -torch.sigmoid(-f.double()) / n * 0.5
+    assert abs(float(out) - float(ref)) <= 1e-5 * float(ref)
+    assert float((g.cpu().double() - gref).abs().max()) <= 1e-6 * float(gref.abs().max())
+    assert torch.equal(out, out2) and torch.equal(g, g2)
