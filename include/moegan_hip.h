@@ -206,6 +206,10 @@ int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngroups, const 
 
 /* ---- op-level entry points ---- */
 
+/* CLIP image-tower input (CLIPLoss.forward t2i_moe_gan.py:90-94 + the ViT conv1 patchify): clamp [-1,1], bilinear
+   R->res (align_corners=False) from NHWC [B,R,R,ld] (channels 0..2), unfolded patch rows [B*(res/patch)^2, 3*patch*patch] bf16. */
+int mg_clip_patches(int dtype, const void* img, int B, int R, int ld, int res, int patch, void* out, void* stream);
+
 /* LayerNorm over C (128/256/512) per row (+ optional LeakyReLU), saving mean/rstd. t2i_moe_gan.py:505-507, :684. */
 int mg_layernorm_fwd(int dtype, const void* x, int64_t ldx, int R, int C, const float* gamma, const float* beta, float eps, void* y, int64_t ldy, float* mean, float* rstd, int act, void* stream);
 

@@ -79,12 +79,23 @@ class ClipImageEncoder:
     def encode_image(self, img):
         """img [B, 3, res, res] (any float dtype, the caller's value range) -> image features [B, output_dim] fp32."""
         B = img.shape[0]
-        p, g, w = self.patch, self.grid, self.width
+        p, g = self.patch, self.grid
         assert tuple(img.shape[1:]) == (3, self.resolution, self.resolution), img.shape
+        patches = img.to(self.dev, torch.bfloat16).reshape(B, 3, g, p, g, p).permute(0, 2, 4, 1, 3, 5)
+        return self._encode_patches(patches.reshape(B * g * g, 3 * p * p), B)
+
+    @torch.no_grad()
+    def encode_generated(self, img_nhwc):
+        """CLIPLoss's input path for a generator image, NHWC [B, R, R, ld] (channels 0..2, any R): clamp, bilinear
+        resize to the tower's resolution and patchify in one kernel (mg_clip_patches), then the tower."""
+        patches = ops.clip_patches(img_nhwc.contiguous(), self.resolution, self.patch)
+        return self._encode_patches(patches, img_nhwc.shape[0])
+
+    def _encode_patches(self, patches, B):
+        g, w = self.grid, self.width
         T = g * g + 1
         # patch embedding (conv1, stride = kernel = patch, no bias) as one GEMM over unfolded patches
-        patches = img.to(self.dev, torch.bfloat16).reshape(B, 3, g, p, g, p).permute(0, 2, 4, 1, 3, 5)
-        emb = ops.linear(patches.reshape(B * g * g, 3 * p * p), self.W_patch, out_dtype=torch.float32)
+        emb = ops.linear(patches, self.W_patch, out_dtype=torch.float32)
         x = torch.empty(B, T, w, device=self.dev, dtype=torch.float32)
         x[:, 0] = self.cls
         x[:, 1:] = emb.view(B, g * g, w)

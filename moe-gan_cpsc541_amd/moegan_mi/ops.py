@@ -775,6 +775,17 @@ def d_loss(img_real, img_fake, tb, perm, out, g_img, g_fake, g_tb, real_out=None
          ptr(g_tb), ptr(real_out), ptr(mism_out), ptr(fake_out), S())
 
 
+def clip_patches(img, res=224, patch=32):
+    """Generator image NHWC [B, R, R, ld] (channels 0..2) -> CLIP ViT patch rows [B*(res/patch)^2, 3*patch*patch] bf16:
+    clamp, bilinear resize to res, unfold (mg_clip_patches)."""
+    B, R, R2, ld = img.shape
+    assert R == R2 and img.is_contiguous()
+    g = res // patch
+    out = torch.empty(B * g * g, 3 * patch * patch, device=img.device, dtype=torch.bfloat16)
+    call("mg_clip_patches", dt(img), ptr(img), B, R, ld, res, patch, ptr(out), S())
+    return out
+
+
 def g_loss(fake, out, g, scale=1.0):
     call("mg_g_loss", ptr(fake), fake.shape[0], scale, ptr(out), ptr(g), S())
 

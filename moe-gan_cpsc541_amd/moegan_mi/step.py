@@ -55,14 +55,21 @@ class StepConfig:
         self.psi = psi
 
 
-def clip_loss(images_nchw, text, encode_image):
+def clip_loss(images_nchw, text, encode_image, images_nhwc=None):
     """CLIPLoss.forward (t2i_moe_gan.py:75-119): 1 - mean cos(CLIP(image), text), forward only (no gradient,
-    :98-101).  Logging / validation only; values are parity-unpinned (CLIP weights are not available here)."""
+    :98-101).  Logging / validation only; values are parity-unpinned (CLIP weights are not available here).
+    With the build's image tower (``encode_image`` a bound ``ClipImageEncoder`` method) and the generator's NHWC
+    image, clamp + resize + patchify run as one kernel (``encode_generated``); any other encoder gets the NCHW
+    clamp / F.interpolate input of the reference."""
     with torch.no_grad():
-        im = torch.clamp(images_nchw.float(), -1, 1)
-        if im.shape[-1] != 224 or im.shape[-2] != 224:
-            im = F.interpolate(im, size=(224, 224), mode="bilinear", align_corners=False)
-        f = encode_image(im).float()
+        tower = getattr(encode_image, "__self__", None)
+        if images_nhwc is not None and hasattr(tower, "encode_generated"):
+            f = tower.encode_generated(images_nhwc).float()
+        else:
+            im = torch.clamp(images_nchw.float(), -1, 1)
+            if im.shape[-1] != 224 or im.shape[-2] != 224:
+                im = F.interpolate(im, size=(224, 224), mode="bilinear", align_corners=False)
+            f = encode_image(im).float()
         f = f / f.norm(dim=-1, keepdim=True)
         t = text.float() / text.float().norm(dim=-1, keepdim=True)
         sim = torch.nan_to_num((f * t).sum(dim=1))
@@ -269,8 +276,8 @@ class TrainStep:
         # CLIP terms (t2i_moe_gan.py:1385-1387): forward only, they enter g_loss's value but no gradient
         clip16 = clip8 = None
         if self.clip_encoder is not None:
-            clip16 = clip_loss(img16[..., :3].permute(0, 3, 1, 2), text, self.clip_encoder)
-            clip8 = clip_loss(img8[..., :3].permute(0, 3, 1, 2), text, self.clip_encoder)
+            clip16 = clip_loss(img16[..., :3].permute(0, 3, 1, 2), text, self.clip_encoder, images_nhwc=img16)
+            clip8 = clip_loss(img8[..., :3].permute(0, 3, 1, 2), text, self.clip_encoder, images_nhwc=img8)
         # KL (t2i_moe_gan.py:846, :1367-1376, :1402-1404)
         kl2 = torch.stack(kl2s)
         kl_coef = torch.empty(len(kl2s), device=self.dev)

@@ -77,3 +77,26 @@ def test_clip_loss_in_step_and_dropin():
         assert abs(float(loss) - float(exp)) < 1e-4
     finally:
         M.set_clip_model(None)
+
+
+@pytest.mark.parametrize("R,dtype", [(16, torch.float32), (128, torch.bfloat16), (64, torch.bfloat16)])
+def test_clip_patches_match_clamp_interpolate_unfold(R, dtype):
+    """mg_clip_patches (clamp + bilinear resize to 224 + conv1 patchify, from the generator's NHWC channel-padded
+    image) against the reference's input path: torch.clamp, F.interpolate(bilinear, align_corners=False)
+    (t2i_moe_gan.py:90-94) and the unfold, in fp32 then bf16.  Bar: one bf16 rounding step (the fp32 interpolation
+    may differ in the last bit by its evaluation order)."""
+    from moegan_mi import ops
+    from moegan_mi.clip_vit import ClipImageEncoder, random_state_dict
+    B, ld = 3, 8
+    g = torch.Generator(device="cuda").manual_seed(R)
+    nhwc = (torch.randn(B, R, R, ld, device="cuda", generator=g) * 0.8).to(dtype)  # some values beyond [-1, 1]
+    got = ops.clip_patches(nhwc, 224, 32).float()
+    im = torch.clamp(nhwc[..., :3].permute(0, 3, 1, 2).float(), -1, 1)
+    im = F.interpolate(im, size=(224, 224), mode="bilinear", align_corners=False)
+    ref = im.reshape(B, 3, 7, 32, 7, 32).permute(0, 2, 4, 1, 3, 5).reshape(B * 49, 3 * 1024)
+    assert ((got - ref.bfloat16().float()).abs() <= ref.abs() * 2 ** -7 + 1e-6).all()
+    enc = ClipImageEncoder(random_state_dict(768, 2, 32, 224, 512, seed=3), device="cuda")
+    f_gen = enc.encode_generated(nhwc)
+    f_ref = enc.encode_image(im)
+    cos = F.cosine_similarity(f_gen.double(), f_ref.double(), dim=1)
+    assert float(cos.min()) >= 0.9999
