@@ -506,61 +506,66 @@ extern "C" int mg_attn_bwd(int dtype, int gout_dtype, const void* qkv, const voi
 // [-1, 1], bilinear resize R x R -> res x res (align_corners=False, PyTorch's source-index rule: src =
 // max(0, (dst + 0.5) * R / res - 0.5), neighbour clamped at the edge), and write the unfolded patch rows
 // [B * (res/patch)^2, 3 * patch * patch] in (c, kh, kw) order, bf16 -- straight from the generator's NHWC
-// (channel-padded) image.  One thread per 8 consecutive kw of one (patch, c, kh) row segment: 16-B stores.
+// (channel-padded) image.  16-B stores of 8 consecutive kw.
 // ---------------------------------------------------------------------------
 namespace {
-template <typename T>
-__global__ void k_clip_patches(const T* __restrict__ img, int B, int R, int ld, int res, int patch,
-                               bf16_t* __restrict__ out) {
-  const int g = res / patch, segs = patch / 8;
-  const int64_t n = (int64_t)B * g * g * 3 * patch * segs;
+// one block per patch row (b, gy, gx): the clamped source window of the patch (at most 2 + P * R / res pixels a
+// side, R <= res) is staged in LDS once, then thread (c, kh, 8-wide kw segment) interpolates from LDS
+template <typename T, int P>
+__global__ void k_clip_patches(const T* __restrict__ img, int R, int ld, int res, bf16_t* __restrict__ out) {
+  constexpr int WMAX = P + 2;
+  __shared__ float win[3][WMAX][WMAX];
+  const int g = res / P;
+  const int prow = blockIdx.x, gx = prow % g, gy = (prow / g) % g, b = prow / (g * g);
+  const int t = threadIdx.x, sg = t % (P / 8), kh = (t / (P / 8)) % P, c = t / (P * P / 8);
   const float scale = (float)R / (float)res;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
-    int64_t t = v;
-    const int sg = (int)(t % segs); t /= segs;
-    const int kh = (int)(t % patch); t /= patch;
-    const int c = (int)(t % 3); t /= 3;
-    const int gx = (int)(t % g); t /= g;
-    const int gy = (int)(t % g);
-    const int b = (int)(t / g);
-    const int y = gy * patch + kh;
-    float sy = fmaxf(scale * (y + 0.5f) - 0.5f, 0.f);
-    const int y0 = (int)sy, y1 = y0 + (y0 < R - 1 ? 1 : 0);
-    const float ly1 = sy - y0, ly0 = 1.f - ly1;
-    const T* r0 = img + ((int64_t)b * R + y0) * R * ld + c;
-    const T* r1 = img + ((int64_t)b * R + y1) * R * ld + c;
-    u16x8_t o;
+  auto src = [&](int d) { return fmaxf(scale * (d + 0.5f) - 0.5f, 0.f); };
+  const int ya = (int)src(gy * P), xa = (int)src(gx * P);  // window origin (source indices are monotone)
+  const int yb = min((int)src(gy * P + P - 1) + 1, R - 1), xb = min((int)src(gx * P + P - 1) + 1, R - 1);
+  const int wh = yb - ya + 1, ww = xb - xa + 1;
+  for (int e = t; e < wh * ww; e += blockDim.x) {
+    const int yy = e / ww, xx = e - yy * ww;
+    const T* px = img + (((int64_t)b * R + ya + yy) * R + xa + xx) * ld;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int x = gx * patch + sg * 8 + j;
-      float sx = fmaxf(scale * (x + 0.5f) - 0.5f, 0.f);
-      const int x0 = (int)sx, x1 = x0 + (x0 < R - 1 ? 1 : 0);
-      const float lx1 = sx - x0, lx0 = 1.f - lx1;
-      auto cl = [](float a) { return fminf(fmaxf(a, -1.f), 1.f); };
-      const float v00 = cl(ldf(r0, (int64_t)x0 * ld)), v01 = cl(ldf(r0, (int64_t)x1 * ld));
-      const float v10 = cl(ldf(r1, (int64_t)x0 * ld)), v11 = cl(ldf(r1, (int64_t)x1 * ld));
-      o[j] = f2bf(ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
-    }
-    const int64_t row = ((int64_t)b * g + gy) * g + gx;
-    *reinterpret_cast<u16x8_t*>(out + row * (3 * patch * patch) + (c * patch + kh) * patch + sg * 8) = o;
+    for (int ch = 0; ch < 3; ++ch) win[ch][yy][xx] = fminf(fmaxf(ldf(px, ch), -1.f), 1.f);
   }
+  __syncthreads();
+  const int y = gy * P + kh;
+  const float sy = src(y);
+  const int y0 = (int)sy, y1 = y0 + (y0 < R - 1 ? 1 : 0);
+  const float ly1 = sy - y0, ly0 = 1.f - ly1;
+  const float* w0 = &win[c][y0 - ya][0];
+  const float* w1 = &win[c][y1 - ya][0];
+  u16x8_t o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int x = gx * P + sg * 8 + j;
+    const float sx = src(x);
+    const int x0 = (int)sx, x1 = x0 + (x0 < R - 1 ? 1 : 0);
+    const float lx1 = sx - x0, lx0 = 1.f - lx1;
+    const float v00 = w0[x0 - xa], v01 = w0[x1 - xa], v10 = w1[x0 - xa], v11 = w1[x1 - xa];
+    o[j] = f2bf(ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
+  }
+  *reinterpret_cast<u16x8_t*>(out + (int64_t)prow * (3 * P * P) + (c * P + kh) * P + sg * 8) = o;
 }
 }  // namespace
 
 extern "C" int mg_clip_patches(int dtype, const void* img, int B, int R, int ld, int res, int patch, void* out,
                                void* stream) {
   MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
-  MG_REQUIRE(B >= 0 && R >= 1 && ld >= 3 && patch % 8 == 0 && res % patch == 0, "bad clip patch geometry");
+  MG_REQUIRE(patch == 32, "patch must be 32 (ViT-B/32)");
+  MG_REQUIRE(B >= 0 && R >= 1 && R <= res && ld >= 3 && res % patch == 0, "bad clip patch geometry (R <= res)");
   MG_REQUIRE(mg_al16(out), "out must be 16-byte aligned");
+  MG_REQUIRE((int64_t)B * (res / patch) * (res / patch) < (1LL << 31) && (int64_t)R * ld < (1LL << 31),
+             "too many patches");
   if (B == 0) return MG_OK;
-  const int64_t n = (int64_t)B * (res / patch) * (res / patch) * 3 * patch * (patch / 8);
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  const int rows = B * (res / patch) * (res / patch);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == MG_F32)
-    hipLaunchKernelGGL(k_clip_patches<float>, dim3(blocks), dim3(256), 0, st, (const float*)img, B, R, ld, res, patch,
-                       (bf16_t*)out);
+    hipLaunchKernelGGL((k_clip_patches<float, 32>), dim3(rows), dim3(3 * 32 * 32 / 8), 0, st, (const float*)img, R, ld,
+                       res, (bf16_t*)out);
   else
-    hipLaunchKernelGGL(k_clip_patches<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)img, B, R, ld, res,
-                       patch, (bf16_t*)out);
+    hipLaunchKernelGGL((k_clip_patches<bf16_t, 32>), dim3(rows), dim3(3 * 32 * 32 / 8), 0, st, (const bf16_t*)img, R,
+                       ld, res, (bf16_t*)out);
   return mg_check_launch("mg_clip_patches");
 }
