@@ -300,9 +300,10 @@ int mg_moe_combine(int dtype, const void* Y, int64_t ldy, const int32_t* pos_of,
 /* g_gate[t*k+j] = <gout[t], Y[pos_of[t*k+j]]>. */
 int mg_moe_gate_grad(int dtype, int gout_dtype, const void* gout, int64_t ldg, const void* Y, int64_t ldy, const int32_t* pos_of, int T, int k, int C, float* g_gate, void* stream);
 
-/* Router backward per token -> g_raw [T,E], per-image sums gsum [B,E] (+=), temperature grad (+=).  Upstream
-   gradients (each optional): g_gate (combine weights), g_probs + coef[e] (probabilities), g_logits (the clamped
-   logits, the router's second output). */
+/* Router backward per token -> g_raw [T,E], per-image sums gsum [B,E] (written), temperature grad (+=; per-block
+   partials in the stream's workspace, folded in a fixed order: bit-identical run to run).  HW (tokens per image) a
+   power of two <= 256.  Upstream gradients (each optional): g_gate (combine weights), g_probs + coef[e]
+   (probabilities), g_logits (the clamped logits, the router's second output).  Reference :374-389. */
 int mg_router_bwd(const float* probs, const float* zlog, const int32_t* topi, const float* gate, const float* g_gate, const float* g_probs, const float* g_logits, const float* coef, int T, int E, int k, int HW, const float* temperature, float anneal, float* g_raw, float* gsum, float* g_temp, void* stream);
 
 /* g_tok[t] = sum_j gX[pos_of[t*k+j]] + sum_e g_raw[t,e] Wfc[:,e]. */

@@ -399,24 +399,29 @@ __global__ void k_gate_grad(const TG* __restrict__ gout, int64_t ldg, const T* _
   if (ok && tl == 0) g_gate[a] = s;
 }
 
-// per-token router backward: (g_gate, balance coefficients) -> g_raw [T, E]
+// per-token router backward: (g_gate, balance coefficients) -> g_raw [T, E], the per-image sums gsum [B, E] and
+// one temperature-gradient partial per block (tpart; k_fold_partials adds them to the parameter gradient).
+// Every reduction runs in a fixed order (segmented butterflies inside a wave, waves of one image folded in wave
+// order, block partials folded by one block), so the results are bit-identical run to run: the image's tokens are
+// contiguous, an image of HW <= 64 tokens lies inside one wave and one of 128 / 256 tokens inside one block.
 template <int E>
-__global__ void k_router_bwd(const float* __restrict__ probs, const float* __restrict__ zlog,
+__global__ __launch_bounds__(256) void k_router_bwd(const float* __restrict__ probs, const float* __restrict__ zlog,
                              const int* __restrict__ topi, const float* __restrict__ gate,
                              const float* __restrict__ g_gate, const float* __restrict__ g_probs,
                              const float* __restrict__ g_logits,
                              const float* __restrict__ coef, int Tn, int k, int lgHW, const float* __restrict__ temp,
                              float anneal, float* __restrict__ g_raw, float* __restrict__ gsum,
-                             float* __restrict__ g_temp) {
-  __shared__ float red[18 * E];
+                             float* __restrict__ tpart) {
+  __shared__ float red[4 * E];
   __shared__ float tred[4];
-  int t0 = blockIdx.x * blockDim.x;
-  int b0 = t0 >> lgHW;
-  for (int i = threadIdx.x; i < 18 * E; i += blockDim.x) red[i] = 0.f;
-  __syncthreads();
-  int t = t0 + threadIdx.x;
-  float te = teff_of(temp, anneal);
+  const int t0 = blockIdx.x * blockDim.x;
+  const int t = t0 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float te = teff_of(temp, anneal);
   float gt_part = 0.f;
+  float grv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) grv[e] = 0.f;
   if (t < Tn) {
     float p[E], gp[E], z[E];
 #pragma unroll
@@ -484,32 +489,61 @@ __global__ void k_router_bwd(const float* __restrict__ probs, const float* __res
       gs_[e] = (s[e] >= 1e-6f && s[e] <= 1.f) ? gq : 0.f;
       d2 += gs_[e] * s[e];
     }
-    int bl = (t >> lgHW) - b0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       float gl = s[e] * (gs_[e] - d2);
       if (g_logits) gl += g_logits[(int64_t)t * E + e];  // the router's second output, logits (:378-381)
       gl = (z[e] >= -20.f && z[e] <= 20.f) ? gl : 0.f;
       gt_part += -gl * z[e] / te;
-      float gr = gl / te;
-      g_raw[(int64_t)t * E + e] = gr;
-      if (lgHW >= 4) atomicAdd(&red[bl * E + e], gr);
-      else atomicAdd(&gsum[(int64_t)(t >> lgHW) * E + e], gr);  // < 16 tokens per image: > 18 images per block
+      grv[e] = gl / te;
+      g_raw[(int64_t)t * E + e] = grv[e];
     }
   }
+  // per-image sums: butterfly over the image's lanes (all of the wave when the image spans waves)
+  const int seg = lgHW >= 6 ? 64 : (1 << lgHW);
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    for (int o = 1; o < seg; o <<= 1) grv[e] += __shfl_xor(grv[e], o, 64);
+  if (lgHW <= 6) {
+    if ((lane & (seg - 1)) == 0 && t < Tn) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) gsum[(int64_t)(t >> lgHW) * E + e] = grv[e];
+    }
+  } else if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) red[wave * E + e] = grv[e];
+  }
   gt_part = wave_sum(gt_part);
-  if ((threadIdx.x & 63) == 0) tred[threadIdx.x >> 6] = gt_part;
+  if (lane == 0) tred[wave] = gt_part;
   __syncthreads();
-  int tl = min(Tn, t0 + (int)blockDim.x) - 1;
-  int nimg = (tl >> lgHW) - b0 + 1;
-  if (lgHW >= 4)
-    for (int i = threadIdx.x; i < nimg * E; i += blockDim.x) atomicAdd(&gsum[(int64_t)b0 * E + i], red[i]);
-  if (threadIdx.x == 0 && g_temp) {
+  if (lgHW > 6) {  // 128 / 256 tokens per image: 2 / 4 waves of this block, folded in wave order
+    const int wpi = 1 << (lgHW - 6);
+    const int nimg = (min(Tn, t0 + (int)blockDim.x) - t0 + (1 << lgHW) - 1) >> lgHW;
+    for (int i = threadIdx.x; i < nimg * E; i += blockDim.x) {
+      const int bl = i / E, e = i - bl * E;
+      float v = 0.f;
+      for (int w = bl * wpi; w < bl * wpi + wpi; ++w) v += red[w * E + e];
+      gsum[(int64_t)((t0 >> lgHW) + bl) * E + e] = v;
+    }
+  }
+  if (threadIdx.x == 0 && tpart) {
     float tt = 0.f;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tt += tred[i];
     float raw = temp[0] * anneal;
-    if (raw >= 0.5f && raw <= 5.f) atomicAdd(g_temp, tt * anneal);
+    tpart[blockIdx.x] = (raw >= 0.5f && raw <= 5.f) ? tt * anneal : 0.f;
   }
+}
+
+// out[0] += sum of part[0 .. n) in a fixed order (one block: strided thread sums, then a butterfly per wave and
+// the waves in order)
+__global__ __launch_bounds__(256) void k_fold_partials(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float wsum[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] += (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
 }
 
 // g_tok[t, c] = sum_j gX[pos_of[t*k+j], c] + sum_e g_raw[t, e] * Wfc[c, e]
@@ -1007,15 +1041,21 @@ extern "C" int mg_router_bwd(const float* probs, const float* zlog, const int32_
                              const float* temperature, float anneal, float* g_raw, float* gsum, float* g_temp,
                              void* stream) {
   MG_REQUIRE(E == 4 || E == 8 || E == 16 || E == 32, "E must be 4, 8, 16 or 32");
-  MG_REQUIRE(HW >= 1 && (HW & (HW - 1)) == 0, "HW must be a power of two");
+  MG_REQUIRE(HW >= 1 && HW <= 256 && (HW & (HW - 1)) == 0, "HW must be a power of two <= 256");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int lg = 0;
   while ((1 << lg) < HW) ++lg;
   dim3 grid(cdiv(T, 256));
+  float* tpart = nullptr;
+  if (g_temp) {
+    tpart = reinterpret_cast<float*>(mg_workspace((size_t)grid.x * sizeof(float), st));
+    if (!tpart) return MG_ERR_LAUNCH;
+  }
 #define L_(EE) hipLaunchKernelGGL((k_router_bwd<EE>), grid, dim3(256), 0, st, probs, zlog, topi, gate, g_gate, g_probs, g_logits, coef, T, k, lg, \
-                                  temperature, anneal, g_raw, gsum, g_temp)
+                                  temperature, anneal, g_raw, gsum, tpart)
   if (E == 4) L_(4); else if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
 #undef L_
+  if (g_temp) hipLaunchKernelGGL(k_fold_partials, dim3(1), dim3(256), 0, st, tpart, (int)grid.x, g_temp);
   return mg_check_launch("mg_router_bwd");
 }
 

@@ -23,8 +23,12 @@ _SIDES = weakref.WeakSet()  # live SideStreams: joined at every eager boundary (
 
 
 def eager(fn):
-    """Run ``fn`` now; while a capture is active, also make it an eager segment of the replay."""
+    """Run ``fn`` now; while a capture is active, also make it an eager segment of the replay.  Every live side
+    stream is joined first in both cases: an eager segment (an RCCL collective) may read what a side stream
+    wrote, e.g. a block's expert weight gradients handed to a bucketed all-reduce (step.py)."""
     if ACTIVE is None:
+        for side in list(_SIDES):
+            side.join()
         return fn()
     return ACTIVE._eager(fn)
 

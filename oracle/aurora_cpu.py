@@ -46,10 +46,10 @@ def modconv(x, w, P, pre, padding=0, demod=True):
 # ---------------------------------------------------------------------------
 # Modulated Transformation Module  (t2i_moe_gan.py:188-247)
 # ---------------------------------------------------------------------------
-def base_grid(H, W, device=None):
+def base_grid(H, W, device=None, dtype=torch.float32):
     """linspace grid of :226-230 ([H, W, 2], last dim = (x, y))."""
-    gy = torch.linspace(-1, 1, H, device=device).view(H, 1).expand(H, W)
-    gx = torch.linspace(-1, 1, W, device=device).view(1, W).expand(H, W)
+    gy = torch.linspace(-1, 1, H, device=device, dtype=dtype).view(H, 1).expand(H, W)
+    gx = torch.linspace(-1, 1, W, device=device, dtype=dtype).view(1, W).expand(H, W)
     return torch.stack((gx, gy), dim=2)
 
 
@@ -59,7 +59,7 @@ def mtm(x, w, P, pre, use_offset=True):
         o = F.conv2d(x, P[pre + "offset_net.0.weight"], P[pre + "offset_net.0.bias"], padding=1)  # :223
         o = F.leaky_relu(o, 0.2)
         o = F.conv2d(o, P[pre + "offset_net.2.weight"], P[pre + "offset_net.2.bias"], padding=1)
-        grid = base_grid(H, W).unsqueeze(0) + o.permute(0, 2, 3, 1) * 0.05  # :226-235
+        grid = base_grid(H, W, dtype=x.dtype).unsqueeze(0) + o.permute(0, 2, 3, 1) * 0.05  # :226-235
         grid = grid.clamp(-1, 1)  # :236
         x = F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=False)  # :239
     x = modconv(x, w, P, pre + "modulated_conv.", padding=1)
@@ -252,7 +252,7 @@ def generator(z, text, P, eps=None, training=True, anneal=1.0, psi=0.7, topk=Non
     w = mapping(torch.cat([z, text], dim=1), P)  # :793-796
     if psi < 1.0:  # :799-808
         with torch.no_grad():
-            mean = mapping(torch.zeros(1, z.shape[1] + text.shape[1]), P)
+            mean = mapping(torch.zeros(1, z.shape[1] + text.shape[1], dtype=z.dtype), P)
         w = mean + psi * (w - mean)
     x = P["constant"].repeat(B, 1, 1, 1)
     kls, probs = [], []
@@ -272,17 +272,6 @@ def generator(z, text, P, eps=None, training=True, anneal=1.0, psi=0.7, topk=Non
         feats[r] = x
     img8 = modconv(feats[R // 2], w, P, f"to_rgb_{R // 2}.")  # reference (R = 16): to_rgb_8, :831
     img16 = modconv(feats[R], w, P, f"to_rgb_{R}.")  # to_rgb_16, :839
-    return img16, img8, sum(kls), probs
-    for name, r in EXT_BLOCKS:  # progressive extension: returns (R x R image, R/2 x R/2 image, ...)
-        if r > R:
-            break
-        x = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
-        x = conv_block(x, w, P, name + ".conv_block.")
-        if r == R // 2:
-            img8 = modconv(x, w, P, f"to_rgb_{r}.")
-        elif R == 32:
-            img8 = modconv(x_prev, w, P, "to_rgb_16.")
-    img16 = modconv(x, w, P, f"to_rgb_{R}.")
     return img16, img8, sum(kls), probs
 
 
@@ -397,7 +386,7 @@ def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, 
     if kl > 50.0:  # :1369-1370
         kl = torch.clamp(kl, max=50.0)
     if not torch.isfinite(kl):  # :1372-1376
-        kl = torch.tensor(0.0, requires_grad=True)
+        kl = torch.tensor(0.0, dtype=real.dtype, requires_grad=True)
     fake_pred_g = D(f16, text)
     gg = g_loss(fake_pred_g)  # :1379-1382
     if encode_image is not None:
@@ -408,7 +397,7 @@ def train_step(PG, PD, optG, optD, real, text, z, eps_dphase, eps_gphase, perm, 
     gl = gg + (clip_w16 * c16 + clip_w8 * c8) + bal  # :1393
     g_zeroed = not bool(torch.isfinite(gl))
     if g_zeroed:  # :1396-1399
-        gl = torch.tensor(0.0, requires_grad=True)
+        gl = torch.tensor(0.0, dtype=real.dtype, requires_grad=True)
     gl = gl + kl_weight_eff * kl  # :1402-1404
     (gl / acc).backward()  # :1410
     if step_optim:

@@ -20,13 +20,15 @@ def make_inputs(B, E, seed=0, res=64):
     return real, text, z, eps[:3], eps[3:], perm
 
 
-def oracle_models(E, lr=2e-4, seed_g=0, seed_d=50, max_res=16):
-    """Reference-layout fp32 leaves + the reference's AdamW (betas 0.5/0.999, wd 0.01, :1100-1102), with the
-    clipped gradients captured right before each optimizer step.  ``max_res`` > 16: progressive extension."""
+def oracle_models(E, lr=2e-4, seed_g=0, seed_d=50, max_res=16, dtype=torch.float32):
+    """Reference-layout leaves (fp32, or fp64 for an oracle run whose own rounding must stay far below the
+    device's) + the reference's AdamW (betas 0.5/0.999, wd 0.01, :1100-1102), with the clipped gradients captured
+    right before each optimizer step.  ``max_res`` > 16: progressive extension."""
     from moegan_mi.layout import discriminator_shapes, frozen_rgb_prefixes, generator_shapes
-    PG = {n: torch.from_numpy(v) for n, v in fill_state(generator_shapes(E, max_res), seed_g).items()}
+    PG = {n: torch.from_numpy(v).to(dtype) for n, v in fill_state(generator_shapes(E, max_res), seed_g).items()}
     frozen = frozen_rgb_prefixes(max_res)
-    PD = {n: torch.from_numpy(v).requires_grad_(True) for n, v in fill_state(discriminator_shapes(), seed_d).items()}
+    PD = {n: torch.from_numpy(v).to(dtype).requires_grad_(True)
+          for n, v in fill_state(discriminator_shapes(), seed_d).items()}
     for n, v in PG.items():
         # (the reference's to_rgb_8 is a leaf whose .grad stays None; the progressive extension's unused lower
         # to_rgb layers do not reach the loss at all, so they stay out of the optimizer there)
@@ -186,3 +188,118 @@ def whole(grads, names=None):
     """One vector of every gradient in ``grads`` (dict name -> tensor or None), in a fixed name order."""
     names = sorted(n for n, v in grads.items() if v is not None) if names is None else names
     return torch.cat([grads[n].reshape(-1) for n in names]), names
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Router-temperature instrumentation (t2i_moe_gan.py:374-377: logits / clamp(temperature * anneal, .5, 5)).  The
+# scalar gradient is a cancelling sum over tokens of -anneal / te * sum_e dL/dl[t, e] * l[t, e]; the taps below
+# expose its per-token terms on both sides so a test can hold the sum to a floor derived from those terms.
+# ---------------------------------------------------------------------------------------------------------------
+BLOCK_OF_HW = {16: "gen_block_4", 64: "gen_block_8", 256: "gen_block_16"}
+
+
+def router_temp_terms(z, topi, g_gate, coef, te, anneal, k):
+    """fp64 restatement of k_router_bwd's temperature term per token from the kernel's own inputs (scaled logits
+    z [T,E], selection topi [T,k], gate gradient [T,k], balance coefficients [E] or None); returns [T]."""
+    z = z.double()
+    T, E = z.shape
+    s = torch.softmax(z.clamp(-20, 20), dim=1)
+    q = s.clamp(1e-6, 1.0)
+    Sq = q.sum(1, keepdim=True)
+    p = q / Sq
+    gp = torch.zeros(T, E, dtype=torch.float64)
+    if coef is not None:
+        gp += coef.double().view(1, E)
+    ti, gg = topi.long(), g_gate.double()
+    if k == E:
+        gp.scatter_add_(1, ti, gg)
+    else:
+        psel = p.gather(1, ti)
+        S = psel.sum(1, keepdim=True)
+        dot = (gg * (psel / S)).sum(1, keepdim=True)
+        gp.scatter_add_(1, ti, (gg - dot) / S)
+    d1 = (gp * p).sum(1, keepdim=True)
+    gs = torch.where((s >= 1e-6) & (s <= 1.0), (gp - d1) / Sq, torch.zeros_like(gp))
+    gl = s * (gs - (gs * s).sum(1, keepdim=True))
+    gl = torch.where((z >= -20) & (z <= 20), gl, torch.zeros_like(gl))
+    return -(gl * z).sum(1) / te * anneal
+
+
+class DeviceTempTap:
+    """Records, per MoE block, the inputs of the device's router backward (ops.router_bwd) and the amount its
+    kernel added to the temperature gradient."""
+
+    def __init__(self):
+        self.rec = {}
+
+    def __enter__(self):
+        from moegan_mi import ops
+        self.ops, self.orig = ops, ops.router_bwd
+
+        def rb(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, anneal, g_temp, Bn, g_logits=None):
+            before = g_temp.detach().clone()
+            r = self.orig(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, anneal, g_temp, Bn,
+                          g_logits)
+            torch.cuda.synchronize()
+            te = min(max(float(temperature.detach().cpu()[0]) * anneal, 0.5), 5.0)
+            k = topi.shape[1]
+            terms = router_temp_terms(zlog.detach().cpu(), topi.detach().cpu(), g_gate.detach().float().cpu(),
+                                      None if coef is None else coef.detach().cpu(), te, anneal, k)
+            self.rec[BLOCK_OF_HW.get(HW, HW)] = dict(terms=terms, kernel=float((g_temp.detach() - before).cpu()[0]))
+            return r
+        ops.router_bwd = rb
+        return self
+
+    def __exit__(self, *exc):
+        self.ops.router_bwd = self.orig
+        return False
+
+
+class OracleTempTap:
+    """Keeps the oracle router's scaled logits of the gradient-carrying (G-phase) forward of every block, so the
+    per-token temperature terms can be read after the backward (``terms(block)``)."""
+
+    def __init__(self):
+        self.store = {}
+
+    def __enter__(self):
+        self.orig = O.router
+        store = self.store
+
+        def router(feature, text, P, pre, eps=None, training=True, anneal=1.0):
+            wf = O.reparam(P[pre + "feature_mu"], P[pre + "feature_rho"], eps[0])
+            wt = O.reparam(P[pre + "text_mu"], P[pre + "text_rho"], eps[1])
+            wc = O.reparam(P[pre + "combined_mu"], P[pre + "combined_rho"], eps[2])
+            t_eff = (P[pre + "temperature"] * anneal).clamp(0.5, 5.0)  # :375
+            logits = ((torch.cat([feature @ wf, text @ wt], dim=1) @ wc) / t_eff).clamp(-20.0, 20.0)
+            if logits.requires_grad:
+                logits.retain_grad()
+                store[pre.split(".")[0]] = dict(logits=logits, t_eff=float(t_eff.detach()), anneal=anneal)
+            probs = torch.softmax(logits, dim=1).clamp(1e-6, 1.0)
+            return probs / probs.sum(dim=1, keepdim=True), logits
+        assert training_router_matches(self.orig, router)
+        O.router = router
+        return self
+
+    def __exit__(self, *exc):
+        O.router = self.orig
+        return False
+
+    def terms(self, block):
+        s = self.store[block]
+        lg, gr = s["logits"].detach().double(), s["logits"].grad.double()
+        return -(gr * lg).sum(1) / s["t_eff"] * s["anneal"]
+
+
+def training_router_matches(orig, tapped):
+    """The tap re-states the oracle's training router; check it agrees with the oracle on a small random case."""
+    g = torch.Generator().manual_seed(5)
+    C, E, T = 16, 4, 8
+    P = {"r.feature_mu": torch.randn(C, 128, generator=g) * 0.1, "r.feature_rho": torch.full((C, 128), -4.0),
+         "r.text_mu": torch.randn(512, 128, generator=g) * 0.1, "r.text_rho": torch.full((512, 128), -4.0),
+         "r.combined_mu": torch.randn(256, E, generator=g) * 0.1, "r.combined_rho": torch.full((256, E), -4.0),
+         "r.temperature": torch.tensor([1.0])}
+    eps = (torch.randn(C, 128, generator=g), torch.randn(512, 128, generator=g), torch.randn(256, E, generator=g))
+    f, t = torch.randn(T, C, generator=g), torch.randn(T, 512, generator=g)
+    a, b = orig(f, t, P, "r.", eps, True, 3.0), tapped(f, t, P, "r.", eps, True, 3.0)
+    return torch.allclose(a[0], b[0], atol=1e-6) and torch.allclose(a[1], b[1], atol=1e-5)

@@ -1,6 +1,7 @@
-"""Step-level check of the C4 configuration's ingredients together, in the benchmarked precision: the progressive
-generator (here its 32x32 stage, so the CPU oracle stays cheap), 16 experts top-2, bf16, CLIP loss on, one full
-G+D step against the fp32 CPU oracle (oracle.train_step on the same blocks, same epsilon / z / permutation).
+"""Step-level check of the C4 configuration in the benchmarked precision: the progressive generator at the C4 stage
+(128x128, B=2) and at 32x32 (B=4), 16 experts top-2, bf16, CLIP loss on, one full G+D step (128x128 discriminator
+and R1 on the C4 stage) against the fp32 CPU oracle (oracle.train_step on the same blocks, same epsilon / z /
+permutation).
 
 The device's top-2 selections are replayed into the oracle (topk_route(idx=...)), as test_step_bf16_gpu.py does,
 and the CLIP terms use the same image-tower weights on both sides (the device's ClipImageEncoder, the oracle a
@@ -24,10 +25,11 @@ DEV = "cuda"
 torch.set_num_threads(8)
 
 
-def test_c4_ingredients_bf16_step_vs_oracle():
+@pytest.mark.parametrize("R,B", [(32, 4), (128, 2)])
+def test_c4_bf16_step_vs_oracle(R, B):
     from moegan_mi.clip_vit import ClipImageEncoder, random_state_dict
     from test_clip_gpu import torch_vit
-    E, k, B, R = 16, 2, 4, 32
+    E, k = 16, 2
     real, text, z, eps_d, eps_g, perm = make_inputs(B, E, seed=404, res=R)
     sd = random_state_dict(768, 2, 32, 224, 512, seed=5)
     ts = gpu_step(E, k, "bf16", DEV, max_res=R)
@@ -55,7 +57,7 @@ def test_c4_ingredients_bf16_step_vs_oracle():
         dev_vec = torch.cat([(store.gview(n) * coef).reshape(-1).cpu() for n in names])
         ref_vec, _ = whole(rgrads[which], names)
         m[f"{which}_grad_cos"] = cosine(dev_vec, ref_vec)
-    print("C4 ingredients, bf16 step vs fp32 oracle:", {k_: round(v, 5) for k_, v in m.items()})
+    print(f"C4 {R}x{R} B={B}, bf16 step vs fp32 oracle:", {k_: round(v, 5) for k_, v in m.items()})
     for key in ("d_loss", "r1", "g_gan", "balance"):
         assert m[key] <= 2e-2, (key, m[key])
     assert m["img"] <= 5e-2 and m["img_half"] <= 5e-2

@@ -148,3 +148,11 @@ def test_resume_checkpoint_layout(tmp_path):
     assert M.load_resume(path, G2, D2) == (0, 0)
     torch.save(G.state_dict(), path)
     assert M.load_resume(path, G2, D2) == (0, 0)
+
+
+def test_prefetcher_passthrough_on_cpu():
+    """Without a HIP device the prefetcher hands the loader's batches through unchanged (same objects, order)."""
+    from moegan_mi.prefetch import DevicePrefetcher
+    batches = [(torch.full((2, 3), float(i)), torch.full((2, 4), -float(i))) for i in range(3)]
+    out = list(DevicePrefetcher(batches, "cpu"))
+    assert len(out) == 3 and all(a is b for x, y in zip(out, batches) for a, b in zip(x, y))
