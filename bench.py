@@ -38,13 +38,14 @@ def parse():
     ap.add_argument("--experts", type=int, default=8)
     ap.add_argument("--topk", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--config", default="C2", choices=["C2", "C4", "C5"],
+    ap.add_argument("--config", default="C2", choices=["C2", "C4", "C5", "loop"],
                     help="C2 = BASELINE configs[1] (the headline line); C4 = the per-GPU slice of configs[3]: the "
                          "128x128 progressive generator, 16 experts top-2, CLIP loss on; C5 = the per-GPU slice of "
-                         "configs[4]: 32 experts top-4, MX-fp8 3x3 modulated convs")
+                         "configs[4]: 32 experts top-4, MX-fp8 3x3 modulated convs; loop = the C2 workload through the "
+                         "drop-in train_aurora_gan loop (pinned host batches, H2D copy included)")
     ap.add_argument("--fp8", action="store_true", help="MX-fp8 3x3 modulated convs (implied by --config C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--secondary", default="C5,C4",
+    ap.add_argument("--secondary", default="C5,C4,loop",
                     help="comma-separated configs measured after the headline one, each in a child bench.py process "
                          "(N=1 only), reported under 'secondary' in the same JSON line; '' to skip")
     ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU-oracle steps (B=8; ~10-20 s of CPU work)")
@@ -122,23 +123,81 @@ def cpu_baseline(args, E, k):
 
 def run_secondary(cfg, args):
     """Measure another BASELINE config (e.g. C5's single-GPU slice) in a child process -- its own GPU context,
-    graphs and memory -- and return its JSON line (the headline line above stays C2)."""
+    graphs and memory -- and return its JSON line (the headline line above stays C2).  The child runs in its own
+    process group, which is killed after it exits, so no descendant outlives the bench."""
+    import signal
     import subprocess
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--config", cfg, "--steps", str(max(5, args.steps)),
            "--warmup", str(args.warmup), "--no-cpu-baseline", "--secondary", ""]
-    if cfg != "C4":  # C4's FLOP count comes from the per-call attribution pass (no reference formula)
-        cmd.append("--no-families")
     print(f"[bench] secondary config {cfg}: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
-        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-        if r.returncode != 0 or not lines:
-            return {"config": cfg, "error": f"rc={r.returncode}: {r.stderr[-400:]}"}
+        out, err = proc.communicate(timeout=600)
+        lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+        if proc.returncode != 0 or not lines:
+            return {"config": cfg, "error": f"rc={proc.returncode}: {err[-400:]}"}
         rec = json.loads(lines[-1])
-        return {k: rec.get(k) for k in ("metric", "value", "unit", "ms_per_step", "dtype", "config",
-                                         "step_tflops_algorithmic", "step_mfma_frac", "roofline")}
+        return {k: rec.get(k) for k in ("metric", "value", "unit", "ms_per_step", "ms_per_step_median", "dtype",
+                                         "config", "finite", "step_tflops_algorithmic", "step_mfma_frac",
+                                         "roofline", "roofline_families")}
     except Exception as e:  # a report, never the headline value
         return {"config": cfg, "error": repr(e)}
+    finally:
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)  # anything the child left in its group
+        except (ProcessLookupError, PermissionError):
+            pass
+        proc.wait()
+
+
+def loop_bench(args, dev):
+    """Images/sec of the drop-in training loop itself (t2i_moe_gan.train_aurora_gan, reference :1214-1421) on the
+    C2 workload: pinned host batches, each copied host -> HBM by the loop's prefetcher while the previous batch
+    trains, every batch body a replayed hipGraph, the guard word / logged losses read one batch late.  Timed from
+    the host seeing batch ``warmup`` done to it seeing the last batch done (steady state: the first batch of the
+    epoch runs eagerly and is captured)."""
+    import t2i_moe_gan as M
+    B, n = args.batch, args.warmup + args.steps + 1
+    g = torch.Generator().manual_seed(0)
+    imgs = (torch.rand(B * n, 3, 64, 64, generator=g) * 2 - 1).pin_memory()
+    text = torch.randn(B * n, 512, generator=g).pin_memory()
+    loader = [(imgs[i:i + B], text[i:i + B]) for i in range(0, B * n, B)]
+    marks = {}
+
+    def done(epoch, b):
+        marks[b] = time.perf_counter()
+        if b % max(1, n // 4) == 0:
+            print(f"[bench] loop batch {b + 1}/{n} done", file=sys.stderr, flush=True)
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        M.train_aurora_gan(loader, num_epochs=1, lr=2e-4, gradient_accumulation_steps=1, checkpoint_activation=False,
+                           num_experts=args.experts, topk=args.topk, dtype=args.dtype, seed=0, save_dir=tmp,
+                           log_interval=10 ** 9, device=dev, use_graphs=not args.eager, on_batch_done=done)
+    t0, t1 = marks[args.warmup], marks[n - 1]
+    ms = (t1 - t0) / (n - 1 - args.warmup) * 1e3
+    return {"metric": "images/sec (G+D step through the drop-in train_aurora_gan loop, 64x64, H2D copy included)",
+            "value": round(B * 1e3 / ms, 2), "unit": "images/sec", "ms_per_step": round(ms, 3), "dtype": args.dtype,
+            "config": {"workload": f"C2 via train_aurora_gan: 64x64, {args.experts} experts top-{args.topk}, batch "
+                                   f"{B}, {args.dtype}, R1 on, pinned host batches (12.6 MB) copied per batch",
+                       "global_batch": B, "parallelism": "dp1",
+                       "launch": "eager" if args.eager else "hipGraph replay per batch"},
+            "batches_timed": n - 1 - args.warmup}
+
+
+def reap_children():
+    """End (and report) any process this bench started that is still alive: the driver counts leftovers."""
+    try:
+        import psutil
+    except ImportError:
+        return []
+    left = psutil.Process().children(recursive=True)
+    for c in left:
+        try:
+            c.kill()
+        except psutil.Error:
+            pass
+    psutil.wait_procs(left, timeout=10)
+    return [c.pid for c in left]
 
 
 def main():
@@ -168,6 +227,11 @@ def main():
         _lib.call("mg_set_tuning", int(k_), int(v_))
     from moegan_mi.init import init_discriminator, init_generator
     from moegan_mi.step import StepConfig, TrainStep
+    if args.config == "loop":
+        line = loop_bench(args, dev)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        return
 
     E, k, B = args.experts, args.topk, args.batch
     ts = TrainStep(StepConfig(E=E, topk=k, dtype=args.dtype, fp8=args.fp8, max_res=args.max_res), dev,
@@ -235,12 +299,17 @@ def main():
             print(f"[bench] warmup step {i}: {(time.perf_counter() - t_w) * 1e3:.1f} ms", file=sys.stderr, flush=True)
 
     ops.TIMER.active = True
+    # per-step device time for the median: an event between consecutive steps on the stream the
+    # steps are enqueued on (no host synchronisation inside the timed region)
+    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    step_ev[0].record()
     for i in range(args.steps):
         out = one_step()
+        step_ev[i + 1].record()
         if rank == 0 and (i + 1) % max(1, args.steps // 4) == 0:
             print(f"[bench] enqueued {i + 1}/{args.steps} steps", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
@@ -254,6 +323,9 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
     finite = bool(torch.isfinite(out["d_losses"]).all() and torch.isfinite(out["g_gan"]).all())
+    step_ms = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * sum(step_ms[len(step_ms) // 2 - 1:
+                                                                                      len(step_ms) // 2 + 1])
 
     families = fam_meta = None
     if not args.no_families and rank == 0 and world == 1:
@@ -328,6 +400,17 @@ def main():
                 "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                 "traffic": traffic, "traffic_unit": "bytes per launch (HBM, PMC)",
                 "algorithmic_flop_per_launch": flop, "launches_timed": len(kms), "avg_launch_ms": round(avg_ms, 4)}
+        if families:  # the family that takes the most time in the step (rocprof time where committed)
+            def _t(f):
+                return f.get("rocprof_ms_per_step", f["event_ms_per_step"])
+            dom = max((f for f in families if f["bound"] is not None), key=_t, default=None)
+            if dom is not None:
+                roof["dominant"] = {k: dom.get(k) for k in ("family", "bound", "achieved", "peak", "unit", "frac",
+                                                            "launches_per_step", "gflop_per_step", "mb_per_step",
+                                                            "time_source")}
+                roof["dominant"].update({"ms_per_step": round(_t(dom), 4),
+                                         "traffic_mb_per_step": dom.get("traffic_mb_per_step"),
+                                         "share_of_step": round(_t(dom) / ms, 4)})
         if args.config == "C4":  # extension: no reference FLOP formula; the executed MFMA work (roofline.py)
             gf_step = sum(f.get("gflop_per_step", 0.0) for f in (families or []) if f["bound"] == "mfma")
             step_tflops = gf_step * world / (ms * 1e-3) / 1e3 if gf_step else 0.0
@@ -347,7 +430,8 @@ def main():
                 secondary.append(run_secondary(cfg, args))
         line = {"metric": metric, "value": round(value, 2),
                 "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "ms_per_step": round(ms, 3), "ms_per_step_median": round(median_ms, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                 "dtype": args.dtype + ("+mx8" if args.fp8 else ""),
                 "data": "synthetic (U(-1,1) images, N(0,1) 512-d captions, random init)",
                 "config": {"workload": (f"C5 single-GPU slice: 64x64, {E} experts top-{k}, batch {B}/GPU, bf16 with "
@@ -364,6 +448,9 @@ def main():
                 "roofline": roof, "roofline_families": families,
                 "roofline_families_sources": fam_meta, "cpu_baseline": cpu, "secondary": secondary or None}
         print(json.dumps(line), flush=True)
+    left = reap_children()
+    if left:
+        print(f"[bench] ended leftover child processes {left}", file=sys.stderr, flush=True)
     if pg is not None:
         torch.distributed.destroy_process_group()
 

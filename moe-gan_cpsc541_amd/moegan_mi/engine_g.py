@@ -12,6 +12,8 @@ LayerNorm statistics and every parameter gradient stay fp32.
 Randomness is explicit: router epsilon triples, z and the mismatch
 permutation are inputs (SURVEY.md §7 "Randomness parity").
 """
+import os
+
 import torch
 
 from . import _lib as L
@@ -58,6 +60,10 @@ class GeneratorEngine:
         self.E = E
         self.k = topk or E
         self.cdt = cdt
+        # operand dtype of the per-image prefix GEMMs (text projection, mapping, styles and their backward): fp32
+        # even in the bf16 mode, because their rounding is shared by every token of an image and so adds up
+        # coherently (measured on the router temperatures' per-image sums); MOEGAN_PREFIX_BF16=1 = bf16 operands
+        self.pdt = cdt if os.environ.get("MOEGAN_PREFIX_BF16", "0") == "1" else torch.float32
         # MX-fp8 (e4m3 + per-32-channel E8M0 scales) for the 3x3 modulated-conv forward and data-gradient GEMMs
         # (BASELINE config C5); needs the bf16 compute dtype and >= 128 channels on the reduction side
         self.fp8 = bool(fp8)
@@ -91,6 +97,12 @@ class GeneratorEngine:
     def G(self, n):
         return self.st.gview(n)
 
+    def Pp(self, n):
+        return self.P(n) if self.pdt == torch.float32 else self.st.cview(n)
+
+    def _p(self, x, alpha=1.0):
+        return x if (x.dtype == self.pdt and alpha == 1.0) else ops.cast(x, self.pdt, alpha=alpha)
+
     def _c(self, x, alpha=1.0):
         """x in the compute dtype (the mapping / text / style GEMMs run on bf16 operands in bf16 mode, as the
         reference's AMP autocast runs its Linear layers in half precision, t2i_moe_gan.py:1267)."""
@@ -108,7 +120,8 @@ class GeneratorEngine:
             self.style_cols = cols
             self.style_n = nrows
             self.style_W = self.st.data[o0:o0 + nrows * K].view(nrows, K)
-            self.style_Wc = self._cbuf()[o0:o0 + nrows * K].view(nrows, K)
+            self.style_Wc = (self.st.data if self.pdt == torch.float32 else self._cbuf())[o0:o0 + nrows * K].view(
+                nrows, K)
             self.style_b = self.st.data[b0:b0 + nrows]
             self.style_gW = self.st.grad[o0:o0 + nrows * K].view(nrows, K)
             self.style_gb = self.st.grad[b0:b0 + nrows]
@@ -616,7 +629,7 @@ class GeneratorEngine:
         hs = [zt]
         h = zt
         for i in (0, 2, 4):
-            h = ops.linear(h, self.Pc(f"mapping.{i}.weight"), bias=self.P(f"mapping.{i}.bias"), act=LRELU)
+            h = ops.linear(h, self.Pp(f"mapping.{i}.weight"), bias=self.P(f"mapping.{i}.bias"), act=LRELU)
             hs.append(h)
         return h, hs
 
@@ -630,33 +643,33 @@ class GeneratorEngine:
         if text.shape[0] != B and text.shape[0] == 1:
             text = text.expand(B, -1).contiguous()
         # text projection (:682-687, :790)
-        text_c = self._c(text)
-        t0 = ops.linear(text_c, self.Pc("text_projection.0.weight"), bias=self.P("text_projection.0.bias"),
+        text_c = self._p(text)
+        t0 = ops.linear(text_c, self.Pp("text_projection.0.weight"), bias=self.P("text_projection.0.bias"),
                         out_dtype=torch.float32)
         t1, tmu, trs = ops.layernorm_fwd(t0, self.P("text_projection.1.weight"), self.P("text_projection.1.bias"),
                                          act=1)
-        t1c = self._c(t1)
-        text_seq = ops.linear(t1c, self.Pc("text_projection.3.weight"), bias=self.P("text_projection.3.bias"),
+        t1c = self._p(t1)
+        text_seq = ops.linear(t1c, self.Pp("text_projection.3.weight"), bias=self.P("text_projection.3.bias"),
                               out_dtype=torch.float32)
         # mapping + truncation (:793-808)
-        zt = torch.empty(B, z.shape[1] + text.shape[1], device=dev, dtype=self.cdt)
+        zt = torch.empty(B, z.shape[1] + text.shape[1], device=dev, dtype=self.pdt)
         ops.copy2d(z, zt, B, z.shape[1], ldo=zt.shape[1])
         ops.copy2d(text, zt[:, z.shape[1]:], B, text.shape[1], ldo=zt.shape[1])
         h3, hs = self._mapping(zt, save)
         if psi < 1.0:
             if self._mean_latent is None:  # mapping(0): depends on the weights only -> once per prep()
-                zeros = torch.zeros(1, zt.shape[1], device=dev, dtype=self.cdt)
+                zeros = torch.zeros(1, zt.shape[1], device=dev, dtype=self.pdt)
                 m3, _ = self._mapping(zeros, False)
-                self._mean_latent = ops.linear(m3, self.Pc("mapping.6.weight"), bias=self.P("mapping.6.bias"),
+                self._mean_latent = ops.linear(m3, self.Pp("mapping.6.weight"), bias=self.P("mapping.6.bias"),
                                                out_dtype=torch.float32)
             mean = self._mean_latent
             beff = torch.empty(512, device=dev)
             ops.copy2d(self.P("mapping.6.bias").view(1, -1), beff.view(1, -1), 1, 512, alpha=psi)
             ops.copy2d(mean, beff.view(1, -1), 1, 512, alpha=1.0 - psi, accumulate=1)
-            w = ops.linear(h3, self.Pc("mapping.6.weight"), bias=beff, alpha=psi, out_dtype=torch.float32)
+            w = ops.linear(h3, self.Pp("mapping.6.weight"), bias=beff, alpha=psi, out_dtype=torch.float32)
         else:
-            w = ops.linear(h3, self.Pc("mapping.6.weight"), bias=self.P("mapping.6.bias"), out_dtype=torch.float32)
-        w_c = self._c(w)
+            w = ops.linear(h3, self.Pp("mapping.6.weight"), bias=self.P("mapping.6.bias"), out_dtype=torch.float32)
+        w_c = self._p(w)
         # every modulated conv's style in one GEMM: S = w @ [W_mod ...]^T + [b_mod ...] (:158)
         S = S2 = D = None
         if self.style_cols:
@@ -791,34 +804,34 @@ class GeneratorEngine:
             pb.run()
             self._demod_bwd = []
             GS, self._GS = self._GS, None
-            GSc = self._c(GS)
+            GSc = self._p(GS)
             ops.linear_wgrad(GSc, ctx["w_c"], self.style_gW)
             ops.colsum(GS, self.style_gb, defer=True)
             ops.gemm(GSc, self.style_Wc, B, gw.shape[1], self.style_n, b_kc=False, out=gw, ep=E_(accumulate=1))
         # truncation: w = mean + psi (w_full - mean), mean under no_grad
         psi = ctx["psi"]
-        g6 = ops.cast(gw, self.cdt, alpha=psi if psi < 1.0 else 1.0)
+        g6 = ops.cast(gw, self.pdt, alpha=psi if psi < 1.0 else 1.0)
         hs = ctx["hs"]
         ops.linear_wgrad(g6, hs[3], self.G("mapping.6.weight"))
         ops.colsum(g6, self.G("mapping.6.bias"), defer=True)
-        g = ops.linear_dgrad(g6, self.Pc("mapping.6.weight"))
+        g = ops.linear_dgrad(g6, self.Pp("mapping.6.weight"))
         for j, i in enumerate((4, 2, 0)):
             ops.lrelu_mask_mul(g, hs[3 - j], g)
             ops.linear_wgrad(g, hs[2 - j], self.G(f"mapping.{i}.weight"))
             ops.colsum(g, self.G(f"mapping.{i}.bias"), defer=True)
             if i != 0 or want_input_grads:
-                g = ops.linear_dgrad(g, self.Pc(f"mapping.{i}.weight"))
+                g = ops.linear_dgrad(g, self.Pp(f"mapping.{i}.weight"))
         g_zt = g if want_input_grads else None
         # text projection backward
-        g_tsc = self._c(g_ts)
+        g_tsc = self._p(g_ts)
         ops.linear_wgrad(g_tsc, ctx["t1c"], self.G("text_projection.3.weight"))
         ops.colsum(g_ts, self.G("text_projection.3.bias"), defer=True)
-        g_t1 = ops.linear_dgrad(g_tsc, self.Pc("text_projection.3.weight"), out_dtype=torch.float32)
+        g_t1 = ops.linear_dgrad(g_tsc, self.Pp("text_projection.3.weight"), out_dtype=torch.float32)
         ops.lrelu_mask_mul(g_t1, ctx["t1"], g_t1)
         g_t0 = torch.empty_like(g_t1)
         ops.layernorm_bwd(g_t1, ctx["t0"], ctx["tmu"], ctx["trs"], self.P("text_projection.1.weight"), g_t0,
                           self.G("text_projection.1.weight"), self.G("text_projection.1.bias"))
-        ops.linear_wgrad(self._c(g_t0), ctx["text_c"], self.G("text_projection.0.weight"))
+        ops.linear_wgrad(self._p(g_t0), ctx["text_c"], self.G("text_projection.0.weight"))
         ops.colsum(g_t0, self.G("text_projection.0.bias"), defer=True)
         if not want_input_grads:
             return None, None

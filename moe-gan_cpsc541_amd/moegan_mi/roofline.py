@@ -36,9 +36,22 @@ FAMILIES = {
     "r1": ("hbm", ("mg_r1",)),
     "sumsq": ("hbm", ("mg_sumsq",)),
     "adamw": ("hbm", ("mg_adamw_dev", "mg_adamw_dev_shadow", "mg_adamw")),
-    "bias_colsum": ("hbm", ("mg_colsum", "mg_grouped_colsum")),
+    "bias_colsum": ("hbm", ("mg_colsum", "mg_grouped_colsum", "mg_colsum_batch", "mg_segsum", "mg_const_bwd")),
     "weight_prep": ("hbm", ("mg_pack_conv", "mg_pack_conv_flip", "mg_pack_dgrad_s2", "mg_wsq", "mg_wsq_bwd",
-                            "mg_router_reparam", "mg_weight_norm_fwd", "mg_weight_norm_bwd", "mg_quant_mx8")),
+                            "mg_router_reparam", "mg_weight_norm_fwd", "mg_weight_norm_bwd", "mg_quant_mx8",
+                            "mg_prep_batch")),
+    "layernorm": ("hbm", ("mg_layernorm_fwd", "mg_layernorm_bwd")),
+    "router_aux": ("hbm", ("mg_router_bwd", "mg_moe_gate_grad", "mg_moe_token_grad", "mg_router_feat_grad",
+                           "mg_router_param_bwd", "mg_moe_dispatch", "mg_router_kl")),
+    "im2col_col2im": ("hbm", ("mg_im2col_4x4s2", "mg_col2im_4x4s2")),
+    "elementwise": ("hbm", ("mg_cast", "mg_copy2d", "mg_lrelu_mask_mul", "mg_upsample2x_fwd", "mg_upsample2x_bwd",
+                            "mg_const_fwd", "mg_gated_axpy", "mg_select_if", "mg_zero_if", "mg_clip_patches")),
+    "disc_head": ("hbm", ("mg_disc_head_fwd", "mg_disc_head_gmat", "mg_disc_head_sum", "mg_disc_head_bwd_data",
+                          "mg_disc_head_bwd_w", "mg_d_text_bwd")),
+    "mtm_bwd_unfused": ("hbm", ("mg_warp_bwd", "mg_offset_head_bwd")),
+    # scalar losses, guard words, optimizer prologue: a few hundred bytes each, launch-latency bound
+    "losses_flags": ("hbm", ("mg_d_loss", "mg_g_loss", "mg_finite_flag", "mg_flag_window", "mg_kl_coefs", "mg_balance",
+                             "mg_opt_prologue")),
 }
 _FAMILY_OF = {e: f for f, (_, es) in FAMILIES.items() for e in es}
 
@@ -55,13 +68,22 @@ KERNELS = [
     (r"k_router_fwd", "router_fwd"),
     (r"k_gather_rows|k_combine", "dispatch_combine"),
     (r"k_warp_fwd", "warp_fwd"),
-    (r"k_mtm_bwd", "mtm_bwd"),
+    (r"k_mtm_bwd|k_rows_fin", "mtm_bwd"),
     (r"k_bwd_in|k_bwd_out|k_scale_bc", "modconv_bwd_io"),
     (r"k_r1", "r1"),
     (r"k_sumsq", "sumsq"),
     (r"k_adamw", "adamw"),
-    (r"k_colsum|k_grouped_colsum", "bias_colsum"),
-    (r"k_pack_|k_wsq|k_reparam|k_wn_|k_quant_mx8", "weight_prep"),
+    (r"k_colsum|k_grouped_colsum|k_segsum|k_const_bwd", "bias_colsum"),
+    (r"k_pack_|k_wsq|k_reparam|k_wn_|k_quant_mx8|k_prep_batch", "weight_prep"),
+    (r"k_ln_|k_layernorm", "layernorm"),
+    (r"k_router_bwd|k_fold_partials|k_gate_grad|k_token_grad|k_router_feat_grad|k_feat_grad_fin|k_router_param_bwd|"
+     r"k_disp_|k_router_kl", "router_aux"),
+    (r"k_im2col|k_col2im", "im2col_col2im"),
+    (r"k_cast|k_copy2d|k_mask_mul|k_up2|k_const_fwd|k_gated_axpy|k_select_if|k_zero_if|k_clip_patches",
+     "elementwise"),
+    (r"k_head_|k_d_text", "disc_head"),
+    (r"k_warp_bwd|k_offset_head", "mtm_bwd_unfused"),
+    (r"k_d_loss|k_g_loss|k_finite_flag|k_flag_window|k_kl_coefs|k_balance|k_opt_prologue", "losses_flags"),
 ]
 
 
@@ -149,7 +171,118 @@ def work(name, a):
     if name == "mg_weight_norm_bwd":
         return 16.0 * a["O"] * a["K"]
     if name == "mg_colsum":
-        return a["R"] * a["C"] * ELT[a["dtype"]]
+        return a["R"] * a["C"] * ELT[a["dtype"]] + a["C"] * 8
+    if name == "mg_grouped_colsum":  # max_rows = the routed rows (T * k) the engine passes; rs: one fp32 per row
+        return a["max_rows"] * (a["N"] * ELT[a["dtype"]] + (4 if a["rs"] else 0) + 4) + a["G"] * a["N"] * 8
+    if name == "mg_colsum_batch":
+        d = a["descs"]
+        return sum(d[i].R * d[i].C * ELT[d[i].dtype] + d[i].C * 8 for i in range(a["n"]))
+    if name == "mg_segsum":
+        return a["B"] * a["HW"] * a["C"] * ELT[a["dtype"]] + a["B"] * a["C"] * 8
+    if name == "mg_const_bwd":
+        return a["B"] * a["HW"] * a["C"] * ELT[a["dtype"]] + a["HW"] * a["C"] * 8
+    if name == "mg_const_fwd":
+        return a["HW"] * a["C"] * 4 + a["B"] * a["HW"] * a["C"] * ELT[a["dtype"]]
+    if name == "mg_prep_batch":  # per descriptor, the formulas of the single-tensor entry points
+        d, tot = a["descs"], 0.0
+        for i in range(a["n"]):
+            q = d[i]
+            kk = q.KH * q.KW
+            if q.kind == 1:
+                tot += q.Cout * q.Cin * kk * 4 + q.rows * q.Cin * kk * ELT[a["dtype"]]
+            elif q.kind == 2:
+                tot += q.Cout * q.Cin * kk * 4 + q.rows * q.Cout * kk * ELT[a["dtype"]]
+            elif q.kind == 3:
+                tot += q.Cout * q.Cin * 16 * 4 + 16 * q.rows * q.Cout * ELT[a["dtype"]]
+            elif q.kind == 4:
+                tot += q.Cout * q.Cin * kk * 4 + q.rows * q.Cin * 4
+            elif q.kind == 5:
+                tot += q.Cout * q.Cin * (kk * 12 + 4)
+            elif q.kind == 6:
+                tot += 16.0 * q.n
+        return tot
+    if name == "mg_layernorm_fwd":
+        e = ELT[a["dtype"]]
+        return a["R"] * a["C"] * 2 * e + a["R"] * 8 + a["C"] * 8
+    if name == "mg_layernorm_bwd":
+        gx = ELT[a["dtype"]] * (2 if a["accumulate"] else 1)
+        return a["R"] * (a["C"] * (ELT[a["gy_dtype"]] + ELT[a["dtype"]] + gx) + 8) + a["C"] * 16
+    if name == "mg_router_bwd":
+        T, E, k = a["T"], a["E"], a["k"]
+        return T * E * 12 + T * k * 12 + (T * E * 4 if a["g_probs"] else 0) + (T * E * 4 if a["g_logits"] else 0)
+    if name == "mg_moe_gate_grad":  # every routed row of Y and its token's gradient row once
+        T, k, C = a["T"], a["k"], a["C"]
+        return T * k * (C * ELT[a["dtype"]] + 8) + T * C * ELT[a["gout_dtype"]]
+    if name == "mg_moe_token_grad":
+        T, k, C, E = a["T"], a["k"], a["C"], a["E"]
+        gx = T * k * (C * ELT[a["dtype"]] + 4) if a["gX"] else 0
+        return gx + T * E * 4 + C * E * 4 + T * C * ELT[a["out_dtype"]]
+    if name == "mg_router_feat_grad":
+        return a["T"] * (a["C"] * ELT[a["dtype"]] + a["E"] * 4) + a["C"] * a["E"] * 8
+    if name == "mg_router_param_bwd":  # mu, rho, eps, gW read; gmu, grho read-modify-write
+        return 32.0 * a["n"]
+    if name == "mg_moe_dispatch":  # topi + gate in; row_off / perm / pos_of / gate_pos out
+        return a["T"] * a["k"] * 20.0
+    if name == "mg_router_kl":
+        return 8.0 * (a["nf"] + a["nt"] + a["nc"])
+    if name == "mg_im2col_4x4s2":
+        B, H, W = a["B"], a["H"], a["W"]
+        return B * H * W * a["C"] * ELT[a["in_dtype"]] + B * (H // 2) * (W // 2) * a["Kp"] * ELT[a["out_dtype"]]
+    if name == "mg_col2im_4x4s2":
+        B, OH, OW, C = a["B"], a["OH"], a["OW"], a["C"]
+        return B * OH * OW * 16 * C * ELT[a["in_dtype"]] + B * 4 * OH * OW * C * ELT[a["out_dtype"]]
+    if name == "mg_cast":
+        return a["n"] * (ELT[a["in_dtype"]] + ELT[a["out_dtype"]])
+    if name == "mg_copy2d":
+        return a["R"] * a["C"] * (ELT[a["in_dtype"]] + ELT[a["out_dtype"]] * (2 if a["accumulate"] else 1))
+    if name == "mg_lrelu_mask_mul":
+        return a["n"] * (ELT[a["a_dtype"]] + ELT[a["m_dtype"]] + ELT[a["out_dtype"]])
+    if name == "mg_upsample2x_fwd":
+        return a["B"] * a["H"] * a["W"] * a["C"] * ELT[a["dtype"]] * 5
+    if name == "mg_upsample2x_bwd":
+        n = a["B"] * a["H"] * a["W"] * a["C"]
+        return n * 4 * ELT[a["gout_dtype"]] + n * ELT[a["gx_dtype"]] * (2 if a["accumulate"] else 1)
+    if name == "mg_gated_axpy":
+        return 12.0 * a["n"]
+    if name == "mg_select_if":
+        return 8.0 * a["n"]
+    if name == "mg_zero_if":
+        return float(a["bytes"])
+    if name == "mg_clip_patches":  # the 3 image channels in, bf16 patch rows out
+        B, R, res = a["B"], a["R"], a["res"]
+        return B * R * R * 3 * ELT[a["dtype"]] + B * res * res * 3 * 2
+    if name == "mg_disc_head_fwd":
+        return a["B"] * a["Hf"] * a["Hf"] * a["Cf"] * ELT[a["dtype"]] + a["B"] * (a["Hf"] - 3) ** 2 * 4
+    if name == "mg_disc_head_gmat":
+        return a["B"] * (a["Hf"] - 3) ** 2 * 4 + a["B"] * a["Hf"] * a["Hf"] * 16 * ELT[a["out_dtype"]]
+    if name == "mg_disc_head_sum":
+        return a["B"] * a["Hf"] * a["Hf"] * 16 * 4 + a["B"] * (a["Hf"] - 3) ** 2 * 4
+    if name == "mg_disc_head_bwd_data":
+        n = a["B"] * a["Hf"] * a["Hf"] * a["Cf"]
+        return n * (ELT[a["dtype"]] + ELT[a["out_dtype"]]) + a["B"] * (a["Hf"] - 3) ** 2 * 4
+    if name == "mg_disc_head_bwd_w":
+        return a["B"] * a["Hf"] * a["Hf"] * a["Cf"] * ELT[a["dtype"]] + a["B"] * (a["Hf"] - 3) ** 2 * 4
+    if name == "mg_d_text_bwd":
+        return a["B"] * a["Ct"] * 12.0
+    if name == "mg_warp_bwd":
+        P, C = a["B"] * a["H"] * a["W"], a["C"]
+        return P * (C * (ELT[a["gout_dtype"]] + ELT[a["dtype"]] + 8) + 16 + 8)
+    if name == "mg_offset_head_bwd":
+        P = a["B"] * a["H"] * a["W"]
+        return P * (8 + 32 * ELT[a["dtype"]] * 2)
+    if name == "mg_d_loss":
+        B = a["B"]
+        return B * (a["No"] * 2 + a["Nf"]) * 8.0 + B * 8
+    if name == "mg_g_loss":
+        return a["B"] * 8.0
+    if name == "mg_finite_flag":
+        return 4.0 * a["n"]
+    if name == "mg_kl_coefs":
+        return 8.0 * a["R"]
+    if name == "mg_balance":
+        return 8.0 * a["E"]
+    if name in ("mg_flag_window", "mg_opt_prologue"):
+        return 16.0
     if name == "mg_quant_mx8":  # bf16 in, e4m3 + one E8M0 byte per 32 out
         return a["rows"] * a["K"] * (2 + 1 + 1 / 32)
     return None

@@ -351,13 +351,96 @@ def _lr_schedule(lr, num_epochs, lr_warmup_epochs):
     return out
 
 
+class _StepRunner:
+    """Runs the batch body (TrainStep.step) of train_aurora_gan the way bench.py times it: captured once per
+    variant as a chain of hipGraphs (moegan_mi/graphs.py) and replayed on fixed input buffers.
+
+    A variant is everything the step bakes into its launches: the batch shape, the epoch's learning rate,
+    router temperature factor and effective KL weight, and the accumulation window position (zero_grads /
+    step_optim).  The first batch of a new variant runs eagerly on the capture stream -- a real training step
+    that also sizes every lazily allocated buffer -- and the variant is captured right after it (a capture
+    executes nothing), so every later batch of it is one replay.  Graphs of a finished epoch are released when
+    the epoch's scalars change.  A batch whose shape differs from the loader's first batch (a ragged last batch)
+    runs eagerly without capture.  ``enabled=False`` (or a non-HIP device) runs every batch eagerly."""
+
+    def __init__(self, ts, device, enabled=True):
+        self.ts = ts
+        self.enabled = bool(enabled) and torch.device(device).type == "cuda"
+        self.graphs = {}
+        self.epoch_key = None
+        self.shape = None
+
+    def __call__(self, real, text, z, eps_d, eps_g, perm, **kw):
+        if not self.enabled:
+            return self.ts.step(real, text, z, eps_d, eps_g, perm, **kw)
+        from moegan_mi.graphs import SegmentedGraph
+        if self.shape is None:
+            self.shape = tuple(real.shape)
+        if tuple(real.shape) != self.shape:
+            return self.ts.step(real, text, z, eps_d, eps_g, perm, **kw)
+        ekey = (kw["anneal"], kw["lr_g"], kw["lr_d"], kw["eff_kl_weight"], kw.get("acc", 1))
+        if ekey != self.epoch_key:
+            self.graphs.clear()  # the previous epoch's graphs (and their memory pools) go
+            self.epoch_key = ekey
+        key = (kw.get("zero_grads", True), kw.get("step_optim", True))
+        ent = self.graphs.get(key)
+        if ent is None:
+            bufs = dict(real=real.clone(), text=text.clone(), z=z.clone(),
+                        eps_d=[tuple(t.clone() for t in trip) for trip in eps_d], eps_g=eps_g, perm=perm.clone())
+
+            def fn(b=bufs):
+                return self.ts.step(b["real"], b["text"], b["z"], b["eps_d"], b["eps_g"], b["perm"], **kw)
+            g = SegmentedGraph()
+            out = g.run_eager(fn)  # this batch, eagerly
+            outg = g.capture(fn)
+            self.graphs[key] = (g, outg, bufs)
+            return out
+        g, outg, b = ent
+        with torch.no_grad():
+            b["real"].copy_(real)
+            b["text"].copy_(text)
+            b["z"].copy_(z)
+            b["perm"].copy_(perm)
+            for dst, src in zip(b["eps_d"], eps_d):
+                for x, y in zip(dst, src):
+                    x.copy_(y)
+            for dst, src in zip(b["eps_g"], eps_g):
+                for x, y in zip(dst, src):
+                    if x.data_ptr() != y.data_ptr():
+                        x.copy_(y)
+        g.replay()
+        return outg
+
+
+class _NoEvent:
+    def synchronize(self):
+        pass
+
+
+_STAT_KEYS = ("flags", "d_losses", "r1", "g_gan", "balance", "kl", "clip16", "clip8")
+
+
+def _stats_to_host(out):
+    """The step's guard word and logged losses as one asynchronous copy into pinned host memory (read after the
+    NEXT batch is enqueued, so the host never waits for the batch it just launched)."""
+    vals = [out["flags"][:1].float()] + [out[k].reshape(-1)[:1].float() if out.get(k) is not None
+                                         else torch.zeros(1, device=out["flags"].device) for k in _STAT_KEYS[1:]]
+    dev_vec = torch.cat(vals)
+    host = torch.empty(dev_vec.shape, dtype=torch.float32, pin_memory=True)
+    host.copy_(dev_vec, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return host, ev
+
+
 def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, beta1=0.5, beta2=0.999,
                      r1_gamma=10.0, clip_weight_16=0.1, clip_weight_8=0.05, kl_weight=0.001, kl_annealing_epochs=5,
                      lr_warmup_epochs=3, balance_weight=0.01, device=DEVICE, save_dir="./aurora_checkpoints",
                      log_interval=10, save_interval=1000, metric_callback=None, use_amp=True,
                      gradient_accumulation_steps=8, checkpoint_activation=True, batch_memory_limit=20.0,
                      max_resolution=16, *, clip_weight_64=None, clip_weight_32=None, num_experts=NUM_EXPERTS,
-                     topk=None, dtype=None, process_group=None, seed=0, resume_from=None, save_every_epoch=False):
+                     topk=None, dtype=None, process_group=None, seed=0, resume_from=None, save_every_epoch=False,
+                     use_graphs=True, on_batch_done=None):
     """Reference :1029-1669.  ``clip_weight_64``/``clip_weight_32`` (the names train_model.py passes,
     SURVEY.md §0) map to the 16x16 / 8x8 CLIP weights.  ``use_amp`` selects bf16 (the MI355X mixed
     precision; the reference's fp16 GradScaler is not needed) unless ``dtype`` is given.
@@ -369,7 +452,10 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
     decision of ``metric_callback`` (called on rank 0) is broadcast so every rank leaves the loop together.
 
     Loss guards (:1315-1320, :1367-1376, :1396-1399) run inside the step on the device; the loop reads the
-    step's flag word once per batch to print the reference's warnings and to not count a skipped batch.
+    step's flag word once per batch to print the reference's warnings and to not count a skipped batch.  That
+    read (with the logged losses, one pinned copy) is deferred until the next batch has been enqueued.
+    ``use_graphs``: every batch body is a replayed hipGraph (``_StepRunner``, bench.py's launch mode).
+    ``on_batch_done(epoch, batch_idx)``: called when a batch's results have reached the host (bench.py --loop).
     ``resume_from``: a resume checkpoint (:1484-1491 layout, ours or the reference's) to start from;
     ``save_every_epoch``: write that layout after every epoch (the reference's commented-out :1642-1652)."""
     os.makedirs(save_dir, exist_ok=True)
@@ -410,6 +496,7 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
     g_local = torch.Generator(device=device).manual_seed(1_000_003 * (seed + 1) + 7919 * rank)
     g_shared = torch.Generator(device=device).manual_seed(1_000_003 * (seed + 1) + 17)
     from tqdm import tqdm
+    runner = _StepRunner(ts, device, enabled=use_graphs)
     for epoch in range(start_epoch, num_epochs):
         cur_lr = lrs[epoch]
         kl_warmup = min(1.0, (epoch / kl_annealing_epochs) ** 2)
@@ -425,6 +512,34 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
         # batch i+1's host -> HBM copy overlaps batch i's step (moegan_mi/prefetch.py)
         pbar = tqdm(DevicePrefetcher(dataloader, device), desc=f"Epoch {epoch + 1}/{num_epochs}", disable=rank != 0)
         n_batches = len(dataloader)
+        pending = None
+
+        def account(rec):
+            """The reference's per-batch host work for a finished batch (:1315-1320 warnings, :1441-1471 logging)."""
+            nonlocal step
+            host, ev, bidx = rec
+            ev.synchronize()
+            if on_batch_done is not None:
+                on_batch_done(epoch, bidx)
+            v = host.tolist()
+            flags = int(v[0])
+            if flags & 1:
+                print("⚠️ NaN/Inf detected in discriminator loss! Skipping this batch.")
+                return
+            if flags & 2:
+                print("⚠️ NaN or Inf detected in generator loss! Resetting to zero.")
+            if step % log_interval == 0 and rank == 0:
+                d_gan, r1, g_gan, bal, kl, c16, c8 = v[1:8]
+                g_loss = 0.0 if flags & 2 else g_gan + clip_weight_16 * c16 + clip_weight_8 * c8 + bal
+                g_loss += eff_kl * kl
+                logger.info(f"\nStep [{step}] Epoch [{epoch + 1}] Batch [{bidx}/{n_batches}] "
+                            f"D_loss: {d_gan + r1:.4f} (GAN: {d_gan:.4f}, R1: {r1:.4f}), "
+                            f"G_loss: {g_loss:.4f} (GAN: {g_gan:.4f}, Clip16: {c16:.4f}, Clip8: {c8:.4f}, "
+                            f"KL: {kl:.4f}, Balance: {bal:.4f})")
+                pbar.set_postfix({"D_loss": f"{d_gan:.3f}", "R1": f"{r1:.3f}", "G_loss": f"{g_gan:.3f}",
+                                  "KL": f"{kl:.4f}", "Balance": f"{bal:.4f}", "Clip16": f"{c16:.3f}",
+                                  "Clip8": f"{c8:.3f}"})
+            step += 1
         for batch_idx, (real, text) in enumerate(pbar):
             real = real.to(device, non_blocking=True).float()
             text = text.to(device, non_blocking=True).float()
@@ -435,29 +550,18 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
             perm = torch.randperm(B, device=device, generator=g_local).int()
             zero = batch_idx % acc == 0
             stp = (batch_idx + 1) % acc == 0 or (batch_idx + 1) == n_batches
-            out = ts.step(real, text, z, eps_d, eps_g, perm, anneal=temperature_factor, lr_g=cur_lr, lr_d=cur_lr,
-                          eff_kl_weight=eff_kl, acc=acc, zero_grads=zero, step_optim=stp)
-            flags = int(out["flags"][0])  # the step's guard word: one read per batch
-            if flags & 1:
-                print("⚠️ NaN/Inf detected in discriminator loss! Skipping this batch.")
-                continue
-            if flags & 2:
-                print("⚠️ NaN or Inf detected in generator loss! Resetting to zero.")
-            if step % log_interval == 0 and rank == 0:
-                d_gan, r1 = float(out["d_losses"][0]), float(out["r1"][0])
-                g_gan, bal, kl = float(out["g_gan"][0]), float(out["balance"][0]), float(out["kl"][0])
-                c16 = float(out["clip16"][0]) if out["clip16"] is not None else 0.0
-                c8 = float(out["clip8"][0]) if out["clip8"] is not None else 0.0
-                g_loss = 0.0 if flags & 2 else g_gan + clip_weight_16 * c16 + clip_weight_8 * c8 + bal
-                g_loss += eff_kl * kl
-                logger.info(f"\nStep [{step}] Epoch [{epoch + 1}] Batch [{batch_idx}/{n_batches}] "
-                            f"D_loss: {d_gan + r1:.4f} (GAN: {d_gan:.4f}, R1: {r1:.4f}), "
-                            f"G_loss: {g_loss:.4f} (GAN: {g_gan:.4f}, Clip16: {c16:.4f}, Clip8: {c8:.4f}, "
-                            f"KL: {kl:.4f}, Balance: {bal:.4f})")
-                pbar.set_postfix({"D_loss": f"{d_gan:.3f}", "R1": f"{r1:.3f}", "G_loss": f"{g_gan:.3f}",
-                                  "KL": f"{kl:.4f}", "Balance": f"{bal:.4f}", "Clip16": f"{c16:.3f}",
-                                  "Clip8": f"{c8:.3f}"})
-            step += 1
+            out = runner(real, text, z, eps_d, eps_g, perm, anneal=temperature_factor, lr_g=cur_lr, lr_d=cur_lr,
+                         eff_kl_weight=eff_kl, acc=acc, zero_grads=zero, step_optim=stp)
+            if device.type == "cuda":
+                rec = _stats_to_host(out) + (batch_idx,)
+            else:
+                rec = (torch.stack([out[k].reshape(-1)[0].float() if out.get(k) is not None else torch.zeros(())
+                                    for k in _STAT_KEYS]), _NoEvent(), batch_idx)
+            if pending is not None:
+                account(pending)  # the previous batch, now that this one is enqueued
+            pending = rec
+        if pending is not None:
+            account(pending)
         pbar.close()
         if save_every_epoch and rank == 0:
             save_resume(os.path.join(save_dir, f"aurora_checkpoint_epoch_{epoch + 1}.pt"), generator, discriminator,

@@ -226,8 +226,11 @@ def router_temp_terms(z, topi, g_gate, coef, te, anneal, k):
 
 
 class DeviceTempTap:
-    """Records, per MoE block, the inputs of the device's router backward (ops.router_bwd) and the amount its
-    kernel added to the temperature gradient."""
+    """Keeps, per MoE block, the inputs of the device's router backward (ops.router_bwd) and the temperature
+    gradient it writes.  References, not copies: under hipGraph capture they are the graph's static buffers, so
+    ``results()`` read after a replay sees the replayed values; eagerly they are that step's tensors.  Assumes the
+    temperature gradient is zeroed at the start of the G phase (gradient_accumulation_steps = 1), so after the
+    step it holds exactly the router backward kernel's fold."""
 
     def __init__(self):
         self.rec = {}
@@ -237,22 +240,31 @@ class DeviceTempTap:
         self.ops, self.orig = ops, ops.router_bwd
 
         def rb(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, anneal, g_temp, Bn, g_logits=None):
-            before = g_temp.detach().clone()
-            r = self.orig(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, anneal, g_temp, Bn,
-                          g_logits)
-            torch.cuda.synchronize()
-            te = min(max(float(temperature.detach().cpu()[0]) * anneal, 0.5), 5.0)
-            k = topi.shape[1]
-            terms = router_temp_terms(zlog.detach().cpu(), topi.detach().cpu(), g_gate.detach().float().cpu(),
-                                      None if coef is None else coef.detach().cpu(), te, anneal, k)
-            self.rec[BLOCK_OF_HW.get(HW, HW)] = dict(terms=terms, kernel=float((g_temp.detach() - before).cpu()[0]))
-            return r
+            # the temperature as it is now (an enqueued copy: the optimizer updates the parameter later in the step)
+            self.rec[BLOCK_OF_HW.get(HW, HW)] = dict(zlog=zlog, topi=topi, g_gate=g_gate, coef=coef,
+                                                     temperature=temperature.detach().clone(), anneal=anneal,
+                                                     g_temp=g_temp)
+            return self.orig(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temperature, anneal, g_temp, Bn,
+                             g_logits)
         ops.router_bwd = rb
         return self
 
     def __exit__(self, *exc):
         self.ops.router_bwd = self.orig
         return False
+
+    def results(self):
+        """{block: dict(terms=[T] fp64 restatement from the kernel's inputs, kernel=its fold)}."""
+        torch.cuda.synchronize()
+        out = {}
+        for blk, r in self.rec.items():
+            te = min(max(float(r["temperature"].detach().cpu()[0]) * r["anneal"], 0.5), 5.0)
+            k = r["topi"].shape[1]
+            terms = router_temp_terms(r["zlog"].detach().cpu(), r["topi"].detach().cpu(),
+                                      r["g_gate"].detach().float().cpu(),
+                                      None if r["coef"] is None else r["coef"].detach().cpu(), te, r["anneal"], k)
+            out[blk] = dict(terms=terms, kernel=float(r["g_temp"].detach().cpu()[0]))
+        return out
 
 
 class OracleTempTap:
@@ -303,3 +315,69 @@ def training_router_matches(orig, tapped):
     f, t = torch.randn(T, C, generator=g), torch.randn(T, 512, generator=g)
     a, b = orig(f, t, P, "r.", eps, True, 3.0), tapped(f, t, P, "r.", eps, True, 3.0)
     return torch.allclose(a[0], b[0], atol=1e-6) and torch.allclose(a[1], b[1], atol=1e-5)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# hipGraph replay of the product step, exactly as bench.py runs it (SegmentedGraph: warm-up on the capture stream,
+# capture, replay with fixed input buffers)
+# ---------------------------------------------------------------------------------------------------------------
+def step_state(ts):
+    """Every device tensor a training step reads and updates (parameters, moments, bf16 shadow, AdamW step
+    counters, the accumulation-window word)."""
+    ts_ = []
+    for st in (ts.gs, ts.ds):
+        ts_ += [st.data, st.m, st.v, st.step_dev, st.step_dev_kl] + ([st.shadow] if st.shadow is not None else [])
+    return ts_ + [ts.win]
+
+
+def snapshot(ts):
+    return [t.detach().clone() for t in step_state(ts)]
+
+
+def restore(ts, snap):
+    with torch.no_grad():
+        for t, s in zip(step_state(ts), snap):
+            t.copy_(s)
+
+
+class ReplayedStep:
+    """Captures ``ts.step`` on fixed input buffers the way bench.py does and replays it.  The warm-up step that
+    sizes every lazily allocated buffer changes the model; the state from before it is restored after the
+    capture, so the first replay starts where an eager step would."""
+
+    def __init__(self, ts, real, text, z, eps_d, eps_g, perm, tap=None, **kw):
+        from moegan_mi.graphs import SegmentedGraph
+        self.ts = ts
+        dev = ts.dev
+        self.buf = dict(real=real.to(dev).clone(), text=text.to(dev).clone(), z=z.to(dev).clone(),
+                        eps_d=[tuple(t.to(dev).clone() for t in e) for e in eps_d],
+                        eps_g=[tuple(t.to(dev).clone() for t in e) for e in eps_g],
+                        perm=perm.to(dev).int().clone())
+        b = self.buf
+        fn = lambda: ts.step(b["real"], b["text"], b["z"], b["eps_d"], b["eps_g"], b["perm"], **kw)  # noqa: E731
+        snap = snapshot(ts)
+        self.graph = SegmentedGraph()
+        self.graph.run_eager(fn)
+        torch.cuda.synchronize()
+        if tap is not None:
+            with tap:
+                self.out = self.graph.capture(fn)
+        else:
+            self.out = self.graph.capture(fn)
+        torch.cuda.synchronize()
+        restore(ts, snap)
+
+    def __call__(self, real, text, z, eps_d, eps_g, perm):
+        b = self.buf
+        with torch.no_grad():
+            b["real"].copy_(real)
+            b["text"].copy_(text)
+            b["z"].copy_(z)
+            for dst, src in ((b["eps_d"], eps_d), (b["eps_g"], eps_g)):
+                for td, tsrc in zip(dst, src):
+                    for x, y in zip(td, tsrc):
+                        x.copy_(y)
+            b["perm"].copy_(perm.int())
+        self.graph.replay()
+        torch.cuda.synchronize()
+        return self.out

@@ -165,7 +165,7 @@ def test_attention_block_module_vs_oracle(E, topk):
     _check_param_grads(m, P)
 
 
-@pytest.mark.parametrize("cin,cout,H", [(256, 128, 16), (512, 512, 4)])
+@pytest.mark.parametrize("cin,cout,H", [(256, 128, 16), (512, 512, 4), (512, 256, 8)])
 def test_convolution_block_module_vs_oracle(cin, cout, H):
     M = _M()
     B = 2

@@ -15,13 +15,15 @@ Bar, written per check below (SURVEY.md §8(c) asks 2e-2 on outputs and cosine >
     gradient by ~4 % (steputil.bf16_r1_floor) -- and the device sits at 1.5-2x that floor.  SURVEY §8(c)'s
     per-tensor 0.999 is therefore not reachable in bf16 at all; per-tensor parity at 1e-3 is the fp32 mode's
     job (F7 / F8 / F10 in test_engine_gpu.py).  Each tensor's error and floor are printed (a tensor whose own floor
-    is >= 20 % -- an expert few tokens reach at this batch -- is held to FLOOR_X x its floor instead of the cosine);
+    is >= 20 % -- an expert few tokens reach at this batch -- is held to FLOOR_X x its floor instead of the cosine,
+    and a tensor of fewer than 64 elements, a sum over every pixel of the batch, may sit within FLOOR_X x its own
+    whole-step floor instead);
   * the router temperatures (t2i_moe_gan.py:374-377; one scalar per block, a cancelling sum over tokens of
     -anneal/te * sum_e dL/dl * l) are checked on their parts: the kernel's fixed-order fold equals the fp64
-    restatement of its own inputs (1e-5 of the summed magnitudes); the per-token terms are within FLOOR_X x the
-    whole-step floor run's per-token error; the sum is within FLOOR_X x its floor (the floor run's error on the
-    sum or the root-sum-square of its per-token errors, whichever is larger) and has the reference's sign
-    wherever it stands above that floor.  The other single-element tensors (D's head bias / gain) are held to
+    restatement of its own inputs (1e-5 of the summed magnitudes); the per-token terms and the per-image sums
+    (an image's tokens share its style, text and discriminator gradient, so that is where errors add coherently)
+    are each within FLOOR_X x the whole-step floor run's relative error; the block's sum has the reference's sign
+    wherever it exceeds FLOOR_X x the root-sum-square of the floor run's per-image errors.  The other single-element tensors (D's head bias / gain) are held to
     relative error <= max(2e-2, FLOOR_X x floor);
   * top-k expert selection: the device picks a top-k of its own probabilities; its sets equal the oracle's own
     fp32 top-k wherever the oracle margin log(p_(k)/p_(k+1)) exceeds DELTA, DELTA bounds the measured drift of
@@ -47,7 +49,7 @@ import torch
 
 from goldens import T, load
 from oracle import aurora_cpu as O
-from steputil import (DeviceTempTap, OracleTempTap, bf16_module_rounding, bf16_r1_floor, cosine, gpu_step,
+from steputil import (DeviceTempTap, OracleTempTap, ReplayedStep, bf16_module_rounding, bf16_r1_floor, cosine, gpu_step,
                       make_inputs, nchw, oracle_clone, oracle_models, rel_norm_diff, routing_agreement, whole)
 
 pytestmark = pytest.mark.gpu
@@ -103,11 +105,18 @@ def _replay_adamw(store, p_before, mv_before, grad, coef, lr, b1=0.5, b2=0.999, 
     return (err2 / max(ref2, 1e-300)) ** 0.5
 
 
-def _run(E, topk, inputs_per_step, lr=2e-4):
+def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
+    """``replay``: the device step is the hipGraph-captured step replayed on fixed input buffers (bench.py's launch
+    mode, steputil.ReplayedStep) instead of the eager one; every check is the same."""
     ts = gpu_step(E, topk, "bf16", DEV)
     PG, PD, optG, optD, rgrads = oracle_models(E, lr=lr)
     report, fails = [], []
     k = topk or E
+    rs = dtap_replay = None
+    if replay:
+        dtap_replay = DeviceTempTap()
+        rs = ReplayedStep(ts, *inputs_per_step[0], tap=dtap_replay, anneal=3.0, lr_g=lr, lr_d=lr,
+                          eff_kl_weight=EFF_KL)
 
     def check(ok, what):
         if not ok:
@@ -118,10 +127,14 @@ def _run(E, topk, inputs_per_step, lr=2e-4):
         pg_before = {n: v.detach().clone() for n, v in PG.items()}
         pd_before = {n: v.detach().clone() for n, v in PD.items()}
         cu = lambda t: t.to(DEV)  # noqa: E731
-        with DeviceTempTap() as dtap:
-            out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d],
-                          [tuple(map(cu, e)) for e in eps_g], cu(perm.int()), anneal=3.0, lr_g=lr, lr_d=lr,
-                          eff_kl_weight=EFF_KL)
+        if rs is not None:
+            out, dtap = rs(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d],
+                           [tuple(map(cu, e)) for e in eps_g], cu(perm.int())), dtap_replay
+        else:
+            with DeviceTempTap() as dtap:
+                out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d],
+                              [tuple(map(cu, e)) for e in eps_g], cu(perm.int()), anneal=3.0, lr_g=lr, lr_d=lr,
+                              eff_kl_weight=EFF_KL)
         torch.cuda.synchronize()
         assert int(out["flags"][0]) == 0
         routes_d = routes_g = None
@@ -158,7 +171,7 @@ def _run(E, topk, inputs_per_step, lr=2e-4):
                                after_d_step=lambda P: (pd_stepped.update({n: t.detach().clone() for n, t in P.items()}),
                                                        use_device_d(P)))
         # ---- router temperatures (scalar cancelling sums) ----
-        for blk, rec in sorted(dtap.rec.items()):
+        for blk, rec in sorted(dtap.results().items()):
             t_dev, t_ref, t_flo = rec["terms"], rtap.terms(blk), wtap.terms(blk)
             s_dev, s_ref, s_flo = float(t_dev.sum()), float(t_ref.sum()), float(t_flo.sum())
             # (a) the kernel: its fixed-order fp32 fold equals the fp64 restatement of its own inputs
@@ -167,16 +180,19 @@ def _run(E, topk, inputs_per_step, lr=2e-4):
             check(abs(rec["kernel"] - s_dev) <= 1e-5 * scale + 1e-12, report[-1])
             # (b) its per-token terms against the oracle's, within FLOOR_X x the whole-step bf16 floor's
             e_tok, f_tok = rel_norm_diff(t_dev, t_ref), rel_norm_diff(t_flo, t_ref)
-            # (c) the sum within FLOOR_X x its floor: the floor run's own error on the sum, or the root-sum-square
-            # of its per-token errors (the noise a sum of independently perturbed terms carries) if larger -- one
-            # rounding sample alone can land arbitrarily close to the reference by chance
-            f_sum = max(abs(s_flo - s_ref), float((t_flo - t_ref).norm()))
+            # (c) the per-image sums (the image is where errors are coherent: one image's tokens share its style
+            # vector, text and discriminator gradient) within FLOOR_X x the floor run's, relative L2 over the images
+            nimg = len(real)
+            i_dev, i_ref, i_flo = (t.view(nimg, -1).sum(1) for t in (t_dev, t_ref, t_flo))
+            e_img, f_img = rel_norm_diff(i_dev, i_ref), rel_norm_diff(i_flo, i_ref)
+            # (d) the block's sum has the reference's sign wherever it stands above the noise the floor run's
+            # per-image errors put on a sum of independent images (their root-sum-square)
+            f_sum = float((i_flo - i_ref).norm())
             report.append(f"step{si} {blk} temperature gradient {s_dev:+.4e} vs {s_ref:+.4e} (abs err "
-                          f"{abs(s_dev - s_ref):.2e}, floor {f_sum:.2e}); per-token terms rel err {e_tok:.2e} "
-                          f"(floor {f_tok:.2e})")
+                          f"{abs(s_dev - s_ref):.2e}, floor {f_sum:.2e}); per-image sums rel err {e_img:.2e} (floor "
+                          f"{f_img:.2e}); per-token terms rel err {e_tok:.2e} (floor {f_tok:.2e})")
             check(e_tok <= FLOOR_X * f_tok, report[-1])
-            check(abs(s_dev - s_ref) <= FLOOR_X * f_sum, report[-1])
-            # (d) the sign wherever the value stands above that floor
+            check(e_img <= FLOOR_X * f_img, report[-1])
             check(abs(s_ref) <= FLOOR_X * f_sum or s_dev * s_ref > 0, report[-1])
         # ---- routing ----
         for tag, dev_t, dev_p, ref_p in (("D", out["topi_d"], out["probs_d"], ref["probs_d"]),
@@ -249,10 +265,17 @@ def _run(E, topk, inputs_per_step, lr=2e-4):
                 # tokens reach at a test-sized batch) is held to FLOOR_X x its floor instead.  The router
                 # temperatures (single-element cancelling sums) are checked above on their per-token terms; the
                 # other single-element tensors (the discriminator head's bias and gain) by their relative error
+                fw = rel_norm_diff(wgrads[which][n], rg) if wgrads[which].get(n) is not None else fl
                 if n.endswith("router.temperature"):
                     pass
                 elif numel == 1:
                     check(rn <= max(REL, FLOOR_X * fl), f"step{si} grad {which}:{n} rel {rn:.2e} (floor {fl:.2e})")
+                elif numel < 64:
+                    # a few-element sum over every pixel of the batch (the MTM offset heads' biases): its cosine is
+                    # as noisy as the sum is cancelling, so it may instead sit within FLOOR_X x its own whole-step
+                    # bf16 floor
+                    check(c >= COS_TENSOR or rn <= FLOOR_X * fw,
+                          f"step{si} grad {which}:{n} cosine {c:.6f} rel {rn:.2e} (whole-step floor {fw:.2e})")
                 else:
                     check(c >= COS_TENSOR or (fl >= 0.2 and rn <= FLOOR_X * fl),
                           f"step{si} grad {which}:{n} cosine {c:.6f} rel {rn:.2e} (floor {fl:.2e})")
@@ -305,6 +328,13 @@ def test_bf16_c2_step_vs_oracle(B):
     """C2 configuration (E=8 top-2, bf16) at a test-sized batch, two consecutive steps."""
     E = 8
     _run(E, 2, [make_inputs(B, E, seed=100 + B), make_inputs(B, E, seed=200 + B)])
+
+
+def test_bf16_c2_graph_replay_vs_oracle():
+    """The launch mode bench.py times: the C2 step captured as hipGraphs and replayed on fixed input buffers, two
+    consecutive steps at B=8 against the fp32 oracle with every bar of the eager test above."""
+    E = 8
+    _run(E, 2, [make_inputs(8, E, seed=308), make_inputs(8, E, seed=408)], replay=True)
 
 
 def test_bf16_dense_e4_step_vs_F8():
