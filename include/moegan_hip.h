@@ -267,7 +267,9 @@ int mg_lrelu_mask_mul(int a_dtype, const void* a, int m_dtype, const void* m, in
 /* out[b,c] += sum_{p<HW} X[b*HW+p, c]  (per-image sums: cross-attention vector gradient). */
 int mg_segsum(int dtype, const void* X, int64_t ld, int B, int HW, int C, float* out, void* stream);
 
-/* ModulatedConv backward, output side: gyt = gy*d (gy = gz * lrelu'), gdd = -0.5 d^2 sum_pix gy*y; z may carry a fused residual (zsub). t2i_moe_gan.py:154-186. */
+/* ModulatedConv backward, output side: gyt = gy*d (gy = gz * lrelu'), gdd = -0.5 d^2 sum_pix gy*y; z may carry a fused residual (zsub).
+   act: 0 none, 1 = z is LeakyReLU(0.2)(y) (inverted), 2 = z is the pre-activation y itself (stored by the forward's
+   out_pre epilogue when a residual is fused: its sign is exact).  t2i_moe_gan.py:154-186. */
 int mg_modconv_bwd_out(int dtype, int gz_dtype, const void* gz, int64_t ld_gz, const void* z, int64_t ld_z, const void* zsub, int64_t ld_zsub, const float* d, int B, int HW, int Cout, int act, void* gyt, int64_t ld_gyt, float* gdd, void* stream);
 
 /* Row gather: out[r, :C] = src[idx[r] / idx_div, :C] * (rowscale ? rowscale[r] : 1)  (MoE dispatch

@@ -51,7 +51,8 @@ template <typename T, typename TG, int NPL>
 __global__ void k_ln_bwd(const TG* __restrict__ gy, int64_t ldg, const T* __restrict__ x, int64_t ldx, int R,
                          const float* __restrict__ mean, const float* __restrict__ rstd,
                          const float* __restrict__ gamma, T* __restrict__ gx, int64_t ldgx, int accumulate,
-                         float* __restrict__ ggamma, float* __restrict__ gbeta, int rows_per_wave) {
+                         float* __restrict__ ggamma, float* __restrict__ gbeta, int rows_per_wave,
+                         float* __restrict__ part) {
   int lane = threadIdx.x & 63;
   constexpr int C = NPL * 64;
   float pg[NPL], pb[NPL];
@@ -87,7 +88,13 @@ __global__ void k_ln_bwd(const TG* __restrict__ gy, int64_t ldg, const T* __rest
       }
     }
   }
-  if (ggamma) {
+  if (ggamma && part) {  // deterministic mode: the wave's partial row, folded in wave order by the launcher
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      part[(int64_t)wave * 2 * C + lane + 64 * i] = pg[i];
+      part[(int64_t)wave * 2 * C + C + lane + 64 * i] = pb[i];
+    }
+  } else if (ggamma) {
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
       atomicAdd(ggamma + lane + 64 * i, pg[i]);
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd_v(const TG* __restrict__ gy, int
                                                   const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                   T* __restrict__ gx, int64_t ldgx, int accumulate,
                                                   float* __restrict__ ggamma, float* __restrict__ gbeta,
-                                                  int rows_per_wave) {
+                                                  int rows_per_wave, float* __restrict__ part) {
   constexpr int C = LPR * 8, RPW = 64 / LPR;
   __shared__ float red[2][4][C];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sl = lane / LPR, c = (lane % LPR) * 8;
@@ -372,7 +379,8 @@ __global__ __launch_bounds__(256) void k_ln_bwd_v(const TG* __restrict__ gy, int
     const int k = i / C, cc = i - k * C;
     float s = 0.f;
     for (int q = 0; q < nw; ++q) s += red[k][q][cc];
-    atomicAdd((k ? gbeta : ggamma) + cc, s);
+    if (part) part[(int64_t)blockIdx.x * 2 * C + i] = s;  // deterministic mode: folded in block order
+    else atomicAdd((k ? gbeta : ggamma) + cc, s);
   }
 }
 
@@ -423,8 +431,13 @@ extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t
     int rows = std::max(2 * rw, cdiv(R, 1024));
     rows = cdiv(rows, 2 * rw) * 2 * rw;
     dim3 g2(cdiv(cdiv(R, rows), 4)), b2(256);
+    float* part = nullptr;
+    if (ggamma && mg_det()) {
+      part = reinterpret_cast<float*>(mg_workspace((size_t)g2.x * 2 * C * sizeof(float), st));
+      if (!part) return MG_ERR_LAUNCH;
+    }
 #define LV_(T, TG, P) hipLaunchKernelGGL((k_ln_bwd_v<T, TG, P>), g2, b2, 0, st, (const TG*)gy, ldg, (const T*)x, ldx, R, \
-                                         mean, rstd, gamma, (T*)gx, ldgx, accumulate, ggamma, gbeta, rows)
+                                         mean, rstd, gamma, (T*)gx, ldgx, accumulate, ggamma, gbeta, rows, part)
 #define LVC_(T, TG) if (C == 128) LV_(T, TG, 16); else if (C == 256) LV_(T, TG, 32); else LV_(T, TG, 64)
     if (dtype == MG_F32) {
       if (gy_dtype == MG_F32) { LVC_(float, float); } else { LVC_(float, bf16_t); }
@@ -433,12 +446,19 @@ extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t
     }
 #undef LVC_
 #undef LV_
+    if (part) mg_det_fold_rows(part, (int)g2.x, 2 * C, C, ggamma, gbeta, st);
     return mg_check_launch("mg_layernorm_bwd");
   }
   int rpw = std::max(1, std::min(64, R / 1024));
   dim3 grid(cdiv(cdiv(R, rpw), 4)), blk(256);
+  float* part = nullptr;
+  if (ggamma && mg_det()) {
+    part = reinterpret_cast<float*>(mg_workspace((size_t)grid.x * 4 * 2 * C * sizeof(float), st));
+    if (!part) return MG_ERR_LAUNCH;
+    (void)hipMemsetAsync(part, 0, (size_t)grid.x * 4 * 2 * C * sizeof(float), st);  // waves past R leave their row
+  }
 #define L_(T, TG, N) hipLaunchKernelGGL((k_ln_bwd<T, TG, N>), grid, blk, 0, st, (const TG*)gy, ldg, (const T*)x, ldx, R, \
-                                        mean, rstd, gamma, (T*)gx, ldgx, accumulate, ggamma, gbeta, rpw)
+                                        mean, rstd, gamma, (T*)gx, ldgx, accumulate, ggamma, gbeta, rpw, part)
 #define LC_(T, TG) if (C == 128) L_(T, TG, 2); else if (C == 256) L_(T, TG, 4); else L_(T, TG, 8)
   if (dtype == MG_F32) {
     if (gy_dtype == MG_F32) { LC_(float, float); } else { LC_(float, bf16_t); }
@@ -447,6 +467,7 @@ extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t
   }
 #undef LC_
 #undef L_
+  if (part) mg_det_fold_rows(part, (int)grid.x * 4, 2 * C, C, ggamma, gbeta, st);
   return mg_check_launch("mg_layernorm_bwd");
 }
 

@@ -263,6 +263,14 @@ extern "C" int mg_prep_batch(int dtype, int n, const mg_prep_desc* descs, void* 
 extern "C" int mg_colsum_batch(int n, const mg_colsum_desc* descs, void* stream) {
   MG_REQUIRE(n >= 0 && (n == 0 || descs), "bad descriptor table");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (mg_det()) {  // deterministic mode: each sum by mg_colsum's fixed-order fold, one after the other
+    for (int i = 0; i < n; ++i) {
+      const mg_colsum_desc& q = descs[i];
+      int rc = mg_colsum(q.dtype, q.X, q.ld, q.R, q.C, q.out, stream);
+      if (rc) return rc;
+    }
+    return MG_OK;
+  }
   for (int i0 = 0; i0 < n; i0 += kMaxDesc) {
     ColsumArgs a{};
     a.n = 0;

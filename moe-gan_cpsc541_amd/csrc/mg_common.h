@@ -104,12 +104,54 @@ int mg_check_launch(const char* what);
 // Tuning overrides (0 = automatic), set through mg_set_tuning for A/B measurements.
 enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, MG_TUNE_GEMM_TILE = 3,
        MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_XCD = 6, MG_TUNE_WGRAD_MODE = 7,
-       MG_TUNE_WARP_LDS = 8, MG_TUNE_SHORTK = 9, MG_TUNE_ATOMIC_BLOCKS = 10,
+       MG_TUNE_WARP_LDS = 8, MG_TUNE_SHORTK = 9, MG_TUNE_ATOMIC_BLOCKS = 10, MG_TUNE_DETERMINISTIC = 11,
        MG_TUNE_COUNT = 16 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
+// Deterministic mode (mg_set_tuning(MG_TUNE_DETERMINISTIC, 1)): every reduction that crosses workgroups runs in
+// a fixed order -- per-block partial rows in the stream's workspace folded by one pass, or one writer per
+// output element -- instead of fp32 atomics, so a step is bit-reproducible run to run (slower).
+inline bool mg_det() { return g_mg_tune[MG_TUNE_DETERMINISTIC].load(std::memory_order_relaxed) != 0; }
 // Device scratch, one block per (device, stream): caller-owned (mg_set_workspace) or library-owned
 // (grown on demand, never shrunk).  NULL when it cannot be provided (mg_last_error says why).
 void* mg_workspace(size_t bytes, hipStream_t stream);
+
+// Fixed-order fold of partial rows (deterministic mode): out_a[i] += sum_r part[r * ncols + i] for i < na,
+// out_b[i - na] += ... for na <= i < ncols (64 columns x 16 row lanes per block, rows folded in lane order).
+namespace {
+__global__ __launch_bounds__(1024) void k_det_fold_rows(const float* __restrict__ part, int nrows, int ncols, int na,
+                                                        float* __restrict__ out_a, float* __restrict__ out_b) {
+  __shared__ float red[16][64];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + cx;
+  float s = 0.f;
+  if (i < ncols)
+    for (int r = ry; r < nrows; r += 16) s += part[(int64_t)r * ncols + i];
+  red[ry][cx] = s;
+  __syncthreads();
+  if (ry == 0 && i < ncols) {
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) t += red[y][cx];
+    if (i < na) out_a[i] += t;
+    else out_b[i - na] += t;
+  }
+}
+// out[0] += sum of part[0 .. n) in a fixed order (one block)
+__global__ __launch_bounds__(256) void k_det_sum(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float ws[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] += (ws[0] + ws[1]) + (ws[2] + ws[3]);
+}
+}  // namespace
+static inline void mg_det_fold_rows(const float* part, int nrows, int ncols, int na, float* out_a, float* out_b,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_det_fold_rows, dim3((ncols + 63) / 64), dim3(1024), 0, st, part, nrows, ncols, na, out_a, out_b);
+}
 
 #define MG_REQUIRE(cond, msg)                       \
   do {                                              \

@@ -171,7 +171,7 @@ __global__ void k_head_bwd_data(const float* __restrict__ g, int64_t g_bstride, 
 // dW2[c, tap] += sum_b sum_o g[b, o] * h1[b, o + tap, c]   (block per image, thread per channel)
 template <typename T>
 __global__ void k_head_bwd_w(const float* __restrict__ g, int64_t g_bstride, const T* __restrict__ h1, int Hf,
-                             int Cf, float* __restrict__ dW2) {
+                             int Cf, float* __restrict__ dW2, float* __restrict__ part) {
   int b = blockIdx.x;
   int c = threadIdx.x;
   if (c >= Cf) return;
@@ -187,6 +187,11 @@ __global__ void k_head_bwd_w(const float* __restrict__ g, int64_t g_bstride, con
       for (int t = 0; t < 16; ++t)
         acc[t] += gv * ldf(h1, (((int64_t)b * Hf + oy + (t >> 2)) * Hf + ox + (t & 3)) * Cf + c);
     }
+  if (part) {  // deterministic mode: the image's row, folded over images in order by the launcher
+#pragma unroll
+    for (int t = 0; t < 16; ++t) part[((int64_t)b * Cf + c) * 16 + t] = acc[t];
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 16; ++t) atomicAdd(&dW2[c * 16 + t], acc[t]);
 }
@@ -200,7 +205,9 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
                          const float* __restrict__ tb, const int* __restrict__ perm, int B, int No, int Nf,
                          float* __restrict__ out, float* __restrict__ g_img, float* __restrict__ g_fake,
                          float* __restrict__ g_tb, float* __restrict__ real_out, float* __restrict__ mism_out,
-                         float* __restrict__ fake_out) {
+                         float* __restrict__ fake_out, float* __restrict__ part) {
+  // part (deterministic mode): per block [out0, out1, out2, out3, g_tb self, g_tb perm] instead of the atomics
+  // below, folded in block order by k_d_loss_fold
   __shared__ float red[4][16];
   int b = blockIdx.x;
   float sr = 0.f, sm = 0.f, gr = 0.f, gm = 0.f;
@@ -225,6 +232,11 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
     if (threadIdx.x == 0) {
       float a = 0, c = 0;
       for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { a += red[0][k]; c += red[1][k]; }
+      if (part) {
+        float* pr = part + (int64_t)b * 6;
+        pr[0] = a * invf; pr[1] = 0.f; pr[2] = a * invf; pr[3] = 0.f; pr[4] = c; pr[5] = 0.f;
+        return;
+      }
       atomicAdd(&out[2], a * invf);
       atomicAdd(&out[0], a * invf);
       atomicAdd(&g_tb[i], c);
@@ -255,6 +267,11 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
     if (threadIdx.x == 0) {
       float a = 0, c = 0, d = 0, e = 0;
       for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { a += red[0][i]; c += red[1][i]; d += red[2][i]; e += red[3][i]; }
+      if (part) {
+        float* pr = part + (int64_t)b * 6;
+        pr[0] = (a + c) * inv; pr[1] = a * inv; pr[2] = 0.f; pr[3] = c * inv; pr[4] = d; pr[5] = e;
+        return;
+      }
       atomicAdd(&out[1], a * inv);
       atomicAdd(&out[3], c * inv);
       atomicAdd(&out[0], (a + c) * inv);
@@ -269,7 +286,7 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
       sf += (f > 20.f) ? f : log1pf(expf(f));
       float gf = 1.f / (1.f + expf(-f)) / B;
       g_fake[i] = gf;
-      atomicAdd(&g_tb[i], gf);
+      if (!part) atomicAdd(&g_tb[i], gf);  // (deterministic mode: k_d_loss_fold reads g_fake)
     }
     sf = wave_sum(sf);
     if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = sf;
@@ -277,9 +294,33 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
     if (threadIdx.x == 0) {
       float a = 0;
       for (int i = 0; i < (int)(blockDim.x >> 6); ++i) a += red[0][i];
+      if (part) {
+        float* pr = part + (int64_t)b * 6;
+        pr[0] = a / B; pr[1] = 0.f; pr[2] = a / B; pr[3] = 0.f; pr[4] = 0.f; pr[5] = 0.f;
+        return;
+      }
       atomicAdd(&out[2], a / B);
       atomicAdd(&out[0], a / B);
     }
+  }
+}
+
+// Deterministic mode: fold k_d_loss's block rows in block order.  out[k] += sum_blk part[blk][k]; g_tb[i] += own
+// real-block term + the terms of the real blocks b with perm[b] == i + the fake term of image i.
+__global__ __launch_bounds__(256) void k_d_loss_fold(const float* __restrict__ part, int nblk, const int* __restrict__ perm,
+                                                     int B, int Nf, const float* __restrict__ g_fake,
+                                                     float* __restrict__ out, float* __restrict__ g_tb) {
+  if (threadIdx.x < 4) {
+    float s = 0.f;
+    for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * 6 + threadIdx.x];
+    out[threadIdx.x] += s;
+  }
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    float s = part[(int64_t)i * 6 + 4];
+    for (int b = 0; b < B; ++b)
+      if (perm[b] == i) s += part[(int64_t)b * 6 + 5];
+    s += Nf == 1 ? g_fake[i] : part[(int64_t)(B + 1 + i) * 6 + 4];
+    g_tb[i] += s;
   }
 }
 
@@ -318,7 +359,7 @@ __global__ void k_g_loss_fin(const float* __restrict__ part, int nb, int B, floa
 // ~16k atomics on r1 at the memory side).
 template <typename T, typename TU>
 __global__ void k_r1(const T* __restrict__ g, int64_t per, int B, float gamma, float* __restrict__ r1,
-                     TU* __restrict__ u) {
+                     TU* __restrict__ u, float* __restrict__ part) {
   __shared__ float red[16];
   int b = blockIdx.x;
   float s = 0.f;
@@ -347,7 +388,8 @@ __global__ void k_r1(const T* __restrict__ g, int64_t per, int B, float gamma, f
   if (threadIdx.x == 0) {
     float a = 0;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) a += red[i];
-    atomicAdd(r1, a * gamma * 0.5f / B);
+    if (part) part[b] = a * gamma * 0.5f / B;  // deterministic mode: folded in image order
+    else atomicAdd(r1, a * gamma * 0.5f / B);
   }
 }
 
@@ -365,7 +407,8 @@ __global__ void k_mask_mul(const T* __restrict__ a, const TM* __restrict__ m, in
 constexpr int TB_CHUNK = 32;
 __global__ __launch_bounds__(256) void k_d_text_bwd(const float* __restrict__ g_tb, const float* __restrict__ t,
                                                     const float* __restrict__ w2sum, int B, int Ct, int cofs,
-                                                    float* __restrict__ g_tpre, float* __restrict__ dW2) {
+                                                    float* __restrict__ g_tpre, float* __restrict__ dW2,
+                                                    float* __restrict__ part) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -384,6 +427,10 @@ __global__ __launch_bounds__(256) void k_d_text_bwd(const float* __restrict__ g_
   __syncthreads();
   if (q == 0 && c < Ct) {
     float s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    if (part) {  // deterministic mode: one row per image chunk, folded in chunk order into all 16 taps
+      for (int tap = 0; tap < 16; ++tap) part[((int64_t)blockIdx.y * Ct + c) * 16 + tap] = s;
+      return;
+    }
     for (int tap = 0; tap < 16; ++tap) atomicAdd(&dW2[(int64_t)(cofs + c) * 16 + tap], s);
   }
 }
@@ -395,8 +442,15 @@ inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t -
 extern "C" int mg_d_text_bwd(const float* g_tb, const float* t, const float* w2sum, int B, int Ct, int cofs,
                              float* g_tpre, float* dW2, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_d_text_bwd, dim3(cdiv(Ct, 64), cdiv(B, TB_CHUNK)), dim3(256), 0, st, g_tb, t, w2sum, B, Ct,
-                     cofs, g_tpre, dW2);
+  const int nch = cdiv(B, TB_CHUNK);
+  float* part = nullptr;
+  if (mg_det()) {
+    part = reinterpret_cast<float*>(mg_workspace((size_t)nch * Ct * 16 * sizeof(float), st));
+    if (!part) return MG_ERR_LAUNCH;
+  }
+  hipLaunchKernelGGL(k_d_text_bwd, dim3(cdiv(Ct, 64), nch), dim3(256), 0, st, g_tb, t, w2sum, B, Ct,
+                     cofs, g_tpre, dW2, part);
+  if (part) mg_det_fold_rows(part, nch, Ct * 16, Ct * 16, dW2 + (int64_t)cofs * 16, dW2 + (int64_t)cofs * 16, st);
   return mg_check_launch("mg_d_text_bwd");
 }
 
@@ -476,8 +530,14 @@ extern "C" int mg_disc_head_bwd_w(int dtype, const float* g, int64_t g_bstride, 
   MG_REQUIRE(Cf <= 1024, "Cf <= 1024");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int thr = ((Cf + 63) / 64) * 64;
-  if (dtype == MG_F32) hipLaunchKernelGGL(k_head_bwd_w<float>, dim3(B), dim3(thr), 0, st, g, g_bstride, (const float*)h1, Hf, Cf, dW2);
-  else hipLaunchKernelGGL(k_head_bwd_w<bf16_t>, dim3(B), dim3(thr), 0, st, g, g_bstride, (const bf16_t*)h1, Hf, Cf, dW2);
+  float* part = nullptr;
+  if (mg_det()) {
+    part = reinterpret_cast<float*>(mg_workspace((size_t)B * Cf * 16 * sizeof(float), st));
+    if (!part) return MG_ERR_LAUNCH;
+  }
+  if (dtype == MG_F32) hipLaunchKernelGGL(k_head_bwd_w<float>, dim3(B), dim3(thr), 0, st, g, g_bstride, (const float*)h1, Hf, Cf, dW2, part);
+  else hipLaunchKernelGGL(k_head_bwd_w<bf16_t>, dim3(B), dim3(thr), 0, st, g, g_bstride, (const bf16_t*)h1, Hf, Cf, dW2, part);
+  if (part) mg_det_fold_rows(part, B, Cf * 16, Cf * 16, dW2, dW2, st);
   return mg_check_launch("mg_disc_head_bwd_w");
 }
 
@@ -488,8 +548,14 @@ extern "C" int mg_d_loss(const float* img_real, const float* img_fake, const flo
   MG_REQUIRE(B > 0 && No > 0 && Nf > 0, "mg_d_loss: B, No, Nf must be positive");
   // block B (one logit per fake, the reference's 16x16 fakes) or blocks B+1..2B (Nf logits per fake image)
   int grid = Nf == 1 ? B + 1 : 2 * B + 1;
+  float* part = nullptr;
+  if (mg_det()) {
+    part = reinterpret_cast<float*>(mg_workspace((size_t)grid * 6 * sizeof(float), st));
+    if (!part) return MG_ERR_LAUNCH;
+  }
   hipLaunchKernelGGL(k_d_loss, dim3(grid), dim3(256), 0, st, img_real, img_fake, tb, perm, B, No, Nf, out, g_img,
-                     g_fake, g_tb, real_out, mism_out, fake_out);
+                     g_fake, g_tb, real_out, mism_out, fake_out, part);
+  if (part) hipLaunchKernelGGL(k_d_loss_fold, dim3(1), dim3(256), 0, st, part, grid, perm, B, Nf, g_fake, out, g_tb);
   return mg_check_launch("mg_d_loss");
 }
 
@@ -510,10 +576,16 @@ extern "C" int mg_r1(int dtype, const void* g, int64_t per, int B, float gamma, 
                      void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(B);
-#define L_(T, TU) hipLaunchKernelGGL((k_r1<T, TU>), grid, dim3(256), 0, st, (const T*)g, per, B, gamma, r1, (TU*)u)
+  float* part = nullptr;
+  if (mg_det()) {
+    part = reinterpret_cast<float*>(mg_workspace((size_t)B * sizeof(float), st));
+    if (!part) return MG_ERR_LAUNCH;
+  }
+#define L_(T, TU) hipLaunchKernelGGL((k_r1<T, TU>), grid, dim3(256), 0, st, (const T*)g, per, B, gamma, r1, (TU*)u, part)
   if (dtype == MG_F32) { if (u_dtype == MG_F32) L_(float, float); else L_(float, bf16_t); }
   else { if (u_dtype == MG_F32) L_(bf16_t, float); else L_(bf16_t, bf16_t); }
 #undef L_
+  if (part) hipLaunchKernelGGL(k_det_sum, dim3(1), dim3(256), 0, st, part, B, r1);
   return mg_check_launch("mg_r1");
 }
 

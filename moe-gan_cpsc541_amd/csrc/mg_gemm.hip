@@ -84,13 +84,21 @@ void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int
 // Few-tile GEMMs (styles, mapping, router/attention projections at small M) are latency-bound: a
 // 64x64 grid of ~32 blocks walks K serially.  Split K over ~256 blocks into fp32 slabs and apply
 // the real epilogue in a reduction pass.  Returns false when the shape does not qualify.
+// ``want_splits`` > 0 (deterministic mode, an atomic split-K epilogue): exactly that many slabs, any tile count;
+// the reduction pass then adds each output element once.
 template <typename T, typename TO>
 bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
-                      int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, hipStream_t st) {
+                      int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, hipStream_t st, int want_splits = 0) {
   constexpr int TBK = Tile<T>::BK;
   int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
-  if (tiles >= 96 || K < 4 * TBK || a_xf(e)) return false;
-  int splits = (int)std::min<int64_t>(256 / tiles, K / (2 * TBK));
+  if (a_xf(e)) return false;
+  int splits;
+  if (want_splits > 0) {
+    splits = std::max(1, std::min(want_splits, cdiv(K, TBK)));
+  } else {
+    if (tiles >= 96 || K < 4 * TBK) return false;
+    splits = (int)std::min<int64_t>(256 / tiles, K / (2 * TBK));
+  }
   if (splits < 2) return false;
   int kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
   splits = (K + kchunk - 1) / kchunk;
@@ -158,6 +166,15 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
   MG_REQUIRE(!(ep && ep->atomic) || c_dtype == MG_F32, "atomic epilogue requires fp32 C");
   if (K == 0) splits = 1;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (splits > 1 && mg_det()) {  // deterministic mode: fp32 slabs + one fixed-order reduction, not atomics
+    bool done;
+    if (dtype == MG_F32)
+      done = run_splitk_slabs<float, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st, splits);
+    else
+      done = run_splitk_slabs<bf16_t, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st, splits);
+    if (done) return mg_check_launch("mg_gemm (deterministic split-K slabs)");
+    splits = 1;
+  }
   if (splits == 1 && !(ep && ep->atomic) && !g_mg_tune[MG_TUNE_NO_SLABS]) {
     bool done;
     if (dtype == MG_F32)
@@ -235,6 +252,17 @@ extern "C" int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, 
   }
   if (n <= 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (mg_det() && n > 1) {  // deterministic mode: descriptors may accumulate into one output -> one launch each
+    bool atomic = false;
+    for (int i = 0; i < n; ++i) atomic = atomic || (d[i].ep && d[i].ep->atomic);
+    if (atomic) {
+      for (int i = 0; i < n; ++i) {
+        int rc = mg_gemm_batch(dtype, a_kc, b_kc, c_dtype, 1, d + i, stream);
+        if (rc) return rc;
+      }
+      return MG_OK;
+    }
+  }
 #define B_(T, TO)                                                   \
   (a_kc ? (b_kc ? run_batch<T, TO, true, true>(n, d, st) : run_batch<T, TO, true, false>(n, d, st)) \
         : (b_kc ? run_batch<T, TO, false, true>(n, d, st) : run_batch<T, TO, false, false>(n, d, st)))
@@ -653,6 +681,7 @@ extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const
     int rows_per_group = std::max(1, total_rows / std::max(1, ngroups));
     splits = std::max(1, std::min({64, cdiv(big ? 512 : 1024, std::max(1, tiles)), std::max(1, rows_per_group / 1024)}));
   }
+  if (mg_det()) splits = 1;  // deterministic mode: one writer (one atomic add) per element and group
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool xf = a_xf(ep) || b_idx || b_gelu;
 #define MG_GW(T, X) run_grouped_wgrad<T, X>(M, N, ngroups, row_off, total_rows, A, lda, B, ldb, b_idx, b_idx_div, b_gelu, C, splits, ep, st)

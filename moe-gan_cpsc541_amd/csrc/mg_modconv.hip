@@ -31,9 +31,9 @@ __global__ void k_bwd_out(const TG* __restrict__ gz, int64_t ld_gz, const T* __r
     float zz = ldf(z, row * ld_z + o);
     if (zsub) zz -= ldf(zsub, row * ld_zsub + o);  // output had a residual fused in
     float y = zz;
-    if (act) {
+    if (act) {  // act 1: z = LeakyReLU(0.2)(y) (inverted here); act 2: z = y, the stored pre-activation
       if (zz <= 0.f) {
-        y = zz * 5.f;  // invert LeakyReLU(0.2)
+        if (act == 1) y = zz * 5.f;
         g *= 0.2f;
       }
     }
@@ -114,11 +114,11 @@ __global__ __launch_bounds__(256) void k_bwd_out_v(const TG* __restrict__ gz, in
     for (int j = 0; j < 8; ++j) {
       float y = zz[j], y1 = z1[j];
       if (act && zz[j] <= 0.f) {
-        y = zz[j] * 5.f;
+        if (act == 1) y = zz[j] * 5.f;
         g[j] *= 0.2f;
       }
       if (act && z1[j] <= 0.f) {
-        y1 = z1[j] * 5.f;
+        if (act == 1) y1 = z1[j] * 5.f;
         g1[j] *= 0.2f;
       }
       acc[j] += g[j] * y;
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void k_bwd_out_v(const TG* __restrict__ gz, in
     for (int j = 0; j < 8; ++j) {
       float y = zz[j];
       if (act && zz[j] <= 0.f) {
-        y = zz[j] * 5.f;
+        if (act == 1) y = zz[j] * 5.f;
         g[j] *= 0.2f;
       }
       acc[j] += g[j] * y;
@@ -411,6 +411,7 @@ extern "C" int mg_modconv_bwd_in(int gxt_dtype, const void* gxt, int64_t ld_gxt,
   if (vec) {
     vshape(Cin, grid, blk, B);
     grid.z = std::max(1, std::min(cdiv(HW, (int)blk.y * 4), cdiv(1024, (int)(grid.x * grid.y))));
+    if (mg_det()) grid.z = 1;  // deterministic mode: one writer per style-gradient element (no z-split atomics)
   }
 #define L_(TG, T, TO)                                                                                              \
   do {                                                                                                             \

@@ -791,6 +791,63 @@ __global__ __launch_bounds__(NT) void k_grouped_colsum_v(const T* __restrict__ X
   }
 }
 
+// Deterministic mode: per (row chunk, group) partial rows part[(chunk * G + g) * N + n], the row lanes of a
+// block folded in LDS in lane order; k_grouped_colsum_fold then adds, per (group, column), the partials of the
+// chunks that group's rows touch, in chunk order.
+template <typename T>
+__global__ __launch_bounds__(256) void k_grouped_colsum_part(const T* __restrict__ X, int64_t ld,
+                                                             const int* __restrict__ idx, int idx_div,
+                                                             const float* __restrict__ rs,
+                                                             const int* __restrict__ row_off, int G, int N, int rpb,
+                                                             float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
+  const int n = (blockIdx.x * TX + tx) * 8;
+  const bool live = n < N;
+  const int total = row_off[G];
+  const int r0 = blockIdx.y * rpb, r1 = min(total, r0 + rpb);
+  for (int g = 0; g < G; ++g) {
+    const int gs = max(r0, row_off[g]), ge = min(r1, row_off[g + 1]);
+    if (gs >= ge) continue;  // block-uniform
+    float s[8], v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+    if (live) {
+      for (int r = gs + ty; r < ge; r += TY) {
+        const int src = idx ? idx[r] / idx_div : r;
+        ld8(X + (int64_t)src * ld + n, v);
+        const float sc = rs ? rs[r] : 1.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += v[j] * sc;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[(ty * TX + tx) * 8 + j] = s[j];
+    __syncthreads();
+    if (ty == 0 && live) {
+      for (int y = 1; y < TY; ++y)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += red[(y * TX + tx) * 8 + j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part[((int64_t)blockIdx.y * G + g) * N + n + j] = s[j];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_grouped_colsum_fold(const float* __restrict__ part,
+                                                             const int* __restrict__ row_off, int G, int N, int rpb,
+                                                             float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= G * N) return;
+  const int g = i / N, n = i - g * N;
+  const int lo = row_off[g], hi = row_off[g + 1];
+  if (lo >= hi) return;
+  float s = 0.f;
+  for (int c = lo / rpb; c <= (hi - 1) / rpb; ++c) s += part[((int64_t)c * G + g) * N + n];
+  out[i] += s;
+}
+
 // KL of one router, two passes: per-block partial sums over the three (mu, rho) pairs, then one block
 // folds the partials and applies the reference's nan/inf/clamp rules.
 __global__ __launch_bounds__(256) void k_router_kl_part(const float* __restrict__ mf, const float* __restrict__ rf,
@@ -1129,6 +1186,24 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
 extern "C" int mg_grouped_colsum(int dtype, const void* X, int64_t ld, const int32_t* idx, int idx_div, const float* rs,
                                  const int32_t* row_off, int G, int N, int max_rows, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (mg_det() && N % 8 == 0 && ld % 8 == 0 && mg_al16(X) && max_rows > 0) {  // deterministic mode
+    const int cv = N / 8, tx = std::min(cv, 32), ty = 256 / tx;
+    const int cblk = cdiv(cv, tx);
+    const int rpb = std::max(64, cdiv(max_rows, std::max(1, 256 / cblk)));
+    const int nch = cdiv(max_rows, rpb);
+    float* part = reinterpret_cast<float*>(mg_workspace((size_t)nch * G * N * sizeof(float), st));
+    if (!part) return MG_ERR_LAUNCH;
+    dim3 grid(cblk, nch), blk(tx, ty);
+    if (dtype == MG_F32)
+      hipLaunchKernelGGL(k_grouped_colsum_part<float>, grid, blk, 0, st, (const float*)X, ld, idx,
+                         idx_div > 0 ? idx_div : 1, rs, row_off, G, N, rpb, part);
+    else
+      hipLaunchKernelGGL(k_grouped_colsum_part<bf16_t>, grid, blk, 0, st, (const bf16_t*)X, ld, idx,
+                         idx_div > 0 ? idx_div : 1, rs, row_off, G, N, rpb, part);
+    hipLaunchKernelGGL(k_grouped_colsum_fold, dim3(cdiv((int64_t)G * N, 256)), dim3(256), 0, st, part, row_off, G, N,
+                       rpb, out);
+    return mg_check_launch("mg_grouped_colsum (deterministic)");
+  }
   if (N % 8 == 0 && ld % 8 == 0 && mg_al16(X) && max_rows > 0) {
     // 1024-thread blocks, ~256 of them (one per CU, 64 KiB of loads in flight each): a quarter of the
     // same-address atomics of 1024 small blocks, at least 8 rows per row lane

@@ -631,6 +631,21 @@ __global__ __launch_bounds__(1024) void k_mtm_bwd_img(const TG* __restrict__ gou
     }
   }
   __syncthreads();
+  // the LDS atomics above hand out list slots in arrival order: sort every list (a few entries) so the gather
+  // below sums in a fixed order (bit-identical data gradients run to run)
+  for (int q = tid; q < HW; q += nt) {
+    const int e0 = cnt[q], e1 = cnt[q + 1];
+    for (int i = e0 + 1; i < e1; ++i) {
+      const int v = ent[i];
+      int j = i - 1;
+      while (j >= e0 && ent[j] > v) {
+        ent[j + 1] = ent[j];
+        --j;
+      }
+      ent[j + 1] = v;
+    }
+  }
+  __syncthreads();
   const int V = 1 << lgV, items = HW << lgV;
   const TG* gb = gout + row0 * C;
   const T* xb = x + row0 * C;

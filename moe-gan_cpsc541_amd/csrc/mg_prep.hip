@@ -533,7 +533,7 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     int rpb = cdiv(R, rblk);
     rblk = cdiv(R, rpb);
     dim3 grid(cblk, rblk);
-    if (rblk <= 16) {
+    if (rblk <= 16 && (rblk == 1 || !mg_det())) {  // (deterministic mode: one writer per column, or the fold)
       DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum_v<T>, grid, dim3(tx, ty), 0, st, reinterpret_cast<const T*>(X),
                                            ld, R, C, rpb, out, 1));
       return mg_check_launch("mg_colsum");
@@ -548,7 +548,7 @@ extern "C" int mg_colsum(int dtype, const void* X, int64_t ld, int R, int C, flo
     hipLaunchKernelGGL(k_colsum_fin, dim3(cdiv(C, 64)), dim3(1024), 0, st, part, rblk, C, out);
     return mg_check_launch("mg_colsum");
   }
-  int rpb = std::max(16, R / 256);
+  int rpb = mg_det() ? std::max(R, 1) : std::max(16, R / 256);  // deterministic: one row block, one add per column
   dim3 grid(cdiv(C, 256), cdiv(R, rpb));
   DISPATCH_T(dtype, hipLaunchKernelGGL(k_colsum<T>, grid, dim3(256), 0, st, reinterpret_cast<const T*>(X), ld, R, C,
                                        rpb, out));
@@ -634,7 +634,7 @@ extern "C" int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, v
 
 extern "C" int mg_const_bwd(int dtype, const void* g, int C, int HW, int B, float* gc, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int bchunk = std::max(8, cdiv(B, 16));
+  const int bchunk = mg_det() ? std::max(B, 1) : std::max(8, cdiv(B, 16));  // deterministic: one add per element
   DISPATCH_T(dtype, hipLaunchKernelGGL(k_const_bwd<T>, dim3(cdiv(C * HW, 256), cdiv(B, bchunk)), dim3(256), 0, st,
                                        reinterpret_cast<const T*>(g), C, HW, B, bchunk, gc));
   return mg_check_launch("mg_const_bwd");

@@ -181,8 +181,13 @@ class GeneratorEngine:
         d = self._D.get(pre) if self._D is not None else None
         if d is None:
             d = ops.gemm(s2, pk["wsq"], B, rows, Cin, ep=E_(act=RSQRT))  # demod coefficients [B, rows] (:165)
+        # with a residual fused behind the LeakyReLU the backward needs the pre-activation's sign: the epilogue
+        # stores it (reconstructing it as output - residual cancels: a pre-activation below the rounding of the
+        # residual flips its slope -- measured ~1 % gradient error at 8x8 in fp32, far more in bf16)
+        ypre = torch.empty(B * HW, rows, device=self.dev, dtype=self.cdt) if (save and resid is not None and act) \
+            else None
         ep = E_(scale=d, scale_shift=ops.ilog2(HW), scale_ld=rows, act=act, resid=resid,
-                ld_res=resid.shape[-1] if resid is not None else 0)
+                ld_res=resid.shape[-1] if resid is not None else 0, out_pre=ypre, ld_pre=rows if ypre is not None else 0)
         if xs is None:  # x * style, shared by the conv and its weight gradient (the MTM warp writes it itself)
             xs = ops.scale_bc(x, s)
         if "wq" in pk:  # MX-fp8: quantize x * s per 32 channels, e4m3 x e4m3 scaled MFMA
@@ -190,7 +195,12 @@ class GeneratorEngine:
             y = ops.conv2d_mx8(xq.view(B, H, W, Cin), xsc, *pk["wq"], rows, k, k, 1, k // 2, ep=ep, out_dtype=self.cdt)
         else:
             y = ops.conv2d(xs, pk["w"], rows, k, k, 1, k // 2, ep=ep, out_dtype=self.cdt)
-        sv = (x, xs, w, s, s2, d, y, resid, act) if save else None
+        if not save:
+            sv = None
+        elif ypre is not None:  # act 2: z holds the pre-activation itself
+            sv = (x, xs, w, s, s2, d, ypre, None, 2)
+        else:
+            sv = (x, xs, w, s, s2, d, y, resid, act)
         return y, sv
 
     def mc_bwd(self, pre, sv, gz, gx, gw, accumulate=0):

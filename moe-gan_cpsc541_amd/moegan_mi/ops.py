@@ -17,6 +17,16 @@ call, ptr, dt, S = L.call, L.ptr, L.dt, L.stream
 E = L.epilogue
 
 
+TUNE_DETERMINISTIC = 11  # mg_common.h MG_TUNE_DETERMINISTIC
+
+
+def set_deterministic(on=True):
+    """Deterministic mode of the library: every cross-workgroup reduction of the step in a fixed
+    order (partial rows + one fold, or one writer per element) instead of fp32 atomics, so two identically
+    initialised steps give bit-identical results; slower.  Process-wide, like torch's own switch."""
+    call("mg_set_tuning", TUNE_DETERMINISTIC, 1 if on else 0)
+
+
 def _ld(t):
     return t.stride(0) if t.dim() > 1 else t.shape[0]
 

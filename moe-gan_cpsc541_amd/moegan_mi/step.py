@@ -26,6 +26,8 @@ Nothing here synchronises with the host: every loss value stays on the device un
 and all randomness is passed in.  Data parallelism (one process per GPU, RCCL) all-reduces the flat D and
 G gradient buffers, the [E] expert-load vector and the guard word.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -41,7 +43,7 @@ FD, FG = ops.FLAG_D_BAD, ops.FLAG_G_BAD
 class StepConfig:
     def __init__(self, E=4, topk=None, dtype="fp32", r1_gamma=10.0, clip_weight_16=0.1, clip_weight_8=0.05,
                  balance_weight=0.01, beta1=0.5, beta2=0.999, weight_decay=0.01, eps=1e-8, d_clip=0.7, g_clip=0.8,
-                 psi=0.7, fp8=False, max_res=16):
+                 psi=0.7, fp8=False, max_res=16, deterministic=None):
         self.E, self.topk = E, topk
         # generator output resolution: 16 = the reference; 32 / 64 / 128 = the progressive extension (layout.py)
         self.max_res = max_res
@@ -53,6 +55,9 @@ class StepConfig:
         self.beta1, self.beta2, self.weight_decay, self.eps = beta1, beta2, weight_decay, eps
         self.d_clip, self.g_clip = d_clip, g_clip
         self.psi = psi
+        # deterministic mode (ops.set_deterministic): None = the MOEGAN_DETERMINISTIC environment switch
+        self.deterministic = (os.environ.get("MOEGAN_DETERMINISTIC", "0") == "1") if deterministic is None \
+            else bool(deterministic)
 
 
 def clip_loss(images_nchw, text, encode_image, images_nhwc=None):
@@ -80,6 +85,8 @@ class TrainStep:
     def __init__(self, cfg, device="cuda", process_group=None, gstore=None, dstore=None):
         self.cfg = cfg
         self.dev = torch.device(device)
+        if getattr(cfg, "deterministic", False):
+            ops.set_deterministic(True)
         self.cdt = torch.bfloat16 if cfg.dtype == "bf16" else torch.float32
         self.gs = gstore if gstore is not None else ParamStore(
             generator_shapes(cfg.E, getattr(cfg, "max_res", 16)), self.dev,

@@ -133,7 +133,7 @@ def test_progressive_train_step(R, B):
     assert abs(float(out["r1"][0]) - ref["r1"]) < 1e-4 * abs(ref["r1"]) + 1e-7
     assert abs(float(out["g_gan"][0]) - ref["g_loss_gan"]) < 1e-4 * abs(ref["g_loss_gan"])
     assert abs(float(out["balance"][0]) - ref["balance"]) < 1e-3 * ref["balance"] + 1e-7
-    assert out["fake_pred"].shape == (B, (R // 4 - 3) ** 2)
+    assert out["fake_pred"].numel() == B * (R // 4 - 3) ** 2
     # the R1 input gradient d sum D(real) / d real (:1282-1284), every pixel
     _tensor_close(out["r1_grad"][..., :3].permute(0, 3, 1, 2), ref["r1_grad"], 1e-4, 1e-9, "r1_grad")
     fails, rows = [], []
