@@ -31,6 +31,18 @@ def _train(use_graphs, tmp_path, acc=2):
     return G._store.data.clone(), D._store.data.clone()
 
 
+def test_graph_loop_bit_identical_deterministic(tmp_path):
+    """Deterministic mode: the graph-replayed loop's parameters equal the eager loop's bit for bit."""
+    from moegan_mi import ops
+    ops.set_deterministic(True)
+    try:
+        e = _train(False, tmp_path)
+        g = _train(True, tmp_path)
+    finally:
+        ops.set_deterministic(False)
+    assert torch.equal(e[0], g[0]) and torch.equal(e[1], g[1])
+
+
 def test_graph_loop_matches_eager_loop(tmp_path):
     e1 = _train(False, tmp_path)
     e2 = _train(False, tmp_path)
