@@ -203,8 +203,10 @@ class GeneratorEngine:
             sv = (x, xs, w, s, s2, d, y, resid, act)
         return y, sv
 
-    def mc_bwd(self, pre, sv, gz, gx, gw, accumulate=0):
-        """gz: grad of the conv output (post activation / residual). Writes/accumulates gx, accumulates gw."""
+    def mc_bwd(self, pre, sv, gz, gx, gw, accumulate=0, gx_f32=False):
+        """gz: grad of the conv output (post activation / residual). Writes/accumulates gx, accumulates gw.
+        ``gx_f32``: the data gradient stays fp32 up to gx (an MTM's warped-input gradient, which the offset head
+        reduces over channels and pixels into cancelling sums)."""
         x, xs, w, s, s2, d, z, zsub, act = sv
         B, H, W, Cin = x.shape
         HW = H * W
@@ -222,7 +224,8 @@ class GeneratorEngine:
             gq, gsc = ops.quant_mx8(gyt)
             gxt = ops.conv2d_mx8(gq.view(B, H, W, rows), gsc, *pk["wflipq"], Cin, 3, 3, 1, 1, out_dtype=self.cdt)
         elif k == 3:
-            gxt = ops.conv2d(gyt.view(B, H, W, rows), pk["wflip"], Cin, 3, 3, 1, 1)
+            gxt = ops.conv2d(gyt.view(B, H, W, rows), pk["wflip"], Cin, 3, 3, 1, 1,
+                             out_dtype=torch.float32 if gx_f32 else None)
         else:
             gxt = ops.gemm(gyt, pk["w"], P, Cin, rows, b_kc=False)
         batched = self._GS is not None and pre in self.style_cols
@@ -280,8 +283,10 @@ class GeneratorEngine:
             return
         B, H, W, Cin = x.shape
         P = B * H * W
-        g_xw = torch.empty(P, Cin, device=self.dev, dtype=self.cdt)
-        self.mc_bwd(pre + "modulated_conv.", msv, gz, g_xw, gw)
+        # fp32: the offset head's gradient is a sum over channels and pixels of g_xw * (neighbour differences of
+        # x) that largely cancels -- a bf16 g_xw put 3-5x the whole-step bf16 floor on the head biases
+        g_xw = torch.empty(P, Cin, device=self.dev, dtype=torch.float32)
+        self.mc_bwd(pre + "modulated_conv.", msv, gz, g_xw, gw, gx_f32=True)
         opk = self.packs[pre + "offset_net.0."]
         if ops.mtm_bwd_fusable(x) and gx.is_contiguous():
             ga1 = torch.empty(B, H, W, 32, device=self.dev, dtype=self.cdt)

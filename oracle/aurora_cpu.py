@@ -53,6 +53,22 @@ def base_grid(H, W, device=None, dtype=torch.float32):
     return torch.stack((gx, gy), dim=2)
 
 
+# LeakyReLU slope replay (test hook, like the top-k ``routes``): {MTM prefix: bool mask [B, C, H, W]} of a device
+# run's pre-activation signs.  A pre-activation within rounding of 0 can land on the other slope in the device's
+# arithmetic; the gradient at that element then differs by 0.8 g, which no reordering tolerance covers (measured:
+# one flipped element of 32768 at 8x8 puts 4e-3 on a whole fp32 data gradient).  Used by the backward-carrying
+# (grad-enabled) calls only.
+LRELU_SLOPES = None
+
+
+def _mtm_lrelu(y, pre):
+    m = LRELU_SLOPES.get(pre) if LRELU_SLOPES is not None and y.requires_grad else None
+    if m is None:
+        return F.leaky_relu(y, 0.2)
+    assert m.shape == y.shape, (pre, m.shape, y.shape)
+    return torch.where(m, y, 0.2 * y)
+
+
 def mtm(x, w, P, pre, use_offset=True):
     B, C, H, W = x.shape
     if use_offset:
@@ -63,7 +79,7 @@ def mtm(x, w, P, pre, use_offset=True):
         grid = grid.clamp(-1, 1)  # :236
         x = F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=False)  # :239
     x = modconv(x, w, P, pre + "modulated_conv.", padding=1)
-    return F.leaky_relu(x, 0.2)  # :245
+    return _mtm_lrelu(x, pre)  # :245
 
 
 # ---------------------------------------------------------------------------

@@ -184,6 +184,25 @@ class bf16_module_rounding:
         return False
 
 
+class bf16_weights(dict):
+    """The generator's parameter dict as the bf16 device reads it: the weights its MFMA kernels take as bf16
+    operands (modulated / 1x1 / to_rgb conv weights, offset-head first conv, self-attention projections, expert
+    FFNs) come back rounded to bf16 (straight-through: their gradient reaches the fp32 leaf unchanged); the fp32
+    prefix (mapping, text projection, styles), routers, norms, biases and the cross-attention value chain stay
+    fp32, as on the device (engine_g.py).  ``values()`` / ``items()`` still give the leaves, so the oracle's
+    optimizer and gradient clipping are untouched.  A weight rounding is shared by every token of every image, so
+    without it the floor misses the error that adds coherently over an image's tokens."""
+    SUFFIXES = ("modulated_conv.weight", "skip_proj.weight", "proj_in.weight", "proj_out.weight",
+                "offset_net.0.weight", "self_attn.in_proj_weight", "self_attn.out_proj.weight")
+
+    def __getitem__(self, n):
+        v = dict.__getitem__(self, n)
+        if (n.endswith(self.SUFFIXES) or (n.startswith("to_rgb_") and n.endswith(".weight")) or
+                (".experts." in n and n.endswith((".net.0.weight", ".net.2.weight")))):
+            return O.round_bf16_st(v)
+        return v
+
+
 def whole(grads, names=None):
     """One vector of every gradient in ``grads`` (dict name -> tensor or None), in a fixed name order."""
     names = sorted(n for n, v in grads.items() if v is not None) if names is None else names
@@ -381,3 +400,62 @@ class ReplayedStep:
         self.graph.replay()
         torch.cuda.synchronize()
         return self.out
+
+
+
+class lrelu_slope_replay:
+    """Record the device generator's MTM pre-activation signs (GeneratorEngine.mtm_fwd calls that save for the
+    backward) and replay them in the oracle (aurora_cpu.LRELU_SLOPES): the LeakyReLU kink is a discrete decision,
+    replayed like the top-k routes.
+
+        with lrelu_slope_replay() as slopes:
+            ... device step (or the eager warm-up + capture of a ReplayedStep) ...
+        with slopes.oracle():
+            ... oracle forward/backward ...
+
+    The recorder keeps the saved tensors themselves (the pre-activation for a residual-fused MTM, the output
+    otherwise -- same sign) and reads them when ``oracle()`` is entered: after a hipGraph replay they hold that
+    replay's values (held references keep the capture's allocator from reusing their memory)."""
+
+    def __init__(self):
+        self.refs = {}
+
+    def __enter__(self):
+        from moegan_mi.engine_g import GeneratorEngine
+        self._cls = GeneratorEngine
+        self._orig = orig = GeneratorEngine.mtm_fwd
+        refs = self.refs
+
+        def mtm_fwd(eng, pre, x, w, resid=None, save=True):
+            y, sv = orig(eng, pre, x, w, resid=resid, save=save)
+            if save:
+                msv = sv[4]
+                z, zsub, act = msv[6], msv[7], msv[8]
+                assert act in (1, 2) and zsub is None, (pre, act)  # act 2: z = pre-activation; act 1: z = output
+                refs[pre] = (z, tuple(x.shape[:3]), eng.P(pre + "modulated_conv.weight").shape[0])
+            return y, sv
+        GeneratorEngine.mtm_fwd = mtm_fwd
+        return self
+
+    def __exit__(self, *exc):
+        self._cls.mtm_fwd = self._orig
+
+    def masks(self):
+        out = {}
+        for pre, (z, (B, H, W), Cout) in self.refs.items():
+            zz = z.reshape(B * H * W, -1)[:, :Cout].float()
+            out[pre] = (zz > 0).view(B, H, W, Cout).permute(0, 3, 1, 2).cpu()
+        return out
+
+    class _Oracle:
+        def __init__(self, masks):
+            self.m = masks
+
+        def __enter__(self):
+            O.LRELU_SLOPES = self.m
+
+        def __exit__(self, *exc):
+            O.LRELU_SLOPES = None
+
+    def oracle(self):
+        return self._Oracle(self.masks())

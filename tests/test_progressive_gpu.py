@@ -4,8 +4,10 @@ The reference defines no block above 16x16 (gen_block_32 / _64 appear only in th
 create_optimizer_for_active_blocks, t2i_moe_gan.py:1005-1026), so the block list is the build's
 (moegan_mi/layout.py gen_blocks) and this parity is "unpinned" against the reference: both sides compose the
 same pinned reference functions (upsample :657, ConvolutionBlock :604-621 with MTMs that have no offset head
-above 16x16, :199, ModulatedConv to_rgb :154-186), the oracle in plain fp32 PyTorch autograd
-(oracle/aurora_cpu.generator), the device through the HIP engines.  The oracle runs in fp64: in fp32 its own CPU
+above 16x16, :199, ModulatedConv to_rgb :154-186), the oracle in plain PyTorch autograd
+(oracle/aurora_cpu.generator), the device through the HIP engines.  The MTM LeakyReLU slopes the device took are
+replayed in the oracle (steputil.lrelu_slope_replay, like the top-k routes): a pre-activation within rounding of
+0 on the other slope moves a whole data gradient by ~4e-3 (measured, tools/gen_grad_probe.py).  The oracle runs in fp64: in fp32 its own CPU
 grid_sample / conv backward reorderings were measured at up to 5e-3 of a gradient's scale (tools/diag_cb.py), so
 an fp32 oracle cannot hold an fp32 device to F8's bars.  Bars are the fp32 ones of F7 / F8: 1e-4 relative on
 values, 1e-3 on the generator's gradients for a given upstream gradient; for the full step 2e-3 relative L2 and
@@ -19,7 +21,7 @@ import torch
 from goldens import close
 from oracle import aurora_cpu as O
 from oracle.recipe import fill_state
-from steputil import gpu_step, make_inputs, nchw, oracle_models
+from steputil import gpu_step, lrelu_slope_replay, make_inputs, nchw, oracle_models
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -74,8 +76,13 @@ def test_progressive_generator_fwd_bwd(R):
     eps = [tuple(torch.randn(s, generator=g) for s in ((c, 128), (512, 128), (256, E))) for c in (512, 256, 128)]
     P = {n: torch.from_numpy(v).double().requires_grad_(not n.split(".")[-1].startswith("epsilon_"))
          for n, v in vals.items()}
-    img, img_half, kl, probs = O.generator(z.double(), text.double(), P, [tuple(t.double() for t in e) for e in eps],
-                                           True, 3.0, 0.7)
+    epsd = [tuple(t.to(DEV) for t in trip) for trip in eps]
+    with lrelu_slope_replay() as slopes:  # the device's LeakyReLU slopes, replayed in the oracle (steputil)
+        im, ih, kl2s, pr, _, ctx = ge.forward(z.to(DEV), text.to(DEV), epsd, 3.0, 0.7, train=True, save=True,
+                                              want_img8=True)
+    with slopes.oracle():
+        img, img_half, kl, probs = O.generator(z.double(), text.double(), P, [tuple(t.double() for t in e) for e in eps],
+                                               True, 3.0, 0.7)
     assert img.shape == (B, 3, R, R) and img_half.shape == (B, 3, R // 2, R // 2)
     R_img = torch.randn(img.shape, generator=g)
     R_half = torch.randn(img_half.shape, generator=g)
@@ -84,9 +91,6 @@ def test_progressive_generator_fwd_bwd(R):
             sum((p * r.double()).sum() for p, r in zip(probs, Rp)))
     loss.backward()
 
-    epsd = [tuple(t.to(DEV) for t in trip) for trip in eps]
-    im, ih, kl2s, pr, _, ctx = ge.forward(z.to(DEV), text.to(DEV), epsd, 3.0, 0.7, train=True, save=True,
-                                          want_img8=True)
     close(nchw(im), img.detach(), rtol=1e-4, what="img")
     close(nchw(ih), img_half.detach(), rtol=1e-4, what="img_half")
     kl2 = torch.stack(kl2s)
@@ -119,16 +123,18 @@ def test_progressive_train_step(R, B):
     PG, PD, optG, optD, grads = oracle_models(E, max_res=R, dtype=torch.float64)
     gb = {n: v.detach().clone() for n, v in PG.items()}
     db = {n: v.detach().clone() for n, v in PD.items()}
-    d64 = lambda trips: [tuple(t.double() for t in trip) for trip in trips]  # noqa: E731
-    ref = O.train_step(PG, PD, optG, optD, real.double(), text.double(), z.double(), d64(eps_d), d64(eps_g), perm,
-                       kl_weight_eff=1e-8)
-    assert not ref["skipped"]
     ts = gpu_step(E, None, "fp32", max_res=R)
     g0, d0 = ts.gs.data.clone(), ts.ds.data.clone()
     dv = lambda trips: [tuple(t.to(DEV) for t in trip) for trip in trips]  # noqa: E731
-    out = ts.step(real.to(DEV), text.to(DEV), z.to(DEV), dv(eps_d), dv(eps_g), perm.int().to(DEV), anneal=3.0,
-                  eff_kl_weight=1e-8)
-    torch.cuda.synchronize()
+    with lrelu_slope_replay() as slopes:  # the device's LeakyReLU slopes, replayed in the oracle (steputil)
+        out = ts.step(real.to(DEV), text.to(DEV), z.to(DEV), dv(eps_d), dv(eps_g), perm.int().to(DEV), anneal=3.0,
+                      eff_kl_weight=1e-8)
+        torch.cuda.synchronize()
+    d64 = lambda trips: [tuple(t.double() for t in trip) for trip in trips]  # noqa: E731
+    with slopes.oracle():
+        ref = O.train_step(PG, PD, optG, optD, real.double(), text.double(), z.double(), d64(eps_d), d64(eps_g),
+                           perm, kl_weight_eff=1e-8)
+    assert not ref["skipped"]
     assert abs(float(out["d_losses"][0]) - ref["d_loss_gan"]) < 1e-4 * abs(ref["d_loss_gan"])
     assert abs(float(out["r1"][0]) - ref["r1"]) < 1e-4 * abs(ref["r1"]) + 1e-7
     assert abs(float(out["g_gan"][0]) - ref["g_loss_gan"]) < 1e-4 * abs(ref["g_loss_gan"])

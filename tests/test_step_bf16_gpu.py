@@ -49,8 +49,9 @@ import torch
 
 from goldens import T, load
 from oracle import aurora_cpu as O
-from steputil import (DeviceTempTap, OracleTempTap, ReplayedStep, bf16_module_rounding, bf16_r1_floor, cosine, gpu_step,
-                      make_inputs, nchw, oracle_clone, oracle_models, rel_norm_diff, routing_agreement, whole)
+from steputil import (DeviceTempTap, OracleTempTap, ReplayedStep, bf16_module_rounding, bf16_r1_floor, bf16_weights,
+                      cosine, gpu_step, lrelu_slope_replay, make_inputs, nchw, oracle_clone, oracle_models,
+                      rel_norm_diff, routing_agreement, whole)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -113,10 +114,12 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
     report, fails = [], []
     k = topk or E
     rs = dtap_replay = None
+    slopes = lrelu_slope_replay()  # the device's MTM LeakyReLU slopes, replayed in every oracle run
     if replay:
         dtap_replay = DeviceTempTap()
-        rs = ReplayedStep(ts, *inputs_per_step[0], tap=dtap_replay, anneal=3.0, lr_g=lr, lr_d=lr,
-                          eff_kl_weight=EFF_KL)
+        with slopes:
+            rs = ReplayedStep(ts, *inputs_per_step[0], tap=dtap_replay, anneal=3.0, lr_g=lr, lr_d=lr,
+                              eff_kl_weight=EFF_KL)
 
     def check(ok, what):
         if not ok:
@@ -131,7 +134,7 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
             out, dtap = rs(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d],
                            [tuple(map(cu, e)) for e in eps_g], cu(perm.int())), dtap_replay
         else:
-            with DeviceTempTap() as dtap:
+            with DeviceTempTap() as dtap, slopes:
                 out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d],
                               [tuple(map(cu, e)) for e in eps_g], cu(perm.int()), anneal=3.0, lr_g=lr, lr_d=lr,
                               eff_kl_weight=EFF_KL)
@@ -153,19 +156,20 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
         # the bf16 floor: the same oracle step from the same point with only the discriminator's inputs and
         # weights rounded to bf16 (oracle.round_bf16_st) -- how far bf16 operands alone move each gradient
         PGf, PDf, optGf, optDf, fgrads = oracle_clone(PG, PD, optG, optD, lr=lr)
-        O.train_step(PGf, PDf, optGf, optDf, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
-                     kl_weight_eff=EFF_KL, routes_d=routes_d, routes_g=routes_g, d_round=O.round_bf16_st,
-                     after_d_step=use_device_d)
+        with slopes.oracle():
+            O.train_step(PGf, PDf, optGf, optDf, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
+                         kl_weight_eff=EFF_KL, routes_d=routes_d, routes_g=routes_g, d_round=O.round_bf16_st,
+                         after_d_step=use_device_d)
         # ... and the whole-step floor: also the generator's module outputs / their gradients in bf16
         PGw, PDw, optGw, optDw, wgrads = oracle_clone(PG, PD, optG, optD, lr=lr)
         pd_w_stepped = {}
-        with bf16_module_rounding(), OracleTempTap() as wtap:
-            O.train_step(PGw, PDw, optGw, optDw, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
+        with bf16_module_rounding(), OracleTempTap() as wtap, slopes.oracle():
+            O.train_step(bf16_weights(PGw), PDw, optGw, optDw, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
                          kl_weight_eff=EFF_KL, routes_d=routes_d, routes_g=routes_g, d_round=O.round_bf16_st,
                          after_d_step=lambda P: (pd_w_stepped.update({n: t.detach().clone() for n, t in P.items()}),
                                                  use_device_d(P)))
         pd_stepped = {}
-        with OracleTempTap() as rtap:
+        with OracleTempTap() as rtap, slopes.oracle():
             ref = O.train_step(PG, PD, optG, optD, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
                                kl_weight_eff=EFF_KL, routes_d=routes_d, routes_g=routes_g, full=True,
                                after_d_step=lambda P: (pd_stepped.update({n: t.detach().clone() for n, t in P.items()}),

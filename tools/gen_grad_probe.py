@@ -59,7 +59,12 @@ def main(R=32, B=2):
         xw.retain_grad()
         ref[pre] = xw
         y = O.modconv(xw, w, P_, pre + "modulated_conv.", padding=1)
-        return F.leaky_relu(y, 0.2)
+        y.retain_grad()
+        out = F.leaky_relu(y, 0.2)
+        out.retain_grad()
+        ref[pre + "y"] = y
+        ref[pre + "out"] = out
+        return out
     O.mtm = mtm
     img, _, kl, probs = O.generator(z.double(), text.double(), P, d64(eps_g), True, 3.0, 0.7)
     (img * G_img).sum().backward()
@@ -70,10 +75,20 @@ def main(R=32, B=2):
     ge = GeneratorEngine(st, E)
     ge.prep()
     dev = []
+    last = {}
     orig = ops.mtm_bwd_fused
+    orig_bo = ops.modconv_bwd_out
+
+    def bo(gz, z, d, Bn, HW, rows, act, gyt, gdd, zsub=None):
+        r = orig_bo(gz, z, d, Bn, HW, rows, act, gyt, gdd, zsub=zsub)
+        last.update(gz=gz.detach().float().cpu().clone(), z=z.detach().float().cpu().clone(), act=act,
+                    d=d.detach().float().cpu().clone(), gyt=gyt.detach().float().cpu().clone(), rows=rows,
+                    zsub=None if zsub is None else zsub.detach().float().cpu().clone())
+        return r
+    ops.modconv_bwd_out = bo
 
     def fused(g_xw, x, *a, **k):
-        dev.append((tuple(x.shape), g_xw.detach().float().cpu().clone()))
+        dev.append((tuple(x.shape), g_xw.detach().float().cpu().clone(), dict(last)))
         return orig(g_xw, x, *a, **k)
     ops.mtm_bwd_fused = fused
     im, _, _, _, _, ctx = ge.forward(z.cuda(), text.cuda(), [tuple(t.cuda() for t in e) for e in eps_g], 3.0, 0.7,
@@ -83,15 +98,30 @@ def main(R=32, B=2):
     ge.backward(ctx, gpad)
     torch.cuda.synchronize()
     ops.mtm_bwd_fused = orig
+    ops.modconv_bwd_out = orig_bo
     order = []
     for name in ("gen_block_16", "gen_block_8", "gen_block_4"):
         order += [f"{name}.conv_block.mtm2.", f"{name}.conv_block.mtm1."]
     rel = lambda a, b: float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-300))  # noqa
     print(f"image rel err {rel(im[..., :3].permute(0, 3, 1, 2).cpu(), img.detach()):.2e}")
-    for pre, (shape, g) in zip(order, dev):
+    for pre, (shape, g, L) in zip(order, dev):
         C = shape[-1]
         r = ref[pre].grad.permute(0, 2, 3, 1).reshape(-1, C)
-        print(f"{pre:32s} g_xw rel err {rel(g.reshape(-1, C), r):.2e}")
+        Co = ref[pre + "y"].shape[1]
+        nhwc = lambda t: t.detach().permute(0, 2, 3, 1).reshape(-1, Co)  # noqa: E731
+        gz, z = L["gz"][:, :Co], L["z"][:, :Co]
+        line = (f"{pre:32s} g_xw {rel(g.reshape(-1, C), r):.2e} | act {L['act']} zsub {L['zsub'] is not None} "
+                f"g_out {rel(gz, nhwc(ref[pre + 'out'].grad)):.2e}")
+        if L["act"] == 2:
+            line += f" ypre {rel(z, nhwc(ref[pre + 'y'])):.2e}"
+            flips = int(((z > 0) != (nhwc(ref[pre + 'y']) > 0)).sum())
+            line += f" sign flips {flips}/{z.numel()}"
+        else:
+            line += f" z(out) {rel(z, nhwc(ref[pre + 'out'])):.2e}"
+        HW = shape[1] * shape[2]
+        dd = L["d"][:, :Co].repeat_interleave(HW, 0)
+        line += f" g_ypre {rel(L['gyt'][:, :Co] / dd, nhwc(ref[pre + 'y'].grad)):.2e}"
+        print(line)
 
 
 if __name__ == "__main__":
