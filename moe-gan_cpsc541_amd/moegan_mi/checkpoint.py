@@ -81,17 +81,32 @@ def load_optimizer_state_dict(store, sd):
     return {k: g[k] for k in ("lr", "betas", "eps", "weight_decay") if k in g}
 
 
-def save_resume(path, generator, discriminator, epoch, step, lr_g, lr_d, betas=(0.5, 0.999)):
-    """Write the reference's resume layout (t2i_moe_gan.py:1484-1491)."""
-    torch.save({"generator": generator.state_dict(), "discriminator": discriminator.state_dict(),
-                "optimizer_g": optimizer_state_dict(generator._store, lr_g, betas),
-                "optimizer_d": optimizer_state_dict(discriminator._store, lr_d, betas),
-                "epoch": int(epoch), "step": int(step)}, path)
+def save_resume(path, generator, discriminator, epoch, step, lr_g, lr_d, betas=(0.5, 0.999), epoch_complete=False,
+                generators=None):
+    """Write the reference's resume layout (t2i_moe_gan.py:1484-1491).  ``epoch`` is the 0-based epoch the state
+    belongs to, as the reference stores it; ``epoch_complete`` (an extra key, absent from the reference's files)
+    marks a checkpoint written after that epoch finished, so resuming starts at the next one.  ``generators``:
+    name -> torch.Generator whose states are stored too (``rng/<name>``) so a resumed run continues the same z,
+    permutation and router-noise streams."""
+    ck = {"generator": generator.state_dict(), "discriminator": discriminator.state_dict(),
+          "optimizer_g": optimizer_state_dict(generator._store, lr_g, betas),
+          "optimizer_d": optimizer_state_dict(discriminator._store, lr_d, betas),
+          "epoch": int(epoch), "step": int(step), "epoch_complete": bool(epoch_complete)}
+    for name, g in (generators or {}).items():
+        ck["rng/" + name] = g.get_state()
+    torch.save(ck, path)
 
 
-def load_resume(path, generator, discriminator):
-    """Load a resume checkpoint (ours or the reference's); returns (epoch, step).  A model-only checkpoint
-    ({'generator', 'discriminator'}) or a bare generator state dict loads the weights and returns (0, 0)."""
+def resume_start_epoch(ck_epoch, ck):
+    """The epoch a resumed run starts at: the stored one (the reference's mid-epoch checkpoints), or the next when
+    the checkpoint marks its epoch complete."""
+    return int(ck_epoch) + (1 if ck.get("epoch_complete", False) else 0)
+
+
+def load_resume(path, generator, discriminator, generators=None):
+    """Load a resume checkpoint (ours or the reference's); returns (start epoch, step).  A model-only checkpoint
+    ({'generator', 'discriminator'}) or a bare generator state dict loads the weights and returns (0, 0).
+    ``generators``: name -> torch.Generator restored from the checkpoint's ``rng/<name>`` states when present."""
     ck = torch.load(path, map_location="cpu", weights_only=True)
     if "generator" not in ck:  # bare generator state dict (inference.py:44-49)
         generator.load_state_dict(ck)
@@ -103,4 +118,8 @@ def load_resume(path, generator, discriminator):
         load_optimizer_state_dict(generator._store, ck["optimizer_g"])
     if "optimizer_d" in ck:
         load_optimizer_state_dict(discriminator._store, ck["optimizer_d"])
-    return int(ck.get("epoch", 0)), int(ck.get("step", 0))
+    for name, g in (generators or {}).items():
+        st = ck.get("rng/" + name)
+        if st is not None:
+            g.set_state(st)
+    return resume_start_epoch(ck.get("epoch", 0), ck), int(ck.get("step", 0))

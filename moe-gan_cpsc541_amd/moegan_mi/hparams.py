@@ -82,6 +82,13 @@ def given_train_kwargs(params):
     return {name: p[key] for key, (name, _) in TRAIN_KWARGS.items() if key in p}
 
 
+def unapplied_keys(params):
+    """Keys of coerced hyperparameters that neither size the DataLoaders (batch_size) nor map to a
+    ``train_aurora_gan`` keyword: reported by train_model.py instead of being dropped silently."""
+    used = set(TRAIN_KWARGS) | set(CLIP_ALIASES) | {"batch_size"}
+    return {k for k in params if k not in used}
+
+
 def _num(x, what):
     if not isinstance(x, (int, float)) or isinstance(x, bool):
         raise ValueError(f"{what}: expected a number, got {x!r}")

@@ -477,10 +477,6 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
     discriminator = AuroraDiscriminator(dtype=dtype, seed=seed + 1).to(device)
     if checkpoint_activation:
         generator.enable_checkpointing()
-    start_epoch, step = 0, 0
-    if resume_from is not None:
-        start_epoch, step = load_resume(resume_from, generator, discriminator)
-        print(f"Resumed from {resume_from}: epoch {start_epoch}, step {step}")
     cfg = StepConfig(E=num_experts, topk=topk, dtype=dtype, r1_gamma=r1_gamma, clip_weight_16=clip_weight_16,
                      clip_weight_8=clip_weight_8, balance_weight=balance_weight, beta1=beta1, beta2=beta2,
                      max_res=max_resolution)
@@ -495,6 +491,11 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
     # randomness: per-rank z / permutation, rank-shared router noise
     g_local = torch.Generator(device=device).manual_seed(1_000_003 * (seed + 1) + 7919 * rank)
     g_shared = torch.Generator(device=device).manual_seed(1_000_003 * (seed + 1) + 17)
+    start_epoch, step = 0, 0
+    if resume_from is not None:  # also continues the z / permutation / router-noise streams when the file has them
+        start_epoch, step = load_resume(resume_from, generator, discriminator,
+                                        generators={f"local{rank}": g_local, "shared": g_shared})
+        print(f"Resumed from {resume_from}: epoch {start_epoch}, step {step}")
     from tqdm import tqdm
     runner = _StepRunner(ts, device, enabled=use_graphs)
     for epoch in range(start_epoch, num_epochs):
@@ -565,7 +566,8 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
         pbar.close()
         if save_every_epoch and rank == 0:
             save_resume(os.path.join(save_dir, f"aurora_checkpoint_epoch_{epoch + 1}.pt"), generator, discriminator,
-                        epoch + 1, step, cur_lr, cur_lr, (beta1, beta2))
+                        epoch, step, cur_lr, cur_lr, (beta1, beta2), epoch_complete=True,
+                        generators={"local0": g_local, "shared": g_shared})
         if val_dataloader is not None:
             vm = _validate(generator, discriminator, val_dataloader, gan_loss, temperature_factor, eff_kl, device,
                            process_group, g_local)

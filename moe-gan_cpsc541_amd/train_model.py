@@ -27,6 +27,21 @@ KL_WEIGHT = 0.001
 BALANCE_WEIGHT = 0.01
 
 
+class ShardSampler(torch.utils.data.Sampler):
+    """Rank ``rank``'s share of ``n`` validation samples, indices rank::world, with no padding: the all-reduced
+    validation sums then count every sample exactly once, as the single-process reference does
+    (t2i_moe_gan.py:1432-1473).  (DistributedSampler(drop_last=False) repeats samples to even out the shards.)"""
+
+    def __init__(self, n, rank, world):
+        self.idx = list(range(rank, n, world))
+
+    def __iter__(self):
+        return iter(self.idx)
+
+    def __len__(self):
+        return len(self.idx)
+
+
 class ProcessedMSCOCODataset(Dataset):
     """(image, text_embedding) pairs from two .npy files (data_processing_pipeline.py:425-470), memory-mapped."""
 
@@ -74,8 +89,8 @@ def parse_args(argv=None):
     p.add_argument("--clip_weights", type=str, default=None,
                    help="local OpenAI CLIP state_dict / safetensors: enables the (gradient-free) CLIP loss terms")
     p.add_argument("--hyperparameters", type=str, default=None,
-                   help="SageMaker-style hyperparameters.json (string values, sagemaker_train.py:85-102); its keys "
-                        "override the flags above")
+                   help="SageMaker-style hyperparameters.json (string values, sagemaker_train.py:85-102); batch_size "
+                        "and the train_aurora_gan keys override the flags above, other keys are reported as unused")
     return p.parse_args(argv)
 
 
@@ -92,6 +107,12 @@ def main(argv=None):
         device = torch.device("cuda", local)
         dist.init_process_group("nccl")
         pg = dist.group.WORLD
+    hp = {}
+    if args.hyperparameters:  # read before the DataLoaders: batch_size sizes them (sagemaker_train.py:233, :248)
+        from moegan_mi.hparams import load_sagemaker_hyperparameters
+        hp = load_sagemaker_hyperparameters(args.hyperparameters)
+        if "batch_size" in hp:
+            args.batch_size = int(hp["batch_size"])
     if rank == 0:
         print(f"Using device: {device}")
         print(f"Training args: {args}")
@@ -116,19 +137,19 @@ def main(argv=None):
                           num_workers=workers, pin_memory=True, drop_last=True)
     val_dl = None
     if val_ds is not None:  # every rank validates its shard; the sums are all-reduced inside the loop
-        vs = None
-        if world > 1:
-            from torch.utils.data.distributed import DistributedSampler
-            vs = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False, drop_last=False)
+        vs = ShardSampler(len(val_ds), rank, world) if world > 1 else None
         val_dl = DataLoader(val_ds, batch_size=args.batch_size, shuffle=False, sampler=vs, num_workers=workers,
                             pin_memory=True)
     kw = dict(num_epochs=args.epochs, lr=args.lr, beta1=args.beta1, beta2=args.beta2, r1_gamma=args.r1_gamma,
               clip_weight_16=args.clip_weight_64, clip_weight_8=args.clip_weight_32, kl_weight=args.kl_weight,
               balance_weight=args.balance_weight, log_interval=args.log_interval, save_interval=args.save_interval,
               gradient_accumulation_steps=args.gradient_accumulation_steps)
-    if args.hyperparameters:
-        from moegan_mi.hparams import given_train_kwargs, load_sagemaker_hyperparameters
-        kw.update(given_train_kwargs(load_sagemaker_hyperparameters(args.hyperparameters)))
+    if hp:
+        from moegan_mi.hparams import unapplied_keys, given_train_kwargs
+        kw.update(given_train_kwargs(hp))
+        ignored = unapplied_keys(hp)
+        if ignored and rank == 0:
+            print(f"Warning: hyperparameters not used by training: {', '.join(sorted(ignored))}")
     if args.clip_weights:
         M.load_clip_weights(args.clip_weights, device)
     kw.setdefault("max_resolution", args.max_resolution)

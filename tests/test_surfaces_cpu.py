@@ -28,13 +28,26 @@ def test_coercion_matches_sagemaker_rules():
 
 
 def test_train_kwargs_mapping_and_defaults():
-    from moegan_mi.hparams import given_train_kwargs, train_kwargs
+    from moegan_mi.hparams import given_train_kwargs, train_kwargs, unapplied_keys
     kw = train_kwargs({"learning_rate": 1e-4, "epochs": 6, "clip_weight_64": 0.3})
     assert kw["lr"] == 1e-4 and kw["num_epochs"] == 6 and kw["clip_weight_16"] == 0.3
     assert kw["clip_weight_8"] == 0.05 and kw["r1_gamma"] == 10.0  # sagemaker_train.py:271-294 defaults
     assert kw["gradient_accumulation_steps"] == 8 and kw["max_resolution"] == 16
     assert given_train_kwargs({"kl_weight": 0.002, "clip_weight_32": 0.07}) == {"kl_weight": 0.002,
                                                                                   "clip_weight_8": 0.07}
+    # keys that reach neither the loaders nor train_aurora_gan are reported, not dropped silently
+    assert unapplied_keys({"batch_size": 4, "kl_weight": 1e-3, "clip_weight_64": 0.1, "sagemaker_program": "x"}) \
+        == {"sagemaker_program"}
+
+
+def test_validation_shard_has_no_padding():
+    """Each rank validates indices rank::world, every sample exactly once over the ranks (train_model.py), so the
+    all-reduced sums equal the single-process reference's (t2i_moe_gan.py:1519-1639)."""
+    from train_model import ShardSampler
+    for n, world in ((10, 4), (3, 8), (16, 2)):
+        shards = [list(ShardSampler(n, r, world)) for r in range(world)]
+        assert sorted(i for sh in shards for i in sh) == list(range(n))
+        assert all(len(ShardSampler(n, r, world)) == len(sh) for r, sh in enumerate(shards))
 
 
 def test_hpo_config_schema():
@@ -136,9 +149,19 @@ def test_resume_checkpoint_layout(tmp_path):
     path = os.path.join(tmp_path, "ck.pt")
     M.save_resume(path, G, D, epoch=3, step=40, lr_g=1e-4, lr_d=1e-4)
     ck = torch.load(path, weights_only=True)
-    assert set(ck) == {"generator", "discriminator", "optimizer_g", "optimizer_d", "epoch", "step"}
+    # the reference's keys (:1484-1491) plus our end-of-epoch marker
+    assert set(ck) == {"generator", "discriminator", "optimizer_g", "optimizer_d", "epoch", "step", "epoch_complete"}
     G2, D2 = M.AuroraGenerator(seed=5), M.AuroraDiscriminator(seed=6)
-    assert M.load_resume(path, G2, D2) == (3, 40)
+    assert M.load_resume(path, G2, D2) == (3, 40)  # a mid-epoch checkpoint resumes that (0-based) epoch
+    # an end-of-epoch checkpoint resumes at the next epoch and continues the stored random streams
+    g = torch.Generator().manual_seed(11)
+    torch.randn(5, generator=g)
+    M.save_resume(path, G, D, epoch=3, step=40, lr_g=1e-4, lr_d=1e-4, epoch_complete=True,
+                  generators={"shared": g})
+    expect = torch.randn(4, generator=g)
+    g2 = torch.Generator().manual_seed(0)
+    assert M.load_resume(path, G2, D2, generators={"shared": g2, "absent": torch.Generator()}) == (4, 40)
+    assert torch.equal(torch.randn(4, generator=g2), expect)
     for k, v in G.state_dict().items():
         assert torch.equal(G2.state_dict()[k], v), k
     off, numel = G._store.offsets["mapping.0.weight"]
