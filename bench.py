@@ -344,14 +344,19 @@ def main():
             print(f"[bench] family attribution: {fam_total:.3f} ms of call time in the attributed step "
                   f"(host_bound={at.host_bound})", file=sys.stderr, flush=True)
 
-        def _prof(name):  # committed rocprofv3 records of this same workload (tools/gpu_families.sh)
-            path = os.path.join(REPO, "profiles", name)
-            if not os.path.exists(path):
-                return None
-            rec = json.load(open(path))
-            ok = (rec.get("batch") == B and rec.get("dtype") == args.dtype and rec.get("experts") == E and
-                  bool(rec.get("fp8", False)) == args.fp8 and rec.get("max_res", 16) == args.max_res)
-            return rec if ok else None
+        def _prof(name):  # committed rocprofv3 records of this same workload (tools/gpu_families.sh): the
+            # config's own file (family_time_C5.json ...) first, then the C2 one
+            stem, ext = os.path.splitext(name)
+            for path in (os.path.join(REPO, "profiles", f"{stem}_{args.config}{ext}"),
+                         os.path.join(REPO, "profiles", name)):
+                if not os.path.exists(path):
+                    continue
+                rec = json.load(open(path))
+                ok = (rec.get("batch") == B and rec.get("dtype") == args.dtype and rec.get("experts") == E and
+                      bool(rec.get("fp8", False)) == args.fp8 and rec.get("max_res", 16) == args.max_res)
+                if ok:
+                    return rec
+            return None
 
         ftime, ftraf = _prof("family_time.json"), _prof("family_traffic.json")
         for f in families:

@@ -76,7 +76,6 @@ def load_optimizer_state_dict(store, sd):
             if len(steps) > 1:
                 raise ValueError(f"parameters of one optimizer range carry different step counts {sorted(steps)}")
             cnt.fill_(steps.pop() if steps else 0)
-    store.step_count = int(store.step_dev[0])
     g = groups[0]
     return {k: g[k] for k in ("lr", "betas", "eps", "weight_decay") if k in g}
 

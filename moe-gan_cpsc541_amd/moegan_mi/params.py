@@ -98,7 +98,6 @@ class ParamStore:
         self.grad = torch.zeros(self.total, device=self.device, dtype=torch.float32)
         self.m = torch.zeros(self.total, device=self.device, dtype=torch.float32)
         self.v = torch.zeros(self.total, device=self.device, dtype=torch.float32)
-        self.step_count = 0  # host mirror (eager steps); the optimizer reads the device counter below
         self.step_dev = torch.zeros(1, device=self.device, dtype=torch.int32)
         self.step_dev_kl = torch.zeros(1, device=self.device, dtype=torch.int32)  # AdamW step of [n_main, n_opt)
         self.acc = None  # gradient accumulated over a window (gradient_accumulation_steps > 1), ensure_acc()
@@ -108,6 +107,13 @@ class ParamStore:
         self.shadow = None
         if shadow_dtype is not None and shadow_dtype != torch.float32:
             self.shadow = torch.zeros(self.total, device=self.device, dtype=shadow_dtype)
+
+    @property
+    def step_count(self):
+        """Optimizer steps taken (AdamW's step of the main range): the device counter, which the gated update
+        advances inside the step -- so eager steps, hipGraph replays and guard-skipped batches all count right
+        (a host mirror would also count captures, which execute nothing).  Reading it synchronises."""
+        return int(self.step_dev[0])
 
     def style_block(self):
         """(weight matrix view [sum Cin, 512], bias view [sum Cin], {prefix: column offset}) of the contiguous

@@ -176,7 +176,6 @@ class TrainStep:
         """clip_grad_norm_ + AdamW over ``grad[:n_opt]`` (torch semantics, :1333-1337 / :1417-1421).  ``ranges``:
         [(lo, hi, step counter, window bit)] -- each range is one gated launch with its own step counter."""
         n = store.n_opt
-        store.step_count += 1
         if grad_scale != 1.0:  # (loss / accumulation_steps) of the reference == scaling the summed gradient
             grad[:n].mul_(grad_scale)
         ss = torch.empty(1, device=self.dev)

@@ -1,6 +1,6 @@
 """Kernel time per family per step from a rocprofv3 --kernel-trace CSV of bench.py.
 
-  python tools/family_time.py run_kernel_trace.csv OUT.json [batch E dtype]
+  python tools/family_time.py run_kernel_trace.csv OUT.json [batch E dtype [fp8]]
 
 The window runs from the first to the last dispatch of ``k_d_loss`` (launched once per training step), i.e.
 exactly (#k_d_loss - 1) whole steps of whatever the traced command ran (eager warm-up, hipGraph replays and the
@@ -21,6 +21,7 @@ def main():
     batch = int(sys.argv[3]) if len(sys.argv) > 3 else 256
     experts = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     dtype = sys.argv[5] if len(sys.argv) > 5 else "bf16"
+    fp8 = len(sys.argv) > 6 and sys.argv[6] in ("1", "fp8", "mx8")
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     anchors = [i for i, r in enumerate(rows) if "k_d_loss" in r["Kernel_Name"]]
     if len(anchors) < 2:
@@ -38,7 +39,7 @@ def main():
     span = (int(win[-1]["End_Timestamp"]) - int(win[0]["Start_Timestamp"])) / 1e6 / steps
     busy = sum(t.values()) / steps
     fams = {f: {"ms_per_step": round(t[f] / steps, 4), "dispatches_per_step": round(n[f] / steps, 1)} for f in t}
-    rec = {"batch": batch, "experts": experts, "dtype": dtype, "steps_in_window": steps,
+    rec = {"batch": batch, "experts": experts, "dtype": dtype, "fp8": fp8, "steps_in_window": steps,
            "busy_ms_per_step": round(busy, 4), "span_ms_per_step": round(span, 4),
            "source": f"rocprofv3 --kernel-trace of bench.py, {steps} steps between the first and last k_d_loss",
            "families": fams}
