@@ -41,6 +41,11 @@ constexpr int NTHREADS = 256;
 #ifndef MG_EPI_BLOCK_SYNC
 #define MG_EPI_BLOCK_SYNC 0
 #endif
+// single LDS buffer with two register stages (prefetch distance two K steps) for tiles of at most
+// MG_SB2_MAX_TILE outputs
+#ifndef MG_SB2_MAX_TILE
+#define MG_SB2_MAX_TILE 0
+#endif
 #ifndef MG_GLDS
 #define MG_GLDS 0  // measured: on par with register staging at C2 (gemm 4096^3 +9%, expert GEMMs -20%)
 #endif
@@ -646,7 +651,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   constexpr bool GLDS = MG_GLDS && sizeof(T) == 2 && A_KC && B_KC && AL::kGlds && BL::kGlds &&
                         2 * STAGE * (int)sizeof(T) <= 65536;
   constexpr int NBUF = (GLDS || (2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE)) ? 2 : 1;
-  constexpr int NS = NBUF == 2 ? MG_NSTAGE : 1;
+  constexpr bool SB2 = NBUF == 1 && BM * BN <= MG_SB2_MAX_TILE;
+  constexpr int NS = NBUF == 2 ? MG_NSTAGE : (SB2 ? 2 : 1);
   __shared__ __attribute__((aligned(16))) T smem[NBUF * STAGE];
   static_assert(4 * 16 * (WN + 4) * 4 <= (int)sizeof(T) * STAGE, "epilogue staging does not fit");
 
@@ -834,6 +840,29 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
         }
       }
       __syncthreads();
+    }
+  } else if constexpr (SB2) {
+    // one LDS buffer, two register stages: the loads of step t+2 are issued right after step t's registers went
+    // to LDS, so two multiplies (not one) cover each load's latency.  Straight-line body over two K steps with
+    // tail-safe loads throughout (past kend they read zeros), so no branch splits the load stream and the
+    // compiler's vmcnt waits count only the older stage.
+    T* const As = smem;
+    T* const Bs = smem + A_ELEMS;
+    using TT = std::true_type;
+    gload(I0{}, kbeg, TT{});
+    gload(I1{}, kbeg + TBK, TT{});
+    for (int k0 = kbeg; k0 < kend; k0 += 2 * TBK) {
+      __syncthreads();
+      sstore(I0{}, k0, As, Bs);
+      __syncthreads();
+      gload(I0{}, k0 + 2 * TBK, TT{});
+      compute(As, Bs);
+      if (k0 + TBK >= kend) break;
+      __syncthreads();
+      sstore(I1{}, k0 + TBK, As, Bs);
+      __syncthreads();
+      gload(I1{}, k0 + 3 * TBK, TT{});
+      compute(As, Bs);
     }
   } else {
     // one LDS buffer, one register stage: store, barrier, prefetch the next step, multiply

@@ -162,25 +162,37 @@ class _RoundBoth(torch.autograd.Function):
 
 
 class bf16_module_rounding:
-    """Context manager: the oracle's module outputs (modulated convs, MTMs, convolution / attention blocks,
-    expert FFNs) and the gradients flowing back through them are rounded to bf16 -- a coarse model of a bf16
-    device (which also rounds many more intermediates and its weights).  With ``d_round=oracle.round_bf16_st``
-    on the discriminator this gives the bf16 FLOOR of a whole step's gradients: how far bf16 storage alone,
-    in otherwise exact fp32 arithmetic, moves them."""
-    NAMES = ("modconv", "mtm", "attention_block", "expert_ffn", "conv_block")
+    """Context manager: the tensors the bf16 device stores in bf16 -- module outputs (modulated convs, MTMs,
+    convolution / attention blocks, expert FFNs, the MoE layer's combined output, multi-head attention outputs)
+    and the block-internal activations that feed its MFMA GEMMs (LayerNorm outputs, the expert FFN's GELU'd hidden
+    activation) -- are rounded to bf16 in the oracle, values and the gradients flowing back through them.  With
+    ``d_round=oracle.round_bf16_st`` on the discriminator this gives the bf16 FLOOR of a whole step's gradients:
+    how far bf16 storage alone, in otherwise exact fp32 arithmetic, moves them.  (The LayerNorm / GELU / MHA /
+    MoE-output points are the device's bf16 tensors ``n1``/``n2``/``n3``, ``Hid``, the attention output and the
+    combine output, engine_g.py; the oracle computes them in fp32.)"""
+    NAMES = ("modconv", "mtm", "attention_block", "expert_ffn", "conv_block", "mha", "sparse_moe")
+    FUNCS = ("layer_norm", "gelu")  # torch.nn.functional, as the oracle calls them inside the blocks
 
     def __enter__(self):
         self.orig = {n: getattr(O, n) for n in self.NAMES}
-        for n, f in self.orig.items():
-            def wrap(*a, f=f, **k):
+        self.orig_f = {n: getattr(O.F, n) for n in self.FUNCS}
+
+        def wrapper(f):
+            def wrap(*a, **k):
                 r = f(*a, **k)
                 return (_RoundBoth.apply(r[0]),) + tuple(r[1:]) if isinstance(r, tuple) else _RoundBoth.apply(r)
-            setattr(O, n, wrap)
+            return wrap
+        for n, f in self.orig.items():
+            setattr(O, n, wrapper(f))
+        for n, f in self.orig_f.items():
+            setattr(O.F, n, wrapper(f))
         return self
 
     def __exit__(self, *exc):
         for n, f in self.orig.items():
             setattr(O, n, f)
+        for n, f in self.orig_f.items():
+            setattr(O.F, n, f)
         return False
 
 

@@ -59,7 +59,7 @@ REL = 2e-2        # bf16 outputs, relative L2
 COS = 0.999       # whole-model gradient cosine ...
 FLOOR_X = 2.5     # ... or its relative error within FLOOR_X x the bf16 step floor (bf16_module_rounding)
 COS_DELTA = 0.98  # |g|-weighted whole-model AdamW delta cosine
-COS_TENSOR = 0.9  # every tensor's gradient direction (structure, not precision)
+COS_TENSOR = 0.99  # every tensor's gradient direction, or within FLOOR_X x its own whole-step bf16 floor
 DELTA = 0.25      # logit-space near-tie margin for the top-k comparison (bounds the measured bf16 drift)
 EFF_KL = 0.001 * 1e-5
 torch.set_num_threads(8)
@@ -104,6 +104,18 @@ def _replay_adamw(store, p_before, mv_before, grad, coef, lr, b1=0.5, b2=0.999, 
         err2 += float((d_dev - d_ref).pow(2).sum())
         ref2 += float(d_ref.pow(2).sum())
     return (err2 / max(ref2, 1e-300)) ** 0.5
+
+
+@pytest.fixture(autouse=True)
+def _deterministic():
+    """Every cross-workgroup reduction in a fixed order (ops.set_deterministic), so each run of this test sees the
+    same device numbers: the bars below judge bf16 precision, not the run-to-run order of fp32 atomics (the
+    atomic and fixed-order modes are the same arithmetic in a different summation order,
+    tests/test_graph_replay_gpu.py)."""
+    from moegan_mi import ops
+    ops.set_deterministic(True)
+    yield
+    ops.set_deterministic(False)
 
 
 def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
@@ -197,7 +209,10 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
                           f"{f_img:.2e}); per-token terms rel err {e_tok:.2e} (floor {f_tok:.2e})")
             check(e_tok <= FLOOR_X * f_tok, report[-1])
             check(e_img <= FLOOR_X * f_img, report[-1])
-            check(abs(s_ref) <= FLOOR_X * f_sum or s_dev * s_ref > 0, report[-1])
+            # (e) the block's scalar itself within FLOOR_X x its floor, and the reference's sign wherever the
+            # reference stands above that floor
+            check(abs(s_dev - s_ref) <= FLOOR_X * f_sum, report[-1])
+            check(abs(s_ref) <= f_sum or s_dev * s_ref > 0, report[-1])
         # ---- routing ----
         for tag, dev_t, dev_p, ref_p in (("D", out["topi_d"], out["probs_d"], ref["probs_d"]),
                                          ("G", out["topi"], out["probs"], ref["probs"])):
@@ -264,7 +279,8 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
                 g = (gbuf[off:off + numel] * coef).cpu()
                 c, rn = cosine(g, rg), rel_norm_diff(g, rg)
                 fl = rel_norm_diff(fgrads[which][n], rg)
-                worst.append((c, rn, fl, which + ":" + n))
+                fw_ = rel_norm_diff(wgrads[which][n], rg) if wgrads[which].get(n) is not None else fl
+                worst.append((c, rn, fw_, which + ":" + n))
                 # direction bar per tensor; a tensor whose own bf16 floor is already >= 20 % (an expert that few
                 # tokens reach at a test-sized batch) is held to FLOOR_X x its floor instead.  The router
                 # temperatures (single-element cancelling sums) are checked above on their per-token terms; the
@@ -281,8 +297,9 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
                     check(c >= COS_TENSOR or rn <= FLOOR_X * fw,
                           f"step{si} grad {which}:{n} cosine {c:.6f} rel {rn:.2e} (whole-step floor {fw:.2e})")
                 else:
-                    check(c >= COS_TENSOR or (fl >= 0.2 and rn <= FLOOR_X * fl),
-                          f"step{si} grad {which}:{n} cosine {c:.6f} rel {rn:.2e} (floor {fl:.2e})")
+                    # cosine >= COS_TENSOR, or within FLOOR_X x the tensor's own whole-step bf16 floor
+                    check(c >= COS_TENSOR or rn <= FLOOR_X * fw,
+                          f"step{si} grad {which}:{n} cosine {c:.6f} rel {rn:.2e} (whole-step floor {fw:.2e})")
                 dd = (store.data[off:off + numel] - before[off:off + numel]).cpu()
                 rd = ((pd_stepped[n] if which == "D" else P[n].detach()) - pbefore[n]).reshape(-1)
                 w = rg.reshape(-1).abs()
