@@ -849,19 +849,33 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     T* const As = smem;
     T* const Bs = smem + A_ELEMS;
     using TT = std::true_type;
+    // scheduling barriers pin the issue order (stage 0 before stage 1, each reload before its multiply) so on
+    // both paths into the loop head stage 0 is the older stage and its wait is vmcnt(#stage-1 loads), not 0
     gload(I0{}, kbeg, TT{});
+    __builtin_amdgcn_sched_barrier(0);
     gload(I1{}, kbeg + TBK, TT{});
-    for (int k0 = kbeg; k0 < kend; k0 += 2 * TBK) {
+    __builtin_amdgcn_sched_barrier(0);
+    // whole pairs of K steps in the loop (one exit: the waits at its head see one load order), an odd last
+    // step after it
+    int k0 = kbeg;
+    for (; k0 + TBK < kend; k0 += 2 * TBK) {
       __syncthreads();
       sstore(I0{}, k0, As, Bs);
       __syncthreads();
       gload(I0{}, k0 + 2 * TBK, TT{});
+      __builtin_amdgcn_sched_barrier(0);
       compute(As, Bs);
-      if (k0 + TBK >= kend) break;
       __syncthreads();
       sstore(I1{}, k0 + TBK, As, Bs);
       __syncthreads();
       gload(I1{}, k0 + 3 * TBK, TT{});
+      __builtin_amdgcn_sched_barrier(0);
+      compute(As, Bs);
+    }
+    if (k0 < kend) {
+      __syncthreads();
+      sstore(I0{}, k0, As, Bs);
+      __syncthreads();
       compute(As, Bs);
     }
   } else {
