@@ -408,7 +408,8 @@ struct Epi {
   const float* addvec; int add_shift; int64_t add_ld;  // v += addvec[(m >> add_shift)*add_ld + n]
   int rm_mode, rm_Mc, rm_lgOW, rm_lgOHW;  // rm_mode 1: stride-2 transposed-conv class rows -> NHWC rows
   TO* Cpre; int64_t ldc_pre;  // optional: store the pre-activation value too (row m, column n)
-  int64_t zstride;  // split-K partial slabs: output offset blockIdx.z * zstride (raw partial epilogue)
+  int64_t zstride;  // split-K partial slabs: output offset zi * zstride (raw partial epilogue)
+  int zi;           // this block's split index (set by gemm_kernel: blockIdx.z, or its XCD-ordered remap)
   int vec_ok;       // host-checked: 8-column vector path legal (alignment / pitches, no remap, no atomics)
   int g;
   MG_DEV void set_group(int gg) { g = gg; }
@@ -484,7 +485,7 @@ struct Epi {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += t[j];
     }
-    TO* c = C + (int64_t)g * gstride_c + (int64_t)m * ldc + n + (int64_t)blockIdx.z * zstride;
+    TO* c = C + (int64_t)g * gstride_c + (int64_t)m * ldc + n + (int64_t)zi * zstride;
     if (accumulate) {
       ld8(c, t);
 #pragma unroll
@@ -512,7 +513,7 @@ struct Epi {
     if (resid) v += ldf(resid, (int64_t)m * ld_res + n);
     int64_t nn = n;
     if (remap_taps > 0) nn = (int64_t)(n & ((1 << remap_lgcin) - 1)) * remap_taps + (n >> remap_lgcin);
-    int64_t idx = (int64_t)g * gstride_c + (int64_t)m * ldc + nn + (int64_t)blockIdx.z * zstride;
+    int64_t idx = (int64_t)g * gstride_c + (int64_t)m * ldc + nn + (int64_t)zi * zstride;
     if (atomic) {
       atomicAdd(reinterpret_cast<float*>(C) + idx, v);
     } else {
@@ -529,7 +530,7 @@ struct Grouping {
   const int* row_off;    // [ngroups+1] row (mode 1) / reduction (mode 2) offsets
   const int* tile_off;   // mode 1: [ngroups+1] prefix of ceil(rows_g / BM)
   int rows_per_group;    // mode 3: ngroups equal groups of this many rows (no tables)
-  int swz;               // mode 0: XCD-aware tile order
+  int swz;               // mode 0: XCD-aware tile order (1: every launch, 2: split-K launches only)
 };
 
 // ---------------------------------------------------------------------------
@@ -901,21 +902,26 @@ template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, 
 __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M, int N, int K, int kchunk, Grouping grp) {
   constexpr int TBK = Tile<T>::BK;
   // ---- resolve tile / group ----
-  int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  if (grp.mode == 0 && grp.swz) {
-    // XCD-aware tile order: blocks that share an XCD (linear id % 8) take a contiguous run of
-    // (m-tile, n-tile) work items, n fastest -- neighbouring m-tiles (overlapping implicit-conv input
-    // rows) and all n-tiles of one m-tile then meet in the same L2.
-    const int gx = gridDim.x, gy = gridDim.y, nb = gx * gy;
-    const int bid = blockIdx.x + blockIdx.y * gx;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (grp.mode == 0 && grp.swz && (grp.swz == 1 || gridDim.z > 1)) {
+    // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs by linear id, so blocks that
+    // share an XCD (linear id % 8) take a contiguous run of (split, m-tile, n-tile) work items, n fastest --
+    // all tiles of one K split (which read the same operand rows: a split-K weight gradient re-reads its
+    // operands once per output tile) and neighbouring m-tiles then meet in the same L2.
+    const int gx = gridDim.x, gy = gridDim.y, gxy = gx * gy, nb = gxy * gridDim.z;
+    const int bid = bx + by * gx + bz * gxy;
     const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
     const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    m0 = (w / gy) * BM;
-    n0 = (w - (w / gy) * gy) * BN;
+    bz = w / gxy;
+    const int rem = w - bz * gxy;
+    bx = rem / gy;
+    by = rem - bx * gy;
   }
+  int m0 = bx * BM, n0 = by * BN;
+  ep.zi = bz;
   int mrow_base = 0;  // global row offset of this group (mode 1)
   int Mloc = M;
-  int kbeg = blockIdx.z * kchunk, kend = min(K, kbeg + kchunk);
+  int kbeg = bz * kchunk, kend = min(K, kbeg + kchunk);
   int g = 0;
   if (grp.mode == 1) {
     int t = blockIdx.x;
@@ -988,7 +994,7 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   dim3 grid(gx, cdiv(N, BN), gz);
   EP e2 = ep;
   e2.vec_ok = e2.host_vec_ok() ? 1 : 0;
-  if (grp.mode == 0) grp.swz = g_mg_tune[MG_TUNE_XCD] == 1 ? 1 : 0;  // measured: no gain at these shapes
+  if (grp.mode == 0) grp.swz = g_mg_tune[MG_TUNE_XCD];
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP, TAG>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
                      K, kchunk, grp);
 }

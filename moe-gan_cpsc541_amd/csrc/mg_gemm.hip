@@ -12,6 +12,8 @@ namespace {
 
 
 constexpr Grouping kNoGroup{0, 1, nullptr, nullptr, 0};
+// plain (ungrouped) launch with the tuned XCD tile order (MG_TUNE_XCD), for the direct split-K slab launches
+inline Grouping xcd_group() { Grouping g = kNoGroup; g.swz = g_mg_tune[MG_TUNE_XCD]; return g; }
 
 inline bool a_xf(const mg_epilogue* e) { return e && (e->a_idx || e->a_rowscale || e->a_gelu); }
 
@@ -114,7 +116,7 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
     dim3 grid(cdiv(M, 64), cdiv(N, 64), splits);
     hipLaunchKernelGGL((gemm_kernel<T, 64, 64, decltype(akc)::value, decltype(bkc)::value, decltype(la),
                                     decltype(lb), Epi<float>>),
-                       grid, dim3(NTHREADS), 0, st, la, lb, slab, M, N, K, kchunk, kNoGroup);
+                       grid, dim3(NTHREADS), 0, st, la, lb, slab, M, N, K, kchunk, xcd_group());
   };
   const T* Ap = reinterpret_cast<const T*>(A);
   const T* Bp = reinterpret_cast<const T*>(B);
@@ -316,7 +318,7 @@ bool conv_slabs_t(const void* x, int B, int H, int W, int Cin, const void* wpack
   LdKC<T> lb{reinterpret_cast<const T*>(wpack), K, Cout, K, nullptr, 1, nullptr, 0};
   dim3 grid(cdiv(M, BM), cdiv(Cout, BN), splits);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, true, LdKCConv<T, false, SC>, LdKC<T>, Epi<float>>), grid,
-                     dim3(NTHREADS), 0, st, la, lb, slab, M, Cout, K, kchunk, kNoGroup);
+                     dim3(NTHREADS), 0, st, la, lb, slab, M, Cout, K, kchunk, xcd_group());
   auto ep = make_epi<TO>(y, ldy, e);
   ep.vec_ok = ep.host_vec_ok() ? 1 : 0;
   int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
@@ -490,7 +492,7 @@ bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, i
   slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
   dim3 grid(cdiv(Cout, BM), cdiv(N, BN), splits);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, false, LdMC<T>, LdMCConv<T, XF>, Epi<float>>), grid, dim3(NTHREADS),
-                     0, st, la, lb, slab, Cout, N, P, kchunk, kNoGroup);
+                     0, st, la, lb, slab, Cout, N, P, kchunk, xcd_group());
   // (Cout x Cin / CC) blocks: enough to spread the slab reads over the chip, >= 8 channels per segment
   int lgCC = ilog2(Cin);
   while (lgCC > 3 && (int64_t)Cout * (Cin >> lgCC) < 1024) --lgCC;

@@ -221,65 +221,60 @@ __global__ void k_disp_scan(int* __restrict__ blk_counts, int nblk, int E, int b
   }
 }
 
-// each thread owns DCH/256 = 16 consecutive assignments of the block's chunk
+// Positions of a block's DCH assignments in the expert-sorted order, in assignment order within each expert (the
+// same order as a serial pass).  The block walks its chunk in DCH / 256 rounds of 256 consecutive assignments (one
+// per thread); per round and expert, a wave ballot gives the wave's count (popcount) and each lane's rank among
+// the wave's lanes of that expert (mbcnt) -- a few instructions per expert, no per-thread E-wide scans.  One
+// thread per expert then turns the (round, wave) counts into exclusive bases in assignment order.
 template <int E>
-__global__ void k_disp_scatter(const int* __restrict__ topi, const float* __restrict__ gate, int n,
-                               const int* __restrict__ blk_base, const int* __restrict__ row_off,
-                               int* __restrict__ perm, int* __restrict__ pos_of, float* __restrict__ gate_pos) {
-  constexpr int PER = DCH / 256;
-  __shared__ int wtot[4][E];
-  int a0 = blockIdx.x * DCH + threadIdx.x * PER;
-  // the thread's PER assignments into registers first: independent loads in flight (a dependent chain of PER
-  // global loads per loop would cost PER round trips)
-  int ex_r[PER];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) ex_r[i] = a0 + i < n ? topi[a0 + i] : -1;
-  int loc[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) loc[e] = 0;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-#pragma unroll
-    for (int e = 0; e < E; ++e) loc[e] += (ex_r[i] == e);
-  }
-  // exclusive prefix of loc[e] over the block's 256 threads (thread order = assignment order): inclusive wave
-  // scans, then the preceding waves' totals
+__global__ __launch_bounds__(256) void k_disp_scatter(const int* __restrict__ topi, const float* __restrict__ gate,
+                                                      int n, const int* __restrict__ blk_base,
+                                                      const int* __restrict__ row_off, int* __restrict__ perm,
+                                                      int* __restrict__ pos_of, float* __restrict__ gate_pos) {
+  constexpr int R = DCH / 256;
+  __shared__ int wc[R * 4][E];  // count of expert e in (round r, wave w); then its exclusive base
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int incl[E];
+  const int a0 = blockIdx.x * DCH;
+  // every round's assignment into registers first (independent loads in flight)
+  int ex_r[R];
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    int v = loc[e];
+  for (int r = 0; r < R; ++r) {
+    const int a = a0 + r * 256 + (int)threadIdx.x;
+    ex_r[r] = a < n ? topi[a] : -1;
+  }
+  int rk[R];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int u = __shfl_up(v, d, 64);
-      if (lane >= d) v += u;
+  for (int r = 0; r < R; ++r) {
+    int rank = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint64_t m = __ballot(ex_r[r] == e);
+      if (ex_r[r] == e)
+        rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (lane == 0) wc[r * 4 + wid][e] = __popcll(m);
     }
-    incl[e] = v;
-    if (lane == 63) wtot[wid][e] = v;
+    rk[r] = rank;
   }
   __syncthreads();
-  int off[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    int base = 0;
-    for (int w = 0; w < wid; ++w) base += wtot[w][e];
-    off[e] = row_off[e] + blk_base[blockIdx.x * E + e] + base + incl[e] - loc[e];
+  if ((int)threadIdx.x < E) {  // (round, wave) order = assignment order
+    const int e = threadIdx.x;
+    int base = row_off[e] + blk_base[blockIdx.x * E + e];
+    for (int q = 0; q < R * 4; ++q) {
+      const int c = wc[q][e];
+      wc[q][e] = base;
+      base += c;
+    }
   }
-  float g_r[PER];
+  __syncthreads();
 #pragma unroll
-  for (int i = 0; i < PER; ++i) g_r[i] = a0 + i < n ? gate[a0 + i] : 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int a = a0 + i;
-    if (a < n) {
-      const int ex = ex_r[i];
-      int pos = 0;
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        if (ex == e) pos = off[e]++;
+  for (int r = 0; r < R; ++r) {
+    const int a = a0 + r * 256 + (int)threadIdx.x;
+    const int ex = ex_r[r];
+    if (a < n && (unsigned)ex < (unsigned)E) {
+      const int pos = wc[r * 4 + wid][ex] + rk[r];
       perm[pos] = a;
       pos_of[a] = pos;
-      gate_pos[pos] = g_r[i];
+      gate_pos[pos] = gate[a];
     }
   }
 }
