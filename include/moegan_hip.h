@@ -418,6 +418,21 @@ int mg_weight_norm_fwd(const float* v, const float* g, int O, int K, float* W, f
 /* weight_norm backward: gg += sum gW v/||v||, gv += (g/||v||)(gW - gg_o v/||v||). */
 int mg_weight_norm_bwd(const float* v, const float* g, const float* norm, const float* gW, int O, int K, float* gv, float* gg, void* stream);
 
+/* Batched weight_norm of several layers in one launch (the discriminator's four, t2i_moe_gan.py:869-886): per
+   descriptor, bwd = 0 computes W and norm from (v, g) as mg_weight_norm_fwd; bwd = 1 accumulates gv and gg from
+   (v, g, norm, gW) as mg_weight_norm_bwd.  One block per output row; at most 8 descriptors per launch. */
+typedef struct mg_wn_desc {
+  int32_t O, K;
+  const float* v;
+  const float* g;
+  float* norm;     /* fwd: out; bwd: in */
+  float* W;        /* fwd: out */
+  const float* gW; /* bwd: in */
+  float* gv;       /* bwd: +=  */
+  float* gg;       /* bwd: +=  */
+} mg_wn_desc;
+int mg_weight_norm_batch(int bwd, int n, const mg_wn_desc* descs, void* stream);
+
 /* out[0] += sum x^2 (clip_grad_norm_ total norm, t2i_moe_gan.py:1336/1420); deterministic (fixed-order fold). */
 int mg_sumsq(const float* x, int64_t n, float* out, void* stream);
 

@@ -181,9 +181,8 @@ __global__ __launch_bounds__(1024) void k_colsum_fin(const float* __restrict__ p
 }
 
 // weight norm: W[o] = g[o] * v[o] / ||v[o]||  (t2i_moe_gan.py:869-886, torch weight_norm dim=0)
-__global__ void k_wn_fwd(const float* __restrict__ v, const float* __restrict__ g, int O, int K,
-                         float* __restrict__ W, float* __restrict__ norm) {
-  int o = blockIdx.x;
+MG_DEV void wn_fwd_row(const float* __restrict__ v, const float* __restrict__ g, int o, int K,
+                       float* __restrict__ W, float* __restrict__ norm) {
   __shared__ float red[16];
   float s = 0.f;
   for (int k = threadIdx.x; k < K; k += blockDim.x) {
@@ -205,10 +204,14 @@ __global__ void k_wn_fwd(const float* __restrict__ v, const float* __restrict__ 
   for (int k = threadIdx.x; k < K; k += blockDim.x) W[(int64_t)o * K + k] = v[(int64_t)o * K + k] * sc;
 }
 
+__global__ void k_wn_fwd(const float* __restrict__ v, const float* __restrict__ g, int O, int K,
+                         float* __restrict__ W, float* __restrict__ norm) {
+  wn_fwd_row(v, g, blockIdx.x, K, W, norm);
+}
+
 // gg[o] += sum_k gW*v/n ; gv = (g/n) * (gW - (gg_o/n) * v)
-__global__ void k_wn_bwd(const float* __restrict__ v, const float* __restrict__ g, const float* __restrict__ norm,
-                         const float* __restrict__ gW, int O, int K, float* __restrict__ gv, float* __restrict__ gg) {
-  int o = blockIdx.x;
+MG_DEV void wn_bwd_row(const float* __restrict__ v, const float* __restrict__ g, const float* __restrict__ norm,
+                       const float* __restrict__ gW, int o, int K, float* __restrict__ gv, float* __restrict__ gg) {
   __shared__ float red[16];
   float n = norm[o];
   float s = 0.f;
@@ -229,6 +232,28 @@ __global__ void k_wn_bwd(const float* __restrict__ v, const float* __restrict__ 
     int64_t i = (int64_t)o * K + k;
     gv[i] += a * (gW[i] - b * v[i]);
   }
+}
+
+__global__ void k_wn_bwd(const float* __restrict__ v, const float* __restrict__ g, const float* __restrict__ norm,
+                         const float* __restrict__ gW, int O, int K, float* __restrict__ gv, float* __restrict__ gg) {
+  wn_bwd_row(v, g, norm, gW, blockIdx.x, K, gv, gg);
+}
+
+// several layers' weight norms (forward or backward) in one launch: block -> (descriptor, output row)
+constexpr int kWnMax = 8;
+struct WnArgs {
+  mg_wn_desc d[kWnMax];
+  int row_off[kWnMax + 1];
+  int n, bwd;
+};
+__global__ void k_wn_batch(WnArgs a) {
+  const int b = blockIdx.x;
+  int p = 0;
+  while (p + 1 < a.n && b >= a.row_off[p + 1]) ++p;
+  const mg_wn_desc& q = a.d[p];
+  const int o = b - a.row_off[p];
+  if (a.bwd) wn_bwd_row(q.v, q.g, q.norm, q.gW, o, q.K, q.gv, q.gg);
+  else wn_fwd_row(q.v, q.g, o, q.K, q.W, q.norm);
 }
 
 // sum of squares of n floats, accumulated into out[0] -- deterministically: <= 1024 blocks write one partial
@@ -566,6 +591,29 @@ extern "C" int mg_weight_norm_bwd(const float* v, const float* g, const float* n
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_wn_bwd, dim3(O), dim3(256), 0, st, v, g, norm, gW, O, K, gv, gg);
   return mg_check_launch("mg_weight_norm_bwd");
+}
+
+extern "C" int mg_weight_norm_batch(int bwd, int n, const mg_wn_desc* descs, void* stream) {
+  MG_REQUIRE(n >= 0 && (n == 0 || descs), "bad descriptor table");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int i0 = 0; i0 < n; i0 += kWnMax) {
+    WnArgs a{};
+    a.bwd = bwd ? 1 : 0;
+    int rows = 0;
+    for (int i = i0; i < n && i < i0 + kWnMax; ++i) {
+      const mg_wn_desc& q = descs[i];
+      MG_REQUIRE(q.O > 0 && q.K > 0 && q.v && q.g && q.norm, "bad weight-norm descriptor");
+      MG_REQUIRE(bwd ? (q.gW && q.gv && q.gg) : (q.W != nullptr), "weight-norm descriptor misses an operand");
+      a.d[a.n] = q;
+      a.row_off[a.n++] = rows;
+      rows += q.O;
+    }
+    a.row_off[a.n] = rows;
+    hipLaunchKernelGGL(k_wn_batch, dim3(rows), dim3(256), 0, st, a);
+    int rc = mg_check_launch("mg_weight_norm_batch");
+    if (rc) return rc;
+  }
+  return MG_OK;
 }
 
 extern "C" int mg_sumsq(const float* x, int64_t n, float* out, void* stream) {

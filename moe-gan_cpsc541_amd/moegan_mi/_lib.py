@@ -46,12 +46,19 @@ class ColsumDesc(ctypes.Structure):
     _fields_ = [("dtype", _i32), ("R", _i32), ("C", _i32), ("ld", _i64), ("X", _c_void_p), ("out", _c_void_p)]
 
 
+class WnDesc(ctypes.Structure):
+    """Mirror of ``mg_wn_desc``."""
+    _fields_ = [("O", _i32), ("K", _i32), ("v", _c_void_p), ("g", _c_void_p), ("norm", _c_void_p), ("W", _c_void_p),
+                ("gW", _c_void_p), ("gv", _c_void_p), ("gg", _c_void_p)]
+
+
 # Argument types are derived from include/moegan_hip.h itself, so the binding
 # cannot drift from the C ABI (the header travels with the library).
 _HEADER = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "moegan_hip.h"))
 _CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "size_t": ctypes.c_size_t, "float": _f32,
           "void": _c_void_p, "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc),
-          "mg_prep_desc": ctypes.POINTER(PrepDesc), "mg_colsum_desc": ctypes.POINTER(ColsumDesc)}
+          "mg_prep_desc": ctypes.POINTER(PrepDesc), "mg_colsum_desc": ctypes.POINTER(ColsumDesc),
+          "mg_wn_desc": ctypes.POINTER(WnDesc)}
 _RESTYPE = {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "const char*": ctypes.c_char_p}
 SIG_RE = r"\b(int|int64_t|const char\*)\s+(mg_\w+)\(([^)]*)\);"
 
@@ -70,7 +77,8 @@ def _parse_header(path=_HEADER):
                 continue
             base = a.replace("const ", "").split()[0].rstrip("*")
             if "*" in a:
-                types.append(_CTYPE[base] if base in ("mg_epilogue", "mg_gemm_desc", "mg_prep_desc", "mg_colsum_desc")
+                types.append(_CTYPE[base] if base in ("mg_epilogue", "mg_gemm_desc", "mg_prep_desc", "mg_colsum_desc",
+                                                          "mg_wn_desc")
                              else _c_void_p)
             else:
                 types.append(_CTYPE[base])

@@ -51,9 +51,9 @@ class DiscriminatorEngine:
     # ------------------------------------------------------------------
     def prep(self):
         """Weight-norm the four layers and pack them (call after every D optimizer step)."""
-        W, norm = {}, {}
-        for pre in WN_LAYERS:
-            W[pre], norm[pre] = ops.weight_norm_fwd(self.P(pre + "weight_v"), self.P(pre + "weight_g"))
+        outs = ops.weight_norm_fwd_batch([(self.P(pre + "weight_v"), self.P(pre + "weight_g")) for pre in WN_LAYERS])
+        W = {pre: o[0] for pre, o in zip(WN_LAYERS, outs)}
+        norm = {pre: o[1] for pre, o in zip(WN_LAYERS, outs)}
         self.W, self.norm = W, norm
         cdt = self.cdt
         pb = ops.PrepBatch(cdt)  # the packs in one launch
@@ -138,9 +138,8 @@ class DiscriminatorEngine:
 
     def finish_grads(self):
         # reference weight layout: conv_layers.0 packed as [o][tap*3+c] in the GEMM -> remap to [o][c][kh][kw]
-        for pre in WN_LAYERS:
-            ops.weight_norm_bwd(self.P(pre + "weight_v"), self.P(pre + "weight_g"), self.norm[pre], self.dW[pre],
-                                self.G(pre + "weight_v"), self.G(pre + "weight_g"))
+        ops.weight_norm_bwd_batch([(self.P(pre + "weight_v"), self.P(pre + "weight_g"), self.norm[pre], self.dW[pre],
+                                    self.G(pre + "weight_v"), self.G(pre + "weight_g")) for pre in WN_LAYERS])
 
     # ------------------------------------------------------------------
     def d_phase(self, real_nchw, text, fake_img, fake_layout, perm, r1_gamma):
@@ -269,7 +268,8 @@ class DiscriminatorEngine:
         g_tb = ops.zeros(B, device=self.dev)
         ops.segsum(g_logits, B, g_logits.shape[1], 1, g_tb.view(B, 1), ld=1)
         self.begin_grads()
-        g_img = torch.zeros(B, H, H, 4, device=self.dev, dtype=torch.float32) if want_input else None
+        # the image gradient is consumed inside the step (the generator backward): from the per-step zero arena
+        g_img = ops.zeros(B, H, H, 4, device=self.dev) if want_input else None
         self.stack_backward(f, g_logits, want_params=True, g_input=g_img)
         self._text_head_bwd(g_tb, ctx["t"], ctx["text"])
         self.side.join()

@@ -436,6 +436,28 @@ def weight_norm_bwd(v, g, norm, gW, gv, gg):
     call("mg_weight_norm_bwd", ptr(v), ptr(g), ptr(norm), ptr(gW), O, v[0].numel(), ptr(gv), ptr(gg), S())
 
 
+def weight_norm_fwd_batch(layers):
+    """[(v, g)] -> [(W, norm)] for every layer in one launch (mg_weight_norm_batch)."""
+    outs, descs = [], []
+    for v, g in layers:
+        O, K = v.shape[0], v[0].numel()
+        W = torch.empty_like(v)
+        norm = torch.empty(O, device=v.device, dtype=torch.float32)
+        outs.append((W, norm))
+        descs.append(L.WnDesc(O, K, ptr(v), ptr(g), ptr(norm), ptr(W), None, None, None))
+    arr = (L.WnDesc * len(descs))(*descs)
+    call("mg_weight_norm_batch", 0, len(descs), arr, S())
+    return outs
+
+
+def weight_norm_bwd_batch(layers):
+    """[(v, g, norm, gW, gv, gg)]: gv, gg accumulate every layer's weight-norm backward in one launch."""
+    descs = [L.WnDesc(v.shape[0], v[0].numel(), ptr(v), ptr(g), ptr(norm), None, ptr(gW), ptr(gv), ptr(gg))
+             for v, g, norm, gW, gv, gg in layers]
+    arr = (L.WnDesc * len(descs))(*descs)
+    call("mg_weight_norm_batch", 1, len(descs), arr, S())
+
+
 def sumsq(x, out):
     call("mg_sumsq", ptr(x), x.numel(), ptr(out), S())
     return out

@@ -38,7 +38,8 @@ FAMILIES = {
     "adamw": ("hbm", ("mg_adamw_dev", "mg_adamw_dev_shadow", "mg_adamw")),
     "bias_colsum": ("hbm", ("mg_colsum", "mg_grouped_colsum", "mg_colsum_batch", "mg_segsum", "mg_const_bwd")),
     "weight_prep": ("hbm", ("mg_pack_conv", "mg_pack_conv_flip", "mg_pack_dgrad_s2", "mg_wsq", "mg_wsq_bwd",
-                            "mg_router_reparam", "mg_weight_norm_fwd", "mg_weight_norm_bwd", "mg_quant_mx8",
+                            "mg_router_reparam", "mg_weight_norm_fwd", "mg_weight_norm_bwd", "mg_weight_norm_batch",
+                            "mg_quant_mx8",
                             "mg_prep_batch")),
     "layernorm": ("hbm", ("mg_layernorm_fwd", "mg_layernorm_bwd")),
     "router_aux": ("hbm", ("mg_router_bwd", "mg_moe_gate_grad", "mg_moe_token_grad", "mg_router_feat_grad",
@@ -170,6 +171,9 @@ def work(name, a):
         return 8.0 * a["O"] * a["K"]
     if name == "mg_weight_norm_bwd":
         return 16.0 * a["O"] * a["K"]
+    if name == "mg_weight_norm_batch":  # per descriptor, the single-layer formulas above
+        d = a["descs"]
+        return sum((16.0 if a["bwd"] else 8.0) * d[i].O * d[i].K for i in range(a["n"]))
     if name == "mg_colsum":
         return a["R"] * a["C"] * ELT[a["dtype"]] + a["C"] * 8
     if name == "mg_grouped_colsum":  # max_rows = the routed rows (T * k) the engine passes; rs: one fp32 per row
