@@ -42,6 +42,11 @@ extern "C" {
 
 #define MG_F32 0
 #define MG_BF16 1
+/* mg_gemm / mg_gemm_batch only: fp32 operands and accumulation, the MFMA products taken as split bf16
+   (hi * hi + hi * lo + lo * hi with hi = bf16(x), lo = bf16(x - hi)): ~2^-16 relative per product instead of the
+   exact-fp32 MFMA's 2^-24, at the bf16 MFMA rate.  The bf16 mode's fp32 GEMMs (mapping, text projection, styles,
+   demodulation, router / cross-attention vectors) use it; the fp32 parity mode keeps MG_F32. */
+#define MG_F32X3 2
 
 /* epilogue activation codes */
 #define MG_ACT_NONE 0

@@ -546,6 +546,10 @@ template <typename T> struct Tile;
 template <> struct Tile<bf16_t> { static constexpr int BK = 64, PADK = 0, PADM = 32; };
 template <> struct Tile<float> { static constexpr int BK = 32, PADK = 4, PADM = 16; };
 
+// K step of a GEMM instantiation: X3 (fp32 operands multiplied as split bf16, hi*hi + hi*lo + lo*hi) stages its
+// tiles as bf16 images, so it takes the bf16 step
+template <typename T, bool X3> constexpr int tile_bk() { return X3 ? Tile<bf16_t>::BK : Tile<T>::BK; }
+
 template <typename T> MG_DEV constexpr int mc_swz(int k) { return sizeof(T) == 2 ? ((k >> 3) & 1) << 4 : 0; }
 // KC image element offset of (row r, k) for bf16: 16-B chunk (k / 8) stored at chunk (k / 8) ^ (r & 7)
 // of an unpadded 128-B row -- conflict-free ds_read_b128 fragment reads and ds_write_b128 stores.
@@ -629,15 +633,18 @@ MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const E
 }
 
 // One output tile: C[m0.., n0..] of rows [mrow_base, mrow_base + Mloc) over k in [kbeg, kend).
-template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP>
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP, bool X3 = false>
 MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, int Mloc, int N, int kbeg, int kend,
                       int mrow_base) {
+  static_assert(!X3 || std::is_same<T, float>::value, "split-bf16 staging takes fp32 operands");
   constexpr int VEC = VecOf<T>::N;
   typedef typename VecOf<T>::type vec_t;
-  constexpr int TBK = Tile<T>::BK;
-  constexpr int LDK = TBK + Tile<T>::PADK;
-  constexpr int LDA = A_KC ? LDK : BM + Tile<T>::PADM;
-  constexpr int LDB = B_KC ? LDK : BN + Tile<T>::PADM;
+  // LT: element type of the LDS images (X3: bf16 hi / lo images of the fp32 operands, bf16 tile geometry)
+  typedef typename std::conditional<X3, bf16_t, T>::type LT;
+  constexpr int TBK = tile_bk<T, X3>();
+  constexpr int LDK = TBK + Tile<LT>::PADK;
+  constexpr int LDA = A_KC ? LDK : BM + Tile<LT>::PADM;
+  constexpr int LDB = B_KC ? LDK : BN + Tile<LT>::PADM;
   constexpr int A_ELEMS = A_KC ? BM * LDK : TBK * LDA;
   constexpr int B_ELEMS = B_KC ? BN * LDK : TBK * LDB;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
@@ -647,15 +654,16 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   static_assert(A_VPT >= 1 && B_VPT >= 1, "tile too small for 256 threads");
   // LDS: NBUF stages of (A tile, B tile), reused by the epilogue to stage accumulators.  Double
   // buffering (with a second register stage) when two stages fit the 64 KiB static limit.
-  constexpr int STAGE = A_ELEMS + B_ELEMS;
+  // X3: (A_hi, A_lo, B_hi, B_lo) images in one stage
+  constexpr int STAGE = (X3 ? 2 : 1) * (A_ELEMS + B_ELEMS);
   // LDS-DMA staging (bf16, both operands k-contiguous without transforms): two LDS stages, no registers
-  constexpr bool GLDS = MG_GLDS && sizeof(T) == 2 && A_KC && B_KC && AL::kGlds && BL::kGlds &&
+  constexpr bool GLDS = MG_GLDS && !X3 && sizeof(T) == 2 && A_KC && B_KC && AL::kGlds && BL::kGlds &&
                         2 * STAGE * (int)sizeof(T) <= 65536;
-  constexpr int NBUF = (GLDS || (2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE)) ? 2 : 1;
-  constexpr bool SB2 = NBUF == 1 && BM * BN <= MG_SB2_MAX_TILE;
+  constexpr int NBUF = (GLDS || (!X3 && 2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE)) ? 2 : 1;
+  constexpr bool SB2 = NBUF == 1 && !X3 && BM * BN <= MG_SB2_MAX_TILE;
   constexpr int NS = NBUF == 2 ? MG_NSTAGE : (SB2 ? 2 : 1);
-  __shared__ __attribute__((aligned(16))) T smem[NBUF * STAGE];
-  static_assert(4 * 16 * (WN + 4) * 4 <= (int)sizeof(T) * STAGE, "epilogue staging does not fit");
+  __shared__ __attribute__((aligned(16))) LT smem[NBUF * STAGE];
+  static_assert(4 * 16 * (WN + 4) * 4 <= (int)sizeof(LT) * STAGE, "epilogue staging does not fit");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -705,8 +713,38 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     else gload(R, k0, std::true_type{});
   };
   // register stage R (K step k0) -> LDS buffer (As, Bs)
-  auto sstore = [&](auto R, int k0, T* As, T* Bs) {
+  auto sstore = [&](auto R, int k0, LT* As, LT* Bs) {
     constexpr int r = decltype(R)::value;
+    if constexpr (X3) {
+      // fp32 vector -> bf16 hi = rn(v), lo = rn(v - hi); the 4 elements land as 8-byte runs in the hi and lo
+      // images (KC: half a 16-B chunk of the swizzled row; MC: 4 columns, the 16-column swizzle keeps them whole)
+      auto split_store = [&](const f32x4_t& v, LT* hi_img, LT* lo_img, int off) {
+        typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+        u16x4 h, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          h[j] = f2bf(v[j]);
+          l[j] = f2bf(v[j] - bf2f(h[j]));
+        }
+        *reinterpret_cast<u16x4*>(&hi_img[off]) = h;
+        *reinterpret_cast<u16x4*>(&lo_img[off]) = l;
+      };
+#pragma unroll
+      for (int i = 0; i < A_VPT; ++i) {
+        vec_t v = ra[r][i];
+        A.fix(as_[i], k0, v);
+        const int off = A_KC ? kc_off<LT>(a_r[i], a_k[i], LDK) : a_k[i] * LDA + (a_r[i] ^ mc_swz<LT>(a_k[i]));
+        split_store(v, As, As + A_ELEMS, off);
+      }
+#pragma unroll
+      for (int i = 0; i < B_VPT; ++i) {
+        vec_t v = rb[r][i];
+        B.fix(bs_[i], k0, v);
+        const int off = B_KC ? kc_off<LT>(b_r[i], b_k[i], LDK) : b_k[i] * LDB + (b_r[i] ^ mc_swz<LT>(b_k[i]));
+        split_store(v, Bs, Bs + B_ELEMS, off);
+      }
+      return;
+    } else {
 #pragma unroll
     for (int i = 0; i < A_VPT; ++i) {
       vec_t v = ra[r][i];
@@ -721,6 +759,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
       if constexpr (B_KC) *reinterpret_cast<vec_t*>(&Bs[kc_off<T>(b_r[i], b_k[i], LDK)]) = v;
       else *reinterpret_cast<vec_t*>(&Bs[b_k[i] * LDB + (b_r[i] ^ mc_swz<T>(b_k[i]))]) = v;
     }
+    }
   };
 
   f32x4_t acc[FM][FN];
@@ -731,8 +770,37 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 
   const int fr = lane & 15, fq = lane >> 4;
   // one K step of MFMAs from the LDS buffer (As, Bs)
-  auto compute = [&](const T* As, const T* Bs) {
-    if constexpr (sizeof(T) == 2) {
+  auto compute = [&](const LT* As, const LT* Bs) {
+    if constexpr (X3) {
+      // three bf16 products per fragment pair: hi*hi + hi*lo + lo*hi (the lo*lo term is below fp32 rounding of
+      // the sum); images: As = A_hi, As + A_ELEMS = A_lo, Bs = B_hi, Bs + B_ELEMS = B_lo
+      auto frag = [&](const LT* img, int ld, bool kc, int row0, int kk) {
+        if (kc) return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&img[kc_off<LT>(row0 + fr, kk * 32 + fq * 8, ld)]));
+        return mc_frag_bf16(img, ld, kk * 32, row0, lane);
+      };
+#pragma unroll
+      for (int kk = 0; kk < TBK / 32; ++kk) {
+        bf16x8_t ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          ah[i] = frag(As, LDA, A_KC, wm * WM + i * 16, kk);
+          al[i] = frag(As + A_ELEMS, LDA, A_KC, wm * WM + i * 16, kk);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          bh[j] = frag(Bs, LDB, B_KC, wn * WN + j * 16, kk);
+          bl[j] = frag(Bs + B_ELEMS, LDB, B_KC, wn * WN + j * 16, kk);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          }
+      }
+    } else if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int kk = 0; kk < TBK / 32; ++kk) {
         bf16x8_t af[FM], bfv[FN];
@@ -780,7 +848,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     // retires only step t's (issued earlier), a raw barrier publishes them, and a second barrier keeps
     // step t+2's DMA from overwriting the buffer while another wave still reads it.
     static_assert(A_VPT + B_VPT < 64, "vmcnt range");
-    auto issue = [&](int k0, T* buf) {
+    auto issue = [&](int k0, LT* buf) {
       if (k0 + TBK <= kend) {
 #pragma unroll
         for (int i = 0; i < A_VPT; ++i) A.template glds<false, TBK>(rA, as_[i], k0, kend, buf + (i * 4 + wid) * 8 * LDK);
@@ -798,7 +866,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     const int nsteps = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
     if (nsteps > 0) issue(kbeg, smem);
     for (int t = 0; t < nsteps; ++t) {
-      T* cur = smem + (t & 1) * STAGE;
+      LT* cur = smem + (t & 1) * STAGE;
       if (t + 1 < nsteps) {
         issue(kbeg + (t + 1) * TBK, smem + ((t + 1) & 1) * STAGE);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_VPT + B_VPT) : "memory");
@@ -827,11 +895,11 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     const int nsteps = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
     for (int t = 0; t < nsteps; ++t) {
       const int k0 = kbeg + t * TBK;
-      const T* cur = smem + (t & 1) * STAGE;
+      const LT* cur = smem + (t & 1) * STAGE;
       compute(cur, cur + A_ELEMS);
       const int kn = k0 + TBK;
       if (kn < kend) {
-        T* nxt = smem + ((t + 1) & 1) * STAGE;
+        LT* nxt = smem + ((t + 1) & 1) * STAGE;
         if (NS == 1 || (t & 1)) {
           sstore(I0{}, kn, nxt, nxt + A_ELEMS);
           if (kn + NS * TBK < kend) gload_any(I0{}, kn + NS * TBK);
@@ -847,8 +915,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     // to LDS, so two multiplies (not one) cover each load's latency.  Straight-line body over two K steps with
     // tail-safe loads throughout (past kend they read zeros), so no branch splits the load stream and the
     // compiler's vmcnt waits count only the older stage.
-    T* const As = smem;
-    T* const Bs = smem + A_ELEMS;
+    LT* const As = smem;
+    LT* const Bs = smem + (X3 ? 2 : 1) * A_ELEMS;
     using TT = std::true_type;
     // scheduling barriers pin the issue order (stage 0 before stage 1, each reload before its multiply) so on
     // both paths into the loop head stage 0 is the older stage and its wait is vmcnt(#stage-1 loads), not 0
@@ -881,8 +949,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     }
   } else {
     // one LDS buffer, one register stage: store, barrier, prefetch the next step, multiply
-    T* const As = smem;
-    T* const Bs = smem + A_ELEMS;
+    LT* const As = smem;
+    LT* const Bs = smem + (X3 ? 2 : 1) * A_ELEMS;
     if (kbeg < kend) gload_any(I0{}, kbeg);
     for (int k0 = kbeg; k0 < kend; k0 += TBK) {
       __syncthreads();
@@ -898,9 +966,9 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 
 
 // TAG only names the instantiation (1 = MoE expert GEMMs) so profiles can attribute its dispatches.
-template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP, int TAG = 0>
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP, int TAG = 0, bool X3 = false>
 __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M, int N, int K, int kchunk, Grouping grp) {
-  constexpr int TBK = Tile<T>::BK;
+  constexpr int TBK = tile_bk<T, X3>();
   // ---- resolve tile / group ----
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (grp.mode == 0 && grp.swz && (grp.swz == 1 || gridDim.z > 1)) {
@@ -952,7 +1020,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   A.set_group(g);
   B.set_group(g);
   ep.set_group(g);
-  gemm_tile<T, BM, BN, A_KC, B_KC>(A, B, ep, m0, n0, Mloc, N, kbeg, kend, mrow_base);
+  gemm_tile<T, BM, BN, A_KC, B_KC, AL, BL, EP, X3>(A, B, ep, m0, n0, Mloc, N, kbeg, kend, mrow_base);
 }
 
 // ---------------------------------------------------------------------------
@@ -969,22 +1037,22 @@ struct BatchArgs {
   int n;
 };
 
-template <typename T, bool A_KC, bool B_KC, class AL, class BL, typename TO>
+template <typename T, bool A_KC, bool B_KC, class AL, class BL, typename TO, bool X3 = false>
 __global__ __launch_bounds__(NTHREADS) void gemm_batch_kernel(BatchArgs<TO, AL, BL> args) {
   const int t = blockIdx.x;
   int p = 0;
   while (p + 1 < args.n && t >= args.tile_off[p + 1]) ++p;
   const int lt = t - args.tile_off[p];
   const int tm = lt / args.tiles_n[p], tn = lt - tm * args.tiles_n[p];
-  gemm_tile<T, 64, 64, A_KC, B_KC>(args.a[p], args.b[p], args.e[p], tm * 64, tn * 64, args.M[p], args.N[p], 0,
-                                   args.K[p], 0);
+  gemm_tile<T, 64, 64, A_KC, B_KC, AL, BL, Epi<TO>, X3>(args.a[p], args.b[p], args.e[p], tm * 64, tn * 64, args.M[p],
+                                                          args.N[p], 0, args.K[p], 0);
 }
 
 // launch helper: picks the grid; grouped-M launches an upper bound of tiles.
-template <typename T, int BM, int BN, bool A_KC, bool B_KC, int TAG = 0, class AL, class BL, class EP>
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, int TAG = 0, bool X3 = false, class AL, class BL, class EP>
 inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, int K, int splits, Grouping grp,
                         int max_tiles_m, hipStream_t st) {
-  constexpr int TBK = Tile<T>::BK;
+  constexpr int TBK = tile_bk<T, X3>();
   int kchunk = K;
   if (grp.mode != 2 && splits > 1) kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
   if (grp.mode != 2) splits = (K + kchunk - 1) / kchunk;
@@ -995,7 +1063,7 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   EP e2 = ep;
   e2.vec_ok = e2.host_vec_ok() ? 1 : 0;
   if (grp.mode == 0) grp.swz = g_mg_tune[MG_TUNE_XCD];
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP, TAG>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP, TAG, X3>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
                      K, kchunk, grp);
 }
 

@@ -17,7 +17,7 @@ inline Grouping xcd_group() { Grouping g = kNoGroup; g.swz = g_mg_tune[MG_TUNE_X
 
 inline bool a_xf(const mg_epilogue* e) { return e && (e->a_idx || e->a_rowscale || e->a_gelu); }
 
-template <typename T, typename TO, int BM, int BN, bool AK, bool BKc, bool XF>
+template <typename T, typename TO, int BM, int BN, bool AK, bool BKc, bool XF, bool X3 = false>
 void run_plain(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
                const mg_epilogue* e, int splits, hipStream_t st) {
   auto ep = make_epi<TO>(C, ldc, e);
@@ -29,35 +29,40 @@ void run_plain(int M, int N, int K, const void* A, int64_t lda, const void* B, i
     LdKC<T, XF> la{reinterpret_cast<const T*>(A), lda, M, K, aidx, adiv, ars, agelu};
     if constexpr (BKc) {
       LdKC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
-      launch_gemm<T, BM, BN, true, true>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
+      launch_gemm<T, BM, BN, true, true, 0, X3>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
     } else {
       LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
-      launch_gemm<T, BM, BN, true, false>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
+      launch_gemm<T, BM, BN, true, false, 0, X3>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
     }
   } else {
     LdMC<T, XF> la{reinterpret_cast<const T*>(A), lda, M, K, aidx, adiv, ars, agelu};
     if constexpr (BKc) {
       LdKC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
-      launch_gemm<T, BM, BN, false, true>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
+      launch_gemm<T, BM, BN, false, true, 0, X3>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
     } else {
       LdMC<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, nullptr, 1, nullptr, 0};
-      launch_gemm<T, BM, BN, false, false>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
+      launch_gemm<T, BM, BN, false, false, 0, X3>(la, lb, ep, M, N, K, splits, kNoGroup, 0, st);
     }
   }
 }
 
-template <typename T, typename TO, int BM, int BN, bool XF = false>
+template <typename T, typename TO, int BM, int BN, bool XF = false, bool X3 = false>
 void run_plain_orient(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
                       int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, int splits, hipStream_t st) {
-  if (a_kc && b_kc) run_plain<T, TO, BM, BN, true, true, XF>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
-  else if (a_kc) run_plain<T, TO, BM, BN, true, false, XF>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
-  else if (b_kc) run_plain<T, TO, BM, BN, false, true, XF>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
-  else run_plain<T, TO, BM, BN, false, false, XF>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  if (a_kc && b_kc) run_plain<T, TO, BM, BN, true, true, XF, X3>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else if (a_kc) run_plain<T, TO, BM, BN, true, false, XF, X3>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else if (b_kc) run_plain<T, TO, BM, BN, false, true, XF, X3>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+  else run_plain<T, TO, BM, BN, false, false, XF, X3>(M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
 }
 
-template <typename T, typename TO>
+template <typename T, typename TO, bool X3 = false>
 void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
                      int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, int splits, hipStream_t st) {
+  if constexpr (X3) {  // split-bf16 fp32 GEMMs (small-M prefix / demodulation products): 64x64 tiles only
+    if (a_xf(e)) run_plain_orient<T, TO, 64, 64, true, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+    else run_plain_orient<T, TO, 64, 64, false, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+    return;
+  }
   if (a_xf(e)) {  // loader transforms: generic 64x64 instantiation
     run_plain_orient<T, TO, 64, 64, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
     return;
@@ -88,10 +93,10 @@ void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int
 // the real epilogue in a reduction pass.  Returns false when the shape does not qualify.
 // ``want_splits`` > 0 (deterministic mode, an atomic split-K epilogue): exactly that many slabs, any tile count;
 // the reduction pass then adds each output element once.
-template <typename T, typename TO>
+template <typename T, typename TO, bool X3 = false>
 bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
                       int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, hipStream_t st, int want_splits = 0) {
-  constexpr int TBK = Tile<T>::BK;
+  constexpr int TBK = tile_bk<T, X3>();
   int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
   if (a_xf(e)) return false;
   int splits;
@@ -115,7 +120,7 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
   auto go = [&](auto la, auto lb, auto akc, auto bkc) {
     dim3 grid(cdiv(M, 64), cdiv(N, 64), splits);
     hipLaunchKernelGGL((gemm_kernel<T, 64, 64, decltype(akc)::value, decltype(bkc)::value, decltype(la),
-                                    decltype(lb), Epi<float>>),
+                                    decltype(lb), Epi<float>, 0, X3>),
                        grid, dim3(NTHREADS), 0, st, la, lb, slab, M, N, K, kchunk, xcd_group());
   };
   const T* Ap = reinterpret_cast<const T*>(A);
@@ -143,9 +148,11 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
 extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t lda, int a_kc, const void* B,
                        int64_t ldb, int b_kc, void* C, int64_t ldc, int c_dtype, const mg_epilogue* ep, int splits,
                        void* stream) {
-  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16 || dtype == MG_F32X3, "bad dtype");
   MG_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return MG_OK;
+  const bool x3 = dtype == MG_F32X3;
+  if (x3) dtype = MG_F32;  // fp32 storage; the MFMA products run on split bf16
   const int vec = dtype == MG_F32 ? 4 : 8;
   MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
   MG_REQUIRE(lda % vec == 0 && ldb % vec == 0, "lda/ldb must be multiples of the 16-byte vector");
@@ -170,7 +177,9 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (splits > 1 && mg_det()) {  // deterministic mode: fp32 slabs + one fixed-order reduction, not atomics
     bool done;
-    if (dtype == MG_F32)
+    if (x3)
+      done = run_splitk_slabs<float, float, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st, splits);
+    else if (dtype == MG_F32)
       done = run_splitk_slabs<float, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st, splits);
     else
       done = run_splitk_slabs<bf16_t, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st, splits);
@@ -179,7 +188,10 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
   }
   if (splits == 1 && !(ep && ep->atomic) && !g_mg_tune[MG_TUNE_NO_SLABS]) {
     bool done;
-    if (dtype == MG_F32)
+    if (x3)
+      done = c_dtype == MG_F32 ? run_splitk_slabs<float, float, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st)
+                               : run_splitk_slabs<float, bf16_t, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st);
+    else if (dtype == MG_F32)
       done = c_dtype == MG_F32 ? run_splitk_slabs<float, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st)
                                : run_splitk_slabs<float, bf16_t>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st);
     else
@@ -187,7 +199,10 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
                                : run_splitk_slabs<bf16_t, bf16_t>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, st);
     if (done) return mg_check_launch("mg_gemm (split-K slabs)");
   }
-  if (dtype == MG_F32) {
+  if (x3) {
+    if (c_dtype == MG_F32) run_plain_tiles<float, float, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
+    else run_plain_tiles<float, bf16_t, true>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
+  } else if (dtype == MG_F32) {
     if (c_dtype == MG_F32) run_plain_tiles<float, float>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
     else run_plain_tiles<float, bf16_t>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, ep, splits, st);
   } else {
@@ -201,7 +216,7 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
 // batched small GEMMs
 // ---------------------------------------------------------------------------
 namespace {
-template <typename T, typename TO, bool AK, bool BKc>
+template <typename T, typename TO, bool AK, bool BKc, bool X3 = false>
 int run_batch(int n, const mg_gemm_desc* d, hipStream_t st) {
   using AL = typename std::conditional<AK, LdKC<T>, LdMC<T>>::type;
   using BL = typename std::conditional<BKc, LdKC<T>, LdMC<T>>::type;
@@ -229,7 +244,7 @@ int run_batch(int n, const mg_gemm_desc* d, hipStream_t st) {
     if (!used) continue;
     args.tile_off[used] = tiles;
     args.n = used;
-    hipLaunchKernelGGL((gemm_batch_kernel<T, AK, BKc, AL, BL, TO>), dim3(tiles), dim3(NTHREADS), 0, st, args);
+    hipLaunchKernelGGL((gemm_batch_kernel<T, AK, BKc, AL, BL, TO, X3>), dim3(tiles), dim3(NTHREADS), 0, st, args);
   }
   return mg_check_launch("mg_gemm_batch");
 }
@@ -237,8 +252,9 @@ int run_batch(int n, const mg_gemm_desc* d, hipStream_t st) {
 
 extern "C" int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, const mg_gemm_desc* d,
                              void* stream) {
-  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16, "bad dtype");
-  const int vec = dtype == MG_F32 ? 4 : 8;
+  MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16 || dtype == MG_F32X3, "bad dtype");
+  const int vec = dtype == MG_BF16 ? 8 : 4;
+  const int mdt = dtype == MG_F32X3 ? MG_F32 : dtype;  // storage dtype
   for (int i = 0; i < n; ++i) {
     const mg_gemm_desc& q = d[i];
     MG_REQUIRE(q.M >= 0 && q.N >= 0 && q.K >= 0, "negative size");
@@ -248,8 +264,8 @@ extern "C" int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, 
     MG_REQUIRE(b_kc ? (q.K % vec == 0) : (q.N % vec == 0), "B vector dim must be a multiple of the vector");
     MG_REQUIRE(!(q.ep && q.ep->atomic) || c_dtype == MG_F32, "atomic epilogue requires fp32 C");
     MG_REQUIRE(!a_xf(q.ep), "A loader transforms (a_idx / a_rowscale / a_gelu) are not supported by mg_gemm_batch");
-    MG_REQUIRE(under2g((a_kc ? (int64_t)q.M : q.K) * q.lda, dtype) &&
-                   under2g((b_kc ? (int64_t)q.N : q.K) * q.ldb, dtype) && under2g((int64_t)q.M * q.ldc, c_dtype),
+    MG_REQUIRE(under2g((a_kc ? (int64_t)q.M : q.K) * q.lda, mdt) &&
+                   under2g((b_kc ? (int64_t)q.N : q.K) * q.ldb, mdt) && under2g((int64_t)q.M * q.ldc, c_dtype),
                "an operand exceeds 2 GiB (32-bit buffer offsets)");
   }
   if (n <= 0) return MG_OK;
@@ -265,10 +281,11 @@ extern "C" int mg_gemm_batch(int dtype, int a_kc, int b_kc, int c_dtype, int n, 
       return MG_OK;
     }
   }
-#define B_(T, TO)                                                   \
-  (a_kc ? (b_kc ? run_batch<T, TO, true, true>(n, d, st) : run_batch<T, TO, true, false>(n, d, st)) \
-        : (b_kc ? run_batch<T, TO, false, true>(n, d, st) : run_batch<T, TO, false, false>(n, d, st)))
+#define B_(T, TO, ...)                                                                                          \
+  (a_kc ? (b_kc ? run_batch<T, TO, true, true, ##__VA_ARGS__>(n, d, st) : run_batch<T, TO, true, false, ##__VA_ARGS__>(n, d, st)) \
+        : (b_kc ? run_batch<T, TO, false, true, ##__VA_ARGS__>(n, d, st) : run_batch<T, TO, false, false, ##__VA_ARGS__>(n, d, st)))
   if (dtype == MG_F32) return c_dtype == MG_F32 ? B_(float, float) : B_(float, bf16_t);
+  if (dtype == MG_F32X3) return c_dtype == MG_F32 ? B_(float, float, true) : B_(float, bf16_t, true);
   return c_dtype == MG_F32 ? B_(bf16_t, float) : B_(bf16_t, bf16_t);
 #undef B_
 }

@@ -125,12 +125,30 @@ def ilog2(v):
 # ---------------------------------------------------------------------------
 # GEMM family
 # ---------------------------------------------------------------------------
+MG_F32X3 = 2  # include/moegan_hip.h: fp32 operands, split-bf16 MFMA products
+_F32X3 = [False]
+
+
+def set_f32x3(on):
+    """fp32-operand GEMMs (mg_gemm / mg_gemm_batch) as split-bf16 products (MG_F32X3) while ``on``: the bf16
+    training step's fp32 prefix / demodulation / router-vector GEMMs (TrainStep.step sets it for the step's
+    duration); the fp32 parity mode keeps exact-fp32 MFMA.  Returns the previous setting."""
+    prev = _F32X3[0]
+    _F32X3[0] = bool(on)
+    return prev
+
+
+def _gdt(A):
+    d = dt(A)
+    return MG_F32X3 if (d == L.MG_F32 and _F32X3[0]) else d
+
+
 def gemm(A, B, M, N, K, *, a_kc=True, b_kc=True, out=None, out_dtype=None, lda=None, ldb=None, ldc=None,
          ep=None, splits=1):
     """C[M,N] = epilogue(op(A) @ op(B)) (mg_gemm)."""
     if out is None:
         out = torch.empty(M, N, device=A.device, dtype=out_dtype or A.dtype)
-    call("mg_gemm", dt(A), M, N, K, ptr(A), lda if lda is not None else _ld(A), int(a_kc), ptr(B),
+    call("mg_gemm", _gdt(A), M, N, K, ptr(A), lda if lda is not None else _ld(A), int(a_kc), ptr(B),
          ldb if ldb is not None else _ld(B), int(b_kc), ptr(out), ldc if ldc is not None else _ld(out),
          dt(out), ep, splits, S())
     return out
@@ -150,7 +168,7 @@ def gemm_batch(problems, *, a_kc=True, b_kc=True):
         keep.append(ep)
         arr[i] = L.GemmDesc(q["M"], q["N"], q["K"], ptr(A), q.get("lda", _ld(A)), ptr(B), q.get("ldb", _ld(B)),
                             ptr(out), q.get("ldc", _ld(out)), ctypes.pointer(ep) if ep is not None else None)
-    call("mg_gemm_batch", dt(problems[0]["A"]), int(a_kc), int(b_kc), dt(problems[0]["out"]), n, arr, S())
+    call("mg_gemm_batch", _gdt(problems[0]["A"]), int(a_kc), int(b_kc), dt(problems[0]["out"]), n, arr, S())
 
 
 def linear(x, W, bias=None, act=0, out=None, out_dtype=None, **epk):

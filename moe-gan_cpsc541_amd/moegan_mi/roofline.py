@@ -16,7 +16,7 @@ import torch
 
 from . import _lib as L
 
-ELT = {0: 4, 1: 2}  # MG_F32, MG_BF16
+ELT = {0: 4, 1: 2, 2: 4}  # MG_F32, MG_BF16, MG_F32X3 (fp32 storage)
 MX8_PEAK_TFLOPS = 5000.0  # dense MX-fp8 MFMA peak (MI355X_MICROARCH.md: 2x the bf16 rate per clock)
 
 # family -> (bound, entry points)

@@ -207,10 +207,14 @@ class TrainStep:
         matters only when the D optimizer has not stepped yet in the window (acc > 1)."""
         ops.ARENA.begin(self.dev)
         ops.COLSUMS.active = True  # bias-gradient column sums batched per backward (flushed below)
+        # bf16 mode: the fp32-operand GEMMs (prefix, demodulation, router / cross-attention vectors) as split-bf16
+        # products (ops.set_f32x3); the fp32 parity mode keeps exact-fp32 MFMA
+        x3_prev = ops.set_f32x3(self.cdt == torch.bfloat16 and os.environ.get("MOEGAN_F32X3", "1") == "1")
         try:
             return self._step(real, text, z, eps_d, eps_g, perm, anneal, lr_g, lr_d, eff_kl_weight, prep, acc,
                               zero_grads, step_optim)
         finally:
+            ops.set_f32x3(x3_prev)
             ops.ARENA.end()
             ops.COLSUMS.active = False
             ops.COLSUMS.items = []
