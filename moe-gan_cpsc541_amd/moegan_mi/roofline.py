@@ -60,7 +60,8 @@ _FAMILY_OF = {e: f for f, (_, es) in FAMILIES.items() for e in es}
 KERNELS = [
     (r"k_wgrad_fold|splitk_reduce_kernel<mg::Epi<float>", "conv_wgrad+fold"),
     (r"k_mx8_conv", "conv_fwd_mx8"),
-    (r"gemm_kernel<.*, 1>\(|k_moe_ffn_fwd", "expert_gemm"),  # TAG = 1 instantiations (mg_gemm.h), fused FFN
+    # TAG = 1 instantiations (mg_gemm.h: "..., TAG, X3>("), fused FFN
+    (r"gemm_kernel<.*, 1(, (true|false))?>\(|k_moe_ffn_fwd", "expert_gemm"),
     (r"gemm_kernel<[^>]*LdKCConvT", "conv_dgrad_s2"),
     (r"gemm_kernel<.*LdMCConv", "conv_wgrad+fold"),
     (r"gemm_kernel<.*LdKCConv", "conv_fwd"),
