@@ -299,6 +299,46 @@ struct LdMCConv {
   }
 };
 
+// MC conv columns for the weight gradient of a stride-1 "same" convolution (H = OH, W = OW) with OW <= TBK and
+// OH <= 32: the input pixel of output pixel p through tap (dh, dw) is p + dh*W + dw, so the slot keeps that byte
+// offset minus the step's (k0 * Cin) part, the column's validity (ow = kofs mod OW is the same every step, because
+// k0 is a multiple of TBK and so of OW) and a 32-bit mask of the output rows whose tap row lies inside the image.
+// A K step then costs an add / and / shift for the row test and one add + select for the offset (the generic
+// LdMCConv decodes b, oh, ow and rebuilds the address per vector).
+template <typename T>
+struct LdMCConvS1 {
+  typedef typename VecOf<T>::type vec_t;
+  const T* x; int lgCin, lgOW, OH, W, KW, pad, K, cols;
+  struct Slot { int32_t voff; uint32_t bad_rows; int kr; int kofs; };
+  static constexpr bool kGlds = false;
+  MG_DEV void set_group(int) {}
+  MG_DEV rsrc_t rsrc() const { return make_rsrc(x); }
+  MG_DEV Slot slot(int c0, int kofs, bool ok) const {
+    const int Cin = 1 << lgCin;
+    const int tap = c0 >> lgCin, ci = c0 & (Cin - 1);
+    const int kh = tap / KW, dh = kh - pad, dw = tap - kh * KW - pad;
+    const int ow = kofs & ((1 << lgOW) - 1);
+    Slot s;
+    s.kofs = kofs;
+    s.kr = kofs >> lgOW;
+    s.voff = (((kofs + dh * W + dw) << lgCin) + ci) * (int)sizeof(T);
+    uint32_t bad = 0u;
+    for (int oh = 0; oh < OH; ++oh)
+      if ((unsigned)(oh + dh) >= (unsigned)OH) bad |= 1u << oh;
+    if (!ok || c0 >= cols || (unsigned)(ow + dw) >= (unsigned)W) bad = 0xffffffffu;
+    s.bad_rows = bad;
+    return s;
+  }
+  template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {
+    const int oh = ((k0 >> lgOW) + s.kr) & (OH - 1);
+    bool bad = (s.bad_rows >> oh) & 1u;
+    if constexpr (TAIL) bad = bad || (k0 + s.kofs >= kend);
+    const uint32_t off = bad ? MG_OOB : (uint32_t)(s.voff + (k0 << lgCin) * (int)sizeof(T));
+    return bload<vec_t>(r, off, 0);
+  }
+  MG_DEV void fix(const Slot&, int, vec_t&) const {}
+};
+
 // KC, data gradient of a 4x4 / stride-2 / pad-1 convolution ("transposed conv"),
 // split into the 4 output-parity classes (py, px).  Row r (class-major) =
 // (class, b, i, j) -> input-grid pixel (b, 2i+py, 2j+px); k = t*Cg + co with

@@ -488,6 +488,11 @@ __global__ __launch_bounds__(256) void k_wgrad_fold(const float* __restrict__ ws
 
 // Weight gradient with split-K into fp32 slabs written by the 8-column vector epilogue (coalesced, no atomics),
 // then k_wgrad_fold.  Returns false when the workspace cannot be had (caller falls back to atomics).
+// stride-1 "same" convolution whose weight gradient can use the cheap-address column loader (LdMCConvS1)
+inline bool wgrad_s1(int H, int W, int KH, int KW, int stride, int pad, int tbk) {
+  return stride == 1 && KH == KW && 2 * pad == KH - 1 && W <= tbk && H <= 32 && pow2(H) && pow2(W);
+}
+
 template <typename T, int BM, int BN, bool XF = false>
 bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin, const float* sc,
                      int Cout, int KH, int KW, int stride, int pad, float* gw, int splits, hipStream_t st) {
@@ -508,8 +513,14 @@ bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, i
   slab.zstride = MN;
   slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
   dim3 grid(cdiv(Cout, BM), cdiv(N, BN), splits);
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, false, LdMC<T>, LdMCConv<T, XF>, Epi<float>>), grid, dim3(NTHREADS),
-                     0, st, la, lb, slab, Cout, N, P, kchunk, xcd_group());
+  if (!XF && !g_mg_tune[MG_TUNE_S1_OFF] && wgrad_s1(H, W, KH, KW, stride, pad, TBK)) {
+    LdMCConvS1<T> lb1{reinterpret_cast<const T*>(x), ilog2(Cin), ilog2(OW), OH, W, KW, pad, P, N};
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, false, LdMC<T>, LdMCConvS1<T>, Epi<float>>), grid,
+                       dim3(NTHREADS), 0, st, la, lb1, slab, Cout, N, P, kchunk, xcd_group());
+  } else {
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, false, LdMC<T>, LdMCConv<T, XF>, Epi<float>>), grid,
+                       dim3(NTHREADS), 0, st, la, lb, slab, Cout, N, P, kchunk, xcd_group());
+  }
   // (Cout x Cin / CC) blocks: enough to spread the slab reads over the chip, >= 8 channels per segment
   int lgCC = ilog2(Cin);
   while (lgCC > 3 && (int64_t)Cout * (Cin >> lgCC) < 1024) --lgCC;

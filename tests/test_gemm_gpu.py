@@ -265,3 +265,35 @@ def test_conv_narrow_output(dtype, tol, Cout):
     y = ops.conv2d(xn, wp, Cout, 3, 3, 1, 1, out_dtype=torch.float32, ep=ops.E(bias=bias, act=L.ACT_LRELU))
     torch.cuda.synchronize()
     assert rel(y.permute(0, 3, 1, 2), ref) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,H,Cin,Cout,k", [(256, 4, 512, 512, 3), (37, 8, 256, 256, 3), (16, 16, 128, 128, 3),
+                                            (6, 32, 64, 32, 3), (9, 16, 256, 128, 1), (256, 16, 128, 32, 3)])
+def test_conv_wgrad_stride1_loader(dtype, B, H, Cin, Cout, k):
+    """Weight gradients of stride-1 "same" convolutions (the generator's modulated 3x3 / 1x1 convs and MTM offset
+    heads, t2i_moe_gan.py:169-180) through the cheap-address column loader (LdMCConvS1): bit-identical to the
+    generic implicit-conv loader (MG_TUNE_S1_OFF = 12 switches it back: same values, same summation order), and
+    equal to the torch reference within the dtype's tolerance."""
+    from moegan_mi import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(B * H + Cin)
+    x = torch.randn(B, H, H, Cin, device=DEV, generator=g).to(dtype)
+    gy = torch.randn(B, H, H, Cout, device=DEV, generator=g).to(dtype)
+    pad = k // 2
+    gw1 = torch.zeros(Cout, Cin, k, k, device=DEV)
+    ops.conv2d_wgrad(gy, x, Cout, k, k, 1, pad, gw1)
+    L.call("mg_set_tuning", 12, 1)
+    try:
+        gw0 = torch.zeros(Cout, Cin, k, k, device=DEV)
+        ops.conv2d_wgrad(gy, x, Cout, k, k, 1, pad, gw0)
+    finally:
+        L.call("mg_set_tuning", 12, 0)
+    torch.cuda.synchronize()
+    xr = x.float().permute(0, 3, 1, 2).contiguous()
+    wr = torch.zeros(Cout, Cin, k, k, device=DEV, requires_grad=True)
+    (F.conv2d(xr, wr, padding=pad) * gy.float().permute(0, 3, 1, 2)).sum().backward()
+    assert rel(gw1, wr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+    if dtype == torch.bfloat16:  # slabs + fixed-order fold: deterministic, so the two loaders agree bit for bit
+        assert torch.equal(gw1, gw0)
+    else:
+        assert rel(gw1, gw0) < 1e-6
