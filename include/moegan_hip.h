@@ -298,7 +298,7 @@ int mg_router_reparam(const float* mu, const float* rho, const float* eps, int64
 /* BayesianRouter.forward on tokens (t2i_moe_gan.py:335-402): logits = tok@Wfc + Lt[b], temperature/clamp/softmax/clamp/renorm, top-k (lowest index on ties), gate weights (renormalised for k<E, probs for k==E, 1 in eval). zlog = scaled pre-clamp logits. */
 int mg_router_fwd(int dtype, const void* tok, int64_t ld, int T, int C, const float* Wfc, const float* Lt, int E, int k, int HW, const float* temperature, float anneal, int eval_mode, float* probs, float* zlog, int32_t* topi, float* gate, void* stream);
 
-/* Deterministic per-expert position lists (token order): row_off/tile_off (BM=bm), perm[pos]=assignment, pos_of[assignment]=pos, gate_pos. ws: int32 [ceil(T*k/4096)*E]. */
+/* Deterministic per-expert position lists (token order): row_off/tile_off (BM=bm), perm[pos]=assignment, pos_of[assignment]=pos, gate_pos. ws: int32 [ceil(T*k/1024)*E]. */
 int mg_moe_dispatch(const int32_t* topi, const float* gate, int T, int k, int E, int bm, int32_t* ws, int32_t* row_off, int32_t* tile_off, int32_t* perm, int32_t* pos_of, float* gate_pos, void* stream);
 
 /* out[t] = resid[t] + sum_j gate[t,j] Y[pos_of[t*k+j]]  (SparseMoE combine + AttentionBlock residual, t2i_moe_gan.py:465-470, :571). */

@@ -182,7 +182,7 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
 }
 
 // ---- dispatch: deterministic per-expert position lists ----
-constexpr int DCH = 4096;  // assignments per block
+constexpr int DCH = 1024;  // assignments per block (C2 16x16 layer: 128 blocks)
 __global__ void k_disp_count(const int* __restrict__ topi, int n, int E, int* __restrict__ blk_counts) {
   extern __shared__ int cnt[];
   for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
@@ -209,6 +209,52 @@ __global__ void k_disp_scan(int* __restrict__ blk_counts, int nblk, int E, int b
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    int r = 0, tl = 0;
+    for (int i = 0; i < E; ++i) {
+      row_off[i] = r;
+      tile_off[i] = tl;
+      r += tot[i];
+      tl += (tot[i] + bm - 1) / bm;
+    }
+    row_off[E] = r;
+    tile_off[E] = tl;
+  }
+}
+
+// Parallel form of k_disp_scan for nblk * E <= 16384: the block counts are staged in LDS, 1024 / E lanes per expert
+// sum contiguous runs of blocks, the E expert threads scan those run sums, and every lane writes its run's
+// exclusive bases back (same values as the serial scan).
+__global__ __launch_bounds__(1024) void k_disp_scan_par(int* __restrict__ blk_counts, int nblk, int E, int bm,
+                                                        int* __restrict__ row_off, int* __restrict__ tile_off) {
+  extern __shared__ int sm[];  // [nblk * E] counts | [1024] run sums | [32] expert totals
+  const int n = nblk * E, tid = threadIdx.x;
+  int* run = sm + n;
+  int* tot = run + 1024;
+  for (int i = tid; i < n; i += 1024) sm[i] = blk_counts[i];
+  __syncthreads();
+  const int P = 1024 / E, e = tid % E, part = tid / E;
+  const int chunk = (nblk + P - 1) / P, b0 = part * chunk, b1 = min(nblk, b0 + chunk);
+  int s = 0;
+  for (int b = b0; b < b1; ++b) s += sm[b * E + e];
+  run[part * E + e] = s;
+  __syncthreads();
+  if (tid < E) {
+    int acc = 0;
+    for (int q = 0; q < P; ++q) {
+      const int c = run[q * E + tid];
+      run[q * E + tid] = acc;
+      acc += c;
+    }
+    tot[tid] = acc;
+  }
+  __syncthreads();
+  int base = run[part * E + e];
+  for (int b = b0; b < b1; ++b) {
+    const int c = sm[b * E + e];
+    blk_counts[b * E + e] = base;
+    base += c;
+  }
+  if (tid == 0) {
     int r = 0, tl = 0;
     for (int i = 0; i < E; ++i) {
       row_off[i] = r;
@@ -1042,7 +1088,11 @@ extern "C" int mg_moe_dispatch(const int32_t* topi, const float* gate, int T, in
   int nb = cdiv(n, DCH);
   MG_REQUIRE(nb <= 65535, "too many assignments");
   hipLaunchKernelGGL(k_disp_count, dim3(nb), dim3(256), E * sizeof(int), st, topi, n, E, ws);
-  hipLaunchKernelGGL(k_disp_scan, dim3(1), dim3(64), 0, st, ws, nb, E, bm, row_off, tile_off);
+  if ((int64_t)nb * E <= 16384)
+    hipLaunchKernelGGL(k_disp_scan_par, dim3(1), dim3(1024), (size_t)(nb * E + 1024 + 32) * sizeof(int), st, ws, nb, E,
+                       bm, row_off, tile_off);
+  else
+    hipLaunchKernelGGL(k_disp_scan, dim3(1), dim3(64), 0, st, ws, nb, E, bm, row_off, tile_off);
 #define L_(EE) hipLaunchKernelGGL((k_disp_scatter<EE>), dim3(nb), dim3(256), 0, st, topi, gate, n, ws, row_off, perm, pos_of, gate_pos)
   if (E == 4) L_(4); else if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
 #undef L_

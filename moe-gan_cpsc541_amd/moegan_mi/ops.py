@@ -638,7 +638,7 @@ def moe_dispatch(topi, gate, E_, bm=128):
     T, k = topi.shape
     dev = topi.device
     n = T * k
-    ws = torch.empty(((n + 4095) // 4096) * E_, device=dev, dtype=torch.int32)
+    ws = torch.empty(((n + 1023) // 1024) * E_, device=dev, dtype=torch.int32)  # per-chunk counts (mg_moe.hip DCH)
     row_off = torch.empty(E_ + 1, device=dev, dtype=torch.int32)
     tile_off = torch.empty(E_ + 1, device=dev, dtype=torch.int32)
     perm = torch.empty(n, device=dev, dtype=torch.int32)
