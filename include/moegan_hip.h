@@ -91,9 +91,6 @@ typedef struct mg_epilogue {
   int64_t add_ld;
   void* out_pre;       /* optional second output: the value before the activation (same dtype as C) */
   int64_t ld_pre;
-  float* colsum;       /* optional, mg_gemm_grouped only: colsum[g * N + n] += sum over the group's rows of the stored
-                          value (the bias gradient of a grouped data-gradient GEMM, fp32 atomics; NULL in the
-                          deterministic mode, whose callers run the fixed-order mg_grouped_colsum instead) */
 } mg_epilogue;
 
 const char* mg_last_error(void);

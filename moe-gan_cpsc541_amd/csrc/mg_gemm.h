@@ -450,7 +450,6 @@ struct Epi {
   TO* Cpre; int64_t ldc_pre;  // optional: store the pre-activation value too (row m, column n)
   int64_t zstride;  // split-K partial slabs: output offset zi * zstride (raw partial epilogue)
   int zi;           // this block's split index (set by gemm_kernel: blockIdx.z, or its XCD-ordered remap)
-  float* colsum;    // optional: colsum[g * N + n] += column sums of the stored tile (vector epilogue only)
   int vec_ok;       // host-checked: 8-column vector path legal (alignment / pitches, no remap, no atomics)
   int g;
   MG_DEV void set_group(int gg) { g = gg; }
@@ -630,11 +629,6 @@ MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const E
   const int fr = lane & 15, fq = lane >> 4;
   constexpr int CSP = WN + 4;  // staging pitch in floats (16-B aligned rows)
   float* cs = reinterpret_cast<float*>(smem) + wid * 16 * CSP;
-  // column sums of the stored values (bias gradients of grouped data-gradient GEMMs): a lane's column group is
-  // the same in every iteration (64 is a multiple of the WN / 8 groups), its rows are summed in registers
-  float csum[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) csum[j] = 0.f;
   // each wave stages through its own LDS band: one block barrier retires the K loop's reads of the
   // tiles, after that a wave only orders its own LDS writes and reads (wave-scope fence)
   __syncthreads();
@@ -663,10 +657,6 @@ MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const E
 #pragma unroll
           for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
           ep.vec8(mrow_base + m, n, v);
-          if (ep.colsum) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) csum[j] += v[j];
-          }
         } else {
           for (int j = 0; j < 8 && n + j < N; ++j) ep(mrow_base + m, n + j, src[j]);
         }
@@ -678,20 +668,6 @@ MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const E
         int m = mb + rr, n = nb + cc;
         if (m < Mloc && n < N) ep(mrow_base + m, n, cs[rr * CSP + cc]);
       }
-    }
-  }
-  if (ep.colsum && ep.vec_ok) {
-    // lanes of one column group (lane mod WN/8) fold with xor shuffles; the group's first lane adds its 8 sums
-    constexpr int CG = WN / 8;
-#pragma unroll
-    for (int off = CG; off < 64; off <<= 1)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) csum[j] += __shfl_xor(csum[j], off, 64);
-    if (lane < CG) {
-      const int n = n0 + wn * WN + lane * 8;
-      // the tail columns of the last tile hold no output (their sums are 0 and are skipped)
-      for (int j = 0; j < 8; ++j)
-        if (n + j < N) atomicAdd(ep.colsum + (int64_t)ep.g * N + n + j, csum[j]);
     }
   }
 }

@@ -150,7 +150,6 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
                        void* stream) {
   MG_REQUIRE(dtype == MG_F32 || dtype == MG_BF16 || dtype == MG_F32X3, "bad dtype");
   MG_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
-  MG_REQUIRE(!(ep && ep->colsum), "the colsum epilogue is for mg_gemm_grouped");
   if (M == 0 || N == 0) return MG_OK;
   const bool x3 = dtype == MG_F32X3;
   if (x3) dtype = MG_F32;  // fp32 storage; the MFMA products run on split bf16
@@ -678,10 +677,6 @@ extern "C" int mg_gemm_grouped(int dtype, int total_rows, int N, int K, int ngro
                  under2g((int64_t)total_rows * ldc, c_dtype),
              "an operand exceeds 2 GiB (32-bit buffer offsets)");
   MG_REQUIRE(aligned16(A) && aligned16(B), "A/B must be 16-byte aligned");
-  if (ep && ep->colsum) {  // the column sums ride on the 8-column vector epilogue
-    const Epi<float> chk = make_epi<float>(C, ldc, ep);
-    MG_REQUIRE(N % 8 == 0 && chk.host_vec_ok(), "colsum epilogue needs N % 8 == 0 and the vector epilogue");
-  }
   if (max_tiles <= 0 || N == 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define MG_GRP4(T, TO, X)                                                                                       \

@@ -36,7 +36,6 @@ Epi<TO> make_epi(void* C, int64_t ldc, const mg_epilogue* e) {
   ep.ldc_pre = e ? e->ld_pre : 0;
   ep.zstride = 0;
   ep.zi = 0;
-  ep.colsum = e ? e->colsum : nullptr;
   ep.vec_ok = 0;
   ep.g = 0;
   return ep;

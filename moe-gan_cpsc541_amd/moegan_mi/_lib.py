@@ -26,8 +26,7 @@ class Epilogue(ctypes.Structure):
                 ("ld_aux", _i64), ("resid", _c_void_p), ("ld_res", _i64), ("accumulate", _i32),
                 ("atomic", _i32), ("remap_lgcin", _i32), ("remap_taps", _i32), ("a_idx", _c_void_p),
                 ("a_idx_div", _i32), ("a_rowscale", _c_void_p), ("a_gelu", _i32), ("addvec", _c_void_p),
-                ("add_shift", _i32), ("add_ld", _i64), ("out_pre", _c_void_p), ("ld_pre", _i64),
-                ("colsum", _c_void_p)]
+                ("add_shift", _i32), ("add_ld", _i64), ("out_pre", _c_void_p), ("ld_pre", _i64)]
 
 
 class GemmDesc(ctypes.Structure):
@@ -169,11 +168,10 @@ def dt(t):
 
 def epilogue(alpha=1.0, bias=None, scale=None, scale_shift=0, scale_ld=0, rowscale=None, act=0, aux=None,
              ld_aux=0, resid=None, ld_res=0, accumulate=0, atomic=0, remap_lgcin=0, remap_taps=0, a_idx=None,
-             a_idx_div=1, a_rowscale=None, a_gelu=0, addvec=None, add_shift=0, add_ld=0, out_pre=None, ld_pre=0,
-             colsum=None):
+             a_idx_div=1, a_rowscale=None, a_gelu=0, addvec=None, add_shift=0, add_ld=0, out_pre=None, ld_pre=0):
     e = Epilogue(alpha, ptr(bias), ptr(scale), scale_shift, scale_ld, ptr(rowscale), act, ptr(aux), ld_aux,
                  ptr(resid), ld_res, accumulate, atomic, remap_lgcin, remap_taps, ptr(a_idx), a_idx_div,
-                 ptr(a_rowscale), a_gelu, ptr(addvec), add_shift, add_ld, ptr(out_pre), ld_pre, ptr(colsum))
+                 ptr(a_rowscale), a_gelu, ptr(addvec), add_shift, add_ld, ptr(out_pre), ld_pre)
     # keep the tensors alive until the launch has been enqueued
-    e._keep = (bias, scale, rowscale, aux, resid, a_idx, a_rowscale, addvec, out_pre, colsum)
+    e._keep = (bias, scale, rowscale, aux, resid, a_idx, a_rowscale, addvec, out_pre)
     return e

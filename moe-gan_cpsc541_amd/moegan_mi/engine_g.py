@@ -539,12 +539,8 @@ class GeneratorEngine:
         gG = ops.gather_rows(g_out, perm, k, rowscale=sv["gate_pos"])
         # expert layer 2: dH = gG @ W2_e, times GELU'(pre)
         gP = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
-        gb1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias", self.st.grad)
-        # the layer-1 bias gradient (column sums of gP per expert) rides on this GEMM's epilogue; the deterministic
-        # mode keeps the fixed-order grouped column sum below instead of the epilogue's fp32 atomics
-        fused_gb1 = not ops.deterministic()
         ops.gemm_grouped(gG, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
-                         out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd, colsum=gb1 if fused_gb1 else None))
+                         out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd))
         gW2 = self.st.group_view(ex + "0.net.2.weight", f"{ex}{E-1}.net.2.weight", self.st.grad)
         gb2 = self.st.group_view(ex + "0.net.2.bias", f"{ex}{E-1}.net.2.bias", self.st.grad)
         self.side.run(lambda: (ops.gemm_grouped_wgrad(gG, sv["Hid"], row_off, n, C, Hd, gW2),
@@ -554,8 +550,9 @@ class GeneratorEngine:
         ops.gemm_grouped(gP, sv["W1"], row_off, tile_off, sv["max_tiles"], C, Hd, b_kc=False, b_gstride=Hd * C,
                          out=gX, ldb=C)
         gW1 = self.st.group_view(ex + "0.net.0.weight", f"{ex}{E-1}.net.0.weight", self.st.grad)
+        gb1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias", self.st.grad)
         self.side.run(lambda: (ops.gemm_grouped_wgrad(gP, sv["Xg"], row_off, n, Hd, C, gW1),
-                               None if fused_gb1 else ops.grouped_colsum(gP, row_off, Hd, n, gb1)), gP)
+                               ops.grouped_colsum(gP, row_off, Hd, n, gb1)), gP)
         if self.on_grad_final is not None:  # this block's expert parameters receive no further gradient
             lo = self.st.offsets[ex + "0.net.0.weight"][0]
             o, nl = self.st.offsets[f"{ex}{E-1}.net.2.bias"]

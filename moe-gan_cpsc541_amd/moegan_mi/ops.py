@@ -25,15 +25,6 @@ def set_deterministic(on=True):
     order (partial rows + one fold, or one writer per element) instead of fp32 atomics, so two identically
     initialised steps give bit-identical results; slower.  Process-wide, like torch's own switch."""
     call("mg_set_tuning", TUNE_DETERMINISTIC, 1 if on else 0)
-    _DET[0] = bool(on)
-
-
-_DET = [False]
-
-
-def deterministic():
-    """Whether the library's deterministic mode is on (set_deterministic)."""
-    return _DET[0]
 
 
 def _ld(t):

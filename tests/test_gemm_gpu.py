@@ -297,42 +297,3 @@ def test_conv_wgrad_stride1_loader(dtype, B, H, Cin, Cout, k):
         assert torch.equal(gw1, gw0)
     else:
         assert rel(gw1, gw0) < 1e-6
-
-
-@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-3)])
-@pytest.mark.parametrize("C,H4", [(128, 512), (256, 1024)])
-def test_grouped_colsum_epilogue(dtype, tol, C, H4):
-    """The expert layer-1 bias gradient fused into the data-gradient GEMM's epilogue (mg_epilogue.colsum:
-    colsum[g, n] += sum over the group's rows of the stored value; t2i_moe_gan.py:257-260 backward):
-    gP = (gG @ W2_e) * GELU'(pre) and its per-expert column sums, against the separate fixed-order grouped
-    column sum of the same gP (the epilogue sums the values before the output rounding) and torch."""
-    g = torch.Generator(device=DEV).manual_seed(C)
-    E = 4
-    counts = [37, 0, 300, 129]
-    rows = sum(counts)
-    row_off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=DEV)
-    tiles = [(c + 127) // 128 for c in counts]
-    tile_off = torch.tensor([0] + list(torch.tensor(tiles).cumsum(0)), dtype=torch.int32, device=DEV)
-    gG = torch.randn(rows, C, device=DEV, generator=g).to(dtype)
-    W2 = (torch.randn(E, C, H4, device=DEV, generator=g) / 16).to(dtype)
-    pre = torch.randn(rows, H4, device=DEV, generator=g).to(dtype)
-    gP = torch.empty(rows, H4, device=DEV, dtype=dtype)
-    gb = torch.full((E, H4), 0.5, device=DEV)  # accumulates into what is there
-    ops.gemm_grouped(gG, W2.reshape(E * C, H4), row_off, tile_off, sum(tiles) + 2, H4, C, b_kc=False,
-                     b_gstride=C * H4, out=gP, ldb=H4,
-                     ep=L.epilogue(act=L.ACT_MUL_GELU_GRAD, aux=pre, ld_aux=H4, colsum=gb))
-    sep = torch.full((E, H4), 0.5, device=DEV)
-    ops.grouped_colsum(gP, row_off, H4, rows, sep)
-    torch.cuda.synchronize()
-    x = pre.double()
-    cdf = 0.5 * (1 + torch.erf(x / 2 ** 0.5))
-    gelu_grad = cdf + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
-    ref = torch.empty(rows, H4, device=DEV, dtype=torch.float64)
-    for e in range(E):
-        r0, r1 = int(row_off[e]), int(row_off[e + 1])
-        ref[r0:r1] = (gG[r0:r1].double() @ W2[e].double()) * gelu_grad[r0:r1]
-    ref_b = torch.stack([0.5 + ref[int(row_off[e]):int(row_off[e + 1])].sum(0) for e in range(E)])
-    assert rel(gP, ref) < (1e-5 if dtype == torch.float32 else 2e-2)
-    assert rel(gb, ref_b) < (1e-5 if dtype == torch.float32 else 1e-2)  # bf16: polynomial GELU' in the epilogue
-    assert rel(gb, sep) < tol
-    assert torch.equal(gb[1], torch.full((H4,), 0.5, device=DEV))  # the empty expert gets nothing
