@@ -173,16 +173,22 @@ class bf16_module_rounding:
     NAMES = ("modconv", "mtm", "attention_block", "expert_ffn", "conv_block", "mha", "sparse_moe")
     FUNCS = ("layer_norm", "gelu")  # torch.nn.functional, as the oracle calls them inside the blocks
 
+    def __init__(self, attention_internals=True):
+        self.attention_internals = attention_internals
+
     def __enter__(self):
         self.orig = {n: getattr(O, n) for n in self.NAMES}
         self.orig_f = {n: getattr(O.F, n) for n in self.FUNCS}
+        inner = dict(self.orig)
+        if self.attention_internals:  # the multi-head attention with the MFMA kernel's bf16 operands (below)
+            inner["mha"] = _mha_bf16_internals
 
         def wrapper(f):
             def wrap(*a, **k):
                 r = f(*a, **k)
                 return (_RoundBoth.apply(r[0]),) + tuple(r[1:]) if isinstance(r, tuple) else _RoundBoth.apply(r)
             return wrap
-        for n, f in self.orig.items():
+        for n, f in inner.items():
             setattr(O, n, wrapper(f))
         for n, f in self.orig_f.items():
             setattr(O.F, n, wrapper(f))
@@ -194,6 +200,34 @@ class bf16_module_rounding:
         for n, f in self.orig_f.items():
             setattr(O.F, n, f)
         return False
+
+
+_ORACLE_MHA = O.mha
+
+
+def _mha_bf16_internals(q_in, kv_in, P, pre, heads=8):
+    """oracle.mha (nn.MultiheadAttention forward, t2i_moe_gan.py:545-555) with the tensors the device's attention
+    path stores or feeds to its MFMAs in bf16 rounded (values and gradients): the q / k / v projections, the
+    softmax probabilities (the P of P @ V; their gradient stands in for the kernel's bf16 dS) and the head outputs
+    before the out-projection.  The cross-attention over the single text token runs in fp32 on the device (its
+    softmax is 1: the value chain text_proj -> v -> out_proj, engine_g._block_vectors), so it is left exact."""
+    import math
+    if kv_in.shape[1] == 1:
+        return _ORACLE_MHA(q_in, kv_in, P, pre, heads)
+    r = _RoundBoth.apply
+    B, Tq, C = q_in.shape
+    Tk = kv_in.shape[1]
+    Wi, bi = P[pre + "in_proj_weight"], P[pre + "in_proj_bias"]
+    q = r(O.F.linear(q_in, Wi[:C], bi[:C]))
+    k = r(O.F.linear(kv_in, Wi[C:2 * C], bi[C:2 * C]))
+    v = r(O.F.linear(kv_in, Wi[2 * C:], bi[2 * C:]))
+    d = C // heads
+    q = q.view(B, Tq, heads, d).transpose(1, 2)
+    k = k.view(B, Tk, heads, d).transpose(1, 2)
+    v = v.view(B, Tk, heads, d).transpose(1, 2)
+    att = r(torch.softmax((q / math.sqrt(d)) @ k.transpose(-1, -2), dim=-1))
+    o = r((att @ v).transpose(1, 2).reshape(B, Tq, C))
+    return O.F.linear(o, P[pre + "out_proj.weight"], P[pre + "out_proj.bias"])
 
 
 class bf16_weights(dict):
