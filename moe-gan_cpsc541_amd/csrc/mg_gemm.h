@@ -47,6 +47,9 @@ constexpr int NTHREADS = 256;
 #define MG_SB2_MAX_TILE 0
 #endif
 // raise the wave priority over the K step's MFMA phase (A/B switch; MI355X_MICROARCH.md: static priority)
+#ifndef MG_EPI_PREFETCH
+#define MG_EPI_PREFETCH 1
+#endif
 #ifndef MG_SETPRIO
 #define MG_SETPRIO 1  // measured: step 9.273 -> 9.245 ms, 4096^3 953 -> 1066 TF/s, D conv1 751 -> 815 TF/s
 #endif
@@ -476,8 +479,32 @@ struct Epi {
     if (addvec && (!al(addvec) || add_ld % 4)) return false;
     return true;
   }
-  // 8 consecutive columns n..n+7 (all < N), only when vec_ok
-  MG_DEV void vec8(int m, int n, float* v) const {
+  // The one row-streamed epilogue operand -- the *_GRAD aux, else the residual -- is loaded for a whole tile
+  // before the epilogue's band loop (epi_tile): its HBM latency then overlaps the accumulator staging instead of
+  // stalling every 16-row band (expert gP GEMM, 131072 x 512 x 128 with GELU': 141 -> 120 us measured).
+  typedef typename VecOf<TO>::type ovec_t;
+  static constexpr int OV = 8 / VecOf<TO>::N;  // 16-B vectors per 8 columns: 1 (bf16), 2 (fp32)
+  struct Pf { ovec_t v[OV]; };
+  MG_DEV int pf_kind() const {
+    return (aux && (act == ACT_MUL_GELU_GRAD || act == ACT_MUL_LRELU_GRAD)) ? 1 : (resid ? 2 : 0);
+  }
+  MG_DEV void pf_load(int m, int n, Pf& p) const {
+    if (rm_mode == 1) m = remap_row(m);
+    const TO* src = pf_kind() == 1 ? aux + (int64_t)m * ld_aux + n : resid + (int64_t)m * ld_res + n;
+#pragma unroll
+    for (int j = 0; j < OV; ++j) p.v[j] = *reinterpret_cast<const ovec_t*>(src + j * VecOf<TO>::N);
+  }
+  MG_DEV static void pf_unpack(const Pf& p, float* t) {
+#pragma unroll
+    for (int j = 0; j < OV; ++j)
+#pragma unroll
+      for (int i = 0; i < VecOf<TO>::N; ++i) {
+        if constexpr (sizeof(TO) == 2) t[j * VecOf<TO>::N + i] = bf2f(p.v[j][i]);
+        else t[j * VecOf<TO>::N + i] = p.v[j][i];
+      }
+  }
+  // 8 consecutive columns n..n+7 (all < N), only when vec_ok; pf = the prefetched pf_kind() operand
+  __attribute__((always_inline)) MG_DEV void vec8(int m, int n, float* v, const Pf* pf = nullptr) const {
     if (rm_mode == 1) m = remap_row(m);
     float t[8];
 #pragma unroll
@@ -500,11 +527,13 @@ struct Epi {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = sizeof(TO) == 2 ? gelu_fast(v[j]) : gelu_erf(v[j]);
     } else if (act == ACT_MUL_GELU_GRAD) {
-      ld8(aux + (int64_t)m * ld_aux + n, t);
+      if (pf) pf_unpack(*pf, t);
+      else ld8(aux + (int64_t)m * ld_aux + n, t);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] *= sizeof(TO) == 2 ? gelu_fast_grad(t[j]) : gelu_erf_grad(t[j]);
     } else if (act == ACT_MUL_LRELU_GRAD) {
-      ld8(aux + (int64_t)m * ld_aux + n, t);
+      if (pf) pf_unpack(*pf, t);
+      else ld8(aux + (int64_t)m * ld_aux + n, t);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] *= lrelu_grad(t[j]);
     } else if (act == ACT_RSQRT_EPS) {
@@ -525,7 +554,8 @@ struct Epi {
       for (int j = 0; j < 8; ++j) v[j] += t[j];
     }
     if (resid) {
-      ld8(resid + (int64_t)m * ld_res + n, t);
+      if (pf && pf_kind() == 2) pf_unpack(*pf, t);
+      else ld8(resid + (int64_t)m * ld_res + n, t);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += t[j];
     }
@@ -624,7 +654,7 @@ MG_DEV bf16x8_t mc_frag_bf16(const bf16_t* img, int ld, int kr0, int c0, int lan
 // consecutive lanes on consecutive columns.  Static indexing keeps acc in registers; the loop keeps the
 // inlined epilogue code small.  Waves are arranged 2x2, each owning a (BM/2)x(BN/2) block of 16x16 fragments
 // in the MFMA C/D layout (dtype-independent on gfx950).
-template <int BM, int BN, class EP>
+template <int BM, int BN, class EP, bool PF = false>
 MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const EP& ep, int m0, int n0, int Mloc,
                      int N, int mrow_base) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
@@ -633,6 +663,25 @@ MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const E
   const int fr = lane & 15, fq = lane >> 4;
   constexpr int CSP = WN + 4;  // staging pitch in floats (16-B aligned rows)
   float* cs = reinterpret_cast<float*>(smem) + wid * 16 * CSP;
+  // vector path with a streamed operand: every band's loads issued up front (NE 8-column groups per lane)
+  // (only where the prefetched tile fits in 32 VGPRs: 64x64 / 128x32 tiles, 128x128 bf16 -- wider tiles spill)
+  constexpr int NE = (2 * WN + 63) / 64;
+  // PF: instantiated for the expert GEMMs only (turned on for every tile it cost the step 0.18 ms: code size /
+  // register allocation of the other kernels); bf16 operands only (fp32 ones spilled)
+  constexpr bool kPf = PF && MG_EPI_PREFETCH && EP::OV == 1 && FM * NE * 4 <= 32;
+  const bool pfp = kPf && ep.vec_ok && ep.pf_kind() != 0;
+  typename EP::Pf pf[kPf ? FM : 1][kPf ? NE : 1];
+  if constexpr (kPf) if (pfp) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int t = 0; t < NE; ++t) {
+        const int e = lane + 64 * t;
+        const int rr = e / (WN / 8), cc = (e - rr * (WN / 8)) * 8;
+        const int m = m0 + wm * WM + i * 16 + rr, n = n0 + wn * WN + cc;
+        if (e < 2 * WN && m < Mloc && n + 8 <= N) ep.pf_load(mrow_base + m, n, pf[i][t]);
+      }
+  }
   // each wave stages through its own LDS band: one block barrier retires the K loop's reads of the
   // tiles, after that a wave only orders its own LDS writes and reads (wave-scope fence)
   __syncthreads();
@@ -647,7 +696,25 @@ MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const E
     if (MG_EPI_BLOCK_SYNC) __syncthreads();
     else { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
     const int mb = m0 + wm * WM + i * 16, nb = n0 + wn * WN;
-    if (ep.vec_ok) {
+    if (kPf && pfp) {
+#pragma unroll
+      for (int t = 0; t < (kPf ? NE : 0); ++t) {
+        const int e = lane + 64 * t;
+        const int rr = e / (WN / 8), cc = (e - rr * (WN / 8)) * 8;
+        const int m = mb + rr, n = nb + cc;
+        if (e >= 2 * WN || m >= Mloc) continue;
+        const float* src = cs + rr * CSP + cc;
+        if (n + 8 <= N) {
+          float v[8];
+          f32x4_t a = *reinterpret_cast<const f32x4_t*>(src), b = *reinterpret_cast<const f32x4_t*>(src + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+          ep.vec8(mrow_base + m, n, v, &pf[kPf ? i : 0][kPf ? t : 0]);
+        } else {
+          for (int j = 0; j < 8 && n + j < N; ++j) ep(mrow_base + m, n + j, src[j]);
+        }
+      }
+    } else if (ep.vec_ok) {
       // 8 consecutive columns per lane: vector loads of the epilogue operands, one 16-B store (bf16)
 #pragma unroll 1
       for (int e = lane; e < 2 * WN; e += 64) {
@@ -677,7 +744,8 @@ MG_DEV void epi_tile(const f32x4_t (&acc)[BM / 32][BN / 32], void* smem, const E
 }
 
 // One output tile: C[m0.., n0..] of rows [mrow_base, mrow_base + Mloc) over k in [kbeg, kend).
-template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP, bool X3 = false>
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP, bool X3 = false,
+          bool PF = false>
 MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, int Mloc, int N, int kbeg, int kend,
                       int mrow_base) {
   static_assert(!X3 || std::is_same<T, float>::value, "split-bf16 staging takes fp32 operands");
@@ -1007,7 +1075,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     }
   }
 
-  epi_tile<BM, BN>(acc, smem, ep, m0, n0, Mloc, N, mrow_base);
+  epi_tile<BM, BN, EP, PF>(acc, smem, ep, m0, n0, Mloc, N, mrow_base);
 }
 
 
@@ -1066,7 +1134,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   A.set_group(g);
   B.set_group(g);
   ep.set_group(g);
-  gemm_tile<T, BM, BN, A_KC, B_KC, AL, BL, EP, X3>(A, B, ep, m0, n0, Mloc, N, kbeg, kend, mrow_base);
+  gemm_tile<T, BM, BN, A_KC, B_KC, AL, BL, EP, X3, TAG == 1>(A, B, ep, m0, n0, Mloc, N, kbeg, kend, mrow_base);
 }
 
 // ---------------------------------------------------------------------------

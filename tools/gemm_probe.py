@@ -87,6 +87,37 @@ def main():
     cases.append(("expert_fc1", 2.0 * E_ * rows * 512 * 128,
                   lambda: ops.gemm_grouped(Ae, We, row_off, tile_off, E_ * rows // 128, 512, 128, b_gstride=512 * 128,
                                            out=oute, ep=ops.E(act=L.ACT_GELU))))
+    # expert layer-2 data gradient with GELU' (the backward's gP GEMM, B = W2 [C, Hd] N-contiguous)
+    W2e = rn(E_ * 128, 512, dt=bf, sc=0.05)
+    gGe = rn(E_ * rows, 128, dt=bf)
+    Pre_e = rn(E_ * rows, 512, dt=bf)
+    gPe = torch.empty(E_ * rows, 512, device=dev, dtype=bf)
+    cases.append(("expert_gP", 2.0 * E_ * rows * 512 * 128,
+                  lambda: ops.gemm_grouped(gGe, W2e, row_off, tile_off, E_ * rows // 128 + E_, 512, 128, b_kc=False,
+                                           b_gstride=128 * 512, out=gPe, ldb=512,
+                                           ep=ops.E(act=L.ACT_MUL_GELU_GRAD, aux=Pre_e, ld_aux=512))))
+    cases.append(("expert_gP_noaux", 2.0 * E_ * rows * 512 * 128,
+                  lambda: ops.gemm_grouped(gGe, W2e, row_off, tile_off, E_ * rows // 128 + E_, 512, 128, b_kc=False,
+                                           b_gstride=128 * 512, out=gPe, ldb=512)))
+    # expert layer-1 data gradient gX = gP W1 (K = 512)
+    W1e = rn(E_ * 512, 128, dt=bf, sc=0.05)
+    gXe = torch.empty(E_ * rows, 128, device=dev, dtype=bf)
+    cases.append(("expert_gX", 2.0 * E_ * rows * 512 * 128,
+                  lambda: ops.gemm_grouped(gPe, W1e, row_off, tile_off, E_ * rows // 128 + E_, 128, 512, b_kc=False,
+                                           b_gstride=512 * 128, out=gXe, ldb=128)))
+    # D conv0 at 64x64 (K = 48 im2col columns)
+    cols0 = rn(B * 1024, 48, dt=bf)
+    W0 = rn(128, 48, dt=bf, sc=0.1)
+    b0 = rn(128)
+    cases.append(("d_conv0_fwd", 2.0 * B * 1024 * 128 * 48,
+                  lambda: ops.linear(cols0, W0, bias=b0, act=L.ACT_LRELU)))
+    ga0 = rn(B * 1024, 128, dt=bf)
+    dW0 = torch.zeros(128, 48, device=dev)
+    cases.append(("d_conv0_wgrad", 2.0 * B * 1024 * 128 * 48,
+                  lambda: ops.gemm(ga0, cols0, 128, 48, B * 1024, a_kc=False, b_kc=False, out=dW0,
+                                   ep=ops.E(atomic=1), splits=0)))
+    cases.append(("d_conv0_dgrad", 2.0 * B * 1024 * 128 * 48,
+                  lambda: ops.gemm(ga0, W0, B * 1024, 48, 128, b_kc=False, out_dtype=torch.float32)))
     # fused expert FFN (fc1 + GELU + fc2 on chip), no-grad and saved forms
     We1 = rn(E_, 512, 128, dt=bf, sc=0.08)
     We2 = rn(E_, 128, 512, dt=bf, sc=0.04)
