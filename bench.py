@@ -162,10 +162,12 @@ def loop_bench(args, dev):
     imgs = (torch.rand(B * n, 3, 64, 64, generator=g) * 2 - 1).pin_memory()
     text = torch.randn(B * n, 512, generator=g).pin_memory()
     loader = [(imgs[i:i + B], text[i:i + B]) for i in range(0, B * n, B)]
-    marks = {}
+    marks, bad = {}, []
 
-    def done(epoch, b):
+    def done(epoch, b, flags):
         marks[b] = time.perf_counter()
+        if flags & 3:
+            bad.append(b)
         if b % max(1, n // 4) == 0:
             print(f"[bench] loop batch {b + 1}/{n} done", file=sys.stderr, flush=True)
     import tempfile
@@ -177,6 +179,7 @@ def loop_bench(args, dev):
     ms = (t1 - t0) / (n - 1 - args.warmup) * 1e3
     return {"metric": "images/sec (G+D step through the drop-in train_aurora_gan loop, 64x64, H2D copy included)",
             "value": round(B * 1e3 / ms, 2), "unit": "images/sec", "ms_per_step": round(ms, 3), "dtype": args.dtype,
+            "finite": not bad,  # no batch raised a non-finite D / G loss guard
             "config": {"workload": f"C2 via train_aurora_gan: 64x64, {args.experts} experts top-{args.topk}, batch "
                                    f"{B}, {args.dtype}, R1 on, pinned host batches (12.6 MB) copied per batch",
                        "global_batch": B, "parallelism": "dp1",

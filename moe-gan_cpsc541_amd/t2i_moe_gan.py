@@ -455,7 +455,8 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
     step's flag word once per batch to print the reference's warnings and to not count a skipped batch.  That
     read (with the logged losses, one pinned copy) is deferred until the next batch has been enqueued.
     ``use_graphs``: every batch body is a replayed hipGraph (``_StepRunner``, bench.py's launch mode).
-    ``on_batch_done(epoch, batch_idx)``: called when a batch's results have reached the host (bench.py --loop).
+    ``on_batch_done(epoch, batch_idx, flags)``: called when a batch's results have reached the host (bench.py
+    --loop); ``flags`` is the batch's guard word (bit 0: non-finite D loss, bit 1: non-finite G loss).
     ``resume_from``: a resume checkpoint (:1484-1491 layout, ours or the reference's) to start from;
     ``save_every_epoch``: write that layout after every epoch (the reference's commented-out :1642-1652)."""
     os.makedirs(save_dir, exist_ok=True)
@@ -520,10 +521,10 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
             nonlocal step
             host, ev, bidx = rec
             ev.synchronize()
-            if on_batch_done is not None:
-                on_batch_done(epoch, bidx)
             v = host.tolist()
             flags = int(v[0])
+            if on_batch_done is not None:
+                on_batch_done(epoch, bidx, flags)
             if flags & 1:
                 print("⚠️ NaN/Inf detected in discriminator loss! Skipping this batch.")
                 return

@@ -118,6 +118,36 @@ def test_grouped_gemm_and_wgrad(dtype, tol, C):
     assert rel(gW, refw) < tol * 2
 
 
+@pytest.mark.parametrize("C,H4", [(128, 512), (256, 1024)])
+def test_grouped_gelu_grad_epilogue(C, H4):
+    """The expert backward's gP GEMM (engine_g.moe_bwd): gP = (gG @ W2_e) * GELU'(pre), B = W2 [E, C, H4]
+    N-contiguous, bf16.  Its epilogue loads the pre-activation for the whole tile ahead of the band loop
+    (MG_EPI_PREFETCH); ragged groups, an empty group and a partial last tile cover the row guards."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    E = 4
+    counts = [200, 0, 333, 129]
+    rows = sum(counts)
+    row_off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=DEV)
+    tiles = [(c + 127) // 128 for c in counts]
+    tile_off = torch.tensor([0] + list(torch.tensor(tiles).cumsum(0)), dtype=torch.int32, device=DEV)
+    gG = (torch.randn(rows, C, device=DEV, generator=g) * 0.5).bfloat16()
+    W2 = (torch.randn(E, C, H4, device=DEV, generator=g) / 16).bfloat16()
+    pre = (torch.randn(rows, H4, device=DEV, generator=g) * 1.5).bfloat16()
+    out = torch.full((rows, H4), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.gemm_grouped(gG, W2, row_off, tile_off, sum(tiles) + E, H4, C, b_kc=False, b_gstride=C * H4, out=out,
+                     ldb=H4, ep=L.epilogue(act=L.ACT_MUL_GELU_GRAD, aux=pre, ld_aux=H4))
+    torch.cuda.synchronize()
+    x = pre.float()
+    dgelu = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    ref = torch.empty(rows, H4, device=DEV)
+    for e in range(E):
+        r0, r1 = int(row_off[e]), int(row_off[e + 1])
+        ref[r0:r1] = gG[r0:r1].float() @ W2[e].float()
+    ref = ref * dgelu
+    assert torch.isfinite(out.float()).all()
+    assert ((out.float() - ref).abs() <= 1e-2 * ref.abs() + 2e-3).all()
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
 @pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (1, 0), (0, 0)])
 def test_gemm_batch_matches_individual(dtype, tol, a_kc, b_kc):

@@ -25,7 +25,7 @@ def _train(use_graphs, tmp_path, acc=2):
     G, D = M.train_aurora_gan(_loader(), num_epochs=1, lr=2e-4, gradient_accumulation_steps=acc,
                               checkpoint_activation=False, num_experts=8, topk=2, dtype="bf16", seed=0,
                               save_dir=str(tmp_path), log_interval=1, device=DEV, use_graphs=use_graphs,
-                              on_batch_done=lambda e, b: seen.append(b))
+                              on_batch_done=lambda e, b, f: seen.append(b))
     torch.cuda.synchronize()
     assert seen == [0, 1, 2, 3]
     return G._store.data.clone(), D._store.data.clone()
