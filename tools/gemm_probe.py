@@ -72,6 +72,14 @@ def main():
     gw1 = torch.zeros(256, 128, 4, 4, device=dev)
     cases.append(("d_conv1_wgrad", 2.0 * B * 256 * 256 * 2048,
                   lambda: ops.conv2d_wgrad(gy1, h0, 256, 4, 4, 2, 1, gw1)))
+    # 1x1 conv weight gradients (attention-block / skip projections): M x N small, K = B*H*W pixels
+    for tag, (H_, ci, co) in {"w1x1_16_128": (16, 128, 128), "w1x1_16_256": (16, 256, 128), "w1x1_8_256": (8, 256, 256),
+                              "w1x1_4_512": (4, 512, 512), "w1x1_16_8": (16, 128, 8)}.items():
+        gyq = rn(B * H_ * H_, co, dt=bf)
+        xq = rn(B, H_, H_, ci, dt=bf)
+        gwq = torch.zeros(co, ci, 1, 1, device=dev)
+        cases.append((tag, 2.0 * B * H_ * H_ * co * ci,
+                      lambda gyq=gyq, xq=xq, gwq=gwq, co=co: ops.conv2d_wgrad(gyq, xq, co, 1, 1, 1, 0, gwq)))
     gl = rn(B * 256, 512, dt=bf)
     xl = rn(B * 256, 128, dt=bf)
     gwl = torch.zeros(512, 128, device=dev)
