@@ -144,6 +144,17 @@ def main():
     gWe = torch.zeros(E_, 128, 512, device=dev)
     cases.append(("expert_wgrad", 2.0 * E_ * rows * 512 * 128,
                   lambda: ops.gemm_grouped_wgrad(gG, Hid, row_off, E_ * rows, 128, 512, gWe)))
+    # discriminator head / R1 LReLU' products (one K step, bf16 in / out, streamed aux)
+    Gh = rn(B * 256, 16, dt=bf)
+    W2i = rn(256, 16, dt=bf, sc=0.2)
+    h1a = rn(B * 256, 256, dt=bf)
+    cases.append(("d_head_ga1", 2.0 * B * 256 * 256 * 16,
+                  lambda: ops.gemm(Gh, W2i, B * 256, 256, 16, out_dtype=torch.bfloat16,
+                                   ep=ops.E(act=L.ACT_MUL_LRELU_GRAD, aux=h1a, ld_aux=256))))
+    h0a = rn(B * 1024, 128, dt=bf)
+    cases.append(("d_r1_m0v0", 2.0 * B * 1024 * 128 * 48,
+                  lambda: ops.gemm(cols0, W0, B * 1024, 128, 48, out_dtype=torch.bfloat16,
+                                   ep=ops.E(act=L.ACT_MUL_LRELU_GRAD, aux=h0a, ld_aux=128))))
     # calibration: square bf16 GEMM
     Ab = rn(4096, 4096, dt=bf)
     Bb = rn(4096, 4096, dt=bf)
