@@ -302,6 +302,10 @@ __global__ void k_d_loss(const float* __restrict__ img, const float* __restrict_
       atomicAdd(&out[2], a / B);
       atomicAdd(&out[0], a / B);
     }
+  } else if (part && threadIdx.x == 0) {
+    // Nf > 1: block B has no work (the fakes are blocks B+1..2B), but k_d_loss_fold sums every row
+    float* pr = part + (int64_t)b * 6;
+    pr[0] = 0.f; pr[1] = 0.f; pr[2] = 0.f; pr[3] = 0.f; pr[4] = 0.f; pr[5] = 0.f;
   }
 }
 

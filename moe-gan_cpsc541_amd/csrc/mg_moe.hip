@@ -1088,6 +1088,8 @@ extern "C" int mg_moe_dispatch(const int32_t* topi, const float* gate, int T, in
   int nb = cdiv(n, DCH);
   MG_REQUIRE(nb <= 65535, "too many assignments");
   hipLaunchKernelGGL(k_disp_count, dim3(nb), dim3(256), E * sizeof(int), st, topi, n, E, ws);
+  // gfx950 assumption: at the 16384-count cutoff the parallel scan takes (16384 + 1056) * 4 B = 69.7 KB of dynamic
+  // LDS, over the 64 KB of older parts but within the 160 KB a gfx950 workgroup may use
   if ((int64_t)nb * E <= 16384)
     hipLaunchKernelGGL(k_disp_scan_par, dim3(1), dim3(1024), (size_t)(nb * E + 1024 + 32) * sizeof(int), st, ws, nb, E,
                        bm, row_off, tile_off);

@@ -82,23 +82,25 @@ def load_optimizer_state_dict(store, sd):
 
 def save_resume(path, generator, discriminator, epoch, step, lr_g, lr_d, betas=(0.5, 0.999), epoch_complete=False,
                 generators=None):
-    """Write the reference's resume layout (t2i_moe_gan.py:1484-1491).  ``epoch`` is the 0-based epoch the state
-    belongs to, as the reference stores it; ``epoch_complete`` (an extra key, absent from the reference's files)
-    marks a checkpoint written after that epoch finished, so resuming starts at the next one.  ``generators``:
-    name -> torch.Generator whose states are stored too (``rng/<name>``) so a resumed run continues the same z,
-    permutation and router-noise streams."""
+    """Write the reference's resume layout (t2i_moe_gan.py:1484-1491) with only the reference's keys.  ``epoch``
+    is the 0-based epoch the state belongs to.  A mid-epoch checkpoint stores it as is (:1489); an end-of-epoch
+    one (``epoch_complete``) stores ``epoch + 1``, as the reference's end-of-epoch file does (:1648), so a tool
+    that reads 'epoch' the reference's way resumes at the next epoch.  ``generators``: name -> torch.Generator
+    state (or the generator itself) stored as ``rng/<name>``, so a resumed run continues the same z, permutation
+    and router-noise streams (every rank's local stream under data parallelism: ``rng/local<r>``)."""
     ck = {"generator": generator.state_dict(), "discriminator": discriminator.state_dict(),
           "optimizer_g": optimizer_state_dict(generator._store, lr_g, betas),
           "optimizer_d": optimizer_state_dict(discriminator._store, lr_d, betas),
-          "epoch": int(epoch), "step": int(step), "epoch_complete": bool(epoch_complete)}
+          "epoch": int(epoch) + (1 if epoch_complete else 0), "step": int(step)}
     for name, g in (generators or {}).items():
-        ck["rng/" + name] = g.get_state()
+        ck["rng/" + name] = g.get_state() if hasattr(g, "get_state") else g
     torch.save(ck, path)
 
 
 def resume_start_epoch(ck_epoch, ck):
-    """The epoch a resumed run starts at: the stored one (the reference's mid-epoch checkpoints), or the next when
-    the checkpoint marks its epoch complete."""
+    """The epoch a resumed run starts at: the stored one (the reference's convention: a mid-epoch checkpoint
+    repeats its epoch, an end-of-epoch one already stores the next).  Round-3 files stored the 0-based epoch plus
+    an ``epoch_complete`` flag; they still resume at the next epoch."""
     return int(ck_epoch) + (1 if ck.get("epoch_complete", False) else 0)
 
 

@@ -34,11 +34,17 @@ def eager(fn):
 
 
 class SegmentedGraph:
-    def __init__(self):
+    """``stream`` / ``pool``: share the capture stream (so the library's per-stream workspace) and the graph memory
+    pool with other SegmentedGraphs that are replayed one at a time in stream order (the variants of one training
+    loop): a pool's blocks that one capture freed are reused by the next capture, while tensors a graph still
+    holds (its outputs) stay out of reach of the others."""
+
+    def __init__(self, stream=None, pool=None):
         self.items = []  # ("graph", CUDAGraph) | ("eager", fn)
-        self.pool = None
+        self.pool = pool
         self._cur = None
-        self.stream = torch.cuda.Stream()  # capture stream (the library keeps one workspace per stream)
+        # capture stream (the library keeps one workspace per stream)
+        self.stream = stream if stream is not None else torch.cuda.Stream()
 
     def run_eager(self, fn, *args, **kwargs):
         """Run ``fn`` eagerly on the capture stream: the warm-up that sizes every lazily allocated buffer,
@@ -54,7 +60,8 @@ class SegmentedGraph:
         same shapes, so every lazily sized buffer exists).  Returns fn's result (tensors in the graph pool)."""
         global ACTIVE
         assert ACTIVE is None, "nested capture"
-        self.pool = torch.cuda.graph_pool_handle()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
         self.stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.stream):
             ACTIVE = self

@@ -361,7 +361,12 @@ class _StepRunner:
     that also sizes every lazily allocated buffer -- and the variant is captured right after it (a capture
     executes nothing), so every later batch of it is one replay.  Graphs of a finished epoch are released when
     the epoch's scalars change.  A batch whose shape differs from the loader's first batch (a ragged last batch)
-    runs eagerly without capture.  ``enabled=False`` (or a non-HIP device) runs every batch eagerly."""
+    runs eagerly without capture.  ``enabled=False`` (or a non-HIP device) runs every batch eagerly.
+
+    All variants share one capture stream (one library workspace) and one graph memory pool: they replay one at
+    a time on the same stream, so the step temporaries of one variant may reuse another's; only each variant's
+    output tensors stay private (with acc = 8 the loop keeps three variants alive).  Peak memory of
+    the loop is measured by tests/test_loop_gpu.py."""
 
     def __init__(self, ts, device, enabled=True):
         self.ts = ts
@@ -369,6 +374,7 @@ class _StepRunner:
         self.graphs = {}
         self.epoch_key = None
         self.shape = None
+        self.stream = self.pool = None
 
     def __call__(self, real, text, z, eps_d, eps_g, perm, **kw):
         if not self.enabled:
@@ -390,9 +396,12 @@ class _StepRunner:
 
             def fn(b=bufs):
                 return self.ts.step(b["real"], b["text"], b["z"], b["eps_d"], b["eps_g"], b["perm"], **kw)
-            g = SegmentedGraph()
+            if self.stream is None:
+                self.stream = torch.cuda.Stream()
+            g = SegmentedGraph(stream=self.stream, pool=self.pool)
             out = g.run_eager(fn)  # this batch, eagerly
             outg = g.capture(fn)
+            self.pool = g.pool
             self.graphs[key] = (g, outg, bufs)
             return out
         g, outg, b = ent
@@ -565,10 +574,6 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
         if pending is not None:
             account(pending)
         pbar.close()
-        if save_every_epoch and rank == 0:
-            save_resume(os.path.join(save_dir, f"aurora_checkpoint_epoch_{epoch + 1}.pt"), generator, discriminator,
-                        epoch, step, cur_lr, cur_lr, (beta1, beta2), epoch_complete=True,
-                        generators={"local0": g_local, "shared": g_shared})
         if val_dataloader is not None:
             vm = _validate(generator, discriminator, val_dataloader, gan_loss, temperature_factor, eff_kl, device,
                            process_group, g_local)
@@ -581,11 +586,32 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
                 flag = torch.tensor([1 if stop else 0], device=device, dtype=torch.int32)
                 dist.broadcast(flag, src=dist.get_global_rank(process_group, 0), group=process_group)
                 stop = bool(flag.item())
-            if stop:
-                if rank == 0:
-                    print("Early stopping triggered by metric callback")
-                break
+        else:
+            stop = False
+        if save_every_epoch:  # after validation (which draws from g_local), every rank's local stream
+            _save_epoch(save_dir, generator, discriminator, epoch, step, cur_lr, (beta1, beta2), g_local, g_shared,
+                        process_group, rank)
+        if stop:
+            if rank == 0:
+                print("Early stopping triggered by metric callback")
+            break
     return generator, discriminator
+
+
+def _save_epoch(save_dir, generator, discriminator, epoch, step, cur_lr, betas, g_local, g_shared, process_group,
+                rank):
+    """End-of-epoch resume file (the reference's commented-out :1642-1652 layout, 'epoch' = epoch + 1), written by
+    rank 0 with every rank's local generator state (``rng/local<r>``) gathered over the process group."""
+    states = {f"local{rank}": g_local.get_state()}
+    if process_group is not None:
+        import torch.distributed as dist
+        got = [None] * dist.get_world_size(process_group)
+        dist.all_gather_object(got, (rank, g_local.get_state()), group=process_group)
+        states = {f"local{r}": st for r, st in got}
+    if rank == 0:
+        states["shared"] = g_shared.get_state()
+        save_resume(os.path.join(save_dir, f"aurora_checkpoint_epoch_{epoch + 1}.pt"), generator, discriminator,
+                    epoch, step, cur_lr, cur_lr, betas, epoch_complete=True, generators=states)
 
 
 def _validate(generator, discriminator, loader, gan_loss, temperature_factor, eff_kl, device, process_group=None,

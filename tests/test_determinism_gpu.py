@@ -10,16 +10,16 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _one_step(B, det, seed=7):
+def _one_step(B, det, seed=7, res=64):
     import bench
     from moegan_mi.init import init_discriminator, init_generator
     from moegan_mi.step import StepConfig, TrainStep
     E, k = 8, 2
-    ts = TrainStep(StepConfig(E=E, topk=k, dtype="bf16", deterministic=det), DEV)
+    ts = TrainStep(StepConfig(E=E, topk=k, dtype="bf16", deterministic=det, max_res=16 if res == 64 else res), DEV)
     init_generator(ts.gs, seed=0)
     init_discriminator(ts.ds, seed=1)
     g = torch.Generator(device=DEV).manual_seed(seed)
-    real = torch.rand(B, 3, 64, 64, device=DEV, generator=g) * 2 - 1
+    real = torch.rand(B, 3, res, res, device=DEV, generator=g) * 2 - 1
     text = torch.randn(B, 512, device=DEV, generator=g)
     z = torch.randn(B, 512, device=DEV, generator=g)
     fd, eps_d = bench.eps_buffers(E, DEV)
@@ -64,3 +64,21 @@ def test_deterministic_mode_matches_default_mode():
     g_d = torch.cat([v.reshape(-1) for v in d[1].values()]).double()
     g_n = torch.cat([v.reshape(-1) for v in n[1].values()]).double()
     assert float((g_d - g_n).norm() / g_n.norm()) < 1e-3
+
+
+def test_deterministic_mode_multi_logit_fakes():
+    """Deterministic mode with the progressive generator at 32^2 (real and fake images 32x32, so the D loss sees
+    Nf = 25 logits per fake image and k_d_loss runs 2B+1 blocks): the logged D losses agree with the default
+    (atomic) mode -- block B, idle when Nf > 1, still writes its (zero) partial row for the fixed-order fold
+     -- and two deterministic steps are bit-identical."""
+    from moegan_mi import ops
+    try:
+        a = _one_step(4, True, res=32)
+        b = _one_step(4, True, res=32)
+    finally:
+        ops.set_deterministic(False)
+    n = _one_step(4, False, res=32)
+    for k in a[0]:
+        assert torch.equal(a[0][k], b[0][k]), k
+        assert torch.allclose(a[0][k], n[0][k], rtol=1e-4, atol=1e-7), (k, a[0][k], n[0][k])
+    assert torch.isfinite(a[0]["d_losses"]).all()

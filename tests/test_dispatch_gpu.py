@@ -2,7 +2,8 @@
 dispatch of the top-k assignments): bit-exact against a stable sort of the assignments by expert.  Covers
 E = 4 / 8 / 16 / 32 (C2: 8, C5: 32), k = 1 / 2 / 4, ragged chunk tails (the kernels work in 1024-assignment
 chunks), experts that receive no assignment, the skewed routing of an early-training router, and a size whose
-chunk-count table exceeds the parallel scan's LDS table (the serial scan then runs)."""
+chunk-count table exceeds the parallel scan's LDS table (the serial scan then runs), and the largest table the parallel scan takes
+(E=32, k=4, T=131072: 512 chunks x 32 = 16384 counts, ~70 KB of dynamic LDS, within gfx950's 160 KB per CU)."""
 import pytest
 import torch
 
@@ -24,7 +25,8 @@ def _reference(topi, gate, E, bm):
 
 @pytest.mark.parametrize("E,k,T,skew", [(8, 2, 65536, False), (32, 4, 65536, False), (32, 4, 4096, True),
                                         (16, 2, 3001, False), (4, 1, 1, False), (8, 2, 5, True),
-                                        (32, 4, 16384, True), (4, 4, 777, False), (32, 4, 140000, False)])
+                                        (32, 4, 16384, True), (4, 4, 777, False), (32, 4, 140000, False),
+                                        (32, 4, 131072, False)])
 def test_dispatch_matches_stable_sort(E, k, T, skew):
     from moegan_mi import ops
     g = torch.Generator(device=DEV).manual_seed(E * 1000 + k * 10 + T)

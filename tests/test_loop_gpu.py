@@ -19,15 +19,15 @@ def _loader(B=8, n=4, seed=3):
     return [(imgs[i:i + B], text[i:i + B]) for i in range(0, B * n, B)]
 
 
-def _train(use_graphs, tmp_path, acc=2):
+def _train(use_graphs, tmp_path, acc=2, B=8, n=4):
     import t2i_moe_gan as M
     seen = []
-    G, D = M.train_aurora_gan(_loader(), num_epochs=1, lr=2e-4, gradient_accumulation_steps=acc,
+    G, D = M.train_aurora_gan(_loader(B, n), num_epochs=1, lr=2e-4, gradient_accumulation_steps=acc,
                               checkpoint_activation=False, num_experts=8, topk=2, dtype="bf16", seed=0,
                               save_dir=str(tmp_path), log_interval=1, device=DEV, use_graphs=use_graphs,
                               on_batch_done=lambda e, b, f: seen.append(b))
     torch.cuda.synchronize()
-    assert seen == [0, 1, 2, 3]
+    assert seen == list(range(n))
     return G._store.data.clone(), D._store.data.clone()
 
 
@@ -52,3 +52,23 @@ def test_graph_loop_matches_eager_loop(tmp_path):
         noise, err = rel(e2[i], e1[i]), rel(g[i], e1[i])
         print(f"{name}: graph-loop rel err {err:.3e}, eager loop spread {noise:.3e}")
         assert err <= REPLAY_X * noise + 1e-6, (name, err, noise)
+
+
+def test_graph_loop_peak_memory_acc8(tmp_path):
+    """The reference's default window (gradient_accumulation_steps=8, :1043) makes the loop capture three variants
+    (window start / middle / end).  They share one capture stream and one graph pool (t2i_moe_gan._StepRunner), so
+    the replayed loop's peak allocated memory stays near the eager loop's instead of growing with the variant
+    count."""
+    import gc
+    B, n = 64, 8
+    peaks = {}
+    for mode in (False, True):
+        gc.collect()
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        _train(mode, tmp_path, acc=8, B=B, n=n)
+        peaks[mode] = (torch.cuda.max_memory_allocated() - base) / 2 ** 20
+    print(f"acc=8, B={B}: peak allocated above baseline: eager loop {peaks[False]:.0f} MiB, "
+          f"graph-replayed loop (3 variants) {peaks[True]:.0f} MiB")
+    assert peaks[True] <= 1.5 * peaks[False] + 64, peaks

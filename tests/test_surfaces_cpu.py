@@ -149,15 +149,17 @@ def test_resume_checkpoint_layout(tmp_path):
     path = os.path.join(tmp_path, "ck.pt")
     M.save_resume(path, G, D, epoch=3, step=40, lr_g=1e-4, lr_d=1e-4)
     ck = torch.load(path, weights_only=True)
-    # the reference's keys (:1484-1491) plus our end-of-epoch marker
-    assert set(ck) == {"generator", "discriminator", "optimizer_g", "optimizer_d", "epoch", "step", "epoch_complete"}
+    # exactly the reference's keys (:1484-1491)
+    assert set(ck) == {"generator", "discriminator", "optimizer_g", "optimizer_d", "epoch", "step"}
     G2, D2 = M.AuroraGenerator(seed=5), M.AuroraDiscriminator(seed=6)
     assert M.load_resume(path, G2, D2) == (3, 40)  # a mid-epoch checkpoint resumes that (0-based) epoch
-    # an end-of-epoch checkpoint resumes at the next epoch and continues the stored random streams
+    # an end-of-epoch checkpoint stores epoch + 1 as the reference's does (:1648), resumes at the next epoch and
+    # continues the stored random streams
     g = torch.Generator().manual_seed(11)
     torch.randn(5, generator=g)
     M.save_resume(path, G, D, epoch=3, step=40, lr_g=1e-4, lr_d=1e-4, epoch_complete=True,
                   generators={"shared": g})
+    assert torch.load(path, weights_only=True)["epoch"] == 4
     expect = torch.randn(4, generator=g)
     g2 = torch.Generator().manual_seed(0)
     assert M.load_resume(path, G2, D2, generators={"shared": g2, "absent": torch.Generator()}) == (4, 40)
@@ -166,6 +168,11 @@ def test_resume_checkpoint_layout(tmp_path):
         assert torch.equal(G2.state_dict()[k], v), k
     off, numel = G._store.offsets["mapping.0.weight"]
     assert torch.equal(G2._store.m[off:off + numel], G._store.m[off:off + numel]) and int(G2._store.step_dev[0]) == 2
+    # a round-3 file (0-based epoch + epoch_complete flag) still resumes at the next epoch
+    ck = torch.load(path, weights_only=True)
+    ck.update(epoch=3, epoch_complete=True)
+    torch.save(ck, path)
+    assert M.load_resume(path, G2, D2)[0] == 4
     # model-only checkpoints (sagemaker_train.py:297-301) and bare generator state dicts load too
     torch.save({"generator": G.state_dict(), "discriminator": D.state_dict()}, path)
     assert M.load_resume(path, G2, D2) == (0, 0)
