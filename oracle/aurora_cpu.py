@@ -308,11 +308,14 @@ def round_bf16_st(t):
 
 
 def discriminator(img, text, PD, rnd=None):
-    """``rnd`` (floor measurements only): applied to the image and to every effective weight."""
+    """``rnd`` (floor measurements only): applied to the image and to every effective weight; its optional ``act``
+    attribute to the two conv activations (the tensors a bf16 device stores between the layers)."""
     r = rnd or (lambda t: t)
-    h = F.leaky_relu(F.conv2d(r(img), r(wn(PD, "conv_layers.0.")), PD["conv_layers.0.bias"], stride=2, padding=1),
-                     0.2)
-    h = F.leaky_relu(F.conv2d(h, r(wn(PD, "conv_layers.2.")), PD["conv_layers.2.bias"], stride=2, padding=1), 0.2)
+    a = getattr(rnd, "act", None) or (lambda t: t)
+    h = a(F.leaky_relu(F.conv2d(r(img), r(wn(PD, "conv_layers.0.")), PD["conv_layers.0.bias"], stride=2, padding=1),
+                       0.2))
+    h = a(F.leaky_relu(F.conv2d(h, r(wn(PD, "conv_layers.2.")), PD["conv_layers.2.bias"], stride=2, padding=1),
+                       0.2))
     t = F.leaky_relu(F.linear(text, r(wn(PD, "text_projection.0.")), PD["text_projection.0.bias"]), 0.2)
     t = t[:, :, None, None].expand(-1, -1, h.shape[2], h.shape[3])  # :898-899
     out = F.conv2d(torch.cat([h, t], dim=1), r(wn(PD, "output_layer.0.")), PD["output_layer.0.bias"])

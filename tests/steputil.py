@@ -149,16 +149,64 @@ def bf16_r1_floor(PD, real, text):
     return rel_norm_diff(g_of(Pb, bf(real)), g_of(P0, real))
 
 
+class Rounder:
+    """Value rounding to bf16 precision (result kept in the input's dtype): round-to-nearest-even, or -- with a
+    ``seed`` -- nearest-even on a rescaled grid, x -> bf16(x * s) / s with a fixed non-power-of-two s per seed.
+    That is another realization of the same noise: the relative grid spacing, so the error distribution, is the
+    nearest-even one, while which values round which way is independent of realization 0; equal values still round
+    alike (as on the device, where an image's broadcast style, the repeated constant or a shared weight round once
+    for every token).  (Stochastic rounding was measured as a poor yardstick: drawing a direction per element
+    averages that coherent error away -- its floors came out 0.6x the nearest-even ones after the sqrt(2)
+    variance correction.)"""
+
+    def __init__(self, seed=None):
+        self.seed = seed
+        self.noise_scale = 1.0
+        self.s = 1.0 if seed is None else 2.0 ** ((seed % 7 + 1) / 8.0)  # in (1, 2): never a power of two
+
+    def __call__(self, x):
+        if self.seed is None:
+            return x.bfloat16().to(x.dtype)
+        xd = x.detach().double()
+        out = (xd * self.s).bfloat16().double() / self.s
+        # the rounding offset as a constant: x's autograd graph (the R1 double backward) passes through
+        return x + (out.to(x.dtype) - x.detach())
+
+    def st(self, t):
+        """Straight-through: the value rounded, the gradient passed unchanged (oracle.round_bf16_st's role)."""
+        return t + (self(t.detach()) - t.detach())
+
+    def d_round(self):
+        """The discriminator's rounding for oracle.train_step(d_round=...): image and effective weights
+        straight-through, the two conv activations rounded in value and gradient (the device's bf16 h0 / h1 and
+        their bf16 gradients g_a0 / g_a1, engine_d.py)."""
+        return _DRound(self)
+
+
+class _DRound:
+    def __init__(self, rounder):
+        self.rounder = rounder
+
+    def __call__(self, t):
+        return self.rounder.st(t)
+
+    def act(self, t):
+        return _RoundBoth.apply(t)
+
+
+_ROUNDER = [Rounder()]  # the rounding _RoundBoth applies (bf16_module_rounding sets it)
+
+
 class _RoundBoth(torch.autograd.Function):
     """bf16 rounding of a value and of the gradient flowing back through it."""
 
     @staticmethod
     def forward(ctx, x):
-        return x.bfloat16().float()
+        return _ROUNDER[0](x)
 
     @staticmethod
     def backward(ctx, g):
-        return g.bfloat16().float()
+        return _ROUNDER[0](g)
 
 
 class bf16_module_rounding:
@@ -173,10 +221,13 @@ class bf16_module_rounding:
     NAMES = ("modconv", "mtm", "attention_block", "expert_ffn", "conv_block", "mha", "sparse_moe")
     FUNCS = ("layer_norm", "gelu")  # torch.nn.functional, as the oracle calls them inside the blocks
 
-    def __init__(self, attention_internals=True):
+    def __init__(self, attention_internals=True, rounder=None):
         self.attention_internals = attention_internals
+        self.rounder = rounder or Rounder()
 
     def __enter__(self):
+        self.prev_rounder = _ROUNDER[0]
+        _ROUNDER[0] = self.rounder
         self.orig = {n: getattr(O, n) for n in self.NAMES}
         self.orig_f = {n: getattr(O.F, n) for n in self.FUNCS}
         inner = dict(self.orig)
@@ -199,6 +250,7 @@ class bf16_module_rounding:
             setattr(O, n, f)
         for n, f in self.orig_f.items():
             setattr(O.F, n, f)
+        _ROUNDER[0] = self.prev_rounder
         return False
 
 
@@ -241,11 +293,13 @@ class bf16_weights(dict):
     SUFFIXES = ("modulated_conv.weight", "skip_proj.weight", "proj_in.weight", "proj_out.weight",
                 "offset_net.0.weight", "self_attn.in_proj_weight", "self_attn.out_proj.weight")
 
+    rounder = None  # a Rounder (None: nearest-even, oracle.round_bf16_st)
+
     def __getitem__(self, n):
         v = dict.__getitem__(self, n)
         if (n.endswith(self.SUFFIXES) or (n.startswith("to_rgb_") and n.endswith(".weight")) or
                 (".experts." in n and n.endswith((".net.0.weight", ".net.2.weight")))):
-            return O.round_bf16_st(v)
+            return O.round_bf16_st(v) if self.rounder is None else self.rounder.st(v)
         return v
 
 

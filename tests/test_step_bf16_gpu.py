@@ -6,26 +6,26 @@ Bar, written per check below (SURVEY.md §8(c) asks 2e-2 on outputs and cosine >
   * losses, discriminator logits, generated images and routing probabilities: relative L2 error <= 2e-2;
   * gradients (clipped, as handed to AdamW): per model, the WHOLE gradient vector (all parameters concatenated)
     has cosine >= 0.999 with the oracle's, or -- where bf16 cannot reach that -- a relative error within 2.5x
-    the step's bf16 FLOOR: the same oracle step from the same point with the discriminator's operands and every
-    tensor the generator stores in bf16 (module outputs, LayerNorm outputs, expert hidden activations, attention
-    and MoE outputs; values and gradients) rounded to bf16 (steputil.bf16_module_rounding, bf16_weights).  Every
-    tensor keeps cosine >= 0.93 or a relative error within FLOOR_X x its own whole-step floor (measured worst:
-    0.94-0.96 on the offset heads and on experts that few tokens reach, whose error carries the per-image coherent
-    component described at the temperature check).  Measured: the discriminator reaches cosine 0.99999; the generator's floor alone is ~7 % (cosine
-    0.997), because its whole backward starts from the image gradient of a LeakyReLU discriminator -- rounding
-    only that discriminator's input image and weights already moves it by ~5 % (cosine 0.9989), and the R1 input
-    gradient by ~4 % (steputil.bf16_r1_floor) -- and the device's per-tensor error sits at a median 0.9-1.25x
-    that floor (max 3-11x, on experts that few tokens reach).  SURVEY §8(c)'s per-tensor 0.999 is therefore not
-    reachable in bf16 at all; per-tensor parity at 1e-3 is the fp32 mode's job (F7 / F8 / F10 in
+    the step's bf16 FLOOR: the same oracle step from the same point with the discriminator's operands and
+    activations and every tensor the generator stores in bf16 (module outputs, LayerNorm outputs, expert hidden
+    activations, attention and MoE outputs; values and gradients) rounded to bf16 (steputil.bf16_module_rounding,
+    bf16_weights, Rounder.d_round).  The floor of a tensor is the root-mean-square over FLOOR_RUNS realizations of
+    that rounding (nearest-even, and nearest-even on rescaled grids: the same error distribution, independent
+    patterns): one realization alone is a noisy yardstick -- between two realizations the per-tensor error ratio
+    was measured from 0.03x to 34x, which is what the round-3 single-floor ratios (max 8-22x) were measuring.
+    Every multi-element tensor keeps cosine >= COS_TENSOR or a relative error within FLOOR_X x its floor, and no
+    multi-element tensor's error exceeds RATIO_MAX x its floor (measured max 1.7-3.2x, median 0.7-1.3x).  The
+    generator's whole floor is ~5-10 % (cosine 0.995-0.999): its backward starts from the image gradient of a
+    LeakyReLU discriminator -- rounding only that discriminator's input image and weights already moves it by ~5 %
+    (cosine 0.9989), and the R1 input gradient by ~4 % (steputil.bf16_r1_floor).  SURVEY §8(c)'s per-tensor 0.999
+    is therefore not reachable in bf16 at all; per-tensor parity at 1e-3 is the fp32 mode's job (F7 / F8 / F10 in
     test_engine_gpu.py).  Each tensor's error and floor are printed;
   * the router temperatures (t2i_moe_gan.py:374-377; one scalar per block, a cancelling sum over tokens of
     -anneal/te * sum_e dL/dl * l) are checked on their parts: the kernel's fixed-order fold equals the fp64
-    restatement of its own inputs (1e-5 of the summed magnitudes); the per-token terms are within FLOOR_X x the
-    whole-step floor run's relative error; the block's sum has the reference's sign wherever the reference exceeds
-    FLOOR_X x the root-sum-square of the floor run's per-image errors.  The per-image sums (an image's tokens share
-    its style, text and discriminator gradient) and the block sum are printed with their floor ratios -- they are
-    not held to FLOOR_X (see the comment at the check).  The other single-element tensors (D's head bias / gain)
-    are held to relative error <= max(2e-2, FLOOR_X x floor);
+    restatement of its own inputs (1e-5 of the summed magnitudes); the per-token terms and (from MIN_IMAGES images
+    up) the per-image sums are within FLOOR_X x the floor's relative error; the block's sum has the reference's
+    sign wherever the reference exceeds FLOOR_X x the floor's noise on it.  The other single-element tensors (D's
+    head bias / gain) are held to relative error <= max(2e-2, FLOOR_X x floor);
   * top-k expert selection: the device picks a top-k of its own probabilities; its sets equal the oracle's own
     fp32 top-k wherever the oracle margin log(p_(k)/p_(k+1)) exceeds DELTA, DELTA bounds the measured drift of
     that margin, flips stay below 10 % of tokens; the oracle then replays the device's selection
@@ -50,8 +50,8 @@ import torch
 
 from goldens import T, load
 from oracle import aurora_cpu as O
-from steputil import (DeviceTempTap, OracleTempTap, ReplayedStep, bf16_module_rounding, bf16_r1_floor, bf16_weights,
-                      cosine, gpu_step, lrelu_slope_replay, make_inputs, nchw, oracle_clone, oracle_models,
+from steputil import (DeviceTempTap, OracleTempTap, ReplayedStep, Rounder, bf16_module_rounding, bf16_r1_floor,
+                      bf16_weights, cosine, gpu_step, lrelu_slope_replay, make_inputs, nchw, oracle_clone, oracle_models,
                       rel_norm_diff, routing_agreement, whole)
 
 pytestmark = pytest.mark.gpu
@@ -60,7 +60,10 @@ REL = 2e-2        # bf16 outputs, relative L2
 COS = 0.999       # whole-model gradient cosine ...
 FLOOR_X = 2.5     # ... or its relative error within FLOOR_X x the bf16 step floor (bf16_module_rounding)
 COS_DELTA = 0.98  # |g|-weighted whole-model AdamW delta cosine
-COS_TENSOR = 0.93  # every tensor's gradient direction, or within FLOOR_X x its own whole-step bf16 floor
+COS_TENSOR = 0.97  # every tensor's gradient direction, or within FLOOR_X x its own whole-step bf16 floor
+RATIO_MAX = 5.0   # no multi-element tensor's gradient error above RATIO_MAX x its whole-step floor
+FLOOR_RUNS = 3    # floor realizations: nearest-even + 2 rescaled-grid nearest-even roundings (steputil.Rounder)
+MIN_IMAGES = 4    # per-image temperature sums are held from this many images up
 DELTA = 0.25      # logit-space near-tie margin for the top-k comparison (bounds the measured bf16 drift)
 EFF_KL = 0.001 * 1e-5
 torch.set_num_threads(8)
@@ -173,14 +176,30 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
             O.train_step(PGf, PDf, optGf, optDf, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
                          kl_weight_eff=EFF_KL, routes_d=routes_d, routes_g=routes_g, d_round=O.round_bf16_st,
                          after_d_step=use_device_d)
-        # ... and the whole-step floor: also the generator's module outputs / their gradients in bf16
-        PGw, PDw, optGw, optDw, wgrads = oracle_clone(PG, PD, optG, optD, lr=lr)
-        pd_w_stepped = {}
-        with bf16_module_rounding(), OracleTempTap() as wtap, slopes.oracle():
-            O.train_step(bf16_weights(PGw), PDw, optGw, optDw, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
-                         kl_weight_eff=EFF_KL, routes_d=routes_d, routes_g=routes_g, d_round=O.round_bf16_st,
-                         after_d_step=lambda P: (pd_w_stepped.update({n: t.detach().clone() for n, t in P.items()}),
-                                                 use_device_d(P)))
+        # ... and the whole-step floor: also the generator's module outputs / their gradients and the
+        # discriminator's activations in bf16.  FLOOR_RUNS realizations: nearest-even rounding (realization 0, whose
+        # update is the delta floor below) and nearest-even on rescaled grids (steputil.Rounder: the same error
+        # distribution, an independent pattern); a tensor's floor is their root-mean-square -- one realization
+        # alone is a noisy yardstick for a tensor that few tokens reach (the floor-vs-floor spread is reported)
+        floors = []
+        for fi in range(FLOOR_RUNS):
+            rounder = Rounder() if fi == 0 else Rounder(seed=fi + 3 * si)
+            PGw, PDw, optGw, optDw, wgrads = oracle_clone(PG, PD, optG, optD, lr=lr)
+            pd_w_stepped = {}
+            PGw_r = bf16_weights(PGw)
+            PGw_r.rounder = rounder
+            with bf16_module_rounding(rounder=rounder), OracleTempTap() as wtap, slopes.oracle():
+                O.train_step(PGw_r, PDw, optGw, optDw, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
+                             kl_weight_eff=EFF_KL, routes_d=routes_d, routes_g=routes_g, d_round=rounder.d_round(),
+                             after_d_step=lambda P, keep=pd_w_stepped: (
+                                 keep.update({n: t.detach().clone() for n, t in P.items()}), use_device_d(P)))
+            floors.append(dict(grads=wgrads, tap=wtap, pd_stepped=pd_w_stepped, PG=PGw, PD=PDw,
+                               scale=rounder.noise_scale))
+        PGw, PDw, wgrads, wtap, pd_w_stepped = (floors[0][k] for k in ("PG", "PD", "grads", "tap", "pd_stepped"))
+
+        def ens(errs):
+            """Root-mean-square over the floor realizations of their (scaled) errors."""
+            return (sum((e * f["scale"]) ** 2 for e, f in zip(errs, floors)) / len(floors)) ** 0.5
         pd_stepped = {}
         with OracleTempTap() as rtap, slopes.oracle():
             ref = O.train_step(PG, PD, optG, optD, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
@@ -189,31 +208,34 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
                                                        use_device_d(P)))
         # ---- router temperatures (scalar cancelling sums) ----
         for blk, rec in sorted(dtap.results().items()):
-            t_dev, t_ref, t_flo = rec["terms"], rtap.terms(blk), wtap.terms(blk)
-            s_dev, s_ref, s_flo = float(t_dev.sum()), float(t_ref.sum()), float(t_flo.sum())
+            t_dev, t_ref = rec["terms"], rtap.terms(blk)
+            t_flos = [f["tap"].terms(blk) for f in floors]
+            s_dev, s_ref = float(t_dev.sum()), float(t_ref.sum())
             # (a) the kernel: its fixed-order fp32 fold equals the fp64 restatement of its own inputs
             scale = float(t_dev.abs().sum())
             report.append(f"step{si} {blk} temperature kernel {rec['kernel']:+.6e} vs fp64 restatement {s_dev:+.6e}")
             check(abs(rec["kernel"] - s_dev) <= 1e-5 * scale + 1e-12, report[-1])
             # (b) its per-token terms against the oracle's, within FLOOR_X x the whole-step bf16 floor's
-            e_tok, f_tok = rel_norm_diff(t_dev, t_ref), rel_norm_diff(t_flo, t_ref)
+            e_tok = rel_norm_diff(t_dev, t_ref)
+            f_tok = ens([rel_norm_diff(t, t_ref) for t in t_flos])
             # (c) the per-image sums (the image is where errors are coherent: one image's tokens share its style
-            # vector, text and discriminator gradient) within FLOOR_X x the floor run's, relative L2 over the images
+            # vector, text and discriminator gradient) within FLOOR_X x the floor's, relative L2 over the images
             nimg = len(real)
-            i_dev, i_ref, i_flo = (t.view(nimg, -1).sum(1) for t in (t_dev, t_ref, t_flo))
-            e_img, f_img = rel_norm_diff(i_dev, i_ref), rel_norm_diff(i_flo, i_ref)
-            # (d) the block's sum has the reference's sign wherever it stands above the noise the floor run's
-            # per-image errors put on a sum of independent images (their root-sum-square)
-            f_sum = float((i_flo - i_ref).norm())
+            i_dev, i_ref = (t.view(nimg, -1).sum(1) for t in (t_dev, t_ref))
+            i_flos = [t.view(nimg, -1).sum(1) for t in t_flos]
+            e_img = rel_norm_diff(i_dev, i_ref)
+            f_img = ens([rel_norm_diff(t, i_ref) for t in i_flos])
+            # (d) the noise the floor's per-image errors put on the block's sum of independent images
+            f_sum = ens([float((t - i_ref).norm()) for t in i_flos])
             report.append(f"step{si} {blk} temperature gradient {s_dev:+.4e} vs {s_ref:+.4e} (abs err "
                           f"{abs(s_dev - s_ref):.2e}, floor {f_sum:.2e}); per-image sums rel err {e_img:.2e} (floor "
-                          f"{f_img:.2e}); per-token terms rel err {e_tok:.2e} (floor {f_tok:.2e})")
+                          f"{f_img:.2e}, realizations " + " ".join(f"{rel_norm_diff(t, i_ref) * f['scale']:.2e}"
+                                                                    for t, f in zip(i_flos, floors)) +
+                          f"); per-token terms rel err {e_tok:.2e} (floor {f_tok:.2e})")
             check(e_tok <= FLOOR_X * f_tok, report[-1])
-            # (d) the block's sum has the reference's sign wherever the reference stands above FLOOR_X x that noise.
-            # The per-image sums and the block sum themselves are reported, not held to FLOOR_X: measured over
-            # runs they sit at 0.4-4.3x (per image) and 0.02-3.3x (sum) of the floor run's error, the excess is
-            # coherent within an image and moves with the reduction order alone (deterministic vs atomic mode),
-            # i.e. it is not modelled by rounding the oracle's stored tensors
+            # held from MIN_IMAGES images up: with B = 2 (the F8 fixture) this statistic is two numbers, reported
+            check(nimg < MIN_IMAGES or e_img <= FLOOR_X * f_img, report[-1])
+            # the block's sum has the reference's sign wherever the reference stands above FLOOR_X x that noise
             check(abs(s_ref) <= FLOOR_X * f_sum or s_dev * s_ref > 0, report[-1])
         # ---- routing ----
         for tag, dev_t, dev_p, ref_p in (("D", out["topi_d"], out["probs_d"], ref["probs_d"]),
@@ -268,7 +290,7 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
         report.append(f"step{si} r1_grad: rel err {r:.2e} (bf16 floor {floor:.2e}), cosine {c:.5f}")
         check(r <= max(REL, 1.5 * floor), report[-1])
         # ---- gradients (clipped) and AdamW deltas ----
-        worst, allg, alld, allf = [], [], [], []
+        worst, allg, alld, allf, calib = [], [], [], [], []
         for which, store, before, P, pbefore, gbuf, ss, max_norm in (
                 ("D", ts.ds, d_before, PD, pd_before, out["d_grad"], out["d_grad_sumsq"], 0.7),
                 ("G", ts.gs, g_before, PG, pg_before, out["g_grad"], out["g_grad_sumsq"], 0.8)):
@@ -281,9 +303,13 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
                 g = (gbuf[off:off + numel] * coef).cpu()
                 c, rn = cosine(g, rg), rel_norm_diff(g, rg)
                 fl = rel_norm_diff(fgrads[which][n], rg)
-                # whole-step floor of this tensor (D tensors: the D-operand floor run, which is the same rounding)
-                fw = rel_norm_diff(wgrads[which][n], rg) if wgrads[which].get(n) is not None else fl
-                worst.append((c, rn, fw, which + ":" + n))
+                # whole-step floor of this tensor over the realizations (fallback: the D-operand floor run)
+                fws = [rel_norm_diff(f["grads"][which][n], rg) for f in floors
+                       if f["grads"][which].get(n) is not None]
+                fw = ens(fws) if len(fws) == len(floors) else fl
+                if len(fws) == len(floors) and numel > 1 and fws[0] > 0:
+                    calib.extend(fws[j] * floors[j]["scale"] / fws[0] for j in range(1, len(floors)))
+                worst.append((c, rn, fw, which + ":" + n, numel))
                 # direction bar per tensor: cosine >= COS_TENSOR or within FLOOR_X x the tensor's whole-step floor.
                 # The router temperatures (single-element cancelling sums) are checked above on their per-token
                 # terms; the other single-element tensors (the discriminator head's bias and gain) by their
@@ -318,7 +344,7 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
             cd_min = min(COS_DELTA, 1.0 - FLOOR_X ** 2 * (1.0 - cdf))
             ref_v, order = whole(rgrads[which])
             floor_v, _ = whole(wgrads[which], order)
-            wf = rel_norm_diff(floor_v, ref_v)
+            wf = ens([rel_norm_diff(whole(f["grads"][which], order)[0], ref_v) for f in floors])
             report.append(f"step{si} {which}: whole-model gradient cosine {cg:.6f} rel {rg_:.2e} (bf16 step floor "
                           f"{wf:.2e}, cosine {cosine(floor_v, ref_v):.6f}); |g|-weighted delta cosine {cd:.6f} "
                           f"(floor {cdf:.6f})")
@@ -333,11 +359,18 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
             allf.clear()
         worst.sort()
         report.append(f"step{si}: worst gradient cosines " +
-                      ", ".join(f"{n} {c:.5f} rel {r:.2e} (floor {f:.2e})" for c, r, f, n in worst[:4]))
-        ratios = sorted(r / max(f, 1e-12) for c, r, f, n in worst if f > 0)
+                      ", ".join(f"{n} {c:.5f} rel {r:.2e} (floor {f:.2e})" for c, r, f, n, _ in worst[:4]))
+        ratios = sorted((r / max(f, 1e-12), n) for c, r, f, n, numel in worst
+                        if f > 0 and numel > 1 and not n.endswith("router.temperature"))
         if ratios:
-            report.append(f"step{si}: gradient error / bf16 floor: median {ratios[len(ratios) // 2]:.2f}, "
-                          f"max {ratios[-1]:.2f} over {len(ratios)} tensors")
+            report.append(f"step{si}: gradient error / bf16 floor: median {ratios[len(ratios) // 2][0]:.2f}, "
+                          f"max {ratios[-1][0]:.2f} over {len(ratios)} tensors; largest " +
+                          ", ".join(f"{n} {x:.2f}" for x, n in ratios[-4:]))
+            check(ratios[-1][0] <= RATIO_MAX, report[-1])
+        if calib:  # the same statistic between floor realizations: how noisy one realization is as a yardstick
+            calib.sort()
+            report.append(f"step{si}: floor realization / realization 0 (calibration): median "
+                          f"{calib[len(calib) // 2]:.2f}, max {calib[-1]:.2f}, min {calib[0]:.2f} over {len(calib)}")
         _sync_oracle(ts, PG, PD, optG, optD)
     print("\n".join(report))
     if fails:
