@@ -240,6 +240,20 @@ int mg_im2col_4x4s2(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t
    discriminator's first conv (image gradient of R1, t2i_moe_gan.py:1281-1286, and the G phase). */
 int mg_col2im_4x4s2(int in_dtype, const void* Y, int64_t ldy, int B, int OH, int OW, int C, int out_dtype, void* out, int64_t ldo, void* stream);
 
+/* The discriminator's first conv (conv_layers.0: 3 -> 128, 4x4 / s2 / p1, t2i_moe_gan.py:874-880) as direct MFMA
+   kernels for the bf16 step (replace mg_im2col_4x4s2 + mg_gemm and the dgrad GEMM + mg_col2im_4x4s2 there).
+   w0p: the packed bf16 weight [128][48] (k = tap*3 + c); x: image (MG_F32 or MG_BF16) with element strides
+   sb / sh / sw / sc, B x H x W, 3 channels read; out / aux / g: NHWC bf16 [B, H/2, W/2, 128].
+   mg_d0_fwd: aux == NULL -> out = LeakyReLU(conv(x) + bias) (h0, :880); aux != NULL -> out = conv(x) *
+   LeakyReLU'(aux) (the R1 double backward's forward-mode pass through the layer, :1282-1286).
+   mg_d0_wgrad: dw [128][48] fp32 (GEMM layout) += sum over output pixels of g[p][o] * patch[p][tap*3+c]; fixed
+   order (per-block partials in the stream's workspace, folded in block order).
+   mg_d0_dgrad: out[b, y, x, c] (pitch ldo, c < 3 written; MG_F32 or MG_BF16) = d/d x of sum g * conv(x):
+   the image gradient (R1 :1282, the G phase :1379-1382); OW <= 64, H a multiple of 4. */
+int mg_d0_fwd(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H, int W, const void* w0p, const float* bias, const void* aux, void* out, void* stream);
+int mg_d0_wgrad(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H, int W, const void* g, float* dw, void* stream);
+int mg_d0_dgrad(const void* g, int B, int OH, int OW, const void* w0p, int out_dtype, void* out, int64_t ldo, void* stream);
+
 /* Discriminator output_layer, image channels: out[b,o] = sum h1[b,o+tap,c] W2[c,tap] (t2i_moe_gan.py:885-907). */
 int mg_disc_head_fwd(int dtype, const void* h1, const float* W2, int B, int Hf, int Cf, float* out, void* stream);
 

@@ -18,6 +18,8 @@ m0 = LReLU'(a0), m1 = LReLU'(a1) (piecewise constant, zero second derivative):
     dW1  += wgrad1(x=m0 C0 u, dy=m1 Gh1);   dW2[:256] += head_wgrad(x=v1, dy=ones)
 All weights are weight-normed (g * v / ||v||); gradients flow back to g and v.
 """
+import os
+
 import torch
 
 from . import _lib as L
@@ -32,6 +34,8 @@ class DiscriminatorEngine:
     def __init__(self, store, cdt=torch.float32):
         self.st = store
         self.cdt = cdt
+        # conv_layers.0 on the direct MFMA kernels (mg_d0_*) in the bf16 step; MOEGAN_D0_DIRECT=0: im2col + GEMMs
+        self.direct0 = cdt == torch.bfloat16 and os.environ.get("MOEGAN_D0_DIRECT", "1") == "1"
         self.dev = store.device
         self.ones_cache = {}
         # weight gradients on a side stream, overlapping the data-gradient chain (joined before finish_grads)
@@ -82,8 +86,12 @@ class DiscriminatorEngine:
         else:
             ld = layout[1]
             strides = (H * H * ld, H * ld, ld, 1)
-        cols = ops.im2col_4x4s2(img, strides, B, H, H, 3, 48, self.cdt)  # [B*(H/2)^2, 48]
-        h0 = ops.linear(cols, self.W0p, bias=self.P("conv_layers.0.bias"), act=LRELU).view(B, H // 2, H // 2, 128)
+        if self.direct0:  # direct MFMA conv (mg_d0_fwd): no im2col matrix; the backward re-gathers from the image
+            cols = (img, strides)
+            h0 = ops.d0_fwd(img, strides, B, H, H, self.W0p, bias=self.P("conv_layers.0.bias"))
+        else:
+            cols = ops.im2col_4x4s2(img, strides, B, H, H, 3, 48, self.cdt)  # [B*(H/2)^2, 48]
+            h0 = ops.linear(cols, self.W0p, bias=self.P("conv_layers.0.bias"), act=LRELU).view(B, H // 2, H // 2, 128)
         h1 = ops.conv2d(h0, self.W1p, 256, 4, 4, 2, 1, ep=E_(bias=self.P("conv_layers.2.bias"), act=LRELU),
                         tag="d_conv1")
         return cols, h0, h1
@@ -110,12 +118,27 @@ class DiscriminatorEngine:
         ops.dgrad_s2(g_a1, self.W1cls, 128, g_a0, ep=E_(act=MUL_LRELU_GRAD, aux=f["h0"], ld_aux=128))
         if want_params:
             dW0, gb0 = self.dW["conv_layers.0."].view(128, 48), self.G("conv_layers.0.bias")
-            self.side.run(lambda: (ops.gemm(g_a0.view(-1, 128), f["cols"], 128, 48, g_a0.numel() // 128, a_kc=False,
-                                            b_kc=False, out=dW0, ep=E_(atomic=1), splits=0),
+            self.side.run(lambda: (self._d0_wgrad(f["cols"], g_a0, dW0),
                                    ops.colsum(g_a0.view(-1, 128), gb0, defer=True)), g_a0, f["cols"])
         if g_input is not None:
-            ops.dgrad_s2_small(g_a0, self.W0p, 3, g_input)
+            self._d0_dgrad(g_a0, g_input)
         return g_a1, g_a0
+
+    def _d0_wgrad(self, cols, g, dW0):
+        """dW0 [128, 48] += conv_layers.0 weight gradient; ``cols`` is the im2col matrix, or (image, strides)."""
+        if self.direct0:
+            img, strides = cols
+            B, OH, OW, _ = g.shape
+            ops.d0_wgrad(img, strides, B, 2 * OH, 2 * OW, g, dW0)
+        else:
+            ops.gemm(g.view(-1, 128), cols, 128, 48, g.numel() // 128, a_kc=False, b_kc=False, out=dW0,
+                     ep=E_(atomic=1), splits=0)
+
+    def _d0_dgrad(self, g, out):
+        if self.direct0:
+            ops.d0_dgrad(g, self.W0p, out)
+        else:
+            ops.dgrad_s2_small(g, self.W0p, 3, out)
 
     def _head_bwd(self, g, g_bstride, h1, B, Hf, want_w, wgrad_input=None):
         """g_a1 = lrelu'(a1) * (G @ W2img^T) and (optionally) dW2img += X^T G, G the tap-expanded gradient;
@@ -176,21 +199,25 @@ class DiscriminatorEngine:
         gA0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
         ops.dgrad_s2(gA1, self.W1cls, 128, gA0, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
         gx = ops.zeros(B, Hr, Hr, 4, device=dev)
-        ops.dgrad_s2_small(gA0, self.W0p, 3, gx)  # d sum(real_pred) / d real  (NHWC, channel-padded)
+        self._d0_dgrad(gA0, gx)  # d sum(real_pred) / d real  (NHWC, channel-padded)
         r1 = torch.zeros(1, device=dev)
         u = torch.empty(B, Hr, Hr, 4, device=dev, dtype=self.cdt)
         ops.r1(gx, B, r1_gamma, r1, u)
-        cols_u = ops.im2col_4x4s2(u, (Hr * Hr * 4, Hr * 4, 4, 1), B, Hr, Hr, 3, 48, self.cdt)
-        m0v0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
-        ops.gemm(cols_u, self.W0p, cols_u.shape[0], 128, 48, out=m0v0.view(-1, 128),
-                 ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
+        u_strides = (Hr * Hr * 4, Hr * 4, 4, 1)
+        if self.direct0:
+            cols_u = (u, u_strides)
+            m0v0 = ops.d0_fwd(u, u_strides, B, Hr, Hr, self.W0p, aux=fr["h0"])
+        else:
+            cols_u = ops.im2col_4x4s2(u, u_strides, B, Hr, Hr, 3, 48, self.cdt)
+            m0v0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
+            ops.gemm(cols_u, self.W0p, cols_u.shape[0], 128, 48, out=m0v0.view(-1, 128),
+                     ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
         m1v1 = ops.conv2d(m0v0, self.W1p, 256, 4, 4, 2, 1, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h1"], ld_aux=256))
         dW0, dW1 = self.dW["conv_layers.0."].view(128, 48), self.dW["conv_layers.2."]
         dW2img = self.dW["output_layer.0."].view(384, 16)[:256]
 
         def r1_wgrads():
-            ops.gemm(gA0.view(-1, 128), cols_u, 128, 48, gA0.numel() // 128, a_kc=False, b_kc=False, out=dW0,
-                     ep=E_(atomic=1), splits=0)
+            self._d0_wgrad(cols_u, gA0, dW0)
             ops.conv2d_wgrad(gA1, m0v0, 256, 4, 4, 2, 1, dW1)
             ops.gemm(m1v1.view(-1, 256), G1, 256, 16, B * Hf * Hf, a_kc=False, b_kc=False, out=dW2img,
                      ep=E_(atomic=1), splits=0)

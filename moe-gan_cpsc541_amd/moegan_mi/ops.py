@@ -772,6 +772,29 @@ def upsample2x_bwd(gout, gx, accumulate=0):
 # ---------------------------------------------------------------------------
 # discriminator / losses
 # ---------------------------------------------------------------------------
+def d0_fwd(x, strides, B, H, W, w0p, bias=None, aux=None):
+    """Discriminator conv_layers.0 (3 -> 128, 4x4/s2/p1) direct (bf16): h0 = LeakyReLU(conv(x) + bias), or with
+    ``aux`` = h0 the R1 forward-mode pass conv(x) * LeakyReLU'(h0).  x: image with element strides ``strides``."""
+    out = torch.empty(B, H // 2, W // 2, 128, device=x.device, dtype=torch.bfloat16)
+    sb, sh, sw, sc = strides
+    call("mg_d0_fwd", dt(x), ptr(x), sb, sh, sw, sc, B, H, W, ptr(w0p), ptr(bias), ptr(aux), ptr(out), S())
+    return out
+
+
+def d0_wgrad(x, strides, B, H, W, g, dw):
+    """dw [128, 48] fp32 (GEMM layout) += weight gradient of conv_layers.0 for output gradient g [B, H/2, W/2, 128]."""
+    sb, sh, sw, sc = strides
+    call("mg_d0_wgrad", dt(x), ptr(x), sb, sh, sw, sc, B, H, W, ptr(g), ptr(dw), S())
+    return dw
+
+
+def d0_dgrad(g, w0p, out):
+    """Image gradient of conv_layers.0: g [B, OH, OW, 128] bf16 -> out [B, 2OH, 2OW, ldo] (channels < 3)."""
+    B, OH, OW, _ = g.shape
+    call("mg_d0_dgrad", ptr(g), B, OH, OW, ptr(w0p), dt(out), ptr(out), out.shape[-1], S())
+    return out
+
+
 def im2col_4x4s2(x, strides, B, H, W, C, Kp, dtype):
     out = torch.empty(B * (H // 2) * (W // 2), Kp, device=x.device, dtype=dtype)
     sb, sh, sw, sc = strides

@@ -45,6 +45,7 @@ FAMILIES = {
     "router_aux": ("hbm", ("mg_router_bwd", "mg_moe_gate_grad", "mg_moe_token_grad", "mg_router_feat_grad",
                            "mg_router_param_bwd", "mg_moe_dispatch", "mg_router_kl")),
     "im2col_col2im": ("hbm", ("mg_im2col_4x4s2", "mg_col2im_4x4s2")),
+    "d_conv0": ("hbm", ("mg_d0_fwd", "mg_d0_wgrad", "mg_d0_dgrad")),
     "elementwise": ("hbm", ("mg_cast", "mg_copy2d", "mg_lrelu_mask_mul", "mg_upsample2x_fwd", "mg_upsample2x_bwd",
                             "mg_const_fwd", "mg_gated_axpy", "mg_select_if", "mg_zero_if", "mg_clip_patches")),
     "disc_head": ("hbm", ("mg_disc_head_fwd", "mg_disc_head_gmat", "mg_disc_head_sum", "mg_disc_head_bwd_data",
@@ -81,6 +82,7 @@ KERNELS = [
     (r"k_router_bwd|k_fold_partials|k_gate_grad|k_token_grad|k_router_feat_grad|k_feat_grad_fin|k_router_param_bwd|"
      r"k_disp_|k_router_kl", "router_aux"),
     (r"k_im2col|k_col2im", "im2col_col2im"),
+    (r"k_d0_", "d_conv0"),
     (r"k_cast|k_copy2d|k_mask_mul|k_up2|k_const_fwd|k_gated_axpy|k_select_if|k_zero_if|k_clip_patches",
      "elementwise"),
     (r"k_head_|k_d_text", "disc_head"),
@@ -236,6 +238,13 @@ def work(name, a):
     if name == "mg_col2im_4x4s2":
         B, OH, OW, C = a["B"], a["OH"], a["OW"], a["C"]
         return B * OH * OW * 16 * C * ELT[a["in_dtype"]] + B * 4 * OH * OW * C * ELT[a["out_dtype"]]
+    if name in ("mg_d0_fwd", "mg_d0_wgrad"):  # image read + the 128-channel bf16 map (out / aux / gradient)
+        B, H, W = a["B"], a["H"], a["W"]
+        maps = 1 + (1 if name == "mg_d0_fwd" and a["aux"] else 0)
+        return B * H * W * 3 * ELT[a["in_dtype"]] + maps * B * (H // 2) * (W // 2) * 128 * 2
+    if name == "mg_d0_dgrad":
+        B, OH, OW = a["B"], a["OH"], a["OW"]
+        return B * OH * OW * 128 * 2 + B * 4 * OH * OW * 3 * ELT[a["out_dtype"]]
     if name == "mg_cast":
         return a["n"] * (ELT[a["in_dtype"]] + ELT[a["out_dtype"]])
     if name == "mg_copy2d":

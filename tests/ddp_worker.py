@@ -4,7 +4,9 @@ import os
 import sys
 
 
-def run(rank, world, port, out_dir, B, E, R=16):
+def run(rank, world, port, out_dir, B, E, R=16, topk=None, dtype="fp32", acc=1):
+    """``acc`` > 1: one gradient-accumulation window of ``acc`` batches (seeds 7, 8, ...; t2i_moe_gan.py:1272,
+    :1329, :1353, :1413), the optimizers stepping after the last; gradients of the window are all-reduced once."""
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
     for p in (here, repo, os.path.join(repo, "moe-gan_cpsc541_amd")):
@@ -17,20 +19,30 @@ def run(rank, world, port, out_dir, B, E, R=16):
     from steputil import gpu_step, make_inputs
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        real, text, z, eps_d, eps_g, perm = make_inputs(B * world, E, seed=7, res=64 if R == 16 else R)
+        from moegan_mi import ops
+        if dtype != "fp32":
+            ops.set_deterministic(True)  # the same device numbers as the single-process reference run
         sl = slice(rank * B, (rank + 1) * B)
-        local_perm = torch.randperm(B, generator=torch.Generator().manual_seed(100 + rank))
-        ts = gpu_step(E, None, "fp32", "cuda:0", max_res=R)
+        ts = gpu_step(E, topk, dtype, "cuda:0", max_res=R)
         ts.pg, ts.world = dist.group.WORLD, world
         cu = lambda t: t.to("cuda:0")  # noqa: E731
-        out = ts.step(cu(real[sl].contiguous()), cu(text[sl].contiguous()), cu(z[sl].contiguous()),
-                      [tuple(map(cu, e)) for e in eps_d], [tuple(map(cu, e)) for e in eps_g], cu(local_perm.int()),
-                      anneal=3.0, eff_kl_weight=0.001 * 1e-5)
+        g0, d0 = ts.gs.data.cpu().clone(), ts.ds.data.cpu().clone()
+        perms = []
+        for i in range(acc):
+            real, text, z, eps_d, eps_g, perm = make_inputs(B * world, E, seed=7 + i, res=64 if R == 16 else R)
+            local_perm = torch.randperm(B, generator=torch.Generator().manual_seed(100 + rank + 10 * i))
+            perms.append(local_perm)
+            out = ts.step(cu(real[sl].contiguous()), cu(text[sl].contiguous()), cu(z[sl].contiguous()),
+                          [tuple(map(cu, e)) for e in eps_d], [tuple(map(cu, e)) for e in eps_g],
+                          cu(local_perm.int()), anneal=3.0, eff_kl_weight=0.001 * 1e-5, acc=acc,
+                          zero_grads=i == 0, step_optim=i == acc - 1)
         torch.cuda.synchronize()
         res = {k: out[k].detach().cpu().clone() for k in ("d_losses", "r1", "g_gan", "balance", "d_grad", "g_grad",
                                                           "d_grad_sumsq", "g_grad_sumsq", "flags")}
         res["g_data"], res["d_data"] = ts.gs.data.cpu().clone(), ts.ds.data.cpu().clone()
-        res["local_perm"] = local_perm
+        res["g_before"], res["d_before"] = g0, d0
+        res["local_perm"] = perms[0]
+        res["local_perms"] = torch.stack(perms)
         torch.save(res, os.path.join(out_dir, f"rank{rank}.pt"))
     finally:
         dist.destroy_process_group()

@@ -69,6 +69,65 @@ def test_two_rank_trainstep_matches_single_process(tmp_path, R):
         assert rel_norm_diff(res[0][key], ref) <= 1e-5, key
 
 
+def test_two_rank_bf16_topk_accumulation_window(tmp_path):
+    """C3's routing (E=8 top-2) in the benchmarked bf16 mode under data parallelism with a gradient-accumulation
+    window of two batches (reference default gradient_accumulation_steps=8, t2i_moe_gan.py:1043; accumulation
+    :1272, :1329, :1353, :1413): 2 gloo ranks x B=2 per batch against one process stepping the whole batches.
+    Both sides run the deterministic mode.  Checked after the window: the all-reduced window gradients (the D
+    gradient includes the reference's G-phase leak of the first batch, :1272 vs :1407) against the single
+    process's at the bf16 bars (cosine >= 0.999 per model), every rank's updated parameters bit-identical, and
+    the AdamW update's |g|-weighted cosine with the single process's >= 0.99."""
+    import torch.multiprocessing as mp
+    from ddp_worker import run
+    world, B, E, k, acc = 2, 2, 8, 2, 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=run, args=(r, world, port, str(tmp_path), B, E, 16, k, "bf16", acc))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0, p.exitcode
+    res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    from moegan_mi import ops
+    ops.set_deterministic(True)
+    try:
+        ts = gpu_step(E, k, "bf16", "cuda")
+        cu = lambda t: t.to("cuda")  # noqa: E731
+        for i in range(acc):
+            real, text, z, eps_d, eps_g, _ = make_inputs(B * world, E, seed=7 + i)
+            perm = torch.cat([res[r]["local_perms"][i] + r * B for r in range(world)])
+            out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d],
+                          [tuple(map(cu, e)) for e in eps_g], cu(perm.int()), anneal=3.0, eff_kl_weight=0.001 * 1e-5,
+                          acc=acc, zero_grads=i == 0, step_optim=i == acc - 1)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_deterministic(False)
+    for r in range(world):
+        assert int(res[r]["flags"][0]) == 0
+        assert abs(float(res[r]["balance"][0]) - float(out["balance"][0])) <= 2e-2 * float(out["balance"][0])
+    for key, ref in (("d_grad", out["d_grad"]), ("g_grad", out["g_grad"])):
+        got = res[0][key]
+        c = cosine(got, ref)
+        print(f"{key}: window gradient cosine {c:.6f}, rel {rel_norm_diff(got, ref):.2e}")
+        assert c >= 0.999, (key, c)
+    for key in ("d_data", "g_data"):
+        assert torch.equal(res[0][key], res[1][key]), key
+    for key, before, store, g in (("d_data", "d_before", ts.ds, out["d_grad"]), ("g_data", "g_before", ts.gs,
+                                                                                   out["g_grad"])):
+        n = store.n_opt
+        w = g[:n].abs().cpu()
+        d_dp = (res[0][key][:n] - res[0][before][:n]) * w
+        d_sp = (store.data[:n].cpu() - res[0][before][:n]) * w
+        c = cosine(d_dp, d_sp)
+        print(f"{key}: |g|-weighted update cosine {c:.6f}")
+        assert c >= 0.99, (key, c)
+
+
 def test_bench_two_rank_graph_replay():
     """bench.py's N>1 path (captured hipGraph segments + eager all-reduces) with 2 gloo ranks on one GPU."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",

@@ -123,3 +123,34 @@ def test_train_aurora_gan_runs(tmp_path):
     assert len(seen) == 2 and all(np.isfinite(v) for m in seen for v in m.values())
     assert G._store.step_count == 4 and D._store.step_count == 4
     assert torch.isfinite(G.flat).all() and torch.isfinite(D.flat).all()
+
+
+def test_validate_losses_vs_oracle():
+    """The validation pass of train_aurora_gan (_validate, reference :1519-1639: eval-mode generator -- router mean
+    weights, hard top-1, KL 0 -- then D on real / fake / mismatched text, the D loss and the generator loss with
+    kl_weight) on one batch, fp32, against the oracle's eval-mode composition of the same pinned functions
+    (oracle.generator(training=False), discriminator, d_loss, g_loss) with the same z and permutation draws."""
+    M = _M()
+    from moegan_mi.layout import discriminator_shapes, generator_shapes
+    G, D = _gen(M), _disc(M)
+    g = torch.Generator().manual_seed(11)
+    B = 3
+    real = torch.rand(B, 3, 64, 64, generator=g) * 2 - 1
+    text = torch.randn(B, 512, generator=g)
+    vm = M._validate(G, D, [(real, text)], M.AuroraGANLoss(DEV), 3.0, 1e-3, DEV,
+                     gen=torch.Generator(device=DEV).manual_seed(5))
+    gen = torch.Generator(device=DEV).manual_seed(5)  # the same draws, in _validate's order
+    z = torch.randn(B, 512, device=DEV, generator=gen).cpu()
+    perm = torch.randperm(B, device=DEV, generator=gen).cpu()
+    PG = {k: torch.from_numpy(v) for k, v in fill_state(generator_shapes(4), 0).items()}
+    PD = {k: torch.from_numpy(v) for k, v in fill_state(discriminator_shapes(), 50).items()}
+    with torch.no_grad():
+        img16, img8, kl, _ = O.generator(z, text, PG, None, False, 3.0, 0.7)
+        rp, fp, mp = (O.discriminator(real, text, PD), O.discriminator(img16, text, PD),
+                      O.discriminator(real, text[perm], PD))
+        d_ref = float(O.d_loss(rp, fp, mp))
+        g_ref = float(O.g_loss(fp) + 1e-3 * kl)
+    assert float(kl) == 0.0
+    assert abs(vm["val_d_loss"] - d_ref) <= 1e-4 * abs(d_ref), (vm, d_ref)
+    assert abs(vm["val_g_loss"] - g_ref) <= 1e-4 * abs(g_ref), (vm, g_ref)
+    assert G.training and D.training  # _validate restores train mode (:1638-1639)
