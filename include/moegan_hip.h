@@ -248,8 +248,11 @@ int mg_col2im_4x4s2(int in_dtype, const void* Y, int64_t ldy, int B, int OH, int
    LeakyReLU'(aux) (the R1 double backward's forward-mode pass through the layer, :1282-1286).
    mg_d0_wgrad: dw [128][48] fp32 (GEMM layout) += sum over output pixels of g[p][o] * patch[p][tap*3+c]; fixed
    order (per-block partials in the stream's workspace, folded in block order).
-   mg_d0_dgrad: out[b, y, x, c] (pitch ldo, c < 3 written; MG_F32 or MG_BF16) = d/d x of sum g * conv(x):
-   the image gradient (R1 :1282, the G phase :1379-1382); OW <= 64, H a multiple of 4. */
+   mg_d0_dgrad: out[b, y, x, c] (pitch ldo, c < 3; MG_F32 or MG_BF16) = d/d x of sum g * conv(x): the image
+   gradient (R1 :1282, the G phase :1379-1382); OW <= 64, H a multiple of 4.  When ldo is one 16-B vector
+   (4 fp32 / 8 bf16) the padding channels 3 .. ldo-1 are written as 0, otherwise they are left untouched.
+   The forward and the weight gradient take fp32 planar images (NCHW, sw = 1) or bf16 interleaved ones (NHWC,
+   sc = 1, pixel pitch sw a multiple of 4); W / 2 a power of two in [4, 64]. */
 int mg_d0_fwd(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H, int W, const void* w0p, const float* bias, const void* aux, void* out, void* stream);
 int mg_d0_wgrad(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H, int W, const void* g, float* dw, void* stream);
 int mg_d0_dgrad(const void* g, int B, int OH, int OW, const void* w0p, int out_dtype, void* out, int64_t ldo, void* stream);

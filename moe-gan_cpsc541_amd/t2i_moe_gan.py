@@ -386,7 +386,8 @@ class _StepRunner:
             return self.ts.step(real, text, z, eps_d, eps_g, perm, **kw)
         ekey = (kw["anneal"], kw["lr_g"], kw["lr_d"], kw["eff_kl_weight"], kw.get("acc", 1))
         if ekey != self.epoch_key:
-            self.graphs.clear()  # the previous epoch's graphs (and their memory pools) go
+            self.graphs.clear()  # the previous epoch's graphs go, and with the last of them their memory pool
+            self.pool = None  # (a released pool cannot be captured into again: the next capture makes a new one)
             self.epoch_key = ekey
         key = (kw.get("zero_grads", True), kw.get("step_optim", True))
         ent = self.graphs.get(key)

@@ -45,6 +45,12 @@ cols = ops.im2col_4x4s2(x, xs, B, H, H, 3, 48, torch.bfloat16)
 cases = {
     "d0_fwd real (direct)": lambda: ops.d0_fwd(x, xs, B, H, H, w0p, bias=bias),
     "d0_fwd real (im2col+gemm)": old_fwd,
+    "d0_fwd real (direct, staged store)": lambda: (L.call("mg_set_tuning", 13, 2),
+                                                  ops.d0_fwd(x, xs, B, H, H, w0p, bias=bias),
+                                                  L.call("mg_set_tuning", 13, 0)),
+    "d0_fwd r1 u (direct, staged store)": lambda: (L.call("mg_set_tuning", 13, 2),
+                                                  ops.d0_fwd(u, us, B, H, H, w0p, aux=h0),
+                                                  L.call("mg_set_tuning", 13, 0)),
     "d0_fwd r1 u (direct)": lambda: ops.d0_fwd(u, us, B, H, H, w0p, aux=h0),
     "d0_fwd r1 u (im2col+gemm)": old_fwd_u,
     "d0_wgrad real (direct)": lambda: ops.d0_wgrad(x, xs, B, H, H, gy, dw),
