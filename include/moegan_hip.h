@@ -209,6 +209,14 @@ int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const int32_t* r
    Hd % 64 == 0; grid = max_tiles blocks. */
 int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off, int max_tiles, const void* X, int64_t ldx, const int32_t* x_idx, int x_idx_div, const void* W1, const float* b1, const void* W2, const float* b2, void* pre, void* hid, void* Y, void* stream);
 
+/* Fused expert FFN backward, first half (t2i_moe_gan.py:257-263 backward, per dispatch group g): for the rows r of
+   each group, gP[r] = (gG[r] W2_g) * GELU'(pre[r]) ([total_rows, Hd] bf16, written for the weight gradient of W1),
+   gX[r] = gP[r] W1_g ([total_rows, C] bf16), and gb1[g] (fp32 [ngroups, Hd], accumulated; NULL skips it) +=
+   sum over the group's rows of gP (the bf16 values), folded in a fixed order.  gP and gX are bit-identical to
+   mg_gemm_grouped (gG x W2 with the GELU' epilogue, then gP x W1).  bf16, C = 128, Hd % 64 == 0; W1 [G, Hd, C],
+   W2 [G, C, Hd]; grid = max_tiles blocks of 128 rows. */
+int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1, const void* W2, void* gP, void* gX, float* gb1, void* stream);
+
 /* ---- op-level entry points ---- */
 
 /* CLIP image-tower input (CLIPLoss.forward t2i_moe_gan.py:90-94 + the ViT conv1 patchify): clamp [-1,1], bilinear

@@ -204,6 +204,244 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Fused expert FFN backward, first half (t2i_moe_gan.py:257-263 backward): per 128-row tile of one expert's
+// dispatched rows, walking the hidden dimension in 64-unit chunks,
+//   GEMM1  gH = gG W2_e[:, chunk]        (K = C; W2 chunk staged as an MC image [c][h], transposed reads)
+//          gP = gH * GELU'(Pre)          (the same fp32 product and bf16 rounding as mg_gemm_grouped's epilogue)
+//          gP -> HBM (the weight gradient of W1 reads it), -> LDS (A of GEMM2), column sums -> gb1 partial row
+//   GEMM2  gX += gP_chunk W1_e[chunk, :] (K = 64 per chunk, the [128 x C] accumulator in registers)
+// so gP is written once and never re-read for gX or gb1 (the unfused path wrote gP, read it for gX, for the bias
+// column sums and for gW1).  GEMM1 / GEMM2 run the MFMA sequence of the two grouped GEMMs they replace, in the
+// same k order: gP and gX are bit-identical to that path; gb1 sums the rows in a fixed order (per-tile partial
+// rows folded per expert in tile order).  LDS: gG tile 32 KiB + W2 chunk 16 + W1 chunk 16 + gP chunk 16 = 80 KiB,
+// two blocks per CU.  bf16, C = 128.
+template <int C>
+struct FfnBwdSmem {
+  bf16_t gs[FBM * C];    // gG tile, KC image (A of GEMM1); the bf16 gX tile at the end
+  bf16_t w2[C * FHC];    // W2_e[:, chunk] as an MC image [c][h] (k-rows c), pitch FHC; column sums reuse it
+  bf16_t w1[FHC * C];    // W1_e[chunk, :] as an MC image [h][c] (k-rows h), pitch C
+  bf16_t hs[FBM * FHC];  // gP chunk, KC image (A of GEMM2)
+};
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+MG_DEV int mswz(int k) { return ((k >> 3) & 1) << 4; }
+MG_DEV int mci(int k, int c, int ld) { return k * ld + (c ^ mswz(k)); }
+// lane (g = lane>>4, i = lane&15) gets column c0+i of k-rows kr0+8g .. kr0+8g+7
+MG_DEV bf16x8_t mc_frag(const bf16_t* img, int ld, int kr0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int k = kr0 + 8 * g + q;
+  auto base = (__attribute__((address_space(3))) char*)(img);
+  const int col = (c0 ^ mswz(k)) + 4 * p;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + (k * ld + col) * 2));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + ((k + 4) * ld + col) * 2));
+  u16x8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+template <int C>
+__device__ __forceinline__ void ffn_bwd_body(
+    const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
+    const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part) {
+  __shared__ FfnBwdSmem<C> sm;
+  const int t = blockIdx.x;
+  int g = -1;
+  for (int i = 0; i < ngroups; ++i)
+    if (t >= tile_off[i] && t < tile_off[i + 1]) {
+      g = i;
+      break;
+    }
+  if (g < 0) return;  // past the last tile (the grid is an upper bound)
+  const int r0 = row_off[g] + (t - tile_off[g]) * FBM, rend = row_off[g + 1];
+  const int nrows = rend - r0;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const bf16_t* W1g = W1 + (int64_t)g * Hd * C;
+  const bf16_t* W2g = W2 + (int64_t)g * C * Hd;
+  const bf16_t* preb = Pre + (int64_t)r0 * Hd;
+  bf16_t* gpb = gP + (int64_t)r0 * Hd;
+  float* partb = part + (int64_t)t * Hd;
+
+  // ---- gG tile -> LDS (rows past the group read as zeros) ----
+  constexpr int XV = FBM * C / 8 / FT;
+#pragma unroll
+  for (int j = 0; j < XV; ++j) {
+    const int v = tid + j * FT, r = v / (C / 8), k = (v % (C / 8)) * 8;
+    u16x8_t val = u16x8_t(0);
+    if (r < nrows) val = *reinterpret_cast<const u16x8_t*>(gG + (int64_t)(r0 + r) * C + k);
+    *reinterpret_cast<u16x8_t*>(sm.gs + kci<FBM>(r, k)) = val;
+  }
+  constexpr int WV = FHC * C / 8 / FT;
+  constexpr int FN2 = C / 32;  // GEMM2 column fragments per wave (C / 2 columns)
+  f32x4_t acc2[2][FN2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < FN2; ++b) acc2[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int h0 = 0; h0 < Hd; h0 += FHC) {
+    // this chunk's GELU' operand, issued before the weight staging and GEMM1 so its HBM latency overlaps them
+    u16x4_t pre_r[2][2];
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn) {
+        const int row = wm * 32 + fm * 16 + fr;
+        const int col = wn * 32 + fn * 16 + 4 * (lane >> 4);
+        pre_r[fm][fn] = row < nrows ? *reinterpret_cast<const u16x4_t*>(preb + (int64_t)row * Hd + h0 + col) : u16x4_t(0);
+      }
+    u16x8_t w1r[WV], w2r[WV];
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int v = tid + j * FT;
+      const int c = v / (FHC / 8), q = (v % (FHC / 8)) * 8;   // W2_e[c][h0 + q .. +8]
+      w2r[j] = *reinterpret_cast<const u16x8_t*>(W2g + (int64_t)c * Hd + h0 + q);
+      const int hh = v / (C / 8), c1 = (v % (C / 8)) * 8;     // W1_e[h0 + hh][c1 .. +8]
+      w1r[j] = *reinterpret_cast<const u16x8_t*>(W1g + (int64_t)(h0 + hh) * C + c1);
+    }
+    __syncthreads();  // the previous chunk's GEMM2 / column sums are done with w1, w2 and hs
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int v = tid + j * FT;
+      const int c = v / (FHC / 8), q = (v % (FHC / 8)) * 8;
+      *reinterpret_cast<u16x8_t*>(sm.w2 + mci(c, q, FHC)) = w2r[j];
+      const int hh = v / (C / 8), c1 = (v % (C / 8)) * 8;
+      *reinterpret_cast<u16x8_t*>(sm.w1 + mci(hh, c1, C)) = w1r[j];
+    }
+    __syncthreads();
+    // ---- GEMM1: gH[128 x 64] = gG[128 x C] . W2c[C x 64]; wave (wm, wn): rows wm*32, hidden units wn*32 ----
+    f32x4_t acc1[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc1[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int k0 = 0; k0 < C; k0 += 32) {
+      bf16x8_t a[2], b[2];
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm) a[fm] = frag(sm.gs, kci<FBM>(wm * 32 + fm * 16 + fr, k0 + fk));
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn) b[fn] = mc_frag(sm.w2, FHC, k0, wn * 32 + fn * 16, lane);
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn)  // transposed product: lane holds 4 consecutive hidden units of one row
+          acc1[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[fn], a[fm], acc1[fm][fn], 0, 0, 0);
+    }
+    // ---- gP = gH * GELU'(Pre): HBM (8-B runs) and the LDS image for GEMM2 ----
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn) {
+        const int row = wm * 32 + fm * 16 + fr;
+        const int col = wn * 32 + fn * 16 + 4 * (lane >> 4);
+        const u16x4_t pv = pre_r[fm][fn];
+        u16x4_t gv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          gv[j] = __builtin_bit_cast(unsigned short, f2bf(acc1[fm][fn][j] * gelu_fast_grad(bf2f(pv[j]))));
+        if (row < nrows) *reinterpret_cast<u16x4_t*>(gpb + (int64_t)row * Hd + h0 + col) = gv;
+        *reinterpret_cast<u16x4_t*>(sm.hs + kci<FBM>(row, col)) = gv;  // rows past the group: gG = 0, so gP = 0
+      }
+    __syncthreads();  // hs complete; every GEMM1 read of w2 done
+    // column sums of the bf16 gP chunk (what the weight gradient reads): 8 row groups of 16 per column, in order,
+    // into the free w2 buffer
+    float* red = reinterpret_cast<float*>(sm.w2);  // [8 row groups][64 columns]
+    {
+      const int col = tid & (FHC - 1), rg = tid >> 6;
+      float cs = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) cs += bf2f(sm.hs[kci<FBM>(rg * 16 + rr, col)]);
+      red[rg * FHC + col] = cs;
+    }
+    // ---- GEMM2: gX[128 x C] += hs[128 x 64] . W1c[64 x C]; wave (wm, wn): rows wm*32, cols wn*C/2 ----
+#pragma unroll 1
+    for (int k0 = 0; k0 < FHC; k0 += 32) {
+      bf16x8_t a[2];
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm) a[fm] = frag(sm.hs, kci<FBM>(wm * 32 + fm * 16 + fr, k0 + fk));
+#pragma unroll
+      for (int fn = 0; fn < FN2; ++fn) {
+        const bf16x8_t b = mc_frag(sm.w1, C, k0, wn * (C / 2) + fn * 16, lane);
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+          acc2[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fm], b, acc2[fm][fn], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // red complete
+    if (tid < FHC) {
+      float cs = 0.f;
+#pragma unroll
+      for (int rg = 0; rg < FT / FHC; ++rg) cs += red[rg * FHC + tid];
+      partb[h0 + tid] = cs;
+    }
+  }
+  // ---- epilogue: gX tile, bf16, staged through LDS (the gG tile is dead) for 16-B row stores ----
+  __syncthreads();
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN2; ++fn) {
+      const int col = wn * (C / 2) + fn * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wm * 32 + fm * 16 + 4 * (lane >> 4) + j;
+        sm.gs[row * C + col] = f2bf(acc2[fm][fn][j]);
+      }
+    }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < XV; ++j) {
+    const int v = tid + j * FT, r = v / (C / 8), k = (v % (C / 8)) * 8;
+    if (r < nrows) *reinterpret_cast<u16x8_t*>(gX + (int64_t)(r0 + r) * C + k) = *reinterpret_cast<const u16x8_t*>(sm.gs + r * C + k);
+  }
+}
+
+// two blocks per CU (128 VGPRs, a few spilled) or one with room for the live ranges (A/B: MG_TUNE_FFN_BWD_OCC)
+template <int C>
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_moe_ffn_bwd(
+    const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
+    const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part) {
+  ffn_bwd_body<C>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part);
+}
+template <int C>
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_moe_ffn_bwd_w2(
+    const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
+    const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part) {
+  ffn_bwd_body<C>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part);
+}
+
+// gb1[g][h] += sum over the tiles of group g (tile order) of part[tile][h]: 64 columns x 4 tile lanes per block,
+// eight loads in flight per lane, the four lane sums folded in lane order
+__global__ __launch_bounds__(256) void k_ffn_bias_fold(const float* __restrict__ part, const int* __restrict__ tile_off,
+                                                       int Hd, float* __restrict__ gb1) {
+  __shared__ float red[4][64];
+  const int h = blockIdx.x * 64 + (threadIdx.x & 63), ty = threadIdx.x >> 6, g = blockIdx.y;
+  const int t0 = tile_off[g], t1 = tile_off[g + 1];
+  float s = 0.f;
+  if (h < Hd) {
+    int t = t0 + ty;
+    for (; t + 28 < t1; t += 32) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = part[(int64_t)(t + 4 * q) * Hd + h];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += v[q];
+    }
+    for (; t < t1; t += 4) s += part[(int64_t)t * Hd + h];
+  }
+  red[ty][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ty == 0 && h < Hd) gb1[(int64_t)g * Hd + h] += ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
 }  // namespace
 
 extern "C" int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off,
@@ -230,4 +468,31 @@ extern "C" int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngro
   else L_(256);
 #undef L_
   return mg_check_launch("mg_moe_ffn_fwd");
+}
+
+extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off,
+                              const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1,
+                              const void* W2, void* gP, void* gX, float* gb1, void* stream) {
+  MG_REQUIRE(dtype == MG_BF16, "bf16 only");
+  MG_REQUIRE(C == 128, "C must be 128");
+  MG_REQUIRE(Hd > 0 && Hd % FHC == 0, "Hd must be a multiple of 64");
+  MG_REQUIRE(ngroups >= 1 && ngroups <= 64, "1 <= ngroups <= 64");
+  MG_REQUIRE(mg_al16(gG) && mg_al16(pre) && mg_al16(W1) && mg_al16(W2) && mg_al16(gP) && mg_al16(gX),
+             "operands must be 16-byte aligned");
+  MG_REQUIRE(total_rows >= 0 && max_tiles >= (total_rows + FBM - 1) / FBM, "max_tiles below the row tiles");
+  if (max_tiles <= 0 || total_rows == 0) return MG_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* part = reinterpret_cast<float*>(mg_workspace((size_t)max_tiles * Hd * sizeof(float), st));
+  if (!part) return MG_ERR_ARG;
+  const bool one_block = g_mg_tune[MG_TUNE_FFN_BWD_OCC] == 1;
+#define L_(K)                                                                                                        \
+  hipLaunchKernelGGL(K<128>, dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),                 \
+                     reinterpret_cast<const bf16_t*>(pre), ngroups, row_off, tile_off, Hd,                            \
+                     reinterpret_cast<const bf16_t*>(W1), reinterpret_cast<const bf16_t*>(W2),                        \
+                     reinterpret_cast<bf16_t*>(gP), reinterpret_cast<bf16_t*>(gX), part)
+  if (one_block) L_(k_moe_ffn_bwd_w2);
+  else L_(k_moe_ffn_bwd);
+#undef L_
+  if (gb1) hipLaunchKernelGGL(k_ffn_bias_fold, dim3(cdiv(Hd, 64), ngroups), dim3(256), 0, st, part, tile_off, Hd, gb1);
+  return mg_check_launch("mg_moe_ffn_bwd");
 }

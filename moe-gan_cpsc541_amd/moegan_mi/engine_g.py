@@ -537,22 +537,29 @@ class GeneratorEngine:
         g_gate = ops.moe_gate_grad(g_out, Y, sv["pos_of"], T, k)
         # gate-weighted output gradient in dispatch order: gG[r] = gate[r] * g_out[token(r)]
         gG = ops.gather_rows(g_out, perm, k, rowscale=sv["gate_pos"])
-        # expert layer 2: dH = gG @ W2_e, times GELU'(pre)
-        gP = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
-        ops.gemm_grouped(gG, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
-                         out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd))
         gW2 = self.st.group_view(ex + "0.net.2.weight", f"{ex}{E-1}.net.2.weight", self.st.grad)
         gb2 = self.st.group_view(ex + "0.net.2.bias", f"{ex}{E-1}.net.2.bias", self.st.grad)
+        gW1 = self.st.group_view(ex + "0.net.0.weight", f"{ex}{E-1}.net.0.weight", self.st.grad)
+        gb1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias", self.st.grad)
+        gP = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+        gX = torch.empty(n, C, device=self.dev, dtype=self.cdt)
+        fused = ops.ffn_bwd_fusable(self.cdt, C)
+        if fused:
+            # one pass per 128-row tile: gP = (gG W2_e) * GELU'(pre), gX = gP W1_e, gb1 column sums (mg_moe_ffn_bwd)
+            ops.moe_ffn_bwd(gG, Pre, sv["W1"].view(E, Hd, C), sv["W2"].view(E, C, Hd), row_off, tile_off,
+                            sv["max_tiles"], gP, gX, gb1.view(E, Hd))
+        else:
+            # expert layer 2: dH = gG @ W2_e, times GELU'(pre)
+            ops.gemm_grouped(gG, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
+                             out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd))
         self.side.run(lambda: (ops.gemm_grouped_wgrad(gG, sv["Hid"], row_off, n, C, Hd, gW2),
                                ops.grouped_colsum(gG, row_off, C, n, gb2)), gG)
         # expert layer 1
-        gX = torch.empty(n, C, device=self.dev, dtype=self.cdt)
-        ops.gemm_grouped(gP, sv["W1"], row_off, tile_off, sv["max_tiles"], C, Hd, b_kc=False, b_gstride=Hd * C,
-                         out=gX, ldb=C)
-        gW1 = self.st.group_view(ex + "0.net.0.weight", f"{ex}{E-1}.net.0.weight", self.st.grad)
-        gb1 = self.st.group_view(ex + "0.net.0.bias", f"{ex}{E-1}.net.0.bias", self.st.grad)
+        if not fused:
+            ops.gemm_grouped(gP, sv["W1"], row_off, tile_off, sv["max_tiles"], C, Hd, b_kc=False, b_gstride=Hd * C,
+                             out=gX, ldb=C)
         self.side.run(lambda: (ops.gemm_grouped_wgrad(gP, sv["Xg"], row_off, n, Hd, C, gW1),
-                               ops.grouped_colsum(gP, row_off, Hd, n, gb1)), gP)
+                               None if fused else ops.grouped_colsum(gP, row_off, Hd, n, gb1)), gP)
         if self.on_grad_final is not None:  # this block's expert parameters receive no further gradient
             lo = self.st.offsets[ex + "0.net.0.weight"][0]
             o, nl = self.st.offsets[f"{ex}{E-1}.net.2.bias"]

@@ -285,6 +285,19 @@ def moe_ffn_fwd(X, W1, b1, W2, b2, row_off, tile_off, max_tiles, Y, *, pre=None,
     return Y
 
 
+def moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1=None):
+    """Fused expert FFN backward (mg_moe_ffn_bwd): gP = (gG W2_g) * GELU'(Pre), gX = gP W1_g, gb1 += colsum(gP)."""
+    G, Hd, C = W1.shape
+    call("mg_moe_ffn_bwd", L.MG_BF16, gG.shape[0], C, Hd, G, ptr(row_off), ptr(tile_off), max_tiles, ptr(gG),
+         ptr(Pre), ptr(W1), ptr(W2), ptr(gP), ptr(gX), ptr(gb1), S())
+    return gP, gX
+
+
+def ffn_bwd_fusable(dtype, C):
+    """The fused expert backward (gP and gX in one pass over the rows, gb1 from the same pass): bf16, C = 128."""
+    return dtype == torch.bfloat16 and C == 128 and os.environ.get("MOEGAN_FFN_BWD_FUSED", "1") == "1"
+
+
 def gemm_grouped_wgrad(A, B, row_off, total_rows, M, N, out, *, b_idx=None, b_idx_div=1, b_gelu=0, ep=None,
                        lda=None, ldb=None, splits=0):
     """out[g] (fp32 [G,M,N]) += sum over rows of group g of A[r,:]^T B[r,:]."""

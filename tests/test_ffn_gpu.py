@@ -67,3 +67,49 @@ def test_fused_ffn_matches_grouped_gemms(T, C, E, k):
     hg = torch.nn.functional.gelu(h).to(bf).double()
     y = torch.einsum("rh,rch->rc", hg, W2[e_of].double()) + b2.view(E, C)[e_of].double()
     assert (Y[rows].double() - y).abs().max() <= 2e-2 * y.abs().max() + 1e-3
+
+
+@pytest.mark.parametrize("T,E,k,skew", [(65536, 8, 2, False), (1000, 8, 2, True), (2048, 32, 4, False), (77, 4, 1, True)])
+def test_fused_ffn_backward_matches_grouped_gemms(T, E, k, skew):
+    """Fused expert backward (mg_moe_ffn_bwd, t2i_moe_gan.py:257-263 backward) against the unfused path of
+    engine_g.moe_bwd: gP = gG W2_e with the GELU' epilogue and gX = gP W1_e (mg_gemm_grouped) bit-identical; the
+    bias gradient against mg_grouped_colsum of the same gP (fp32 summation order) and against float64 sums; C = 128
+    (the 16x16 block), empty experts, ragged last tiles, the C5 routing (E=32 top-4)."""
+    C, Hd = 128, 512
+    tok, W1, b1, W2, b2, topi, gate = _case(T, C, E, k, T * 3 + E, empty_expert=skew)
+    row_off, tile_off, perm, pos_of, gate_pos = ops.moe_dispatch(topi, gate, E)
+    n = T * k
+    max_tiles = (n + 127) // 128 + E
+    g = torch.Generator(device=DEV).manual_seed(T + 1)
+    gG = torch.randn(n, C, device=DEV, generator=g).to(bf)
+    Pre = torch.randn(n, Hd, device=DEV, generator=g).to(bf)
+    gP_r = torch.empty(n, Hd, device=DEV, dtype=bf)
+    ops.gemm_grouped(gG, W2.view(-1), row_off, tile_off, max_tiles, Hd, C, b_kc=False, b_gstride=C * Hd, out=gP_r,
+                     ldb=Hd, ep=ops.E(act=L.ACT_MUL_GELU_GRAD, aux=Pre, ld_aux=Hd))
+    gX_r = torch.empty(n, C, device=DEV, dtype=bf)
+    ops.gemm_grouped(gP_r, W1.view(-1), row_off, tile_off, max_tiles, C, Hd, b_kc=False, b_gstride=Hd * C, out=gX_r,
+                     ldb=C)
+    gb1_r = torch.full((E * Hd,), 0.25, device=DEV)
+    ops.grouped_colsum(gP_r, row_off, Hd, n, gb1_r)
+    gP = torch.empty(n, Hd, device=DEV, dtype=bf)
+    gX = torch.empty(n, C, device=DEV, dtype=bf)
+    gb1 = torch.full((E, Hd), 0.25, device=DEV)
+    ops.moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1)
+    torch.cuda.synchronize()
+    assert torch.equal(gP, gP_r)
+    assert torch.equal(gX, gX_r)
+    scale = float((gb1_r - 0.25).abs().max())
+    assert float((gb1.view(-1) - gb1_r).abs().max()) <= 1e-5 * scale + 1e-7
+    # float64 column sums of the bf16 gP, per expert
+    ro = row_off.cpu().tolist()
+    ref = torch.stack([gP[ro[e]:ro[e + 1]].double().sum(0) for e in range(E)]) + 0.25
+    assert float((gb1.double() - ref.to(DEV)).abs().max()) <= 1e-5 * float(ref.abs().max())
+    # and the gradients against float64 math on the same bf16 operands (sampled rows)
+    rows = torch.randperm(n, device=DEV)[:64]
+    e_of = torch.bucketize(rows.int(), row_off[1:].contiguous(), right=True)
+    gh = torch.einsum("rc,rch->rh", gG[rows].double(), W2[e_of].double())
+    p = Pre[rows].double()
+    gelu_grad = 0.5 * (1 + torch.erf(p / 2 ** 0.5)) + p * torch.exp(-p * p / 2) / (2 * torch.pi) ** 0.5
+    assert (gP[rows].double() - gh * gelu_grad).abs().max() <= 1e-2 * (gh * gelu_grad).abs().max()
+    gx = torch.einsum("rh,rhc->rc", gP[rows].double(), W1[e_of].double())
+    assert (gX[rows].double() - gx).abs().max() <= 1e-2 * gx.abs().max()
