@@ -108,6 +108,7 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_S1_OFF = 12,  // 1: weight gradients of stride-1 convs through the generic LdMCConv (A/B)
        MG_TUNE_D0_STORE = 13,  // mg_d0_fwd output path: 0 automatic, 1 straight from the accumulators, 2 LDS-staged rows
        MG_TUNE_FFN_BWD_OCC = 14,  // mg_moe_ffn_bwd: 0 two blocks per CU (128 VGPRs), 1 one block (256 VGPRs)
+       MG_TUNE_WIDE_WGRAD = 15,   // 1: linear-layer weight gradients through the generic split-K GEMM (A/B)
        MG_TUNE_COUNT = 16 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 // Deterministic mode (mg_set_tuning(MG_TUNE_DETERMINISTIC, 1)): every reduction that crosses workgroups runs in
@@ -165,3 +166,7 @@ static inline void mg_det_fold_rows(const float* part, int nrows, int ncols, int
   } while (0)
 
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// mg_wgrad_wide.hip: wide split-K weight gradients (bf16 [K][M] x [K][N] -> fp32 C +=), true when handled
+bool mg_wgrad_wide(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
+                   float alpha, hipStream_t st);

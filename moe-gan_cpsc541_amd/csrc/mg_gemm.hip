@@ -161,6 +161,12 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
   MG_REQUIRE(under2g((a_kc ? (int64_t)M : K) * lda, dtype) && under2g((b_kc ? (int64_t)N : K) * ldb, dtype) &&
                  under2g((int64_t)M * ldc, c_dtype),
              "an operand exceeds 2 GiB (32-bit buffer offsets)");
+  if (splits < 1 && dtype == MG_BF16 && !x3 && !a_kc && !b_kc && c_dtype == MG_F32 && ep && ep->atomic &&
+      !ep->bias && !ep->scale && !ep->rowscale && !ep->act && !ep->aux && !ep->resid && !ep->accumulate &&
+      !ep->remap_taps && !ep->a_idx && !ep->a_rowscale && !ep->a_gelu && !ep->addvec && !ep->out_pre &&
+      mg_wgrad_wide(M, N, K, A, lda, B, ldb, reinterpret_cast<float*>(C), ldc, ep->alpha,
+                    reinterpret_cast<hipStream_t>(stream)))
+    return mg_check_launch("mg_gemm (wide weight gradient)");
   if (splits < 1) {  // auto split-K (atomic fp32 epilogues only): ~512 blocks, >= 256 of K per split
     if (ep && ep->atomic) {
       int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);

@@ -327,3 +327,31 @@ def test_conv_wgrad_stride1_loader(dtype, B, H, Cin, Cout, k):
         assert torch.equal(gw1, gw0)
     else:
         assert rel(gw1, gw0) < 1e-6
+
+
+@pytest.mark.parametrize("M,N,K,alpha", [(384, 128, 65536, 1.0), (128, 128, 65536, 1.0), (256, 256, 16384, 0.5),
+                                         (1536, 512, 4096, 1.0), (256, 16, 65536, 1.0), (136, 200, 5000, 1.0)])
+def test_wide_weight_gradient(M, N, K, alpha):
+    """Linear-layer weight gradients C += alpha * A^T B (bf16 [K][M] x [K][N], fp32 C through an atomic epilogue):
+    the wide split-K kernel (csrc/mg_wgrad_wide.hip) against fp64 on the same bf16 operands and against the generic
+    split-K GEMM (tuning slot 15); fixed-order fold: two calls give the same bits."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn(K, M, device=DEV, generator=g).bfloat16()
+    B = torch.randn(K, N, device=DEV, generator=g).bfloat16()
+    ref = alpha * (A.double().T @ B.double()) + 0.5
+
+    def run():
+        C = torch.full((M, N), 0.5, device=DEV)
+        ops.gemm(A, B, M, N, K, a_kc=False, b_kc=False, out=C, ep=ops.E(alpha=alpha, atomic=1), splits=0)
+        return C
+    C1, C2 = run(), run()
+    L.call("mg_set_tuning", 15, 1)
+    try:
+        C3 = run()
+    finally:
+        L.call("mg_set_tuning", 15, 0)
+    torch.cuda.synchronize()
+    scale = float(ref.abs().max())
+    assert float((C1.double() - ref).abs().max()) <= 2e-6 * scale * (K / 4096) ** 0.5 + 1e-6
+    assert float((C1 - C3).abs().max()) <= 4e-6 * scale * (K / 4096) ** 0.5 + 1e-6
+    assert torch.equal(C1, C2)
