@@ -265,6 +265,15 @@ int mg_d0_fwd(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, i
 int mg_d0_wgrad(int in_dtype, const void* x, int64_t sb, int64_t sh, int64_t sw, int64_t sc, int B, int H, int W, const void* g, float* dw, void* stream);
 int mg_d0_dgrad(const void* g, int B, int OH, int OW, const void* w0p, int out_dtype, void* out, int64_t ldo, void* stream);
 
+/* Discriminator head, image channels, bf16 step (output_layer.0, t2i_moe_gan.py:901-907): mg_d_head_fwd: out[b, oy*Ho
+   + ox] (fp32, Ho = Hf - 3) = sum_{c, kh, kw} h1[b, oy+kh, ox+kw, c] W2[c, kh*4+kw] with w2t the bf16 [16 taps][256]
+   weight (bit-identical to mg_gemm + mg_disc_head_sum).  mg_d_head_bwd: g_a1[b, y, x, c] (bf16) = LeakyReLU'(h1[b,
+   y, x, c]) * sum_tap g[b, y-kh, x-kw] W2[c, tap] with w2c the bf16 [256][16 taps] weight and g [B, Ho*Ho] fp32
+   (image stride g_bstride; 0 broadcasts one map, the R1 pass) -- bit-identical to mg_disc_head_gmat + mg_gemm with
+   the LeakyReLU' epilogue.  h1 / g_a1: NHWC [B, Hf, Hf, 256]; 4 <= Hf <= 32. */
+int mg_d_head_fwd(const void* h1, const void* w2t, int B, int Hf, float* out, void* stream);
+int mg_d_head_bwd(const float* g, int64_t g_bstride, const void* h1, const void* w2c, int B, int Hf, void* ga1, void* stream);
+
 /* Discriminator output_layer, image channels: out[b,o] = sum h1[b,o+tap,c] W2[c,tap] (t2i_moe_gan.py:885-907). */
 int mg_disc_head_fwd(int dtype, const void* h1, const float* W2, int B, int Hf, int Cf, float* out, void* stream);
 

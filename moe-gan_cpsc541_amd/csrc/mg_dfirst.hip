@@ -647,3 +647,114 @@ extern "C" int mg_d0_dgrad(const void* g, int B, int OH, int OW, const void* w0p
 #undef L_
   return mg_check_launch("mg_d0_dgrad");
 }
+
+// ---------------------------------------------------------------------------------------------------------------
+// Discriminator head, image channels (output_layer.0: 4x4 valid conv 256 -> 1, t2i_moe_gan.py:901-907), bf16 step.
+//  * k_dhead_fwd: one block per image: P[px][tap] = h1[px] . W2[:, tap] on MFMA (A rows straight from HBM, the
+//    [16 x 256] tap-major weight as B), P in LDS, out[oy][ox] = sum_tap P[(oy+kh, ox+kw)][tap] in k_head_sum's order.
+//    Replaces the [pixels x 16] fp32 GEMM output + the separate shifted sum (bit-identical: same MFMA k order).
+//  * k_dhead_bwd: one block per image: g_a1[px][c] = LeakyReLU'(h1[px][c]) * sum_tap G[px][tap] W2[c][tap] with the
+//    tap-expanded gradient G[px][tap] = g[y-kh][x-kw] formed in registers from the image's logit gradients (no
+//    [pixels x 16] matrix), the K = 16 product on one MFMA per 16 x 16 block: bit-identical to mg_disc_head_gmat +
+//    mg_gemm with the LeakyReLU' epilogue.
+namespace {
+
+__global__ __launch_bounds__(256) void k_dhead_fwd(const bf16_t* __restrict__ h1, const bf16_t* __restrict__ w2t,
+                                                   int Hf, float* __restrict__ out) {
+  extern __shared__ float Ps[];  // [Hf*Hf][16]
+  const int b = blockIdx.x, npx = Hf * Hf, Ho = Hf - 3;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  bf16x8_t bw[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+    bw[ks] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(w2t + (lane & 15) * 256 + 32 * ks + 8 * (lane >> 4)));
+  const bf16_t* hb = h1 + (int64_t)b * npx * 256;
+  for (int mf = w; mf * 16 < npx; mf += 4) {
+    bf16x8_t a[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      a[ks] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(hb + (int64_t)(16 * mf + (lane & 15)) * 256 + 32 * ks + 8 * (lane >> 4)));
+    f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], bw[ks], acc, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Ps[(16 * mf + 4 * (lane >> 4) + j) * 16 + (lane & 15)] = acc[j];
+  }
+  __syncthreads();
+  for (int o = tid; o < Ho * Ho; o += 256) {
+    const int oy = o / Ho, ox = o - oy * Ho;
+    float s = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 4; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 4; ++kw) s += Ps[((oy + kh) * Hf + ox + kw) * 16 + kh * 4 + kw];
+    out[(int64_t)b * Ho * Ho + o] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dhead_bwd(const float* __restrict__ g, int64_t g_bstride,
+                                                   const bf16_t* __restrict__ h1, const bf16_t* __restrict__ w2c,
+                                                   int Hf, bf16_t* __restrict__ ga1) {
+  __shared__ float gs[32 * 32];
+  const int b = blockIdx.x, npx = Hf * Hf, Ho = Hf - 3;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* gb = g + (int64_t)b * g_bstride;
+  for (int i = tid; i < Ho * Ho; i += 256) gs[i] = gb[i];
+  // W2 rows (channel c = 16 nf + (lane&15)) over the 16 taps; k 16..31 of the 32-wide step are zero
+  bf16x8_t wf[16];
+#pragma unroll
+  for (int nf = 0; nf < 16; ++nf) {
+    u16x8_t v = u16x8_t(0);
+    if ((lane >> 4) < 2) v = *reinterpret_cast<const u16x8_t*>(w2c + (16 * nf + (lane & 15)) * 16 + 8 * (lane >> 4));
+    wf[nf] = __builtin_bit_cast(bf16x8_t, v);
+  }
+  __syncthreads();
+  const bf16_t* hb = h1 + (int64_t)b * npx * 256;
+  bf16_t* ob = ga1 + (int64_t)b * npx * 256;
+  for (int mf = w; mf * 16 < npx; mf += 4) {
+    // G column of pixel px = 16 mf + (lane&15): taps 8(lane>>4) .. +7 (bf16, as mg_disc_head_gmat stores it)
+    const int px = 16 * mf + (lane & 15), y = px / Hf, x = px - (px / Hf) * Hf;
+    u16x8_t gv = u16x8_t(0);
+    if ((lane >> 4) < 2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = 8 * (lane >> 4) + j, oy = y - (tap >> 2), ox = x - (tap & 3);
+        const float v = ((unsigned)oy < (unsigned)Ho && (unsigned)ox < (unsigned)Ho) ? gs[oy * Ho + ox] : 0.f;
+        gv[j] = f2bf(v);
+      }
+    }
+    const bf16x8_t gf = __builtin_bit_cast(bf16x8_t, gv);
+#pragma unroll 4
+    for (int nf = 0; nf < 16; ++nf) {
+      // transposed product: lane holds channels 16 nf + 4(lane>>4) + j of pixel px
+      const f32x4_t acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nf], gf, f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int c = 16 * nf + 4 * (lane >> 4);
+      const u16x4_t m = *reinterpret_cast<const u16x4_t*>(hb + (int64_t)px * 256 + c);
+      u16x4_t o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[j] * lrelu_grad(bf2f(m[j])));
+      *reinterpret_cast<u16x4_t*>(ob + (int64_t)px * 256 + c) = o;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int mg_d_head_fwd(const void* h1, const void* w2t, int B, int Hf, float* out, void* stream) {
+  MG_REQUIRE(B > 0 && Hf >= 4 && Hf <= 32 && (Hf * Hf) % 16 == 0, "4 <= Hf <= 32, Hf^2 a multiple of 16");
+  MG_REQUIRE(mg_al16(h1) && mg_al16(w2t), "16-byte aligned h1 / W2");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_dhead_fwd, dim3(B), dim3(256), (size_t)Hf * Hf * 16 * sizeof(float), st,
+                     reinterpret_cast<const bf16_t*>(h1), reinterpret_cast<const bf16_t*>(w2t), Hf, out);
+  return mg_check_launch("mg_d_head_fwd");
+}
+
+extern "C" int mg_d_head_bwd(const float* g, int64_t g_bstride, const void* h1, const void* w2c, int B, int Hf,
+                             void* ga1, void* stream) {
+  MG_REQUIRE(B > 0 && Hf >= 4 && Hf <= 32 && (Hf * Hf) % 16 == 0, "4 <= Hf <= 32, Hf^2 a multiple of 16");
+  MG_REQUIRE(mg_al16(h1) && mg_al16(w2c) && mg_al16(ga1), "16-byte aligned h1 / W2 / g_a1");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_dhead_bwd, dim3(B), dim3(256), 0, st, g, g_bstride, reinterpret_cast<const bf16_t*>(h1),
+                     reinterpret_cast<const bf16_t*>(w2c), Hf, reinterpret_cast<bf16_t*>(ga1));
+  return mg_check_launch("mg_d_head_bwd");
+}

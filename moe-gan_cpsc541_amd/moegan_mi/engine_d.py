@@ -99,8 +99,11 @@ class DiscriminatorEngine:
     def forward(self, img, layout, text, B, H):
         cols, h0, h1 = self.conv_stack(img, layout, B, H)
         Hf = H // 4
-        P = ops.gemm(h1.view(-1, 256), self.W2t_c, B * Hf * Hf, 16, 256, out_dtype=torch.float32)
-        img_part = ops.disc_head_sum(P, B, Hf)  # [B, (H/4-3)^2]
+        if self.direct0 and Hf <= 32:  # one kernel per image (mg_d_head_fwd)
+            img_part = ops.d_head_fwd(h1, self.W2t_c, B, Hf)
+        else:
+            P = ops.gemm(h1.view(-1, 256), self.W2t_c, B * Hf * Hf, 16, 256, out_dtype=torch.float32)
+            img_part = ops.disc_head_sum(P, B, Hf)  # [B, (H/4-3)^2]
         return dict(cols=cols, h0=h0, h1=h1, img_part=img_part, H=H, B=B)
 
     # ------------------------------------------------------------------
@@ -140,15 +143,20 @@ class DiscriminatorEngine:
         else:
             ops.dgrad_s2_small(g, self.W0p, 3, out)
 
-    def _head_bwd(self, g, g_bstride, h1, B, Hf, want_w, wgrad_input=None):
+    def _head_bwd(self, g, g_bstride, h1, B, Hf, want_w, wgrad_input=None, need_g=False):
         """g_a1 = lrelu'(a1) * (G @ W2img^T) and (optionally) dW2img += X^T G, G the tap-expanded gradient;
         X = h1 (or ``wgrad_input``, the R1 path's m1 v1)."""
         Pn = B * Hf * Hf
-        G = ops.disc_head_gmat(g, g_bstride, B, Hf, self.cdt)
         h1f = h1.view(Pn, 256)
         g_a1 = torch.empty(B, Hf, Hf, 256, device=self.dev, dtype=self.cdt)
-        ops.gemm(G, self.W2img_c, Pn, 256, 16, out=g_a1.view(Pn, 256),
-                 ep=E_(act=MUL_LRELU_GRAD, aux=h1f, ld_aux=256))
+        G = None
+        if want_w or need_g or not (self.direct0 and Hf <= 32):
+            G = ops.disc_head_gmat(g, g_bstride, B, Hf, self.cdt)
+        if self.direct0 and Hf <= 32:  # G formed inside the kernel (mg_d_head_bwd)
+            ops.d_head_bwd(g, g_bstride, h1, self.W2img_c, B, Hf, g_a1)
+        else:
+            ops.gemm(G, self.W2img_c, Pn, 256, 16, out=g_a1.view(Pn, 256),
+                     ep=E_(act=MUL_LRELU_GRAD, aux=h1f, ld_aux=256))
         if want_w:
             X = h1f if wgrad_input is None else wgrad_input.view(Pn, 256)
             dW2img = self.dW["output_layer.0."].view(384, 16)[:256]
@@ -195,7 +203,7 @@ class DiscriminatorEngine:
         Hf = Hr // 4
         Ho = Hf - 3
         g1 = self._ones(Ho * Ho).view(1, -1)
-        gA1, G1 = self._head_bwd(g1, 0, fr["h1"], B, Hf, False)  # m1 * Gh1
+        gA1, G1 = self._head_bwd(g1, 0, fr["h1"], B, Hf, False, need_g=True)  # m1 * Gh1 (G1: dW2's R1 term below)
         gA0 = torch.empty(B, Hr // 2, Hr // 2, 128, device=dev, dtype=self.cdt)
         ops.dgrad_s2(gA1, self.W1cls, 128, gA0, ep=E_(act=MUL_LRELU_GRAD, aux=fr["h0"], ld_aux=128))
         gx = ops.zeros(B, Hr, Hr, 4, device=dev)

@@ -822,6 +822,20 @@ def disc_head_fwd(h1, W2img):
     return out
 
 
+def d_head_fwd(h1, w2t, B, Hf):
+    """Head image part (mg_d_head_fwd, bf16): out [B, (Hf-3)^2] fp32."""
+    Ho = Hf - 3
+    out = torch.empty(B, Ho * Ho, device=h1.device)
+    call("mg_d_head_fwd", ptr(h1), ptr(w2t), B, Hf, ptr(out), S())
+    return out
+
+
+def d_head_bwd(g, g_bstride, h1, w2c, B, Hf, out):
+    """g_a1 = LeakyReLU'(h1) * (G W2img^T) with the tap-expanded G formed in the kernel (mg_d_head_bwd, bf16)."""
+    call("mg_d_head_bwd", ptr(g), g_bstride, ptr(h1), ptr(w2c), B, Hf, ptr(out), S())
+    return out
+
+
 def disc_head_gmat(g, g_bstride, B, Hf, dtype):
     """Tap-expanded head gradient G [B*Hf*Hf, 16] (mg_disc_head_gmat)."""
     G = torch.empty(B * Hf * Hf, 16, device=g.device, dtype=dtype)

@@ -49,6 +49,7 @@ FAMILIES = {
     "elementwise": ("hbm", ("mg_cast", "mg_copy2d", "mg_lrelu_mask_mul", "mg_upsample2x_fwd", "mg_upsample2x_bwd",
                             "mg_const_fwd", "mg_gated_axpy", "mg_select_if", "mg_zero_if", "mg_clip_patches")),
     "disc_head": ("hbm", ("mg_disc_head_fwd", "mg_disc_head_gmat", "mg_disc_head_sum", "mg_disc_head_bwd_data",
+                          "mg_d_head_fwd", "mg_d_head_bwd",
                           "mg_disc_head_bwd_w", "mg_d_text_bwd")),
     "mtm_bwd_unfused": ("hbm", ("mg_warp_bwd", "mg_offset_head_bwd")),
     # scalar losses, guard words, optimizer prologue: a few hundred bytes each, launch-latency bound
@@ -85,7 +86,7 @@ KERNELS = [
     (r"k_d0_", "d_conv0"),
     (r"k_cast|k_copy2d|k_mask_mul|k_up2|k_const_fwd|k_gated_axpy|k_select_if|k_zero_if|k_clip_patches",
      "elementwise"),
-    (r"k_head_|k_d_text", "disc_head"),
+    (r"k_head_|k_d_text|k_dhead_", "disc_head"),
     (r"k_warp_bwd|k_offset_head", "mtm_bwd_unfused"),
     (r"k_d_loss|k_g_loss|k_finite_flag|k_flag_window|k_kl_coefs|k_balance|k_opt_prologue", "losses_flags"),
 ]
@@ -245,6 +246,10 @@ def work(name, a):
     if name == "mg_d0_dgrad":
         B, OH, OW = a["B"], a["OH"], a["OW"]
         return B * OH * OW * 128 * 2 + B * 4 * OH * OW * 3 * ELT[a["out_dtype"]]
+    if name == "mg_d_head_fwd":  # h1 read, logits written
+        return a["B"] * a["Hf"] ** 2 * 256 * 2 + a["B"] * (a["Hf"] - 3) ** 2 * 4
+    if name == "mg_d_head_bwd":  # h1 (LeakyReLU' operand) read, g_a1 written
+        return 2 * a["B"] * a["Hf"] ** 2 * 256 * 2
     if name == "mg_cast":
         return a["n"] * (ELT[a["in_dtype"]] + ELT[a["out_dtype"]])
     if name == "mg_copy2d":

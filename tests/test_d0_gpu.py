@@ -119,3 +119,35 @@ def test_d0_image_gradient(B, H, out_dtype, ldo):
     t = xx.grad.permute(0, 2, 3, 1)
     tol = 1e-5 if out_dtype == torch.float32 else 8e-3
     assert float((out[..., :3].double() - t).abs().max()) <= tol * float(t.abs().max())
+
+
+@pytest.mark.parametrize("B,Hf,bcast", [(4, 16, False), (3, 4, False), (2, 32, False), (5, 8, False), (3, 16, True)])
+def test_d_head_kernels(B, Hf, bcast):
+    """The discriminator head's image part (output_layer.0, t2i_moe_gan.py:901-907) on the one-block-per-image
+    kernels (mg_d_head_fwd / mg_d_head_bwd) against the GEMM path they replace in the bf16 step: P = h1 W2 +
+    mg_disc_head_sum (forward) and mg_disc_head_gmat + GEMM with the LeakyReLU' epilogue (backward), bit-identical;
+    ``bcast``: one gradient map for every image (the R1 pass)."""
+    from moegan_mi import _lib as L
+    from moegan_mi import ops
+    g = torch.Generator(device=DEV).manual_seed(B * 100 + Hf)
+    h1 = torch.randn(B, Hf, Hf, 256, device=DEV, generator=g).bfloat16()
+    W2img = torch.randn(256, 16, device=DEV, generator=g) * 0.05
+    w2c, w2t = W2img.bfloat16().contiguous(), W2img.t().contiguous().bfloat16()
+    Ho = Hf - 3
+    out = ops.d_head_fwd(h1, w2t, B, Hf)
+    P = ops.gemm(h1.view(-1, 256), w2t, B * Hf * Hf, 16, 256, out_dtype=torch.float32)
+    ref = ops.disc_head_sum(P, B, Hf)
+    gl = torch.randn(1 if bcast else B, Ho * Ho, device=DEV, generator=g)
+    gs = 0 if bcast else Ho * Ho
+    ga1 = torch.empty_like(h1)
+    ops.d_head_bwd(gl, gs, h1, w2c, B, Hf, ga1)
+    G = ops.disc_head_gmat(gl, gs, B, Hf, torch.bfloat16)
+    ga1_ref = torch.empty_like(h1)
+    ops.gemm(G, w2c, B * Hf * Hf, 256, 16, out=ga1_ref.view(-1, 256),
+             ep=ops.E(act=L.ACT_MUL_LRELU_GRAD, aux=h1.view(-1, 256), ld_aux=256))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), float((out - ref).abs().max())
+    assert torch.equal(ga1, ga1_ref), float((ga1.float() - ga1_ref.float()).abs().max())
+    # plain fp32 torch on the same bf16 operands
+    t = F.conv2d(h1.float().permute(0, 3, 1, 2), w2c.float().reshape(1, 256, 4, 4))
+    assert float((out - t.reshape(B, -1)).abs().max()) <= 1e-4 * float(t.abs().max())
