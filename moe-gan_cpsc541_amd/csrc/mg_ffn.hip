@@ -284,18 +284,11 @@ __device__ __forceinline__ void ffn_bwd_body(
 #pragma unroll
     for (int b = 0; b < FN2; ++b) acc2[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  for (int h0 = 0; h0 < Hd; h0 += FHC) {
-    // this chunk's GELU' operand, issued before the weight staging and GEMM1 so its HBM latency overlaps them
-    u16x4_t pre_r[2][2];
-#pragma unroll
-    for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-      for (int fn = 0; fn < 2; ++fn) {
-        const int row = wm * 32 + fm * 16 + fr;
-        const int col = wn * 32 + fn * 16 + 4 * (lane >> 4);
-        pre_r[fm][fn] = row < nrows ? *reinterpret_cast<const u16x4_t*>(preb + (int64_t)row * Hd + h0 + col) : u16x4_t(0);
-      }
-    u16x8_t w1r[WV], w2r[WV];
+  // register ring (distance one chunk): the next chunk's weights are loaded right after this chunk's are stored to
+  // LDS, and its GELU' operand right after this chunk's epilogue used it, so both latencies overlap the products
+  u16x8_t w1r[WV], w2r[WV];
+  u16x4_t pre_r[2][2];
+  auto load_w = [&](int h0) {
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
       const int v = tid + j * FT;
@@ -304,6 +297,20 @@ __device__ __forceinline__ void ffn_bwd_body(
       const int hh = v / (C / 8), c1 = (v % (C / 8)) * 8;     // W1_e[h0 + hh][c1 .. +8]
       w1r[j] = *reinterpret_cast<const u16x8_t*>(W1g + (int64_t)(h0 + hh) * C + c1);
     }
+  };
+  auto load_pre = [&](int h0) {
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn) {
+        const int row = wm * 32 + fm * 16 + fr;
+        const int col = wn * 32 + fn * 16 + 4 * (lane >> 4);
+        pre_r[fm][fn] = row < nrows ? *reinterpret_cast<const u16x4_t*>(preb + (int64_t)row * Hd + h0 + col) : u16x4_t(0);
+      }
+  };
+  load_w(0);
+  load_pre(0);
+  for (int h0 = 0; h0 < Hd; h0 += FHC) {
     __syncthreads();  // the previous chunk's GEMM2 / column sums are done with w1, w2 and hs
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
@@ -314,6 +321,7 @@ __device__ __forceinline__ void ffn_bwd_body(
       *reinterpret_cast<u16x8_t*>(sm.w1 + mci(hh, c1, C)) = w1r[j];
     }
     __syncthreads();
+    if (h0 + FHC < Hd) load_w(h0 + FHC);
     // ---- GEMM1: gH[128 x 64] = gG[128 x C] . W2c[C x 64]; wave (wm, wn): rows wm*32, hidden units wn*32 ----
     f32x4_t acc1[2][2];
 #pragma unroll
@@ -348,6 +356,7 @@ __device__ __forceinline__ void ffn_bwd_body(
         if (row < nrows) *reinterpret_cast<u16x4_t*>(gpb + (int64_t)row * Hd + h0 + col) = gv;
         *reinterpret_cast<u16x4_t*>(sm.hs + kci<FBM>(row, col)) = gv;  // rows past the group: gG = 0, so gP = 0
       }
+    if (h0 + FHC < Hd) load_pre(h0 + FHC);
     __syncthreads();  // hs complete; every GEMM1 read of w2 done
     // column sums of the bf16 gP chunk (what the weight gradient reads): 8 row groups of 16 per column, in order,
     // into the free w2 buffer
