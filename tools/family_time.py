@@ -2,9 +2,11 @@
 
   python tools/family_time.py run_kernel_trace.csv OUT.json [batch E dtype [fp8]]
 
-The window runs from the first to the last dispatch of ``k_d_loss`` (launched once per training step), i.e.
-exactly (#k_d_loss - 1) whole steps of whatever the traced command ran (eager warm-up, hipGraph replays and the
-attribution step alike), excluding setup.  Kernels map to families by name (moegan_mi/roofline.py KERNELS).
+The window runs over whole steps between dispatches of ``k_d_loss`` (launched once per training step).  With
+FAMILY_LAST=N (the scripts pass the timed step count minus one) only the last N whole steps count: with bench.py
+--no-families those are hipGraph replays of the timed region, not the eager warm-up steps (a window
+that included the eager and attribution steps made the per-family busy time exceed the timed step).  Kernels map
+to families by name (moegan_mi/roofline.py KERNELS).
 """
 import csv
 import json
@@ -26,6 +28,9 @@ def main():
     anchors = [i for i, r in enumerate(rows) if "k_d_loss" in r["Kernel_Name"]]
     if len(anchors) < 2:
         raise SystemExit("need at least two traced steps")
+    last = int(os.environ.get("FAMILY_LAST", "0"))
+    if last > 0:
+        anchors = anchors[-(last + 1):]
     steps = len(anchors) - 1
     win = rows[anchors[0]:anchors[-1]]
     t = defaultdict(float)
@@ -41,7 +46,8 @@ def main():
     fams = {f: {"ms_per_step": round(t[f] / steps, 4), "dispatches_per_step": round(n[f] / steps, 1)} for f in t}
     rec = {"batch": batch, "experts": experts, "dtype": dtype, "fp8": fp8, "steps_in_window": steps,
            "busy_ms_per_step": round(busy, 4), "span_ms_per_step": round(span, 4),
-           "source": f"rocprofv3 --kernel-trace of bench.py, {steps} steps between the first and last k_d_loss",
+           "source": (f"rocprofv3 --kernel-trace of bench.py, the last {steps} replayed timed steps" if last > 0 else
+                      f"rocprofv3 --kernel-trace of bench.py, {steps} steps between the first and last k_d_loss"),
            "families": fams}
     json.dump(rec, open(out, "w"), indent=1)
     print(f"{steps} steps; busy {busy:.3f} ms/step, span {span:.3f} ms/step")

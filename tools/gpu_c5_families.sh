@@ -7,7 +7,7 @@ TAG=${TAG:-c5}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/c5_prof_$TAG -o run --output-format csv -- \
   python3 bench.py --config C5 --steps 10 --warmup 3 --no-cpu-baseline --secondary "" --no-families \
   > gpurun_out/c5_prof_$TAG.log 2>&1 || { tail -20 gpurun_out/c5_prof_$TAG.log; exit 1; }
-python3 tools/family_time.py gpurun_out/c5_prof_$TAG/run_kernel_trace.csv gpurun_out/family_time_C5_$TAG.json 256 32 bf16 fp8
+FAMILY_LAST=9 python3 tools/family_time.py gpurun_out/c5_prof_$TAG/run_kernel_trace.csv gpurun_out/family_time_C5_$TAG.json 256 32 bf16 fp8
 python3 tools/prof_summary.py gpurun_out/c5_prof_$TAG/run_kernel_stats.csv > gpurun_out/c5_stats_$TAG.txt
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/c5_fetch_$TAG -o run --output-format csv -- \
   python3 bench.py --config C5 --eager --steps 2 --warmup 1 --no-cpu-baseline --no-families --secondary "" \

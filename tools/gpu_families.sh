@@ -6,9 +6,9 @@
 #   TAG=r2b tools/gpu_families.sh
 mkdir -p gpurun_out && export TMPDIR=/tmp
 TAG=${TAG:-r2}
-B="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fam_prof_$TAG -o run --output-format csv -- $B > gpurun_out/fam_prof_$TAG.log 2>&1 || { tail -20 gpurun_out/fam_prof_$TAG.log; exit 1; }
-python3 tools/family_time.py gpurun_out/fam_prof_$TAG/run_kernel_trace.csv gpurun_out/family_time_$TAG.json
+B="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --secondary="
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fam_prof_$TAG -o run --output-format csv -- $B --no-families > gpurun_out/fam_prof_$TAG.log 2>&1 || { tail -20 gpurun_out/fam_prof_$TAG.log; exit 1; }
+FAMILY_LAST=9 python3 tools/family_time.py gpurun_out/fam_prof_$TAG/run_kernel_trace.csv gpurun_out/family_time_$TAG.json
 python3 tools/prof_summary.py gpurun_out/fam_prof_$TAG/run_kernel_stats.csv > gpurun_out/stats_$TAG.txt
 P="python3 bench.py --eager --steps 2 --warmup 1 --no-cpu-baseline --no-families"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/fam_fetch_$TAG -o run --output-format csv -- $P > gpurun_out/fam_fetch_$TAG.log 2>&1 || { tail -20 gpurun_out/fam_fetch_$TAG.log; exit 1; }
