@@ -483,7 +483,7 @@ extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngro
                               const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1,
                               const void* W2, void* gP, void* gX, float* gb1, void* stream) {
   MG_REQUIRE(dtype == MG_BF16, "bf16 only");
-  MG_REQUIRE(C == 128, "C must be 128");
+  MG_REQUIRE(C == 128 || C == 256, "C must be 128 or 256");
   MG_REQUIRE(Hd > 0 && Hd % FHC == 0, "Hd must be a multiple of 64");
   MG_REQUIRE(ngroups >= 1 && ngroups <= 64, "1 <= ngroups <= 64");
   MG_REQUIRE(mg_al16(gG) && mg_al16(pre) && mg_al16(W1) && mg_al16(W2) && mg_al16(gP) && mg_al16(gX),
@@ -493,14 +493,16 @@ extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngro
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* part = reinterpret_cast<float*>(mg_workspace((size_t)max_tiles * Hd * sizeof(float), st));
   if (!part) return MG_ERR_ARG;
-  const bool one_block = g_mg_tune[MG_TUNE_FFN_BWD_OCC] == 1;
-#define L_(K)                                                                                                        \
-  hipLaunchKernelGGL(K<128>, dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),                 \
+  // C = 256: 144 KiB of LDS, one block per CU, so the 256-VGPR form
+  const bool one_block = C == 256 || g_mg_tune[MG_TUNE_FFN_BWD_OCC] == 1;
+#define L_(K, CC)                                                                                                    \
+  hipLaunchKernelGGL(K<CC>, dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),                  \
                      reinterpret_cast<const bf16_t*>(pre), ngroups, row_off, tile_off, Hd,                            \
                      reinterpret_cast<const bf16_t*>(W1), reinterpret_cast<const bf16_t*>(W2),                        \
                      reinterpret_cast<bf16_t*>(gP), reinterpret_cast<bf16_t*>(gX), part)
-  if (one_block) L_(k_moe_ffn_bwd_w2);
-  else L_(k_moe_ffn_bwd);
+  if (C == 256) L_(k_moe_ffn_bwd_w2, 256);
+  else if (one_block) L_(k_moe_ffn_bwd_w2, 128);
+  else L_(k_moe_ffn_bwd, 128);
 #undef L_
   if (gb1) hipLaunchKernelGGL(k_ffn_bias_fold, dim3(cdiv(Hd, 64), ngroups), dim3(256), 0, st, part, tile_off, Hd, gb1);
   return mg_check_launch("mg_moe_ffn_bwd");

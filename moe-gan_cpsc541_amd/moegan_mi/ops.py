@@ -294,8 +294,11 @@ def moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1=None)
 
 
 def ffn_bwd_fusable(dtype, C):
-    """The fused expert backward (gP and gX in one pass over the rows, gb1 from the same pass): bf16, C = 128."""
-    return dtype == torch.bfloat16 and C == 128 and os.environ.get("MOEGAN_FFN_BWD_FUSED", "1") == "1"
+    """The fused expert backward (gP and gX in one pass over the rows, gb1 from the same pass): bf16, C = 128
+    (C = 256 with MOEGAN_FFN_BWD_FUSED256=1: built and tested, not yet measured faster)."""
+    if dtype != torch.bfloat16 or os.environ.get("MOEGAN_FFN_BWD_FUSED", "1") != "1":
+        return False
+    return C == 128 or (C == 256 and os.environ.get("MOEGAN_FFN_BWD_FUSED256", "0") == "1")
 
 
 def gemm_grouped_wgrad(A, B, row_off, total_rows, M, N, out, *, b_idx=None, b_idx_div=1, b_gelu=0, ep=None,

@@ -69,13 +69,17 @@ def test_fused_ffn_matches_grouped_gemms(T, C, E, k):
     assert (Y[rows].double() - y).abs().max() <= 2e-2 * y.abs().max() + 1e-3
 
 
-@pytest.mark.parametrize("T,E,k,skew", [(65536, 8, 2, False), (1000, 8, 2, True), (2048, 32, 4, False), (77, 4, 1, True)])
-def test_fused_ffn_backward_matches_grouped_gemms(T, E, k, skew):
+@pytest.mark.parametrize("occ", [0, 1])
+@pytest.mark.parametrize("T,E,k,skew,C", [(65536, 8, 2, False, 128), (1000, 8, 2, True, 128), (2048, 32, 4, False, 128),
+                                          (77, 4, 1, True, 128), (16384, 8, 2, False, 256), (300, 4, 1, True, 256)])
+def test_fused_ffn_backward_matches_grouped_gemms(T, E, k, skew, C, occ):
     """Fused expert backward (mg_moe_ffn_bwd, t2i_moe_gan.py:257-263 backward) against the unfused path of
     engine_g.moe_bwd: gP = gG W2_e with the GELU' epilogue and gX = gP W1_e (mg_gemm_grouped) bit-identical; the
     bias gradient against mg_grouped_colsum of the same gP (fp32 summation order) and against float64 sums; C = 128
-    (the 16x16 block), empty experts, ragged last tiles, the C5 routing (E=32 top-4)."""
-    C, Hd = 128, 512
+    and 256 (the 16x16 / 8x8 blocks), both occupancy forms (tuning slot 14), empty experts, ragged last tiles, the C5
+    routing (E=32 top-4)."""
+    Hd = 4 * C
+    L.call("mg_set_tuning", 14, occ)
     tok, W1, b1, W2, b2, topi, gate = _case(T, C, E, k, T * 3 + E, empty_expert=skew)
     row_off, tile_off, perm, pos_of, gate_pos = ops.moe_dispatch(topi, gate, E)
     n = T * k
@@ -96,6 +100,7 @@ def test_fused_ffn_backward_matches_grouped_gemms(T, E, k, skew):
     gb1 = torch.full((E, Hd), 0.25, device=DEV)
     ops.moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1)
     torch.cuda.synchronize()
+    L.call("mg_set_tuning", 14, 0)
     assert torch.equal(gP, gP_r)
     assert torch.equal(gX, gX_r)
     scale = float((gb1_r - 0.25).abs().max())

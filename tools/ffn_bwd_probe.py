@@ -11,7 +11,8 @@ from moegan_mi import _lib as L  # noqa: E402
 from moegan_mi import ops  # noqa: E402
 
 bf, DEV = torch.bfloat16, "cuda"
-T, C, E, k = int(os.environ.get("T", "65536")), 128, int(os.environ.get("E", "8")), int(os.environ.get("K", "2"))
+C = int(os.environ.get("C", "128"))
+T, E, k = int(os.environ.get("T", str(65536 * 128 // C))), int(os.environ.get("E", "8")), int(os.environ.get("K", "2"))
 Hd, n = 4 * C, T * k
 g = torch.Generator(device=DEV).manual_seed(0)
 W1 = (torch.randn(E, Hd, C, device=DEV, generator=g) * C ** -0.5).to(bf)
@@ -57,4 +58,4 @@ for name, fn in (("unfused gP+gX+colsum", unfused), ("fused mg_moe_ffn_bwd", fus
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / 20 * 1e3
-    print(f"{name:24s} {us:8.1f} us  {gf / us * 1e3:7.1f} TF/s ({gf:.1f} GF)", flush=True)
+    print(f"C={C} {name:24s} {us:8.1f} us  {gf / us * 1e3:7.1f} TF/s ({gf:.1f} GF)", flush=True)
