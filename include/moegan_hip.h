@@ -267,7 +267,7 @@ int mg_d0_dgrad(const void* g, int B, int OH, int OW, const void* w0p, int out_d
 
 /* Discriminator head, image channels, bf16 step (output_layer.0, t2i_moe_gan.py:901-907): mg_d_head_fwd: out[b, oy*Ho
    + ox] (fp32, Ho = Hf - 3) = sum_{c, kh, kw} h1[b, oy+kh, ox+kw, c] W2[c, kh*4+kw] with w2t the bf16 [16 taps][256]
-   weight (bit-identical to mg_gemm + mg_disc_head_sum).  mg_d_head_bwd: g_a1[b, y, x, c] (bf16) = LeakyReLU'(h1[b,
+   weight (mg_gemm + mg_disc_head_sum up to fp32 summation order).  mg_d_head_bwd: g_a1[b, y, x, c] (bf16) = LeakyReLU'(h1[b,
    y, x, c]) * sum_tap g[b, y-kh, x-kw] W2[c, tap] with w2c the bf16 [256][16 taps] weight and g [B, Ho*Ho] fp32
    (image stride g_bstride; 0 broadcasts one map, the R1 pass) -- bit-identical to mg_disc_head_gmat + mg_gemm with
    the LeakyReLU' epilogue.  h1 / g_a1: NHWC [B, Hf, Hf, 256]; 4 <= Hf <= 32. */

@@ -107,8 +107,8 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_WARP_LDS = 8, MG_TUNE_SHORTK = 9, MG_TUNE_ATOMIC_BLOCKS = 10, MG_TUNE_DETERMINISTIC = 11,
        MG_TUNE_S1_OFF = 12,  // 1: weight gradients of stride-1 convs through the generic LdMCConv (A/B)
        MG_TUNE_D0_STORE = 13,  // mg_d0_fwd output path: 0 automatic, 1 straight from the accumulators, 2 LDS-staged rows
-       MG_TUNE_FFN_BWD_OCC = 14,  // mg_moe_ffn_bwd: 0 two blocks per CU (128 VGPRs), 1 one block (256 VGPRs)
-       MG_TUNE_WIDE_WGRAD = 15,   // 1: linear-layer weight gradients through the generic split-K GEMM (A/B)
+       MG_TUNE_FFN_BWD_OCC = 14,  // mg_moe_ffn_bwd: 0 automatic (one block per CU, 256 VGPRs), 2 two blocks (128 VGPRs)
+       MG_TUNE_WIDE_WGRAD = 15,   // 1: linear-layer weight gradients through the generic split-K GEMM (A/B), 2: wide kernel on every eligible shape
        MG_TUNE_COUNT = 16 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 // Deterministic mode (mg_set_tuning(MG_TUNE_DETERMINISTIC, 1)): every reduction that crosses workgroups runs in

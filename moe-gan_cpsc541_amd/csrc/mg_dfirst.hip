@@ -652,7 +652,7 @@ extern "C" int mg_d0_dgrad(const void* g, int B, int OH, int OW, const void* w0p
 // Discriminator head, image channels (output_layer.0: 4x4 valid conv 256 -> 1, t2i_moe_gan.py:901-907), bf16 step.
 //  * k_dhead_fwd: one block per image: P[px][tap] = h1[px] . W2[:, tap] on MFMA (A rows straight from HBM, the
 //    [16 x 256] tap-major weight as B), P in LDS, out[oy][ox] = sum_tap P[(oy+kh, ox+kw)][tap] in k_head_sum's order.
-//    Replaces the [pixels x 16] fp32 GEMM output + the separate shifted sum (bit-identical: same MFMA k order).
+//    Replaces the [pixels x 16] fp32 GEMM output + the separate shifted sum (fp32 summation-order agreement).
 //  * k_dhead_bwd: one block per image: g_a1[px][c] = LeakyReLU'(h1[px][c]) * sum_tap G[px][tap] W2[c][tap] with the
 //    tap-expanded gradient G[px][tap] = g[y-kh][x-kw] formed in registers from the image's logit gradients (no
 //    [pixels x 16] matrix), the K = 16 product on one MFMA per 16 x 16 block: bit-identical to mg_disc_head_gmat +

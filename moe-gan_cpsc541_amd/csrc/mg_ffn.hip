@@ -411,7 +411,8 @@ __device__ __forceinline__ void ffn_bwd_body(
   }
 }
 
-// two blocks per CU (128 VGPRs, a few spilled) or one with room for the live ranges (A/B: MG_TUNE_FFN_BWD_OCC)
+// two blocks per CU (128 VGPRs, a few spilled; A/B only: MG_TUNE_FFN_BWD_OCC = 2) or one with room for the live
+// ranges (the default: 174 vs 220 us at the C2 step's shapes, profiles/round4_ffn_bwd_probe.txt)
 template <int C>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_moe_ffn_bwd(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
@@ -493,8 +494,8 @@ extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngro
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* part = reinterpret_cast<float*>(mg_workspace((size_t)max_tiles * Hd * sizeof(float), st));
   if (!part) return MG_ERR_ARG;
-  // C = 256: 144 KiB of LDS, one block per CU, so the 256-VGPR form
-  const bool one_block = C == 256 || g_mg_tune[MG_TUNE_FFN_BWD_OCC] == 1;
+  // C = 256: 144 KiB of LDS, one block per CU, so the 256-VGPR form; C = 128: measured faster too
+  const bool one_block = C == 256 || g_mg_tune[MG_TUNE_FFN_BWD_OCC] != 2;
 #define L_(K, CC)                                                                                                    \
   hipLaunchKernelGGL(K<CC>, dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),                  \
                      reinterpret_cast<const bf16_t*>(pre), ngroups, row_off, tile_off, Hd,                            \

@@ -151,6 +151,10 @@ bool mg_wgrad_wide(int M, int N, int K, const void* A, int64_t lda, const void* 
                    float alpha, hipStream_t st) {
   if (g_mg_tune[MG_TUNE_WIDE_WGRAD] == 1) return false;  // A/B: the generic split-K GEMM
   if (K < 2048 || M % 8 || N % 8 || (int64_t)M * N > 1024 * 1024) return false;
+  // measured (profiles/round4_wgrad_wide_probe.txt): a win only when K is long against the tile edges -- the
+  // (384|128) x 128 x 65536 projections, 1.2-1.3x; at K = 4096-16384 the partial-tile folds cost more than the
+  // generic GEMM's re-reads save, and a 16-wide N leaves the MFMA tile mostly empty (2: every eligible shape, tests)
+  if (g_mg_tune[MG_TUNE_WIDE_WGRAD] != 2 && ((int64_t)K < 64 * (int64_t)(M + N) || M < 64 || N < 64)) return false;
   const bool big = M >= 256 && N >= 256;
   const int BM = big ? 256 : 128, BN = big ? 256 : 128;
   const int64_t tiles = (int64_t)cdiv(M, BM) * cdiv(N, BN), MN = (int64_t)M * N;

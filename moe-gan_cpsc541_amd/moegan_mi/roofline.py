@@ -25,7 +25,7 @@ FAMILIES = {
     "conv_fwd_mx8": ("mfma8", ("mg_conv2d_fwd_mx8",)),  # MX-fp8 (C5): priced against the fp8 MFMA peak
     "conv_dgrad_s2": ("mfma", ("mg_conv2d_dgrad_s2",)),
     "conv_wgrad+fold": ("mfma", ("mg_conv2d_wgrad",)),
-    "expert_gemm": ("mfma", ("mg_gemm_grouped", "mg_gemm_grouped_wgrad", "mg_moe_ffn_fwd")),
+    "expert_gemm": ("mfma", ("mg_gemm_grouped", "mg_gemm_grouped_wgrad", "mg_moe_ffn_fwd", "mg_moe_ffn_bwd")),
     "gemm": ("mfma", ("mg_gemm", "mg_gemm_batch")),
     "attention": ("mfma", ("mg_attn_fwd", "mg_attn_bwd")),
     "router_fwd": ("hbm", ("mg_router_fwd",)),
@@ -63,7 +63,7 @@ KERNELS = [
     (r"k_wgrad_fold|splitk_reduce_kernel<mg::Epi<float>", "conv_wgrad+fold"),
     (r"k_mx8_conv", "conv_fwd_mx8"),
     # TAG = 1 instantiations (mg_gemm.h: "..., TAG, X3>("), fused FFN
-    (r"gemm_kernel<.*, 1(, (true|false))?>\(|k_moe_ffn_fwd", "expert_gemm"),
+    (r"gemm_kernel<.*, 1(, (true|false))?>\(|k_moe_ffn_fwd|k_moe_ffn_bwd|k_ffn_bias_fold", "expert_gemm"),
     (r"gemm_kernel<[^>]*LdKCConvT", "conv_dgrad_s2"),
     (r"gemm_kernel<.*LdMCConv", "conv_wgrad+fold"),
     (r"gemm_kernel<.*LdKCConv", "conv_fwd"),
@@ -83,7 +83,8 @@ KERNELS = [
     (r"k_router_bwd|k_fold_partials|k_gate_grad|k_token_grad|k_router_feat_grad|k_feat_grad_fin|k_router_param_bwd|"
      r"k_disp_|k_router_kl", "router_aux"),
     (r"k_im2col|k_col2im", "im2col_col2im"),
-    (r"k_d0_", "d_conv0"),
+    (r"k_d0_|k_fold_cols", "d_conv0"),
+    (r"k_wgrad_wide|k_wide_fold|k_wide_final", "gemm"),
     (r"k_cast|k_copy2d|k_mask_mul|k_up2|k_const_fwd|k_gated_axpy|k_select_if|k_zero_if|k_clip_patches",
      "elementwise"),
     (r"k_head_|k_d_text|k_dhead_", "disc_head"),

@@ -333,8 +333,9 @@ def test_conv_wgrad_stride1_loader(dtype, B, H, Cin, Cout, k):
                                          (1536, 512, 4096, 1.0), (256, 16, 65536, 1.0), (136, 200, 5000, 1.0)])
 def test_wide_weight_gradient(M, N, K, alpha):
     """Linear-layer weight gradients C += alpha * A^T B (bf16 [K][M] x [K][N], fp32 C through an atomic epilogue):
-    the wide split-K kernel (csrc/mg_wgrad_wide.hip) against fp64 on the same bf16 operands and against the generic
-    split-K GEMM (tuning slot 15); fixed-order fold: two calls give the same bits."""
+    the wide split-K kernel (csrc/mg_wgrad_wide.hip, forced onto every eligible shape: tuning slot 15 = 2) against
+    fp64 on the same bf16 operands and against the generic split-K GEMM (slot 15 = 1); fixed-order fold: two calls
+    give the same bits.  The automatic routing (slot 15 = 0) is held to the same fp64 bound."""
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     A = torch.randn(K, M, device=DEV, generator=g).bfloat16()
     B = torch.randn(K, N, device=DEV, generator=g).bfloat16()
@@ -344,9 +345,11 @@ def test_wide_weight_gradient(M, N, K, alpha):
         C = torch.full((M, N), 0.5, device=DEV)
         ops.gemm(A, B, M, N, K, a_kc=False, b_kc=False, out=C, ep=ops.E(alpha=alpha, atomic=1), splits=0)
         return C
-    C1, C2 = run(), run()
-    L.call("mg_set_tuning", 15, 1)
+    C4 = run()
+    L.call("mg_set_tuning", 15, 2)
     try:
+        C1, C2 = run(), run()
+        L.call("mg_set_tuning", 15, 1)
         C3 = run()
     finally:
         L.call("mg_set_tuning", 15, 0)
@@ -355,3 +358,4 @@ def test_wide_weight_gradient(M, N, K, alpha):
     assert float((C1.double() - ref).abs().max()) <= 2e-6 * scale * (K / 4096) ** 0.5 + 1e-6
     assert float((C1 - C3).abs().max()) <= 4e-6 * scale * (K / 4096) ** 0.5 + 1e-6
     assert torch.equal(C1, C2)
+    assert float((C4.double() - ref).abs().max()) <= 2e-6 * scale * (K / 4096) ** 0.5 + 1e-6

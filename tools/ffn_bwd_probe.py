@@ -41,13 +41,13 @@ def fused():
 
 
 gf = 2 * 2.0 * n * C * Hd / 1e9
-def fused_w2():
-    L.call("mg_set_tuning", 14, 1)
+def fused_2blk():
+    L.call("mg_set_tuning", 14, 2)
     fused()
     L.call("mg_set_tuning", 14, 0)
 
 
-for name, fn in (("unfused gP+gX+colsum", unfused), ("fused mg_moe_ffn_bwd", fused), ("fused, 1 block/CU", fused_w2)):
+for name, fn in (("unfused gP+gX+colsum", unfused), ("fused (1 block/CU)", fused), ("fused, 2 blocks/CU", fused_2blk)):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()

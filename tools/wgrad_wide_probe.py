@@ -19,7 +19,7 @@ for M, N, K in SHAPES:
     B = torch.randn(K, N, device=DEV, generator=g).bfloat16()
     C = torch.zeros(M, N, device=DEV)
     res = []
-    for mode in (1, 0):
+    for mode in (1, 2, 0):  # generic, wide (forced), automatic routing
         L.call("mg_set_tuning", 15, mode)
         fn = lambda: ops.gemm(A, B, M, N, K, a_kc=False, b_kc=False, out=C, ep=ops.E(atomic=1), splits=0)  # noqa
         for _ in range(3):
@@ -34,5 +34,5 @@ for M, N, K in SHAPES:
         res.append(s.elapsed_time(e) / 20 * 1e3)
     L.call("mg_set_tuning", 15, 0)
     mb = K * (M + N) * 2 / 1e6
-    print(f"({M:5d},{N:4d},{K:6d}) generic {res[0]:7.1f} us  wide {res[1]:7.1f} us  ({mb:.0f} MB operands: "
-          f"{mb / res[1]:.2f} TB/s wide)", flush=True)
+    print(f"({M:5d},{N:4d},{K:6d}) generic {res[0]:7.1f} us  wide {res[1]:7.1f} us  auto {res[2]:7.1f} us  "
+          f"({mb:.0f} MB operands: {mb / res[1]:.2f} TB/s wide)", flush=True)
