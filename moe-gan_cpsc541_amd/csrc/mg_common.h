@@ -109,7 +109,8 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_D0_STORE = 13,  // mg_d0_fwd output path: 0 automatic, 1 straight from the accumulators, 2 LDS-staged rows
        MG_TUNE_FFN_BWD_OCC = 14,  // mg_moe_ffn_bwd: 0 automatic (one block per CU, 256 VGPRs), 2 two blocks (128 VGPRs)
        MG_TUNE_WIDE_WGRAD = 15,   // 1: linear-layer weight gradients through the generic split-K GEMM (A/B), 2: wide kernel on every eligible shape
-       MG_TUNE_COUNT = 16 };
+       MG_TUNE_NARROW = 16,  // the 32-channel 3x3 convs (offset heads) through the implicit GEMM: 1 all, 2 fwd, 3 dgrad, 4 wgrad
+       MG_TUNE_COUNT = 17 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 // Deterministic mode (mg_set_tuning(MG_TUNE_DETERMINISTIC, 1)): every reduction that crosses workgroups runs in
 // a fixed order -- per-block partial rows in the stream's workspace folded by one pass, or one writer per
@@ -166,6 +167,13 @@ static inline void mg_det_fold_rows(const float* part, int nrows, int ncols, int
   } while (0)
 
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// mg_narrow.hip: direct 3x3 / s1 / p1 convs with a 32-channel side on 4x4 .. 16x16 maps (bf16 NHWC operands)
+bool mg_conv3_direct_ok(int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad, bool wgrad);
+bool mg_conv3_direct(const void* x, int B, int H, int Cin, const void* wpack, int Cout, const mg_epilogue* e, void* y,
+                     int64_t ldy, int y_dtype, hipStream_t st);
+bool mg_wgrad3_direct(const void* gy, int64_t ldg, const void* x, int B, int H, int Cin, float** ws_out, int* splits,
+                      hipStream_t st);
 
 // mg_wgrad_wide.hip: wide split-K weight gradients (bf16 [K][M] x [K][N] -> fp32 C +=), true when handled
 bool mg_wgrad_wide(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,

@@ -363,6 +363,11 @@ template <typename T, typename TO>
 void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW,
                     int stride, int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e,
                     hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {  // 32-channel 3x3 convs on small maps (offset heads): direct, halo tiles in LDS
+    if (!sc && mg_conv3_direct_ok(H, W, Cin, Cout, KH, KW, stride, pad, false) &&
+        mg_conv3_direct(x, B, H, Cin, wpack, Cout, e, y, ldy, std::is_same<TO, float>::value ? MG_F32 : MG_BF16, st))
+      return;
+  }
   const bool small_c = Cin < Tile<T>::BK;  // a K step spans several taps: per-lane tap decode
   if (small_c ? conv_slabs<T, TO, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st)
               : conv_slabs<T, TO, false>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st))
@@ -575,6 +580,16 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
                                                                                       : P / 2048));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == MG_BF16 && !in_scale && Cout == 32 && Cin >= 32 && mg_conv3_direct_ok(H, W, Cin, Cout, KH, KW, stride, pad, true)) {
+    float* ws = nullptr;
+    int ng = 0;
+    if (mg_wgrad3_direct(gy, ldg, x, B, H, Cin, &ws, &ng, st)) {
+      const int lgCC = 3;  // 32 x Cin / 8 fold blocks
+      hipLaunchKernelGGL(k_wgrad_fold, dim3(Cout, Cin >> lgCC), dim3(256), (size_t)9 * sizeof(float) << lgCC, st, ws,
+                         ng, Cout, ilog2(Cin), 9, lgCC, gw);
+      return mg_check_launch("mg_conv2d_wgrad (direct 3x3, 32 channels)");
+    }
+  }
   if (dtype == MG_BF16 && slabs && in_scale && tile == 128 && Cout >= 128 && N >= 128 &&
       run_wgrad_slabs<bf16_t, 128, 128, true>(gy, ldg, x, B, H, W, Cin, in_scale, Cout, KH, KW, stride, pad, gw,
                                                splits, st))

@@ -69,15 +69,27 @@ def _mtm_lrelu(y, pre):
     return torch.where(m, y, 0.2 * y)
 
 
+def offset_act(o):
+    """The offset head's LeakyReLU(0.2) (offset_net.1, t2i_moe_gan.py:199-203), a named step of mtm() so that a
+    bf16 emulation (tests/steputil.bf16_module_rounding) can round the activation the device stores in bf16."""
+    return F.leaky_relu(o, 0.2)
+
+
+def warp(x, grid):
+    """Bilinear sampling of the MTM input at the offset grid (:239); named like offset_act (the device's warped
+    map is bf16, its gradient fp32)."""
+    return F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=False)
+
+
 def mtm(x, w, P, pre, use_offset=True):
     B, C, H, W = x.shape
     if use_offset:
         o = F.conv2d(x, P[pre + "offset_net.0.weight"], P[pre + "offset_net.0.bias"], padding=1)  # :223
-        o = F.leaky_relu(o, 0.2)
+        o = offset_act(o)
         o = F.conv2d(o, P[pre + "offset_net.2.weight"], P[pre + "offset_net.2.bias"], padding=1)
         grid = base_grid(H, W, dtype=x.dtype).unsqueeze(0) + o.permute(0, 2, 3, 1) * 0.05  # :226-235
         grid = grid.clamp(-1, 1)  # :236
-        x = F.grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=False)  # :239
+        x = warp(x, grid)
     x = modconv(x, w, P, pre + "modulated_conv.", padding=1)
     return _mtm_lrelu(x, pre)  # :245
 

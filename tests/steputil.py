@@ -218,7 +218,8 @@ class bf16_module_rounding:
     how far bf16 storage alone, in otherwise exact fp32 arithmetic, moves them.  (The LayerNorm / GELU / MHA /
     MoE-output points are the device's bf16 tensors ``n1``/``n2``/``n3``, ``Hid``, the attention output and the
     combine output, engine_g.py; the oracle computes them in fp32.)"""
-    NAMES = ("modconv", "mtm", "attention_block", "expert_ffn", "conv_block", "mha", "sparse_moe")
+    NAMES = ("modconv", "mtm", "attention_block", "expert_ffn", "conv_block", "mha", "sparse_moe", "offset_act")
+    VALUE_NAMES = ("warp",)  # stored in bf16, gradient kept fp32 (the MTM's warped map; g_xw is fp32, engine_g.py)
     FUNCS = ("layer_norm", "gelu")  # torch.nn.functional, as the oracle calls them inside the blocks
 
     def __init__(self, attention_internals=True, rounder=None):
@@ -228,7 +229,7 @@ class bf16_module_rounding:
     def __enter__(self):
         self.prev_rounder = _ROUNDER[0]
         _ROUNDER[0] = self.rounder
-        self.orig = {n: getattr(O, n) for n in self.NAMES}
+        self.orig = {n: getattr(O, n) for n in self.NAMES + self.VALUE_NAMES}
         self.orig_f = {n: getattr(O.F, n) for n in self.FUNCS}
         inner = dict(self.orig)
         if self.attention_internals:  # the multi-head attention with the MFMA kernel's bf16 operands (below)
@@ -239,8 +240,12 @@ class bf16_module_rounding:
                 r = f(*a, **k)
                 return (_RoundBoth.apply(r[0]),) + tuple(r[1:]) if isinstance(r, tuple) else _RoundBoth.apply(r)
             return wrap
+        def value_wrapper(f):
+            def wrap(*a, **k):
+                return self.rounder.st(f(*a, **k))
+            return wrap
         for n, f in inner.items():
-            setattr(O, n, wrapper(f))
+            setattr(O, n, value_wrapper(f) if n in self.VALUE_NAMES else wrapper(f))
         for n, f in self.orig_f.items():
             setattr(O.F, n, wrapper(f))
         return self
