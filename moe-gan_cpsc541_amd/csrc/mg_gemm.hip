@@ -74,6 +74,14 @@ void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int
     run_plain_orient<T, TO, 64, 64>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
     return;
   }
+  // short K over many rows (the token projections, K = 128 / 256 at 16K-64K rows): each tile's K loop is one or two
+  // steps, so it is bound by load latency and more, smaller tiles keep more bytes in flight (measured at the C2
+  // shapes: 65536 x 256 x 128 26.5 -> 15.7 us, 65536 x 384 x 128 28.5 -> 22.5 us on 64^2;
+  // profiles/round4_shortk_probe.txt)
+  if (tile == 0 && K <= 256 && M >= 16384) {
+    run_plain_orient<T, TO, 64, 64>(a_kc, b_kc, M, N, K, A, lda, B, ldb, C, ldc, e, splits, st);
+    return;
+  }
   if constexpr (sizeof(T) == 2) {
     // 128 x 256 when N fills it and the grid covers the chip (measured: 4096^3 bf16 816 -> 920 TF/s;
     // the step's few-tile projections stay on 128^2 / 64^2)
@@ -403,7 +411,8 @@ void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpa
       run_conv<T, TO, 128, 32>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
       return;
     }
-    if (tile == 257 || (tile == 0 && Cout % 256 == 0 && cdiv(M, 128) * (int64_t)(Cout / 256) >= 480)) {
+    if (tile == 257 || (tile == 0 && Cout % 256 == 0 && cdiv(M, 128) * (int64_t)(Cout / 256) >= 480 &&
+                        !(KH * KW * Cin <= 256 && M >= 16384))) {
       run_conv<T, TO, 128, 256>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
       return;
     }
@@ -412,7 +421,9 @@ void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpa
       return;
     }
   }
-  if (tile == 128 || (tile == 0 && cdiv(M, 128) * (int64_t)cdiv(Cout, 128) >= 480 && Cout > 64))
+  // 1x1 convs over many pixels (K = Cin <= 256): latency-bound single-step tiles, as the short-K GEMMs above
+  const bool short_k = KH * KW * Cin <= 256 && M >= 16384;
+  if (tile == 128 || (tile == 0 && !short_k && cdiv(M, 128) * (int64_t)cdiv(Cout, 128) >= 480 && Cout > 64))
     run_conv<T, TO, 128, 128>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);
   else
     run_conv<T, TO, 64, 64>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st);

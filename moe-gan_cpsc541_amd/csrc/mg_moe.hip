@@ -768,13 +768,20 @@ __global__ __launch_bounds__(NT) void k_grouped_colsum_v(const T* __restrict__ X
                                                          const float* __restrict__ rs, const int* __restrict__ row_off,
                                                          int G, int N, int rows_per_block, float* __restrict__ out) {
   __shared__ float red[NT * 8];
+  __shared__ int ro[65];  // row_off staged once: the group searches below are LDS reads, not chains of dependent
+                          // global loads (8 of them cost ~8 us before the first row was read)
   const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int n = (blockIdx.x * TX + tx) * 8;
-  const int total = row_off[G];
+  {
+    const int t = ty * TX + tx;
+    if (t <= G) ro[t] = row_off[t];
+  }
+  __syncthreads();
+  const int total = ro[G];
   const int r0 = blockIdx.y * rows_per_block, r1 = min(total, r0 + rows_per_block);
   if (r0 >= r1) return;
   int glast = 0;
-  while (glast < G && row_off[glast + 1] <= r1 - 1) ++glast;
+  while (glast < G && ro[glast + 1] <= r1 - 1) ++glast;
   float s[8], v[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = 0.f;
@@ -791,8 +798,8 @@ __global__ __launch_bounds__(NT) void k_grouped_colsum_v(const T* __restrict__ X
         }
       }
       g = 0;
-      while (g < G && row_off[g + 1] <= r) ++g;
-      gend = row_off[g + 1];
+      while (g < G && ro[g + 1] <= r) ++g;
+      gend = ro[g + 1];
     }
     if (!idx && !rs && r + 3 * TY < min(gend, r1)) {  // four rows of one group: independent loads in flight
       float v1[8], v2[8], v3[8];
@@ -842,13 +849,19 @@ __global__ __launch_bounds__(256) void k_grouped_colsum_part(const T* __restrict
                                                              const int* __restrict__ row_off, int G, int N, int rpb,
                                                              float* __restrict__ part) {
   __shared__ float red[256 * 8];
+  __shared__ int ro[65];  // row_off staged once (see k_grouped_colsum_v)
   const int tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int n = (blockIdx.x * TX + tx) * 8;
   const bool live = n < N;
-  const int total = row_off[G];
+  {
+    const int t = ty * TX + tx;
+    if (t <= G) ro[t] = row_off[t];
+  }
+  __syncthreads();
+  const int total = ro[G];
   const int r0 = blockIdx.y * rpb, r1 = min(total, r0 + rpb);
   for (int g = 0; g < G; ++g) {
-    const int gs = max(r0, row_off[g]), ge = min(r1, row_off[g + 1]);
+    const int gs = max(r0, ro[g]), ge = min(r1, ro[g + 1]);
     if (gs >= ge) continue;  // block-uniform
     float s[8], v[8];
 #pragma unroll
