@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   constexpr int TBK = tile_bk<T, X3>();
   // ---- resolve tile / group ----
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (grp.mode == 0 && grp.swz && (grp.swz == 1 || gridDim.z > 1)) {
+  if ((grp.mode == 0 || grp.mode == 1) && grp.swz && (grp.swz == 1 || gridDim.z > 1)) {
     // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs by linear id, so blocks that
     // share an XCD (linear id % 8) take a contiguous run of (split, m-tile, n-tile) work items, n fastest --
     // all tiles of one K split (which read the same operand rows: a split-K weight gradient re-reads its
@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   int kbeg = bz * kchunk, kend = min(K, kbeg + kchunk);
   int g = 0;
   if (grp.mode == 1) {
-    int t = blockIdx.x;
+    int t = bx;
     g = -1;
     for (int i = 0; i < grp.ngroups; ++i)
       if (t >= grp.tile_off[i] && t < grp.tile_off[i + 1]) { g = i; break; }
@@ -1176,7 +1176,11 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   dim3 grid(gx, cdiv(N, BN), gz);
   EP e2 = ep;
   e2.vec_ok = e2.host_vec_ok() ? 1 : 0;
-  if (grp.mode == 0) grp.swz = g_mg_tune[MG_TUNE_XCD];
+  // XCD-aware order (gemm_kernel), A/B only: tuning slot MG_TUNE_XCD 1 every launch (dense or grouped), 2 split-K
+  // launches.  Measured neutral-to-worse on the short-K token projections and the expert GEMMs (their row tiles
+  // re-read per column tile already hit in L2: profiles/round4_xcd_probe.txt), so off by default.
+  const int xcd = g_mg_tune[MG_TUNE_XCD];
+  if (grp.mode == 0 || grp.mode == 1) grp.swz = xcd == 3 ? 0 : xcd;
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP, TAG, X3>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
                      K, kchunk, grp);
 }

@@ -13,7 +13,12 @@ namespace {
 
 constexpr Grouping kNoGroup{0, 1, nullptr, nullptr, 0};
 // plain (ungrouped) launch with the tuned XCD tile order (MG_TUNE_XCD), for the direct split-K slab launches
-inline Grouping xcd_group() { Grouping g = kNoGroup; g.swz = g_mg_tune[MG_TUNE_XCD]; return g; }
+inline Grouping xcd_group() {
+  Grouping g = kNoGroup;
+  const int x = g_mg_tune[MG_TUNE_XCD];
+  g.swz = x == 3 ? 0 : x;
+  return g;
+}
 
 inline bool a_xf(const mg_epilogue* e) { return e && (e->a_idx || e->a_rowscale || e->a_gelu); }
 
@@ -655,8 +660,11 @@ void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_o
                  e ? e->a_gelu : 0};
   Grouping grp{1, ngroups, row_off, tile_off, 0};
   if constexpr (sizeof(T) == 2) {
-    // 128 x 256 tiles (same 128-row tile prefix, half the column tiles)
-    if (g_mg_tune[MG_TUNE_GEMM_TILE] == 257 && N >= 256) {
+    // 128 x 256 tiles (same 128-row tile prefix, half the column tiles): by default for one 256-wide column tile
+    // over a long K (the 8x8 block's expert layer 2, 32768 x 256 x 1024: 44 -> 39 us; wider N measured slower,
+    // profiles/round4_grouped_probe.txt)
+    const int tl = g_mg_tune[MG_TUNE_GEMM_TILE];
+    if ((tl == 257 && N >= 256) || (tl == 0 && N == 256 && K >= 1024)) {
       if constexpr (BKc) {
         LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
         launch_gemm<T, 128, 256, true, true, 1>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
