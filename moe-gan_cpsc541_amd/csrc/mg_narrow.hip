@@ -299,8 +299,9 @@ bool launch_conv(const void* x, int B, int Cin, const void* wpack, int Cout, con
   ep.vec_ok = ep.host_vec_ok() ? 1 : 0;
   if (!ep.vec_ok) return false;
   // few tiles (8x8, 4x4 maps): split the channel chunks over blockIdx.z so ~512 blocks stream the input
+  const int tb = g_mg_tune[MG_TUNE_NARROW_BLOCKS], target = tb > 0 ? tb : 512;
   int splits = 1;
-  while (splits < nch && (int64_t)tiles * cdiv(Cout, CT) * splits < 512 && nch % (2 * splits) == 0) splits *= 2;
+  while (splits < nch && (int64_t)tiles * cdiv(Cout, CT) * splits < target && nch % (2 * splits) == 0) splits *= 2;
   const bf16_t* xb = reinterpret_cast<const bf16_t*>(x);
   const bf16_t* wb = reinterpret_cast<const bf16_t*>(wpack);
   const dim3 grid(tiles, cdiv(Cout, CT), splits);
@@ -363,7 +364,8 @@ bool mg_wgrad3_direct(const void* gy, int64_t ldg, const void* x, int B, int H, 
   if (ldg % 8 || Cin % WG_CC) return false;
   const int P = B * H * H, ntiles = cdiv(P, TP), chunks = Cin / WG_CC;
   // ~256 blocks (one per CU; each streams its tiles with the next one's loads in flight), >= 4 tiles per group
-  int ngroups = std::max(1, std::min(ntiles / 4, 256 / chunks));
+  const int tb = g_mg_tune[MG_TUNE_NARROW_BLOCKS], target = tb > 0 ? tb : 256;
+  int ngroups = std::max(1, std::min(ntiles / 2, target / chunks));
   ngroups = (ngroups + 7) / 8 * 8;  // whole XCD rounds (groups past the last tile exit at once)
   const int tpg = cdiv(ntiles, ngroups);
   float* ws = reinterpret_cast<float*>(mg_workspace((size_t)ngroups * 32 * 9 * Cin * sizeof(float), st));

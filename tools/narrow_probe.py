@@ -14,6 +14,7 @@ from moegan_mi import ops  # noqa: E402
 DEV, bf = "cuda", torch.bfloat16
 B = int(os.environ.get("B", "256"))
 SHAPES = [(16, 256), (16, 128), (8, 512), (8, 256), (4, 512)]
+BLOCKS = [int(b) for b in os.environ.get("BLOCKS", "").split()]
 
 
 def timed(fn, reps=20):
@@ -50,5 +51,11 @@ for S, C in SHAPES:
         t_old = timed(fn)
         L.call("mg_set_tuning", 16, 0)
         t_new = timed(fn)
+        alt = []
+        for blocks in BLOCKS:  # grid-target sweep (tuning slot 17)
+            L.call("mg_set_tuning", 17, blocks)
+            alt.append(timed(fn))
+        L.call("mg_set_tuning", 17, 0)
+        sweep = "  ".join(f"{b}:{t:5.1f}" for b, t in zip(BLOCKS, alt))
         print(f"{S:2d}x{S:<2d} C={C:3d} {name:5s} generic {t_old:6.1f} us  direct {t_new:6.1f} us  "
-              f"({nbytes / 1e6:5.1f} MB: {nbytes / t_new / 1e6:.2f} TB/s)", flush=True)
+              f"({nbytes / 1e6:5.1f} MB: {nbytes / t_new / 1e6:.2f} TB/s)  {sweep}", flush=True)
