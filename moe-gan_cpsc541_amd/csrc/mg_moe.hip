@@ -325,6 +325,95 @@ __global__ __launch_bounds__(256) void k_disp_scatter(const int* __restrict__ to
   }
 }
 
+// k_disp_scatter with the block-count scan folded in (one launch less per dispatch, ~5 us): every block sums the
+// per-block counts of the blocks before it (its bases) and of all blocks (the expert totals -> row offsets) from
+// blk_counts, which k_disp_count left in L2; block 0 also writes row_off / tile_off.  Same positions as the
+// three-kernel form (exclusive prefixes in block order, integer sums).
+template <int E>
+__global__ __launch_bounds__(256) void k_disp_scatter_scan(const int* __restrict__ topi, const float* __restrict__ gate,
+                                                           int n, int nblk, int bm, const int* __restrict__ blk_counts,
+                                                           int* __restrict__ row_off, int* __restrict__ tile_off,
+                                                           int* __restrict__ perm, int* __restrict__ pos_of,
+                                                           float* __restrict__ gate_pos) {
+  constexpr int R = DCH / 256, P = 256 / E;
+  __shared__ int wc[R * 4][E];
+  __shared__ int red_pre[256], red_tot[256];
+  __shared__ int tot_sh[E];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int a0 = blockIdx.x * DCH;
+  int ex_r[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int a = a0 + r * 256 + tid;
+    ex_r[r] = a < n ? topi[a] : -1;
+  }
+  {  // thread (q, e): the counts of expert e in blocks q, q + P, ... (before this block, and in all)
+    const int e = tid % E, q = tid / E;
+    int pre = 0, tot = 0;
+    for (int bb = q; bb < nblk; bb += P) {
+      const int c = blk_counts[bb * E + e];
+      tot += c;
+      pre += bb < (int)blockIdx.x ? c : 0;
+    }
+    red_pre[tid] = pre;
+    red_tot[tid] = tot;
+  }
+  int rk[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    int rank = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint64_t m = __ballot(ex_r[r] == e);
+      if (ex_r[r] == e)
+        rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (lane == 0) wc[r * 4 + wid][e] = __popcll(m);
+    }
+    rk[r] = rank;
+  }
+  __syncthreads();
+  if (tid < E) {
+    int t = 0;
+    for (int q = 0; q < P; ++q) t += red_tot[q * E + tid];
+    tot_sh[tid] = t;
+  }
+  __syncthreads();
+  if (tid < E) {  // (round, wave) order = assignment order
+    const int e = tid;
+    int base = 0;
+    for (int e2 = 0; e2 < e; ++e2) base += tot_sh[e2];
+    for (int q = 0; q < P; ++q) base += red_pre[q * E + e];
+    for (int q = 0; q < R * 4; ++q) {
+      const int c = wc[q][e];
+      wc[q][e] = base;
+      base += c;
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    int r = 0, tl = 0;
+    for (int i = 0; i < E; ++i) {
+      row_off[i] = r;
+      tile_off[i] = tl;
+      r += tot_sh[i];
+      tl += (tot_sh[i] + bm - 1) / bm;
+    }
+    row_off[E] = r;
+    tile_off[E] = tl;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int a = a0 + r * 256 + tid;
+    const int ex = ex_r[r];
+    if (a < n && (unsigned)ex < (unsigned)E) {
+      const int pos = wc[r * 4 + wid][ex] + rk[r];
+      perm[pos] = a;
+      pos_of[a] = pos;
+      gate_pos[pos] = gate[a];
+    }
+  }
+}
+
 // out[t] = resid[t] + sum_j gate[t,j] * Y[pos_of[t*k+j]]
 template <typename T>
 __global__ void k_combine(const T* __restrict__ Y, int64_t ldy, const int* __restrict__ pos_of,
@@ -1101,6 +1190,13 @@ extern "C" int mg_moe_dispatch(const int32_t* topi, const float* gate, int T, in
   int nb = cdiv(n, DCH);
   MG_REQUIRE(nb <= 65535, "too many assignments");
   hipLaunchKernelGGL(k_disp_count, dim3(nb), dim3(256), E * sizeof(int), st, topi, n, E, ws);
+  if (g_mg_tune[MG_TUNE_DISPATCH3] != 1) {  // the scan folded into the scatter (A/B: 1 = three kernels)
+#define L_(EE) hipLaunchKernelGGL((k_disp_scatter_scan<EE>), dim3(nb), dim3(256), 0, st, topi, gate, n, nb, bm, ws, \
+                                  row_off, tile_off, perm, pos_of, gate_pos)
+    if (E == 4) L_(4); else if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
+#undef L_
+    return mg_check_launch("mg_moe_dispatch");
+  }
   // gfx950 assumption: at the 16384-count cutoff the parallel scan takes (16384 + 1056) * 4 B = 69.7 KB of dynamic
   // LDS, over the 64 KB of older parts but within the 160 KB a gfx950 workgroup may use
   if ((int64_t)nb * E <= 16384)

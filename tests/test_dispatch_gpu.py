@@ -3,7 +3,8 @@ dispatch of the top-k assignments): bit-exact against a stable sort of the assig
 E = 4 / 8 / 16 / 32 (C2: 8, C5: 32), k = 1 / 2 / 4, ragged chunk tails (the kernels work in 1024-assignment
 chunks), experts that receive no assignment, the skewed routing of an early-training router, and a size whose
 chunk-count table exceeds the parallel scan's LDS table (the serial scan then runs), and the largest table the parallel scan takes
-(E=32, k=4, T=131072: 512 chunks x 32 = 16384 counts, ~70 KB of dynamic LDS, within gfx950's 160 KB per CU)."""
+(E=32, k=4, T=131072: 512 chunks x 32 = 16384 counts, ~70 KB of dynamic LDS, within gfx950's 160 KB per CU).
+Both launch forms: count + scatter-with-folded-scan (default) and count / scan / scatter (tuning slot 18 = 1)."""
 import pytest
 import torch
 
@@ -27,7 +28,9 @@ def _reference(topi, gate, E, bm):
                                         (16, 2, 3001, False), (4, 1, 1, False), (8, 2, 5, True),
                                         (32, 4, 16384, True), (4, 4, 777, False), (32, 4, 140000, False),
                                         (32, 4, 131072, False)])
-def test_dispatch_matches_stable_sort(E, k, T, skew):
+@pytest.mark.parametrize("three", [0, 1])
+def test_dispatch_matches_stable_sort(E, k, T, skew, three):
+    from moegan_mi import _lib as L
     from moegan_mi import ops
     g = torch.Generator(device=DEV).manual_seed(E * 1000 + k * 10 + T)
     if skew:  # a few experts take most tokens; the upper half of the experts gets none
@@ -38,8 +41,12 @@ def test_dispatch_matches_stable_sort(E, k, T, skew):
         scores = torch.rand(T, E, device=DEV, generator=g)
     topi = scores.topk(k, dim=1).indices.int().contiguous()
     gate = torch.rand(T, k, device=DEV, generator=g)
-    row_off, tile_off, perm, pos_of, gate_pos = ops.moe_dispatch(topi, gate, E)
-    torch.cuda.synchronize()
+    L.call("mg_set_tuning", 18, three)
+    try:
+        row_off, tile_off, perm, pos_of, gate_pos = ops.moe_dispatch(topi, gate, E)
+        torch.cuda.synchronize()
+    finally:
+        L.call("mg_set_tuning", 18, 0)
     r_row, r_tile, r_perm, r_pos, r_gate = _reference(topi, gate, E, 128)
     assert torch.equal(row_off.cpu().long(), r_row)
     assert torch.equal(tile_off.cpu().long(), r_tile)
