@@ -303,16 +303,19 @@ def main():
     real = torch.rand(B, 3, args.res, args.res, device=dev, generator=gen) * 2 - 1
     text = torch.randn(B, 512, device=dev, generator=gen)
     z = torch.randn(B, 512, device=dev, generator=gen)
-    eps_gen = torch.Generator(device=dev).manual_seed(3)  # identical router noise on every rank
     # the step's random inputs live in fixed buffers, refilled before every step (eager or replayed)
     eps_d_flat, eps_d = eps_buffers(E, dev)
     eps_g_flat, eps_g = eps_buffers(E, dev)
     perm = torch.empty(B, device=dev, dtype=torch.int32)
 
+    draws = [0]
+
     def refill():
-        eps_d_flat.normal_(generator=eps_gen)  # fresh router noise for both generator forwards (:349-351)
-        eps_g_flat.normal_(generator=eps_gen)
-        perm.copy_(torch.randperm(B, device=dev, generator=gen))
+        # fresh router noise for both generator forwards (:349-351, identical on every rank) and this rank's
+        # mismatched-caption permutation, one counter-based launch (mg_step_inputs)
+        draws[0] += 1
+        ops.step_inputs(eps_d_flat, eps_g_flat, perm, seed_eps=(3 << 32) + draws[0],
+                        seed_perm=((1000 + rank) << 32) + draws[0])
 
     def run_step():
         return ts.step(real, text, z, eps_d, eps_g, perm, anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8)

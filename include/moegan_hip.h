@@ -510,6 +510,11 @@ int mg_zero_if(void* x, int64_t bytes, const int32_t* flags, int32_t mask, int w
 int mg_gated_axpy(float* acc, const float* g, int64_t n, const int32_t* flags, int32_t mask, void* stream);
 /* out[i] = (flags[0] & mask) ? src[i] : 0  (n <= 4096). */
 int mg_select_if(const float* src, int n, const int32_t* flags, int32_t mask, float* out, void* stream);
+/* A step's random inputs in one launch (csrc/mg_rng.hip): eps_a[0..na) and eps_b[0..nb) ~ N(0, 1) (the router noise
+   of the two generator forwards, t2i_moe_gan.py:302-333) and perm = a uniformly random permutation of 0..B-1 (the
+   mismatched captions, :1278; B <= 4096).  Counter-based: the draws depend only on the two seeds. */
+int mg_step_inputs(float* eps_a, int64_t na, float* eps_b, int64_t nb, int32_t* perm, int B, uint64_t seed_eps,
+                   uint64_t seed_perm, void* stream);
 
 /* generator constant [1,C,4,4] -> NHWC [B,4,4,C] (t2i_moe_gan.py:815). */
 int mg_const_fwd(int dtype, const float* cst, int C, int HW, int B, void* out, void* stream);

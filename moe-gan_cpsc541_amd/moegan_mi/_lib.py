@@ -55,7 +55,8 @@ class WnDesc(ctypes.Structure):
 # Argument types are derived from include/moegan_hip.h itself, so the binding
 # cannot drift from the C ABI (the header travels with the library).
 _HEADER = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "moegan_hip.h"))
-_CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "size_t": ctypes.c_size_t, "float": _f32,
+_CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "uint64_t": ctypes.c_uint64, "size_t": ctypes.c_size_t,
+          "float": _f32,
           "void": _c_void_p, "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc),
           "mg_prep_desc": ctypes.POINTER(PrepDesc), "mg_colsum_desc": ctypes.POINTER(ColsumDesc),
           "mg_wn_desc": ctypes.POINTER(WnDesc)}

@@ -539,6 +539,12 @@ def zero_if(x, flags, mask, when_set=True):
     call("mg_zero_if", ptr(x), x.numel() * x.element_size(), ptr(flags), mask, int(bool(when_set)), S())
 
 
+def step_inputs(eps_a, eps_b, perm, seed_eps, seed_perm):
+    """eps_a, eps_b (fp32) ~ N(0, 1) and perm (int32 [B]) a random permutation, one launch (mg_step_inputs)."""
+    call("mg_step_inputs", ptr(eps_a), eps_a.numel(), ptr(eps_b), eps_b.numel(), ptr(perm), perm.numel(),
+         ctypes.c_uint64(seed_eps & (2 ** 64 - 1)), ctypes.c_uint64(seed_perm & (2 ** 64 - 1)), S())
+
+
 def gated_axpy(acc, g, flags, mask):
     call("mg_gated_axpy", ptr(acc), ptr(g), acc.numel(), ptr(flags), mask, S())
 

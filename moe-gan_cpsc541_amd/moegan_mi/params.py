@@ -193,7 +193,8 @@ class ParamStore:
         self._shadow_version = self.data._version
 
     def zero_grad(self):
-        self.grad.zero_()
+        # the library's 16-B-store fill: torch's fill kernel ran the generator's 38.8 MB at ~1.9 TB/s (21 us per step)
+        ops.zero_if(self.grad, None, 0, when_set=False) if self.grad.is_cuda else self.grad.zero_()
 
     def ensure_acc(self):
         """The window accumulator: with gradient accumulation each batch's gradient is formed in ``grad`` and

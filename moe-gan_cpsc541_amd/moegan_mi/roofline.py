@@ -60,7 +60,8 @@ _FAMILY_OF = {e: f for f, (_, es) in FAMILIES.items() for e in es}
 
 # rocprofv3 kernel name (regex, first match wins) -> family, for PMC attribution
 KERNELS = [
-    (r"k_wgrad_fold|splitk_reduce_kernel<mg::Epi<float>", "conv_wgrad+fold"),
+    (r"k_wgrad_fold|splitk_reduce_kernel<mg::Epi<float>|k_wgrad3_direct", "conv_wgrad+fold"),
+    (r"k_conv3_direct", "conv_fwd"),
     (r"k_mx8_conv", "conv_fwd_mx8"),
     # TAG = 1 instantiations (mg_gemm.h: "..., TAG, X3>("), fused FFN
     (r"gemm_kernel<.*, 1(, (true|false))?>\(|k_moe_ffn_fwd|k_moe_ffn_bwd|k_ffn_bias_fold", "expert_gemm"),
