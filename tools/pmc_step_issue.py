@@ -10,7 +10,7 @@ tot2 = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.Counter()
 seen = set()
 for r in csv.DictReader(open(sys.argv[1])):
-    name = r["Kernel_Name"].replace("unsigned short", "bf16").replace("(anonymous namespace)::", "")[:80]
+    name = r["Kernel_Name"].replace("unsigned short", "bf16").replace("(anonymous namespace)::", "").replace("mg::", "").replace("void ", "")[:110]
     tot[name][r["Counter_Name"]] += float(r["Counter_Value"])
     did = r.get("Dispatch_Id") or r.get("Correlation_Id")
     if (name, did) not in seen:
@@ -18,7 +18,7 @@ for r in csv.DictReader(open(sys.argv[1])):
         calls[name] += 1
 if len(sys.argv) > 3:
     for r in csv.DictReader(open(sys.argv[3])):
-        name = r["Kernel_Name"].replace("unsigned short", "bf16").replace("(anonymous namespace)::", "")[:80]
+        name = r["Kernel_Name"].replace("unsigned short", "bf16").replace("(anonymous namespace)::", "").replace("mg::", "").replace("void ", "")[:110]
         tot2[name][r["Counter_Name"]] += float(r["Counter_Value"])
 steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 allwc = sum(c.get("SQ_WAVE_CYCLES", 0) for c in tot.values())
