@@ -38,10 +38,10 @@ constexpr int TP = 128;  // pixels per tile
 
 // 128-pixel tiles of S x S maps: one image band of TP / S rows (S >= 16) or TP / S^2 whole images.  Staged
 // positions: per image segment (SEGROWS + 2) rows of S + 2 columns (the zero ring of the padding).
-template <int S> struct Geo {
+template <int S, int TPX = TP> struct Geo {
   static constexpr int HW = S * S;
-  static constexpr int SEGROWS = HW >= TP ? TP / S : S;
-  static constexpr int NSEG = HW >= TP ? 1 : TP / HW;
+  static constexpr int SEGROWS = HW >= TPX ? TPX / S : S;
+  static constexpr int NSEG = HW >= TPX ? 1 : TPX / HW;
   static constexpr int PW = S + 2;
   static constexpr int SEGPOS = (SEGROWS + 2) * PW;
   static constexpr int NPOS = NSEG * SEGPOS;
@@ -61,11 +61,14 @@ template <int S> struct Geo {
   static MG_DEV int tap_off(int tap) { return (tap / 3 - 1) * PW + (tap % 3 - 1); }
 };
 
-template <int S, int CC, int CT, typename TO, bool PART>
+// WPX: pixel fragments (16 pixels) per wave -- 2 (128-pixel tiles) or 4 (256-pixel tiles: each weight fragment read
+// from LDS serves four pixel fragments instead of two)
+template <int S, int CC, int CT, typename TO, bool PART, int WPX = 2>
 __global__ __launch_bounds__(NT) void k_conv3_direct(const bf16_t* __restrict__ x, int B, int Cin, int chunks,
                                                      const bf16_t* __restrict__ w, int Cout, Epi<TO> ep,
                                                      float* __restrict__ part, int P) {
-  using G = Geo<S>;
+  constexpr int TP = 64 * WPX;  // pixels per tile (4 waves)
+  using G = Geo<S, TP>;
   constexpr int XP = CC + 8, WPI = 9 * CC + 8;  // LDS pitches (bf16): 8 consecutive rows -> 8 distinct bank quads
   constexpr int XV = CC / 8, NXI = (G::NPOS * XV + NT - 1) / NT, NWI = (CT * 9 * XV + NT - 1) / NT;
   constexpr int WO = CT / 16;
@@ -117,15 +120,15 @@ __global__ __launch_bounds__(NT) void k_conv3_direct(const bf16_t* __restrict__ 
       }
     }
   };
-  // wave wid: pixels 32 wid .. 32 wid + 31 (two fragments) x the CT channels; transposed products leave channels
-  // o0 + 16 of + 4 (lane>>4) + j of pixel 32 wid + 16 mf + (lane&15) in acc[mf][of][j]
-  int pb[2];
+  // wave wid: pixels 16 WPX wid .. (WPX fragments) x the CT channels; transposed products leave channels
+  // o0 + 16 of + 4 (lane>>4) + j of pixel 16 WPX wid + 16 mf + (lane&15) in acc[mf][of][j]
+  int pb[WPX];
 #pragma unroll
-  for (int mf = 0; mf < 2; ++mf) pb[mf] = G::pos(32 * wid + 16 * mf + (lane & 15)) * XP + 8 * (lane >> 4);
+  for (int mf = 0; mf < WPX; ++mf) pb[mf] = G::pos(16 * WPX * wid + 16 * mf + (lane & 15)) * XP + 8 * (lane >> 4);
   const int wb = (lane & 15) * WPI + 8 * (lane >> 4);
-  f32x4_t acc[2][WO];
+  f32x4_t acc[WPX][WO];
 #pragma unroll
-  for (int mf = 0; mf < 2; ++mf)
+  for (int mf = 0; mf < WPX; ++mf)
 #pragma unroll
     for (int of = 0; of < WO; ++of) acc[mf][of] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   load(c_beg);
@@ -139,14 +142,14 @@ __global__ __launch_bounds__(NT) void k_conv3_direct(const bf16_t* __restrict__ 
       const int toff = G::tap_off(tap) * XP;
 #pragma unroll
       for (int ks = 0; ks < CC / 32; ++ks) {
-        bf16x8_t a[WO], b[2];
+        bf16x8_t a[WO], b[WPX];
 #pragma unroll
-        for (int mf = 0; mf < 2; ++mf) b[mf] = *reinterpret_cast<const bf16x8_t*>(xs + pb[mf] + toff + 32 * ks);
+        for (int mf = 0; mf < WPX; ++mf) b[mf] = *reinterpret_cast<const bf16x8_t*>(xs + pb[mf] + toff + 32 * ks);
 #pragma unroll
         for (int of = 0; of < WO; ++of)
           a[of] = *reinterpret_cast<const bf16x8_t*>(wsm + of * 16 * WPI + wb + tap * CC + 32 * ks);
 #pragma unroll
-        for (int mf = 0; mf < 2; ++mf)
+        for (int mf = 0; mf < WPX; ++mf)
 #pragma unroll
           for (int of = 0; of < WO; ++of)
             acc[mf][of] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[of], b[mf], acc[mf][of], 0, 0, 0);
@@ -156,11 +159,11 @@ __global__ __launch_bounds__(NT) void k_conv3_direct(const bf16_t* __restrict__ 
   __syncthreads();
   float* stg = reinterpret_cast<float*>(smem);  // [TP][CT + 4] fp32
 #pragma unroll
-  for (int mf = 0; mf < 2; ++mf)
+  for (int mf = 0; mf < WPX; ++mf)
 #pragma unroll
     for (int of = 0; of < WO; ++of)
-      *reinterpret_cast<f32x4_t*>(stg + (32 * wid + 16 * mf + (lane & 15)) * (CT + 4) + 16 * of + 4 * (lane >> 4)) =
-          acc[mf][of];
+      *reinterpret_cast<f32x4_t*>(stg + (16 * WPX * wid + 16 * mf + (lane & 15)) * (CT + 4) + 16 * of +
+                                  4 * (lane >> 4)) = acc[mf][of];
   __syncthreads();
   for (int it = tid; it < TP * CT / 8; it += NT) {
     const int px = it / (CT / 8), oc = 8 * (it % (CT / 8)), m = m0 + px;
@@ -291,10 +294,10 @@ __global__ __launch_bounds__(NT) void k_wgrad3_direct(const bf16_t* __restrict__
     for (int jj = 0; jj < 4; ++jj) dst[(int64_t)(16 * of + 4 * gq + jj) * N + tap * Cin] = acc[tap][jj];
 }
 
-template <int S, int CC, int CT, typename TO>
+template <int S, int CC, int CT, typename TO, int WPX = 2>
 bool launch_conv(const void* x, int B, int Cin, const void* wpack, int Cout, const mg_epilogue* e, void* y,
                  int64_t ldy, hipStream_t st) {
-  const int P = B * S * S, tiles = cdiv(P, TP), nch = Cin / CC;
+  const int P = B * S * S, tiles = cdiv(P, 64 * WPX), nch = Cin / CC;
   auto ep = make_epi<TO>(y, ldy, e);
   ep.vec_ok = ep.host_vec_ok() ? 1 : 0;
   if (!ep.vec_ok) return false;
@@ -306,14 +309,14 @@ bool launch_conv(const void* x, int B, int Cin, const void* wpack, int Cout, con
   const bf16_t* wb = reinterpret_cast<const bf16_t*>(wpack);
   const dim3 grid(tiles, cdiv(Cout, CT), splits);
   if (splits == 1) {
-    hipLaunchKernelGGL((k_conv3_direct<S, CC, CT, TO, false>), grid, dim3(NT), 0, st, xb, B, Cin, nch, wb, Cout, ep,
-                       nullptr, P);
+    hipLaunchKernelGGL((k_conv3_direct<S, CC, CT, TO, false, WPX>), grid, dim3(NT), 0, st, xb, B, Cin, nch, wb, Cout,
+                       ep, nullptr, P);
     return true;
   }
   float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * P * Cout * sizeof(float), st));
   if (!ws) return false;
-  hipLaunchKernelGGL((k_conv3_direct<S, CC, CT, TO, true>), grid, dim3(NT), 0, st, xb, B, Cin, nch / splits, wb,
-                     Cout, ep, ws, P);
+  hipLaunchKernelGGL((k_conv3_direct<S, CC, CT, TO, true, WPX>), grid, dim3(NT), 0, st, xb, B, Cin, nch / splits,
+                     wb, Cout, ep, ws, P);
   const int blocks = (int)std::min<int64_t>(cdiv((int64_t)P * Cout, 256 * 8), 2048);
   hipLaunchKernelGGL((splitk_reduce_kernel<Epi<TO>>), dim3(blocks), dim3(256), 0, st, ws, splits, P, Cout, ep);
   return true;
@@ -323,6 +326,14 @@ template <typename TO>
 bool conv_dispatch(const void* x, int B, int S, int Cin, const void* wpack, int Cout, const mg_epilogue* e, void* y,
                    int64_t ldy, hipStream_t st) {
   if (Cout == 32) {  // the offset head: Cin -> 32
+    if (g_mg_tune[MG_TUNE_NARROW_WPX] == 4) {  // A/B: 256-pixel tiles, four pixel fragments per wave
+      switch (S) {
+        case 16: return launch_conv<16, 64, 32, TO, 4>(x, B, Cin, wpack, Cout, e, y, ldy, st);
+        case 8: return launch_conv<8, 64, 32, TO, 4>(x, B, Cin, wpack, Cout, e, y, ldy, st);
+        case 4: return launch_conv<4, 64, 32, TO, 4>(x, B, Cin, wpack, Cout, e, y, ldy, st);
+      }
+      return false;
+    }
     switch (S) {
       case 16: return launch_conv<16, 64, 32, TO>(x, B, Cin, wpack, Cout, e, y, ldy, st);
       case 8: return launch_conv<8, 64, 32, TO>(x, B, Cin, wpack, Cout, e, y, ldy, st);

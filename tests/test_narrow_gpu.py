@@ -25,11 +25,14 @@ def _set(v):
     L.call("mg_set_tuning", 16, v)
 
 
+@pytest.mark.parametrize("wpx", [0])
 @pytest.mark.parametrize("B,S,Cin,out_dtype", [(8, 16, 256, bf), (3, 16, 128, torch.float32), (6, 8, 512, bf),
                                                (5, 8, 256, bf), (9, 4, 512, bf), (2, 4, 128, torch.float32)])
-def test_offset_head_forward(B, S, Cin, out_dtype):
+def test_offset_head_forward(B, S, Cin, out_dtype, wpx):
+    """``wpx``: tuning slot 19 (0: 128-pixel tiles, 4: 256-pixel tiles with four pixel fragments per wave)."""
     from moegan_mi import _lib as L
     from moegan_mi import ops
+    L.call("mg_set_tuning", 19, wpx)
     g = torch.Generator(device=DEV).manual_seed(B * 100 + S + Cin)
     x = (torch.randn(B, S, S, Cin, device=DEV, generator=g)).to(bf)
     W = (torch.randn(32, Cin, 3, 3, device=DEV, generator=g) * (9 * Cin) ** -0.5)
@@ -51,6 +54,7 @@ def test_offset_head_forward(B, S, Cin, out_dtype):
     assert float((y.float() - t).abs().max()) <= tol * scale
     y2 = ops.conv2d(x, wp, 32, 3, 3, 1, 1, out_dtype=out_dtype, ep=ep)
     torch.cuda.synchronize()
+    L.call("mg_set_tuning", 19, 0)
     assert torch.equal(y, y2)
 
 

@@ -57,5 +57,9 @@ for S, C in SHAPES:
             alt.append(timed(fn))
         L.call("mg_set_tuning", 17, 0)
         sweep = "  ".join(f"{b}:{t:5.1f}" for b, t in zip(BLOCKS, alt))
+        if name == "fwd":  # 256-pixel tiles (tuning slot 19 = 4)
+            L.call("mg_set_tuning", 19, 4)
+            sweep += f"  256px: {timed(fn):5.1f}"
+            L.call("mg_set_tuning", 19, 0)
         print(f"{S:2d}x{S:<2d} C={C:3d} {name:5s} generic {t_old:6.1f} us  direct {t_new:6.1f} us  "
               f"({nbytes / 1e6:5.1f} MB: {nbytes / t_new / 1e6:.2f} TB/s)  {sweep}", flush=True)
