@@ -749,7 +749,10 @@ extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const
     const bool big = dtype == MG_BF16 && M >= 128 && N >= 128 && g_mg_tune[MG_TUNE_GWGRAD_TILE] != 64;
     int tiles = big ? cdiv(M, 128) * cdiv(N, 128) * ngroups : cdiv(M, 64) * cdiv(N, 64) * ngroups;
     int rows_per_group = std::max(1, total_rows / std::max(1, ngroups));
-    splits = std::max(1, std::min({64, cdiv(big ? 512 : 1024, std::max(1, tiles)), std::max(1, rows_per_group / 1024)}));
+    // ~256 blocks of 128^2 tiles: fewer splits mean fewer fp32 atomic adds per output (measured at the C2 expert
+    // shapes: 512 x 128 over 131072 rows 16 -> 8 splits 70 -> 56 us, 1024 x 256 over 32768 rows 4 -> 2 splits
+    // 56 -> 47 us, profiles/round4_gwgrad_probe.txt)
+    splits = std::max(1, std::min({64, cdiv(big ? 256 : 1024, std::max(1, tiles)), std::max(1, rows_per_group / 1024)}));
   }
   if (mg_det()) splits = 1;  // deterministic mode: one writer (one atomic add) per element and group
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

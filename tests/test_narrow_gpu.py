@@ -25,7 +25,7 @@ def _set(v):
     L.call("mg_set_tuning", 16, v)
 
 
-@pytest.mark.parametrize("wpx", [0])
+@pytest.mark.parametrize("wpx", [0, 4])
 @pytest.mark.parametrize("B,S,Cin,out_dtype", [(8, 16, 256, bf), (3, 16, 128, torch.float32), (6, 8, 512, bf),
                                                (5, 8, 256, bf), (9, 4, 512, bf), (2, 4, 128, torch.float32)])
 def test_offset_head_forward(B, S, Cin, out_dtype, wpx):
