@@ -749,10 +749,12 @@ extern "C" int mg_gemm_grouped_wgrad(int dtype, int M, int N, int ngroups, const
     const bool big = dtype == MG_BF16 && M >= 128 && N >= 128 && g_mg_tune[MG_TUNE_GWGRAD_TILE] != 64;
     int tiles = big ? cdiv(M, 128) * cdiv(N, 128) * ngroups : cdiv(M, 64) * cdiv(N, 64) * ngroups;
     int rows_per_group = std::max(1, total_rows / std::max(1, ngroups));
-    // ~256 blocks of 128^2 tiles: fewer splits mean fewer fp32 atomic adds per output (measured at the C2 expert
-    // shapes: 512 x 128 over 131072 rows 16 -> 8 splits 70 -> 56 us, 1024 x 256 over 32768 rows 4 -> 2 splits
-    // 56 -> 47 us, profiles/round4_gwgrad_probe.txt)
-    splits = std::max(1, std::min({64, cdiv(big ? 256 : 1024, std::max(1, tiles)), std::max(1, rows_per_group / 1024)}));
+    // ~512 blocks of 128^2 tiles.  Isolated with uniform routing, ~256 (fewer splits, fewer fp32 atomic adds) ran the
+    // C2 expert shapes 15-20 % faster (profiles/round4_gwgrad_probe.txt), but in the step -- skewed expert loads, the
+    // largest expert's chunks set the tail -- it measured 8.86 -> 8.93 ms on one box (tools/gpu_gw_ab.sh), so the
+    // target stays 512 (A/B: tuning slot MG_TUNE_GWGRAD_BLOCKS)
+    const int tb = g_mg_tune[MG_TUNE_GWGRAD_BLOCKS], target = big ? (tb > 0 ? tb : 512) : 1024;
+    splits = std::max(1, std::min({64, cdiv(target, std::max(1, tiles)), std::max(1, rows_per_group / 1024)}));
   }
   if (mg_det()) splits = 1;  // deterministic mode: one writer (one atomic add) per element and group
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

@@ -111,6 +111,11 @@ def lib():
             fn.argtypes = list(args)
             fn.restype = res
         _lib = h
+        # A/B across processes (bench.py runs): MOEGAN_TUNE="slot=value,slot=value" sets library tuning slots at load
+        for kv in filter(None, os.environ.get("MOEGAN_TUNE", "").split(",")):
+            k, v = kv.split("=")
+            if h.mg_set_tuning(int(k), int(v)) != 0:
+                raise MGError(f"MOEGAN_TUNE {kv}: {h.mg_last_error().decode()}")
     return _lib
 
 
