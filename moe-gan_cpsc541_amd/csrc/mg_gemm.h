@@ -1149,17 +1149,36 @@ struct BatchArgs {
   Epi<TO> e[MG_BATCH_MAX];
   int M[MG_BATCH_MAX], N[MG_BATCH_MAX], K[MG_BATCH_MAX], tiles_n[MG_BATCH_MAX], tile_off[MG_BATCH_MAX + 1];
   int n;
+  // split-K slabs (SPLIT launches, grid.y = the split count): problem p's split s covers K rows
+  // [s * kchunk[p], +kchunk[p]) and writes its raw fp32 partial to ws + ws_off[p] + s * M[p] * N[p]
+  int kchunk[MG_BATCH_MAX];
+  int64_t ws_off[MG_BATCH_MAX];
+  float* ws;
 };
 
-template <typename T, bool A_KC, bool B_KC, class AL, class BL, typename TO, bool X3 = false>
+template <typename T, bool A_KC, bool B_KC, class AL, class BL, typename TO, bool X3 = false, bool SPLIT = false>
 __global__ __launch_bounds__(NTHREADS) void gemm_batch_kernel(BatchArgs<TO, AL, BL> args) {
   const int t = blockIdx.x;
   int p = 0;
   while (p + 1 < args.n && t >= args.tile_off[p + 1]) ++p;
   const int lt = t - args.tile_off[p];
   const int tm = lt / args.tiles_n[p], tn = lt - tm * args.tiles_n[p];
-  gemm_tile<T, 64, 64, A_KC, B_KC, AL, BL, Epi<TO>, X3>(args.a[p], args.b[p], args.e[p], tm * 64, tn * 64, args.M[p],
-                                                          args.N[p], 0, args.K[p], 0);
+  if constexpr (SPLIT) {
+    const int s = blockIdx.y, kbeg = s * args.kchunk[p], M = args.M[p], N = args.N[p];
+    if (kbeg >= args.K[p]) return;  // this problem has fewer splits (shorter K)
+    Epi<float> slab{};
+    slab.C = args.ws + args.ws_off[p];
+    slab.ldc = N;
+    slab.alpha = 1.f;
+    slab.zstride = (int64_t)M * N;
+    slab.zi = s;
+    slab.vec_ok = (N & 7) == 0;
+    gemm_tile<T, 64, 64, A_KC, B_KC, AL, BL, Epi<float>, X3>(args.a[p], args.b[p], slab, tm * 64, tn * 64, M, N, kbeg,
+                                                             min(args.K[p], kbeg + args.kchunk[p]), 0);
+  } else {
+    gemm_tile<T, 64, 64, A_KC, B_KC, AL, BL, Epi<TO>, X3>(args.a[p], args.b[p], args.e[p], tm * 64, tn * 64,
+                                                            args.M[p], args.N[p], 0, args.K[p], 0);
+  }
 }
 
 // launch helper: picks the grid; grouped-M launches an upper bound of tiles.
@@ -1185,33 +1204,75 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
                      K, kchunk, grp);
 }
 
-// split-K slab reduction: C = epilogue(sum_s ws[s]) for a [M, N] tile set (ws row pitch N).
+// split-K slab reduction: C = epilogue(sum_s ws[s]) for a [M, N] tile set (ws row pitch N), over blocks
+// blk of nblk.  Slabs are added in split order (fixed, whatever the grid); their loads are issued four at a
+// time so the (small, latency-bound) reduction waits about once per four slabs, not once per slab.
 template <class EP>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
-                                                            EP ep) {
+MG_DEV void splitk_reduce_body(const float* __restrict__ ws, int splits, int M, int N, const EP& ep, int blk, int nblk) {
   const int64_t MN = (int64_t)M * N;
   if (ep.vec_ok && (N & 7) == 0) {  // 8 columns per thread: 16-B slab loads, the vector epilogue
     const int64_t n8 = MN >> 3;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n8; q += (int64_t)gridDim.x * 256) {
+    for (int64_t q = (int64_t)blk * 256 + threadIdx.x; q < n8; q += (int64_t)nblk * 256) {
       const int64_t i = q << 3;
-      float v[8], t[8];
-      ld8(ws + i, v);
-      for (int s = 1; s < splits; ++s) {
-        ld8(ws + s * MN + i, t);
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t[4][8];
+      if (splits > 0) ld8(ws + i, v);
+      int s = 1;
+      for (; s + 4 <= splits; s += 4) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += t[j];
+        for (int u = 0; u < 4; ++u) ld8(ws + (s + u) * MN + i, t[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += t[u][j];
+      }
+      for (; s < splits; ++s) {
+        ld8(ws + s * MN + i, t[0]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += t[0][j];
       }
       const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
       ep.vec8(m, n, v);
     }
     return;
   }
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
-    float v = 0.f;
-    for (int s = 0; s < splits; ++s) v += ws[s * MN + i];
+  for (int64_t i = (int64_t)blk * 256 + threadIdx.x; i < MN; i += (int64_t)nblk * 256) {
+    float v = 0.f, t[4];
+    int s = 0;
+    for (; s + 4 <= splits; s += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = ws[(s + u) * MN + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v += t[u];
+    }
+    for (; s < splits; ++s) v += ws[s * MN + i];
     int m = (int)(i / N), n = (int)(i - (int64_t)(i / N) * N);
     ep(m, n, v);
   }
+}
+
+template <class EP>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                            EP ep) {
+  splitk_reduce_body(ws, splits, M, N, ep, blockIdx.x, gridDim.x);
+}
+
+// the batched GEMMs' slab reductions: blocks [blk_off[p], blk_off[p + 1]) reduce problem p's splits[p] slabs
+template <typename TO>
+struct BatchReduceArgs {
+  Epi<TO> e[MG_BATCH_MAX];
+  int64_t ws_off[MG_BATCH_MAX];
+  int M[MG_BATCH_MAX], N[MG_BATCH_MAX], splits[MG_BATCH_MAX], blk_off[MG_BATCH_MAX + 1];
+  int n;
+  const float* ws;
+};
+
+template <typename TO>
+__global__ __launch_bounds__(256) void batch_reduce_kernel(BatchReduceArgs<TO> r) {
+  const int t = blockIdx.x;
+  int p = 0;
+  while (p + 1 < r.n && t >= r.blk_off[p + 1]) ++p;
+  splitk_reduce_body(r.ws + r.ws_off[p], r.splits[p], r.M[p], r.N[p], r.e[p], t - r.blk_off[p],
+                     r.blk_off[p + 1] - r.blk_off[p]);
 }
 
 }  // namespace mg

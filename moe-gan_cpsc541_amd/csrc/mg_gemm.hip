@@ -241,6 +241,7 @@ int run_batch(int n, const mg_gemm_desc* d, hipStream_t st) {
   using BL = typename std::conditional<BKc, LdKC<T>, LdMC<T>>::type;
   for (int i0 = 0; i0 < n; i0 += MG_BATCH_MAX) {
     BatchArgs<TO, AL, BL> args;
+    static_assert(sizeof(args) <= 4096 && sizeof(BatchReduceArgs<TO>) <= 4096, "kernel arguments over 4 KB");
     int cnt = std::min(MG_BATCH_MAX, n - i0), tiles = 0, used = 0;
     for (int j = 0; j < cnt; ++j) {
       const mg_gemm_desc& q = d[i0 + j];
@@ -263,6 +264,48 @@ int run_batch(int n, const mg_gemm_desc* d, hipStream_t st) {
     if (!used) continue;
     args.tile_off[used] = tiles;
     args.n = used;
+    // Few-tile batches (router / cross-attention value-chain products at M = batch) walk K serially in ~100
+    // blocks.  Opt-in (tuning slot 21 = block target): split K into fp32 slabs, then one batched reduction applies
+    // each real epilogue.  The batched GEMMs halve (12.9 -> 7.1 us average) but the reduction launches cost what
+    // that saves: 8.844 / 8.826 ms per step with / without at 512 blocks (same box, three rounds), so off.
+    constexpr int TBK = tile_bk<T, X3>();
+    const int bs = g_mg_tune[MG_TUNE_BATCH_SPLIT];
+    int S = 1;
+    if (bs > 1) {
+      const int target = bs;
+      int maxK = 0;
+      for (int j = 0; j < used; ++j) maxK = std::max(maxK, args.K[j]);
+      if (2 * tiles <= target) S = std::min(target / tiles, maxK / (2 * TBK));
+    }
+    if (S >= 2) {
+      BatchReduceArgs<TO> r;
+      int64_t off = 0;
+      int blks = 0;
+      for (int j = 0; j < used; ++j) {
+        const int K = args.K[j], kc = K > 0 ? cdiv(cdiv(K, S), TBK) * TBK : TBK;
+        const int64_t MN = (int64_t)args.M[j] * args.N[j];
+        args.kchunk[j] = kc;
+        args.ws_off[j] = r.ws_off[j] = off;
+        r.e[j] = args.e[j];
+        r.M[j] = args.M[j];
+        r.N[j] = args.N[j];
+        r.splits[j] = K > 0 ? cdiv(K, kc) : 0;
+        r.blk_off[j] = blks;
+        off += (r.splits[j] * MN + 7) / 8 * 8;  // 32-B aligned slabs
+        blks += (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(MN, args.N[j] % 8 == 0 ? 2048 : 256), 256));
+      }
+      r.blk_off[used] = blks;
+      r.n = used;
+      float* ws = reinterpret_cast<float*>(mg_workspace((size_t)std::max<int64_t>(off, 8) * sizeof(float), st));
+      if (ws) {
+        args.ws = ws;
+        r.ws = ws;
+        hipLaunchKernelGGL((gemm_batch_kernel<T, AK, BKc, AL, BL, TO, X3, true>), dim3(tiles, S), dim3(NTHREADS), 0, st,
+                           args);
+        hipLaunchKernelGGL((batch_reduce_kernel<TO>), dim3(blks), dim3(256), 0, st, r);
+        continue;
+      }
+    }
     hipLaunchKernelGGL((gemm_batch_kernel<T, AK, BKc, AL, BL, TO, X3>), dim3(tiles), dim3(NTHREADS), 0, st, args);
   }
   return mg_check_launch("mg_gemm_batch");

@@ -148,10 +148,57 @@ def test_grouped_gelu_grad_epilogue(C, H4):
     assert ((out.float() - ref).abs() <= 1e-2 * ref.abs() + 2e-3).all()
 
 
-@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2), ("x3", 1e-4)])
 @pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (1, 0), (0, 0)])
-def test_gemm_batch_matches_individual(dtype, tol, a_kc, b_kc):
-    """mg_gemm_batch: 11 problems of different shapes / epilogues (two launches) == plain GEMMs."""
+@pytest.mark.parametrize("split", [0, 512, 64])
+def test_gemm_batch_matches_individual(dtype, tol, a_kc, b_kc, split):
+    """mg_gemm_batch: 11 problems of different shapes / epilogues (two launches) == plain GEMMs; split 0 = one K
+    pass per tile (default), 512 = split-K slabs at a 512-block target (tuning slot 21), 64 = a 64-block target
+    (no split: the batch has more tiles); "x3" = fp32 operands through split-bf16 products."""
+    x3 = dtype == "x3"
+    if x3:
+        dtype = torch.float32
+    L.call("mg_set_tuning", 21, split)
+    prev = ops.set_f32x3(x3)
+    try:
+        _gemm_batch_case(dtype, tol, a_kc, b_kc)
+    finally:
+        ops.set_f32x3(prev)
+        L.call("mg_set_tuning", 21, 0)
+
+
+def test_gemm_batch_split_atomic():
+    """Split-K slabs under atomic epilogues: three problems accumulate into one fp32 output (the value chain's
+    shared text-sequence gradient) and one into its own, each slab sum added once."""
+    L.call("mg_set_tuning", 21, 512)
+    try:
+        _split_atomic_case()
+    finally:
+        L.call("mg_set_tuning", 21, 0)
+
+
+def _split_atomic_case():
+    g = torch.Generator(device=DEV).manual_seed(7)
+    out = torch.randn(256, 512, device=DEV, generator=g)
+    own = torch.randn(128, 256, device=DEV, generator=g)
+    ref = out.double().clone()
+    ref_own = own.double().clone()
+    probs = []
+    for K in (512, 1024, 384):
+        A = torch.randn(256, K, device=DEV, generator=g)
+        Bm = torch.randn(512, K, device=DEV, generator=g) / K ** 0.5
+        probs.append(dict(A=A, B=Bm, M=256, N=512, K=K, out=out, ep=L.epilogue(atomic=1)))
+        ref += A.double() @ Bm.double().T
+    A = torch.randn(128, 640, device=DEV, generator=g)
+    Bm = torch.randn(256, 640, device=DEV, generator=g) / 640 ** 0.5
+    probs.append(dict(A=A, B=Bm, M=128, N=256, K=640, out=own, ep=L.epilogue(atomic=1, alpha=0.5)))
+    ref_own += 0.5 * (A.double() @ Bm.double().T)
+    ops.gemm_batch(probs)
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 1e-5 and rel(own, ref_own) < 1e-5
+
+
+def _gemm_batch_case(dtype, tol, a_kc, b_kc):
     g = torch.Generator(device=DEV).manual_seed(3)
     shapes = [(256, 512, 512), (256, 256, 128), (8, 64, 512), (200, 72, 96), (512, 16, 256), (64, 8, 8),
               (256, 8, 128), (128, 512, 256), (256, 128, 512), (72, 40, 64), (256, 1024, 256)]
