@@ -213,7 +213,8 @@ int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngroups, const 
    each group, gP[r] = (gG[r] W2_g) * GELU'(pre[r]) ([total_rows, Hd] bf16, written for the weight gradient of W1),
    gX[r] = gP[r] W1_g ([total_rows, C] bf16), and gb1[g] (fp32 [ngroups, Hd], accumulated; NULL skips it) +=
    sum over the group's rows of gP (the bf16 values), folded in a fixed order.  gP and gX are bit-identical to
-   mg_gemm_grouped (gG x W2 with the GELU' epilogue, then gP x W1).  bf16, C = 128, Hd % 64 == 0; W1 [G, Hd, C],
+   mg_gemm_grouped (gG x W2 with the GELU' epilogue, then gP x W1).  bf16, C = 128 or 256 (256: 144 KiB of LDS,
+   one block per CU, gfx950), Hd % 64 == 0; W1 [G, Hd, C],
    W2 [G, C, Hd]; grid = max_tiles blocks of 128 rows. */
 int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1, const void* W2, void* gP, void* gX, float* gb1, void* stream);
 

@@ -140,7 +140,9 @@ __global__ __launch_bounds__(256) void k_wide_final(const float* __restrict__ tm
   float s = 0.f;
   for (int g = 0; g < ngrp; ++g) s += tmp[(int64_t)g * MN + i];
   const int64_t m = i / N, n = i - m * N;
-  C[m * ldc + n] += alpha * s;
+  // an atomic add keeps mg_gemm's atomic-epilogue contract (concurrent writers into one gradient buffer, e.g. from
+  // the main and the side stream, accumulate); with one writer it is the same single fp32 addition as C += alpha s
+  atomicAdd(C + m * ldc + n, alpha * s);
 }
 
 }  // namespace

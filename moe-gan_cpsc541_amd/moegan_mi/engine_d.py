@@ -41,6 +41,16 @@ class DiscriminatorEngine:
         # weight gradients on a side stream, overlapping the data-gradient chain (joined before finish_grads)
         self.side = graphs.SideStream(self.dev, enabled=graphs.side_streams_enabled(self.dev))
 
+    def _d0_ok(self, H):
+        """conv_layers.0 on the direct kernels at this (square) image size: mg_d0_* take W / 2 a power of two in
+        [4, 64] and H a multiple of 4; any other even size keeps the im2col + GEMM path."""
+        ow = H // 2
+        return self.direct0 and H % 4 == 0 and 4 <= ow <= 64 and (ow & (ow - 1)) == 0
+
+    def _head_ok(self, Hf):
+        """The per-image head kernels (mg_d_head_*): 4 <= Hf <= 32 and Hf^2 a multiple of 16."""
+        return self.direct0 and 4 <= Hf <= 32 and (Hf * Hf) % 16 == 0
+
     def P(self, n):
         return self.st.view(n)
 
@@ -86,7 +96,7 @@ class DiscriminatorEngine:
         else:
             ld = layout[1]
             strides = (H * H * ld, H * ld, ld, 1)
-        if self.direct0:  # direct MFMA conv (mg_d0_fwd): no im2col matrix; the backward re-gathers from the image
+        if self._d0_ok(H):  # direct MFMA conv (mg_d0_fwd): no im2col matrix; the backward re-gathers from the image
             cols = (img, strides)
             h0 = ops.d0_fwd(img, strides, B, H, H, self.W0p, bias=self.P("conv_layers.0.bias"))
         else:
@@ -99,7 +109,7 @@ class DiscriminatorEngine:
     def forward(self, img, layout, text, B, H):
         cols, h0, h1 = self.conv_stack(img, layout, B, H)
         Hf = H // 4
-        if self.direct0 and Hf <= 32:  # one kernel per image (mg_d_head_fwd)
+        if self._head_ok(Hf):  # one kernel per image (mg_d_head_fwd)
             img_part = ops.d_head_fwd(h1, self.W2t_c, B, Hf)
         else:
             P = ops.gemm(h1.view(-1, 256), self.W2t_c, B * Hf * Hf, 16, 256, out_dtype=torch.float32)
@@ -129,7 +139,7 @@ class DiscriminatorEngine:
 
     def _d0_wgrad(self, cols, g, dW0):
         """dW0 [128, 48] += conv_layers.0 weight gradient; ``cols`` is the im2col matrix, or (image, strides)."""
-        if self.direct0:
+        if isinstance(cols, tuple):
             img, strides = cols
             B, OH, OW, _ = g.shape
             ops.d0_wgrad(img, strides, B, 2 * OH, 2 * OW, g, dW0)
@@ -138,7 +148,7 @@ class DiscriminatorEngine:
                      ep=E_(atomic=1), splits=0)
 
     def _d0_dgrad(self, g, out):
-        if self.direct0:
+        if self._d0_ok(2 * g.shape[1]):
             ops.d0_dgrad(g, self.W0p, out)
         else:
             ops.dgrad_s2_small(g, self.W0p, 3, out)
@@ -150,9 +160,9 @@ class DiscriminatorEngine:
         h1f = h1.view(Pn, 256)
         g_a1 = torch.empty(B, Hf, Hf, 256, device=self.dev, dtype=self.cdt)
         G = None
-        if want_w or need_g or not (self.direct0 and Hf <= 32):
+        if want_w or need_g or not self._head_ok(Hf):
             G = ops.disc_head_gmat(g, g_bstride, B, Hf, self.cdt)
-        if self.direct0 and Hf <= 32:  # G formed inside the kernel (mg_d_head_bwd)
+        if self._head_ok(Hf):  # G formed inside the kernel (mg_d_head_bwd)
             ops.d_head_bwd(g, g_bstride, h1, self.W2img_c, B, Hf, g_a1)
         else:
             ops.gemm(G, self.W2img_c, Pn, 256, 16, out=g_a1.view(Pn, 256),
@@ -212,7 +222,7 @@ class DiscriminatorEngine:
         u = torch.empty(B, Hr, Hr, 4, device=dev, dtype=self.cdt)
         ops.r1(gx, B, r1_gamma, r1, u)
         u_strides = (Hr * Hr * 4, Hr * 4, 4, 1)
-        if self.direct0:
+        if self._d0_ok(Hr):
             cols_u = (u, u_strides)
             m0v0 = ops.d0_fwd(u, u_strides, B, Hr, Hr, self.W0p, aux=fr["h0"])
         else:

@@ -364,9 +364,12 @@ class _StepRunner:
     runs eagerly without capture.  ``enabled=False`` (or a non-HIP device) runs every batch eagerly.
 
     All variants share one capture stream (one library workspace) and one graph memory pool: they replay one at
-    a time on the same stream, so the step temporaries of one variant may reuse another's; only each variant's
-    output tensors stay private (with acc = 8 the loop keeps three variants alive).  Peak memory of
-    the loop is measured by tests/test_loop_gpu.py."""
+    a time on the same stream, so the step temporaries of one variant may reuse another's (with
+    acc = 8 the loop keeps three variants alive).  A variant's output tensors are private only against variants
+    captured BEFORE it: a later capture may place its temporaries in blocks that hold an earlier variant's outputs.
+    Invariant: a variant's outputs are read or copied (train_aurora_gan: _stats_to_host, in stream order right after
+    the replay) before any other variant replays.  tests/test_loop_gpu.py checks the returned values across the
+    variant switches of an acc > 1 window and measures the loop's peak memory."""
 
     def __init__(self, ts, device, enabled=True):
         self.ts = ts
@@ -468,7 +471,14 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
     ``on_batch_done(epoch, batch_idx, flags)``: called when a batch's results have reached the host (bench.py
     --loop); ``flags`` is the batch's guard word (bit 0: non-finite D loss, bit 1: non-finite G loss).
     ``resume_from``: a resume checkpoint (:1484-1491 layout, ours or the reference's) to start from;
-    ``save_every_epoch``: write that layout after every epoch (the reference's commented-out :1642-1652)."""
+    ``save_every_epoch``: write that layout after every epoch (the reference's commented-out :1642-1652).
+
+    Accepted and not applied: ``batch_memory_limit`` (the reference's per-batch ``memory_allocated()`` check that
+    skips a batch above the limit and doubles the accumulation after three skips, :1231-1259) and
+    ``checkpoint_activation`` (recomputation that changes memory, not math, :734-760).  Here every batch body is
+    the same preallocated step (one hipGraph per variant), so its memory is fixed before the first batch: a
+    per-batch check would give the same answer for every batch, and with 288 GB of HBM per GPU the C2 step fits
+    many times over.  The loop logs the step's allocated memory against the limit once, after the first batch."""
     os.makedirs(save_dir, exist_ok=True)
     if clip_weight_64 is not None:
         clip_weight_16 = clip_weight_64
@@ -572,6 +582,10 @@ def train_aurora_gan(dataloader, val_dataloader=None, num_epochs=50, lr=0.0002, 
             if pending is not None:
                 account(pending)  # the previous batch, now that this one is enqueued
             pending = rec
+            if batch_idx == 0 and epoch == start_epoch and rank == 0 and device.type == "cuda" and batch_memory_limit:
+                gb = torch.cuda.memory_allocated(device) / 1e9
+                logger.info(f"batch_memory_limit={batch_memory_limit}GB is not applied (the step's memory is fixed): "
+                            f"{gb:.2f}GB allocated after the first batch")
         if pending is not None:
             account(pending)
         pbar.close()

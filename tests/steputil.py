@@ -159,10 +159,32 @@ class Rounder:
     averages that coherent error away -- its floors came out 0.6x the nearest-even ones after the sqrt(2)
     variance correction.)"""
 
-    def __init__(self, seed=None):
+    def __init__(self, seed=None, offset_ulp=None):
         self.seed = seed
         self.noise_scale = 1.0
         self.s = 1.0 if seed is None else 2.0 ** ((seed % 7 + 1) / 8.0)  # in (1, 2): never a power of two
+        # (fraction, seed): after rounding the MTM offset heads' activation (oracle.offset_act), also move that
+        # fraction of its elements by one bf16 ulp (random direction) -- another valid bf16 evaluation of the same
+        # activation, as two correct kernels that round a few products differently produce (see offset_ulp_move)
+        self.offset_ulp = offset_ulp
+        self._offset_calls = 0
+
+    def offset_ulp_move(self, x):
+        """x (fp32, already on the bf16 grid) with max(1, round(fraction * numel)) elements moved one bf16 ulp up
+        or down.  The elements and directions come from a generator seeded by (seed, call index), so a realization
+        is reproducible; zeros are left alone (their neighbours are denormal)."""
+        frac, seed = self.offset_ulp
+        self._offset_calls += 1
+        g = torch.Generator().manual_seed(1000003 * seed + self._offset_calls)
+        flat = x.detach().reshape(-1).bfloat16().clone()
+        n = max(1, int(round(frac * flat.numel())))
+        idx = torch.randperm(flat.numel(), generator=g)[:n]
+        step = torch.randint(0, 2, (n,), generator=g, dtype=torch.int16) * 2 - 1
+        bits = flat.view(torch.int16)
+        sel = bits[idx]
+        nz = (sel & 0x7FFF) != 0
+        bits[idx] = torch.where(nz, sel + step, sel)
+        return flat.to(x.dtype).view(x.shape)
 
     def __call__(self, x):
         if self.seed is None:
@@ -209,6 +231,21 @@ class _RoundBoth(torch.autograd.Function):
         return _ROUNDER[0](g)
 
 
+class _RoundBothOffset(torch.autograd.Function):
+    """_RoundBoth for the offset heads' activation, with the rounder's one-ulp moves (Rounder.offset_ulp) applied to
+    the rounded value."""
+
+    @staticmethod
+    def forward(ctx, x):
+        r = _ROUNDER[0]
+        y = r(x)
+        return r.offset_ulp_move(y) if r.offset_ulp is not None else y
+
+    @staticmethod
+    def backward(ctx, g):
+        return _ROUNDER[0](g)
+
+
 class bf16_module_rounding:
     """Context manager: the tensors the bf16 device stores in bf16 -- module outputs (modulated convs, MTMs,
     convolution / attention blocks, expert FFNs, the MoE layer's combined output, multi-head attention outputs)
@@ -235,17 +272,18 @@ class bf16_module_rounding:
         if self.attention_internals:  # the multi-head attention with the MFMA kernel's bf16 operands (below)
             inner["mha"] = _mha_bf16_internals
 
-        def wrapper(f):
+        def wrapper(f, rb=_RoundBoth):
             def wrap(*a, **k):
                 r = f(*a, **k)
-                return (_RoundBoth.apply(r[0]),) + tuple(r[1:]) if isinstance(r, tuple) else _RoundBoth.apply(r)
+                return (rb.apply(r[0]),) + tuple(r[1:]) if isinstance(r, tuple) else rb.apply(r)
             return wrap
         def value_wrapper(f):
             def wrap(*a, **k):
                 return self.rounder.st(f(*a, **k))
             return wrap
         for n, f in inner.items():
-            setattr(O, n, value_wrapper(f) if n in self.VALUE_NAMES else wrapper(f))
+            setattr(O, n, value_wrapper(f) if n in self.VALUE_NAMES else
+                    wrapper(f, _RoundBothOffset if n == "offset_act" else _RoundBoth))
         for n, f in self.orig_f.items():
             setattr(O.F, n, wrapper(f))
         return self

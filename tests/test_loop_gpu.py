@@ -31,16 +31,29 @@ def _train(use_graphs, tmp_path, acc=2, B=8, n=4):
     return G._store.data.clone(), D._store.data.clone()
 
 
-def test_graph_loop_bit_identical_deterministic(tmp_path):
-    """Deterministic mode: the graph-replayed loop's parameters equal the eager loop's bit for bit."""
+def test_graph_loop_bit_identical_deterministic(tmp_path, caplog):
+    """Deterministic mode: the graph-replayed loop's parameters equal the eager loop's bit for bit, and so do the
+    per-batch losses it reads back (logged every batch), across the window's variant switches -- a variant's outputs
+    are read before another variant replays (the _StepRunner invariant: the variants share one graph pool)."""
+    import logging
     from moegan_mi import ops
+    caplog.set_level(logging.INFO, logger="t2i_moe_gan")
+    logs = {}
     ops.set_deterministic(True)
     try:
-        e = _train(False, tmp_path)
-        g = _train(True, tmp_path)
+        for mode in (False, True):
+            caplog.clear()
+            res = _train(mode, tmp_path)
+            logs[mode] = [r.getMessage().strip() for r in caplog.records if "D_loss" in r.getMessage()]
+            if mode:
+                g = res
+            else:
+                e = res
     finally:
         ops.set_deterministic(False)
     assert torch.equal(e[0], g[0]) and torch.equal(e[1], g[1])
+    assert len(logs[False]) == 4, logs[False]
+    assert logs[True] == logs[False], (logs[True], logs[False])
 
 
 def test_graph_loop_matches_eager_loop(tmp_path):
