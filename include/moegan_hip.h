@@ -214,9 +214,11 @@ int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngroups, const 
    gX[r] = gP[r] W1_g ([total_rows, C] bf16), and gb1[g] (fp32 [ngroups, Hd], accumulated; NULL skips it) +=
    sum over the group's rows of gP (the bf16 values), folded in a fixed order.  gP and gX are bit-identical to
    mg_gemm_grouped (gG x W2 with the GELU' epilogue, then gP x W1).  bf16, C = 128 or 256 (256: 144 KiB of LDS,
-   one block per CU, gfx950), Hd % 64 == 0; W1 [G, Hd, C],
+   one block per CU, gfx950), Hd % 64 == 0; gb2 (fp32 [ngroups, C], accumulated; NULL skips it) += the column
+   sums of gG over the group's rows (the layer-2 bias gradient, from the gG tile the pass holds in LDS, per-tile
+   partial rows folded in tile order); W1 [G, Hd, C],
    W2 [G, C, Hd]; grid = max_tiles blocks of 128 rows. */
-int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1, const void* W2, void* gP, void* gX, float* gb1, void* stream);
+int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1, const void* W2, void* gP, void* gX, float* gb1, float* gb2, void* stream);
 
 /* ---- op-level entry points ---- */
 
@@ -365,6 +367,20 @@ int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const float* mu_
    KL term keeps a gradient (t2i_moe_gan.py:1396-1404). */
 int mg_router_param_bwd(const float* mu, const float* rho, const float* eps, const float* gW, int64_t n, const float* kl_coef, float* gmu, float* grho, const int32_t* flags, int32_t mask, void* stream);
 
+/* Every router parameter tensor of a backward in one launch (at most 32 descriptors): for each descriptor the
+   arithmetic of mg_router_param_bwd (same results), one shared guard word (flags & mask drops every gW chain). */
+typedef struct mg_router_param_desc {
+  const float* mu;
+  const float* rho;
+  const float* eps;
+  const float* gW;
+  const float* kl_coef;
+  float* gmu;
+  float* grho;
+  int64_t n;
+} mg_router_param_desc;
+int mg_router_param_bwd_batch(int n, const mg_router_param_desc* descs, const int32_t* flags, int32_t mask, void* stream);
+
 /* moe_balance_loss from global per-expert prob sums (t2i_moe_gan.py:951-1000): out[0] = loss, coef[e] = d loss/d probs[t,e] * grad_scale. */
 int mg_balance(const float* load, int E, float T, float weight, float grad_scale, float* out, float* coef, void* stream);
 
@@ -487,6 +503,12 @@ int mg_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, 
 int mg_opt_prologue(float* sumsq, int32_t* step, const int32_t* flags, int32_t skip_mask, const int32_t* win,
                     int32_t run_mask, void* stream);
 
+/* clip_grad_norm_'s sum of squares and the AdamW step counters of one parameter store in two launches instead of
+   mg_opt_prologue + mg_sumsq + one mg_opt_prologue per optimizer launch: out[0] = sum of x[0..n)^2 (written, the fixed
+   fold order of mg_sumsq), then step0[0] += 1 and step1[0] += 1 (NULL = none) each under mg_opt_prologue's gate --
+   not when flags[0] & skip_mask, and only when win[0] & run_mask (run_mask 0 or win NULL: always). */
+int mg_grad_norm_steps(const float* x, int64_t n, float* out, int32_t* step0, int32_t run_mask0, int32_t* step1, int32_t run_mask1, const int32_t* flags, int32_t skip_mask, const int32_t* win, void* stream);
+
 /* mg_adamw with the step count read from device memory (*step >= 1); bias corrections on the device. */
 int mg_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay, const int32_t* step, const float* sumsq, float max_norm, void* stream);
 /* Same update (t2i_moe_gan.py:1333-1421), 16-B vectors, and (shadow_bf16 != NULL) the bf16 compute copy of the
@@ -505,6 +527,21 @@ int mg_finite_flag(const float* x, int n, int32_t bit, int32_t* flags, void* str
 /* Window word update: win[0] &= ~reset_bits unless flags[0] & keep_mask (a skipped batch does not reach the
    reference's zero_grad, t2i_moe_gan.py:1353); then win[0] |= set_bits unless flags[0] & bad_mask. */
 int mg_flag_window(const int32_t* flags, int32_t reset_bits, int32_t keep_mask, int32_t bad_mask, int32_t set_bits, int32_t* win, void* stream);
+
+/* One phase's loss checks and window updates in one launch (mg_finite_flag x n + mg_flag_window x nwin): for each
+   check c with n[c] > 0, flags[0] |= bit[c] if any of x[c][0 .. n[c]) is NaN / Inf; then the nwin (<= 2) window
+   updates in order, each with mg_flag_window's rule on the updated flags. */
+typedef struct mg_guard_desc {
+  const float* x[4];
+  int32_t n[4];
+  int32_t bit[4];
+  int32_t nwin;
+  int32_t reset_bits[2];
+  int32_t keep_mask[2];
+  int32_t bad_mask[2];
+  int32_t set_bits[2];
+} mg_guard_desc;
+int mg_guard_update(const mg_guard_desc* d, int32_t* flags, int32_t* win, void* stream);
 /* x[0..bytes) = 0 when ((flags[0] & mask) != 0) == (when_set != 0). */
 int mg_zero_if(void* x, int64_t bytes, const int32_t* flags, int32_t mask, int when_set, void* stream);
 /* acc[i] += g[i] unless flags[0] & mask (gradient accumulation of a batch that may be skipped). */

@@ -246,7 +246,7 @@ template <int C>
 __device__ __forceinline__ void ffn_bwd_body(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
-    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part) {
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
   __shared__ FfnBwdSmem<C> sm;
   const int t = blockIdx.x;
   int g = -1;
@@ -390,8 +390,26 @@ __device__ __forceinline__ void ffn_bwd_body(
       partb[h0 + tid] = cs;
     }
   }
+  __syncthreads();  // every read of hs / w1 / w2 by the last chunk is done
+  // ---- layer-2 bias gradient (gb2 = column sums of gG over the expert's rows): this tile's partial row from the
+  // gG tile still in LDS -- FT / C row groups per column in order, then the groups in order (fixed order) ----
+  if (part2) {
+    constexpr int RG = FT / C;  // row groups
+    float* red2 = reinterpret_cast<float*>(sm.hs);  // [RG][C] (hs is free)
+    const int col = tid % C, rg = tid / C;
+    float cs = 0.f;
+    for (int rr = rg * (FBM / RG); rr < (rg + 1) * (FBM / RG); ++rr) cs += bf2f(sm.gs[kci<FBM>(rr, col)]);
+    red2[rg * C + col] = cs;
+    __syncthreads();
+    if (tid < C) {
+      float t2 = 0.f;
+#pragma unroll
+      for (int g2 = 0; g2 < RG; ++g2) t2 += red2[g2 * C + tid];
+      part2[(int64_t)t * C + tid] = t2;
+    }
+    __syncthreads();  // the gG tile's reads are done before the gX tile overwrites it
+  }
   // ---- epilogue: gX tile, bf16, staged through LDS (the gG tile is dead) for 16-B row stores ----
-  __syncthreads();
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
@@ -417,15 +435,15 @@ template <int C>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_moe_ffn_bwd(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
-    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part) {
-  ffn_bwd_body<C>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part);
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
+  ffn_bwd_body<C>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2);
 }
 template <int C>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_moe_ffn_bwd_w2(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
-    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part) {
-  ffn_bwd_body<C>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part);
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
+  ffn_bwd_body<C>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2);
 }
 
 // gb1[g][h] += sum over the tiles of group g (tile order) of part[tile][h]: 64 columns x 4 tile lanes per block,
@@ -482,7 +500,7 @@ extern "C" int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngro
 
 extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off,
                               const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1,
-                              const void* W2, void* gP, void* gX, float* gb1, void* stream) {
+                              const void* W2, void* gP, void* gX, float* gb1, float* gb2, void* stream) {
   MG_REQUIRE(dtype == MG_BF16, "bf16 only");
   MG_REQUIRE(C == 128 || C == 256, "C must be 128 or 256");
   MG_REQUIRE(Hd > 0 && Hd % FHC == 0, "Hd must be a multiple of 64");
@@ -492,19 +510,21 @@ extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngro
   MG_REQUIRE(total_rows >= 0 && max_tiles >= (total_rows + FBM - 1) / FBM, "max_tiles below the row tiles");
   if (max_tiles <= 0 || total_rows == 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  float* part = reinterpret_cast<float*>(mg_workspace((size_t)max_tiles * Hd * sizeof(float), st));
+  float* part = reinterpret_cast<float*>(mg_workspace((size_t)max_tiles * (Hd + C) * sizeof(float), st));
   if (!part) return MG_ERR_ARG;
+  float* part2 = gb2 ? part + (size_t)max_tiles * Hd : nullptr;
   // C = 256: 144 KiB of LDS, one block per CU, so the 256-VGPR form; C = 128: measured faster too
   const bool one_block = C == 256 || g_mg_tune[MG_TUNE_FFN_BWD_OCC] != 2;
 #define L_(K, CC)                                                                                                    \
   hipLaunchKernelGGL(K<CC>, dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),                  \
                      reinterpret_cast<const bf16_t*>(pre), ngroups, row_off, tile_off, Hd,                            \
                      reinterpret_cast<const bf16_t*>(W1), reinterpret_cast<const bf16_t*>(W2),                        \
-                     reinterpret_cast<bf16_t*>(gP), reinterpret_cast<bf16_t*>(gX), part)
+                     reinterpret_cast<bf16_t*>(gP), reinterpret_cast<bf16_t*>(gX), part, part2)
   if (C == 256) L_(k_moe_ffn_bwd_w2, 256);
   else if (one_block) L_(k_moe_ffn_bwd_w2, 128);
   else L_(k_moe_ffn_bwd, 128);
 #undef L_
   if (gb1) hipLaunchKernelGGL(k_ffn_bias_fold, dim3(cdiv(Hd, 64), ngroups), dim3(256), 0, st, part, tile_off, Hd, gb1);
+  if (gb2) hipLaunchKernelGGL(k_ffn_bias_fold, dim3(cdiv(C, 64), ngroups), dim3(256), 0, st, part2, tile_off, C, gb2);
   return mg_check_launch("mg_moe_ffn_bwd");
 }

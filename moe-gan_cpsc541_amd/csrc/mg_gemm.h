@@ -79,10 +79,12 @@ MG_DEV u16x8_t vscale1(u16x8_t v, float s) {
   return r;
 }
 MG_DEV f32x4_t vgelu(f32x4_t v) { return f32x4_t{gelu_erf(v[0]), gelu_erf(v[1]), gelu_erf(v[2]), gelu_erf(v[3])}; }
+// bf16 operands: the epilogues' fast erf form (|erf error| <= 1.5e-7, far below the bf16 rounding of the result;
+// the piecewise erff is ~3x the instructions in a loader that runs per K step)
 MG_DEV u16x8_t vgelu(u16x8_t v) {
   u16x8_t r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = f2bf(gelu_erf(bf2f(v[j])));
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(gelu_fast(bf2f(v[j])));
   return r;
 }
 
@@ -605,6 +607,8 @@ struct Grouping {
   const int* tile_off;   // mode 1: [ngroups+1] prefix of ceil(rows_g / BM)
   int rows_per_group;    // mode 3: ngroups equal groups of this many rows (no tables)
   int swz;               // mode 0: XCD-aware tile order (1: every launch, 2: split-K launches only)
+  int sub_shift;         // mode 1: the tables count tiles of (BM << sub_shift) rows; block x = table tile << sub_shift
+                         // + sub-tile (64-row tiles over the dispatch's 128-row tile table)
 };
 
 // ---------------------------------------------------------------------------
@@ -1106,14 +1110,15 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   int kbeg = bz * kchunk, kend = min(K, kbeg + kchunk);
   int g = 0;
   if (grp.mode == 1) {
-    int t = bx;
+    int t = bx >> grp.sub_shift;
     g = -1;
     for (int i = 0; i < grp.ngroups; ++i)
       if (t >= grp.tile_off[i] && t < grp.tile_off[i + 1]) { g = i; break; }
     if (g < 0) return;
     mrow_base = grp.row_off[g];
     Mloc = grp.row_off[g + 1] - mrow_base;
-    m0 = (t - grp.tile_off[g]) * BM;
+    m0 = (t - grp.tile_off[g]) * (BM << grp.sub_shift) + (bx & ((1 << grp.sub_shift) - 1)) * BM;
+    if (m0 >= Mloc) return;  // a sub-tile past the group's last row
   } else if (grp.mode == 3) {
     int tpg = (grp.rows_per_group + BM - 1) / BM;
     g = blockIdx.x / tpg;
@@ -1190,7 +1195,7 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   if (grp.mode != 2 && splits > 1) kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
   if (grp.mode != 2) splits = (K + kchunk - 1) / kchunk;
   if (splits < 1) splits = 1;
-  int gx = grp.mode == 1 ? max_tiles_m : grp.mode == 3 ? cdiv(grp.rows_per_group, BM) * grp.ngroups : cdiv(M, BM);
+  int gx = grp.mode == 1 ? max_tiles_m << grp.sub_shift : grp.mode == 3 ? cdiv(grp.rows_per_group, BM) * grp.ngroups : cdiv(M, BM);
   int gz = grp.mode == 2 ? splits * grp.ngroups : splits;
   dim3 grid(gx, cdiv(N, BN), gz);
   EP e2 = ep;

@@ -703,6 +703,24 @@ void run_grouped(int total_rows, int N, int K, int ngroups, const int32_t* row_o
                  e ? e->a_gelu : 0};
   Grouping grp{1, ngroups, row_off, tile_off, 0};
   if constexpr (sizeof(T) == 2) {
+    // 64 x 64 tiles over the 128-row tile table (two sub-tiles per table tile) for short-K expert GEMMs (layer 1,
+    // K = C; the backward's gG x W2, K = C): load-latency-bound on 128^2 tiles like the dense short-K projections.
+    // Measured at B = 256, E = 8 top-2 (tools/expert_probe.py, profiles/round5_expert_probe.txt): layer 1 with the
+    // bias + GELU + saved pre-activation epilogue 72.8 -> 55.7 us (8x8 block, K = 256), 56.5 -> 46.6 us (4x4, K = 512),
+    // 114 -> 93 us (16x16, K = 128); layer 2 (K = 4C) is no faster, so it keeps 128^2.  A/B: tuning slot
+    // MG_TUNE_GROUPED_SHORTK (0 automatic: K <= 512, -1 never, > 0 that threshold), MG_TUNE_GEMM_TILE = 64 forces.
+    const int tl0 = g_mg_tune[MG_TUNE_GEMM_TILE], sk = g_mg_tune[MG_TUNE_GROUPED_SHORTK];
+    if (tl0 == 64 || (tl0 == 0 && sk >= 0 && K <= (sk > 0 ? sk : 512))) {
+      grp.sub_shift = 1;
+      if constexpr (BKc) {
+        LdKCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
+        launch_gemm<T, 64, 64, true, true, 1>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+      } else {
+        LdMCGroupW<T> lb{reinterpret_cast<const T*>(B), ldb, N, K, b_gstride, nullptr};
+        launch_gemm<T, 64, 64, true, false, 1>(la, lb, ep, total_rows, N, K, 1, grp, max_tiles, st);
+      }
+      return;
+    }
     // 128 x 256 tiles (same 128-row tile prefix, half the column tiles): by default for one 256-wide column tile
     // over a long K (the 8x8 block's expert layer 2, 32768 x 256 x 1024: 44 -> 39 us; wider N measured slower,
     // profiles/round4_grouped_probe.txt)

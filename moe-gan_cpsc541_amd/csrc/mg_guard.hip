@@ -27,6 +27,29 @@ __global__ void k_flag_window(const int32_t* __restrict__ flags, int32_t reset_b
   win[0] = w;
 }
 
+// the loss checks and window updates of one phase in one launch (mg_guard_update): flags[0] |= bit[i] for every check
+// whose scalars are not all finite, then the window updates in order on the updated flags (k_flag_window's rule)
+__global__ void k_guard_update(mg_guard_desc d, int32_t* __restrict__ flags, int32_t* __restrict__ win) {
+  int32_t add = 0;
+  for (int c = 0; c < 4; ++c) {
+    if (d.n[c] <= 0) continue;
+    bool bad = false;
+    for (int i = threadIdx.x; i < d.n[c]; i += 64) bad |= !isfinite(d.x[c][i]);
+    if (__ballot(bad) != 0ull) add |= d.bit[c];
+  }
+  if (threadIdx.x != 0) return;
+  const int32_t f = flags[0] | add;
+  if (add) flags[0] = f;
+  if (d.nwin > 0) {
+    int32_t w = win[0];
+    for (int j = 0; j < d.nwin && j < 2; ++j) {
+      if ((f & d.keep_mask[j]) == 0) w &= ~d.reset_bits[j];
+      if ((f & d.bad_mask[j]) == 0) w |= d.set_bits[j];
+    }
+    win[0] = w;
+  }
+}
+
 MG_DEV bool gate_on(const int32_t* flags, int32_t mask) { return flags && (flags[0] & mask) != 0; }
 
 // x[0 .. words) = 0 when (flags & mask) != 0 equals when_set (4-byte words, 16-B vectors where aligned)
@@ -78,6 +101,15 @@ extern "C" int mg_flag_window(const int32_t* flags, int32_t reset_bits, int32_t 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_flag_window, dim3(1), dim3(64), 0, st, flags, reset_bits, keep_mask, bad_mask, set_bits, win);
   return mg_check_launch("mg_flag_window");
+}
+
+extern "C" int mg_guard_update(const mg_guard_desc* d, int32_t* flags, int32_t* win, void* stream) {
+  MG_REQUIRE(d && flags, "null pointer");
+  MG_REQUIRE(d->nwin >= 0 && d->nwin <= 2 && (d->nwin == 0 || win), "0 <= nwin <= 2 (and a window word)");
+  for (int c = 0; c < 4; ++c) MG_REQUIRE(d->n[c] <= 0 || d->x[c], "null check operand");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_guard_update, dim3(1), dim3(64), 0, st, *d, flags, win);
+  return mg_check_launch("mg_guard_update");
 }
 
 extern "C" int mg_zero_if(void* x, int64_t bytes, const int32_t* flags, int32_t mask, int when_set, void* stream) {

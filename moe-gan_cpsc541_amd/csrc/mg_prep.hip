@@ -300,6 +300,25 @@ __global__ __launch_bounds__(256) void k_sumsq_fin(const float* __restrict__ par
   if (threadIdx.x == 0) out[0] += (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// mg_grad_norm_steps' second launch: the fixed-order fold of k_sumsq_fin written (not accumulated) to out[0], and the
+// gated step counters of the optimizer launches that follow (k_opt_prologue's rule per counter)
+__global__ __launch_bounds__(256) void k_sumsq_fin_steps(const float* __restrict__ part, int nparts, float* __restrict__ out,
+                                                         int32_t* step0, int32_t run0, int32_t* step1, int32_t run1,
+                                                         const int32_t* flags, int32_t skip_mask, const int32_t* win) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];  // fixed order per thread (k_sumsq_fin's)
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    const bool skip = flags && (flags[0] & skip_mask);
+    if (step0 && !skip && !(win && run0 && !(win[0] & run0))) step0[0] += 1;
+    if (step1 && !skip && !(win && run1 && !(win[0] & run1))) step1[0] += 1;
+  }
+}
+
 // One AdamW element update (torch.optim.AdamW single-tensor math, t2i_moe_gan.py:1101-1102), with every
 // multiply-add spelled out: all three AdamW kernels run the identical instruction sequence (bit-exact to
 // each other whatever the surrounding code lets the compiler contract).
@@ -625,6 +644,20 @@ extern "C" int mg_sumsq(const float* x, int64_t n, float* out, void* stream) {
   hipLaunchKernelGGL(k_sumsq, dim3(blocks), dim3(256), 0, st, x, n, part);
   hipLaunchKernelGGL(k_sumsq_fin, dim3(1), dim3(256), 0, st, part, blocks, out);
   return mg_check_launch("mg_sumsq");
+}
+
+extern "C" int mg_grad_norm_steps(const float* x, int64_t n, float* out, int32_t* step0, int32_t run_mask0, int32_t* step1,
+                                  int32_t run_mask1, const int32_t* flags, int32_t skip_mask, const int32_t* win,
+                                  void* stream) {
+  MG_REQUIRE(x && out, "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int blocks = n > 0 ? std::min(nblk(n / 16 + 1), 1024) : 0;
+  float* part = reinterpret_cast<float*>(mg_workspace(1024 * sizeof(float), st));
+  MG_REQUIRE(part, "no workspace");
+  if (blocks > 0) hipLaunchKernelGGL(k_sumsq, dim3(blocks), dim3(256), 0, st, x, n, part);
+  hipLaunchKernelGGL(k_sumsq_fin_steps, dim3(1), dim3(256), 0, st, part, blocks, out, step0, run_mask0, step1, run_mask1,
+                     flags, skip_mask, win);
+  return mg_check_launch("mg_grad_norm_steps");
 }
 
 extern "C" int mg_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,

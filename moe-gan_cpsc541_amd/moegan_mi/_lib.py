@@ -52,6 +52,18 @@ class WnDesc(ctypes.Structure):
                 ("gW", _c_void_p), ("gv", _c_void_p), ("gg", _c_void_p)]
 
 
+class RouterParamDesc(ctypes.Structure):
+    """Mirror of ``mg_router_param_desc``."""
+    _fields_ = [("mu", _c_void_p), ("rho", _c_void_p), ("eps", _c_void_p), ("gW", _c_void_p), ("kl_coef", _c_void_p),
+                ("gmu", _c_void_p), ("grho", _c_void_p), ("n", _i64)]
+
+
+class GuardDesc(ctypes.Structure):
+    """Mirror of ``mg_guard_desc``."""
+    _fields_ = [("x", _c_void_p * 4), ("n", _i32 * 4), ("bit", _i32 * 4), ("nwin", _i32), ("reset_bits", _i32 * 2),
+                ("keep_mask", _i32 * 2), ("bad_mask", _i32 * 2), ("set_bits", _i32 * 2)]
+
+
 # Argument types are derived from include/moegan_hip.h itself, so the binding
 # cannot drift from the C ABI (the header travels with the library).
 _HEADER = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "moegan_hip.h"))
@@ -59,7 +71,8 @@ _CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "uint64_t": ctypes.c_ui
           "float": _f32,
           "void": _c_void_p, "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc),
           "mg_prep_desc": ctypes.POINTER(PrepDesc), "mg_colsum_desc": ctypes.POINTER(ColsumDesc),
-          "mg_wn_desc": ctypes.POINTER(WnDesc)}
+          "mg_wn_desc": ctypes.POINTER(WnDesc), "mg_router_param_desc": ctypes.POINTER(RouterParamDesc),
+          "mg_guard_desc": ctypes.POINTER(GuardDesc)}
 _RESTYPE = {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "const char*": ctypes.c_char_p}
 SIG_RE = r"\b(int|int64_t|const char\*)\s+(mg_\w+)\(([^)]*)\);"
 
@@ -78,9 +91,7 @@ def _parse_header(path=_HEADER):
                 continue
             base = a.replace("const ", "").split()[0].rstrip("*")
             if "*" in a:
-                types.append(_CTYPE[base] if base in ("mg_epilogue", "mg_gemm_desc", "mg_prep_desc", "mg_colsum_desc",
-                                                          "mg_wn_desc")
-                             else _c_void_p)
+                types.append(_CTYPE[base] if base.endswith("_desc") or base == "mg_epilogue" else _c_void_p)
             else:
                 types.append(_CTYPE[base])
             names.append(a.replace("*", " ").split()[-1])

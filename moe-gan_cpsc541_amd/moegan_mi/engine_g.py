@@ -365,7 +365,9 @@ class GeneratorEngine:
             if save:
                 Xg = ops.gather_rows(tok, perm, k)
                 Pre = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
-                Hid = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
+                # the GELU output is recomputed from Pre by the layer-2 weight gradient's loader unless stored
+                # (ops.FFN_SAVE_HID): one [rows x 4C] bf16 write less per step
+                Hid = torch.empty(n, Hd, device=self.dev, dtype=self.cdt) if ops.FFN_SAVE_HID else None
                 ops.moe_ffn_fwd(Xg, W1.view(E, Hd, C), b1, W2.view(E, C, Hd), b2, row_off, tile_off, max_tiles, Y,
                                 pre=Pre, hid=Hid)
             else:
@@ -513,12 +515,13 @@ class GeneratorEngine:
         ops.gemm_batch(pb, a_kc=False, b_kc=False)
         ops.gemm_batch(pc, a_kc=False, b_kc=False)
         ops.gemm_batch(pd)
-        for q in items:
-            r = q["r"]
-            for nm, gWx, epi in (("feature", q["gWf"], 0), ("text", q["gWt"], 1), ("combined", q["gWc"], 2)):
-                ops.router_param_bwd(self.P(r + nm + "_mu"), self.P(r + nm + "_rho"), q["eps"][epi], gWx,
-                                     q["kl_coef"], self.G(r + nm + "_mu"), self.G(r + nm + "_rho"),
-                                     flags=self.guard_flags, mask=ops.FLAG_G_BAD)
+        # the reparameterisation / KL backward of every router parameter of every block: one launch
+        ops.router_param_bwd_batch(
+            [(self.P(q["r"] + nm + "_mu"), self.P(q["r"] + nm + "_rho"), q["eps"][epi], gWx, q["kl_coef"],
+              self.G(q["r"] + nm + "_mu"), self.G(q["r"] + nm + "_rho"))
+             for q in items for nm, gWx, epi in (("feature", q["gWf"], 0), ("text", q["gWt"], 1),
+                                                 ("combined", q["gWc"], 2))],
+            flags=self.guard_flags, mask=ops.FLAG_G_BAD)
 
     def _cbuf(self):
         return self.st.shadow if self.st.shadow is not None else self.st.data
@@ -547,13 +550,16 @@ class GeneratorEngine:
         if fused:
             # one pass per 128-row tile: gP = (gG W2_e) * GELU'(pre), gX = gP W1_e, gb1 column sums (mg_moe_ffn_bwd)
             ops.moe_ffn_bwd(gG, Pre, sv["W1"].view(E, Hd, C), sv["W2"].view(E, C, Hd), row_off, tile_off,
-                            sv["max_tiles"], gP, gX, gb1.view(E, Hd))
+                            sv["max_tiles"], gP, gX, gb1.view(E, Hd), gb2.view(E, C))
         else:
             # expert layer 2: dH = gG @ W2_e, times GELU'(pre)
             ops.gemm_grouped(gG, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
                              out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd))
-        self.side.run(lambda: (ops.gemm_grouped_wgrad(gG, sv["Hid"], row_off, n, C, Hd, gW2),
-                               ops.grouped_colsum(gG, row_off, C, n, gb2)), gG)
+        if sv["Hid"] is not None:
+            gw2 = lambda: ops.gemm_grouped_wgrad(gG, sv["Hid"], row_off, n, C, Hd, gW2)  # noqa: E731
+        else:  # GELU(Pre) formed by the B loader (the forward kept only the pre-activation)
+            gw2 = lambda: ops.gemm_grouped_wgrad(gG, Pre, row_off, n, C, Hd, gW2, b_gelu=1)  # noqa: E731
+        self.side.run(lambda: (gw2(), None if fused else ops.grouped_colsum(gG, row_off, C, n, gb2)), gG)
         # expert layer 1
         if not fused:
             ops.gemm_grouped(gP, sv["W1"], row_off, tile_off, sv["max_tiles"], C, Hd, b_kc=False, b_gstride=Hd * C,

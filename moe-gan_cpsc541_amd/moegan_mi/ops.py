@@ -269,6 +269,13 @@ def gemm_grouped(A, B, row_off, tile_off, max_tiles, N, K, *, b_kc=True, b_gstri
     return out
 
 
+# the fused forward's GELU output is stored for the layer-2 weight gradient (1) or recomputed there from the
+# pre-activation by the GEMM loader (0, default).  Measured at the C2 16x16 block (profiles/round5_expert_probe*.txt):
+# the saved forward 133 -> 90 us without the [rows x 4C] GELU-output write, the weight gradient 74 -> 80 us with
+# GELU on load.
+FFN_SAVE_HID = os.environ.get("MOEGAN_FFN_HID", "0") == "1"
+
+
 def ffn_fusable(dtype, C):
     """The fused expert FFN is used where it measured faster than the two grouped GEMMs: bf16, C = 128
     (B=256, E=8 top-2: 145 -> 116 us no-grad, 170 -> 144 us saved).  C = 256 stays on the grouped GEMMs
@@ -285,11 +292,12 @@ def moe_ffn_fwd(X, W1, b1, W2, b2, row_off, tile_off, max_tiles, Y, *, pre=None,
     return Y
 
 
-def moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1=None):
-    """Fused expert FFN backward (mg_moe_ffn_bwd): gP = (gG W2_g) * GELU'(Pre), gX = gP W1_g, gb1 += colsum(gP)."""
+def moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1=None, gb2=None):
+    """Fused expert FFN backward (mg_moe_ffn_bwd): gP = (gG W2_g) * GELU'(Pre), gX = gP W1_g, gb1 += colsum(gP),
+    gb2 += colsum(gG) (per group)."""
     G, Hd, C = W1.shape
     call("mg_moe_ffn_bwd", L.MG_BF16, gG.shape[0], C, Hd, G, ptr(row_off), ptr(tile_off), max_tiles, ptr(gG),
-         ptr(Pre), ptr(W1), ptr(W2), ptr(gP), ptr(gX), ptr(gb1), S())
+         ptr(Pre), ptr(W1), ptr(W2), ptr(gP), ptr(gX), ptr(gb1), ptr(gb2), S())
     return gP, gX
 
 
@@ -534,6 +542,30 @@ def flag_window(flags, win, *, reset_bits=0, keep_mask=0, bad_mask=0, set_bits=0
     call("mg_flag_window", ptr(flags), reset_bits, keep_mask, bad_mask, set_bits, ptr(win), S())
 
 
+def guard_update(flags, win=None, checks=(), windows=()):
+    """One launch (mg_guard_update) for a phase's loss checks -- ``checks``: (tensor, bit), flags |= bit when the
+    tensor is not all finite -- and then its window updates -- ``windows``: dicts of flag_window's keyword
+    arguments, applied in order on the updated flags."""
+    assert len(checks) <= 4 and len(windows) <= 2
+    d = L.GuardDesc()
+    for i, (t, bit) in enumerate(checks):
+        d.x[i], d.n[i], d.bit[i] = t.data_ptr(), t.numel(), bit
+    d.nwin = len(windows)
+    for j, w in enumerate(windows):
+        d.reset_bits[j], d.keep_mask[j] = w.get("reset_bits", 0), w.get("keep_mask", 0)
+        d.bad_mask[j], d.set_bits[j] = w.get("bad_mask", 0), w.get("set_bits", 0)
+    call("mg_guard_update", ctypes.byref(d), ptr(flags), ptr(win), S())
+
+
+def grad_norm_steps(x, out, steps=(), flags=None, skip_mask=0, win=None):
+    """out[0] = sum of x^2 (mg_grad_norm_steps, written) and, for each (step counter, run mask) in ``steps`` (at
+    most two), the counter advanced under opt_prologue's gate."""
+    assert len(steps) <= 2
+    st = list(steps) + [(None, 0)] * (2 - len(steps))
+    call("mg_grad_norm_steps", ptr(x), x.numel(), ptr(out), ptr(st[0][0]), st[0][1], ptr(st[1][0]), st[1][1],
+         ptr(flags), skip_mask, ptr(win), S())
+
+
 def zero_if(x, flags, mask, when_set=True):
     """x = 0 when (flags & mask) != 0 equals ``when_set``."""
     call("mg_zero_if", ptr(x), x.numel() * x.element_size(), ptr(flags), mask, int(bool(when_set)), S())
@@ -729,6 +761,17 @@ def kl_coefs(kl2, R, eff_w, coef, total):
 def router_param_bwd(mu, rho, eps, gW, kl_coef, gmu, grho, flags=None, mask=0):
     call("mg_router_param_bwd", ptr(mu), ptr(rho), ptr(eps), ptr(gW), mu.numel(), ptr(kl_coef), ptr(gmu),
          ptr(grho), ptr(flags), mask, S())
+
+
+def router_param_bwd_batch(items, flags=None, mask=0):
+    """Every router parameter gradient of a backward in one launch (mg_router_param_bwd_batch).  items: tuples
+    (mu, rho, eps, gW, kl_coef, gmu, grho) as router_param_bwd takes them."""
+    for i in range(0, len(items), 32):
+        part = items[i:i + 32]
+        arr = (L.RouterParamDesc * len(part))()
+        for j, (mu, rho, eps, gW, klc, gmu, grho) in enumerate(part):
+            arr[j] = L.RouterParamDesc(ptr(mu), ptr(rho), ptr(eps), ptr(gW), ptr(klc), ptr(gmu), ptr(grho), mu.numel())
+        call("mg_router_param_bwd_batch", len(part), arr, ptr(flags), mask, S())
 
 
 def balance(load, E_, T, weight, grad_scale, out, coef):

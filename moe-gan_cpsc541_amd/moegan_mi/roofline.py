@@ -34,7 +34,7 @@ FAMILIES = {
     "mtm_bwd": ("hbm", ("mg_mtm_bwd_fused",)),
     "modconv_bwd_io": ("hbm", ("mg_modconv_bwd_in", "mg_modconv_bwd_out", "mg_scale_bc")),
     "r1": ("hbm", ("mg_r1",)),
-    "sumsq": ("hbm", ("mg_sumsq",)),
+    "sumsq": ("hbm", ("mg_sumsq", "mg_grad_norm_steps")),
     "adamw": ("hbm", ("mg_adamw_dev", "mg_adamw_dev_shadow", "mg_adamw")),
     "bias_colsum": ("hbm", ("mg_colsum", "mg_grouped_colsum", "mg_colsum_batch", "mg_segsum", "mg_const_bwd")),
     "weight_prep": ("hbm", ("mg_pack_conv", "mg_pack_conv_flip", "mg_pack_dgrad_s2", "mg_wsq", "mg_wsq_bwd",
@@ -43,7 +43,7 @@ FAMILIES = {
                             "mg_prep_batch")),
     "layernorm": ("hbm", ("mg_layernorm_fwd", "mg_layernorm_bwd")),
     "router_aux": ("hbm", ("mg_router_bwd", "mg_moe_gate_grad", "mg_moe_token_grad", "mg_router_feat_grad",
-                           "mg_router_param_bwd", "mg_moe_dispatch", "mg_router_kl")),
+                           "mg_router_param_bwd", "mg_router_param_bwd_batch", "mg_moe_dispatch", "mg_router_kl")),
     "im2col_col2im": ("hbm", ("mg_im2col_4x4s2", "mg_col2im_4x4s2")),
     "d_conv0": ("hbm", ("mg_d0_fwd", "mg_d0_wgrad", "mg_d0_dgrad")),
     "elementwise": ("hbm", ("mg_cast", "mg_copy2d", "mg_lrelu_mask_mul", "mg_upsample2x_fwd", "mg_upsample2x_bwd",
@@ -54,7 +54,7 @@ FAMILIES = {
     "mtm_bwd_unfused": ("hbm", ("mg_warp_bwd", "mg_offset_head_bwd")),
     # scalar losses, guard words, optimizer prologue: a few hundred bytes each, launch-latency bound
     "losses_flags": ("hbm", ("mg_d_loss", "mg_g_loss", "mg_finite_flag", "mg_flag_window", "mg_kl_coefs", "mg_balance",
-                             "mg_opt_prologue")),
+                             "mg_opt_prologue", "mg_guard_update")),
 }
 _FAMILY_OF = {e: f for f, (_, es) in FAMILIES.items() for e in es}
 
@@ -90,7 +90,8 @@ KERNELS = [
      "elementwise"),
     (r"k_head_|k_d_text|k_dhead_", "disc_head"),
     (r"k_warp_bwd|k_offset_head", "mtm_bwd_unfused"),
-    (r"k_d_loss|k_g_loss|k_finite_flag|k_flag_window|k_kl_coefs|k_balance|k_opt_prologue", "losses_flags"),
+    (r"k_d_loss|k_g_loss|k_finite_flag|k_flag_window|k_guard_update|k_kl_coefs|k_balance|k_opt_prologue",
+     "losses_flags"),
 ]
 
 
@@ -302,8 +303,13 @@ def work(name, a):
         return 8.0 * a["R"]
     if name == "mg_balance":
         return 8.0 * a["E"]
-    if name in ("mg_flag_window", "mg_opt_prologue"):
+    if name in ("mg_flag_window", "mg_opt_prologue", "mg_guard_update"):
         return 16.0
+    if name == "mg_grad_norm_steps":
+        return 4.0 * a["n"]
+    if name == "mg_router_param_bwd_batch":
+        d = a["descs"]
+        return sum(32.0 * d[i].n for i in range(a["n"]))
     if name == "mg_quant_mx8":  # bf16 in, e4m3 + one E8M0 byte per 32 out
         return a["rows"] * a["K"] * (2 + 1 + 1 / 32)
     return None

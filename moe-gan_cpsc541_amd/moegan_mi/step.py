@@ -171,6 +171,16 @@ class TrainStep:
             flags.copy_(bits[0:1] | bits[1:2])
         graphs.eager(run)
 
+    def _guard(self, flags, checks, windows):
+        """A phase's loss guards: the finite checks, the data-parallel agreement on the flag word, the window
+        updates -- one launch (ops.guard_update) without a process group, check / all-reduce / windows with one."""
+        if self.pg is None:
+            ops.guard_update(flags, self.win, checks, windows)
+            return
+        ops.guard_update(flags, None, checks, ())
+        self._allreduce_flags(flags)
+        ops.guard_update(flags, self.win, (), windows)
+
     # ---- optimizer ----
     def _adamw(self, store, grad, lr, max_norm, flags, ranges, grad_scale=1.0):
         """clip_grad_norm_ + AdamW over ``grad[:n_opt]`` (torch semantics, :1333-1337 / :1417-1421).  ``ranges``:
@@ -179,15 +189,14 @@ class TrainStep:
         if grad_scale != 1.0:  # (loss / accumulation_steps) of the reference == scaling the summed gradient
             grad[:n].mul_(grad_scale)
         ss = torch.empty(1, device=self.dev)
-        ops.opt_prologue(ss, None)
-        ops.sumsq(grad[:n], ss)
+        live = [(lo, hi, step_dev, wbit) for lo, hi, step_dev, wbit in ranges if hi > lo]
+        # the norm and every range's device step counter (+1, graph-replayable, gated) in two launches
+        ops.grad_norm_steps(grad[:n], ss, [(step_dev, wbit) for _, _, step_dev, wbit in live], flags=flags,
+                            skip_mask=FD, win=self.win)
         c = self.cfg
         bf16_shadow = store.shadow is not None and store.shadow.dtype == torch.bfloat16
-        for lo, hi, step_dev, wbit in ranges:
-            if hi <= lo:
-                continue
+        for lo, hi, step_dev, wbit in live:
             gate = (flags, FD, self.win, wbit)
-            ops.opt_prologue(None, step_dev, gate=gate)  # device step counter += 1 (graph-replayable), gated
             ops.adamw_dev(store.data[lo:hi], grad[lo:hi], store.m[lo:hi], store.v[lo:hi], lr, c.beta1, c.beta2,
                           c.eps, c.weight_decay, step_dev, ss, max_norm,
                           shadow=store.shadow[lo:hi] if bf16_shadow else None, gate=gate)
@@ -246,10 +255,8 @@ class TrainStep:
         dres = self.de.d_phase(real, text, f16, ("nhwc", 8), perm, c.r1_gamma)
         ops.COLSUMS.flush()
         # guard: NaN / Inf d_loss skips the whole batch (t2i_moe_gan.py:1315-1320)
-        ops.finite_flag(dres["losses"][:1], FD, flags)
-        ops.finite_flag(dres["r1"], FD, flags)
-        self._allreduce_flags(flags)
-        ops.flag_window(flags, self.win, reset_bits=ops.WIN_D if zero_grads else 0, bad_mask=FD, set_bits=ops.WIN_D)
+        self._guard(flags, [(dres["losses"][:1], FD), (dres["r1"], FD)],
+                    [dict(reset_bits=ops.WIN_D if zero_grads else 0, bad_mask=FD, set_bits=ops.WIN_D)])
         if accum:
             ops.gated_axpy(ds.acc, ds.grad, flags, FD)
         dgrad = ds.acc if accum else ds.grad
@@ -294,13 +301,10 @@ class TrainStep:
         kl_total = torch.empty(1, device=self.dev)
         ops.kl_coefs(kl2, len(kl2s), eff_kl_weight, kl_coef, kl_total)
         # guard: NaN / Inf (GAN + CLIP + balance) generator loss -> 0, the KL term stays (:1396-1404)
-        for t in (g_gan, bal, clip16, clip8):
-            if t is not None:
-                ops.finite_flag(t, FG, flags)
-        self._allreduce_flags(flags)
-        ops.flag_window(flags, self.win, reset_bits=(ops.WIN_G_MAIN | ops.WIN_G_KL) if zero_grads else 0,
-                        keep_mask=FD, bad_mask=FD, set_bits=ops.WIN_G_KL)
-        ops.flag_window(flags, self.win, bad_mask=FD | FG, set_bits=ops.WIN_G_MAIN)
+        self._guard(flags, [(t, FG) for t in (g_gan, bal, clip16, clip8) if t is not None],
+                    [dict(reset_bits=(ops.WIN_G_MAIN | ops.WIN_G_KL) if zero_grads else 0, keep_mask=FD, bad_mask=FD,
+                          set_bits=ops.WIN_G_KL),
+                     dict(bad_mask=FD | FG, set_bits=ops.WIN_G_MAIN)])
         # data parallel, one optimizer step per batch: the generator gradient is all-reduced in buckets that
         # start while the backward still runs (expert ranges first); otherwise one collective after it
         g_finish = None

@@ -96,6 +96,36 @@ def test_discriminator_module_vs_oracle(res):
         close(D.flat.grad[off:off + numel].view(st.shapes[n]), PD[n].grad.numpy(), rtol=5e-4, atol=1e-6, what=n)
 
 
+@pytest.mark.parametrize("res", [64, 256])
+def test_discriminator_module_bf16_direct_kernel_limits(res):
+    """The bf16 discriminator at a size the direct conv_layers.0 / head kernels take (64: W/2 = 32, Hf = 16) and at
+    one past their limits (256: W/2 = 128 > 64, Hf = 64 > 32), which falls back to im2col + GEMMs and the GEMM head
+    (DiscriminatorEngine._d0_ok / _head_ok; the implicit convs of conv_layers.2 take power-of-two sizes): logits and
+    the image gradient against the fp32 oracle at the bf16 bar (relative L2 <= 2e-2)."""
+    M = _M()
+    from moegan_mi.layout import discriminator_shapes
+    D = M.AuroraDiscriminator(dtype="bf16")
+    D.load_state_dict({k: torch.from_numpy(v) for k, v in fill_state(discriminator_shapes(), 50).items()})
+    D = D.to(DEV)
+    g = torch.Generator().manual_seed(res)
+    B = 2
+    img = (torch.rand(B, 3, res, res, generator=g) * 2 - 1)
+    text = torch.randn(B, 512, generator=g)
+    PD = {k: v.detach().cpu().clone() for k, v in D.state_dict().items()}
+    ximg = img.clone().requires_grad_(True)
+    ref = O.discriminator(ximg, text, PD)
+    R = torch.randn(ref.shape, generator=g)
+    (ref * R).sum().backward()
+    gimg = img.to(DEV).requires_grad_(True)
+    out = D(gimg, text.to(DEV))
+    (out * R.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    rel = lambda a, b: float((a.detach().double().cpu() - b.double()).norm() / b.double().norm())  # noqa: E731
+    assert out.shape == ref.shape
+    assert rel(out, ref.detach()) <= 2e-2, rel(out, ref.detach())
+    assert rel(gimg.grad, ximg.grad) <= 2e-2, rel(gimg.grad, ximg.grad)
+
+
 def test_sample_and_checkpoint_roundtrip(tmp_path):
     M = _M()
     G = _gen(M)

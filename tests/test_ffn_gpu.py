@@ -98,17 +98,23 @@ def test_fused_ffn_backward_matches_grouped_gemms(T, E, k, skew, C, occ):
     gP = torch.empty(n, Hd, device=DEV, dtype=bf)
     gX = torch.empty(n, C, device=DEV, dtype=bf)
     gb1 = torch.full((E, Hd), 0.25, device=DEV)
-    ops.moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1)
+    gb2 = torch.full((E, C), -0.5, device=DEV)
+    ops.moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1, gb2)
+    gb2_r = torch.full((E * C,), -0.5, device=DEV)
+    ops.grouped_colsum(gG, row_off, C, n, gb2_r)
     torch.cuda.synchronize()
     L.call("mg_set_tuning", 14, 0)
     assert torch.equal(gP, gP_r)
     assert torch.equal(gX, gX_r)
     scale = float((gb1_r - 0.25).abs().max())
     assert float((gb1.view(-1) - gb1_r).abs().max()) <= 1e-5 * scale + 1e-7
-    # float64 column sums of the bf16 gP, per expert
+    # float64 column sums of the bf16 gP (layer-1 bias) and of gG (layer-2 bias), per expert
     ro = row_off.cpu().tolist()
     ref = torch.stack([gP[ro[e]:ro[e + 1]].double().sum(0) for e in range(E)]) + 0.25
     assert float((gb1.double() - ref.to(DEV)).abs().max()) <= 1e-5 * float(ref.abs().max())
+    ref2 = torch.stack([gG[ro[e]:ro[e + 1]].double().sum(0) for e in range(E)]) - 0.5
+    assert float((gb2.double() - ref2.to(DEV)).abs().max()) <= 1e-5 * float(ref2.abs().max())
+    assert float((gb2.view(-1) - gb2_r).abs().max()) <= 1e-5 * float((gb2_r + 0.5).abs().max()) + 1e-7
     # and the gradients against float64 math on the same bf16 operands (sampled rows)
     rows = torch.randperm(n, device=DEV)[:64]
     e_of = torch.bucketize(rows.int(), row_off[1:].contiguous(), right=True)
@@ -118,3 +124,45 @@ def test_fused_ffn_backward_matches_grouped_gemms(T, E, k, skew, C, occ):
     assert (gP[rows].double() - gh * gelu_grad).abs().max() <= 1e-2 * (gh * gelu_grad).abs().max()
     gx = torch.einsum("rh,rhc->rc", gP[rows].double(), W1[e_of].double())
     assert (gX[rows].double() - gx).abs().max() <= 1e-2 * gx.abs().max()
+
+
+@pytest.mark.parametrize("T,C,E,k", [(16384, 256, 8, 2), (4096, 512, 8, 2), (1000, 128, 8, 2), (77, 256, 4, 1)])
+def test_grouped_64x64_subtiles_bit_identical(T, C, E, k):
+    """Grouped expert GEMMs on 64x64 tiles over the dispatch's 128-row tile table (two sub-tiles per table tile,
+    Grouping.sub_shift; tuning slot 3 = 64, and the automatic choice) equal the 128^2-tile launch bit for bit: the same MFMA k order per
+    output element.  Layer 1 with the bias + GELU + saved pre-activation epilogue, layer 2, and the data gradient
+    (MC weight operand); skewed / empty experts and ragged last tiles (rows past a group's end in the second
+    sub-tile)."""
+    tok, W1, b1, W2, b2, topi, gate = _case(T, C, E, k, 7 * T + C, empty_expert=(T == 1000))
+    Hd = 4 * C
+    row_off, tile_off, perm, pos_of, gate_pos = ops.moe_dispatch(topi, gate, E)
+    n = T * k
+    max_tiles = (n + 127) // 128 + E
+    Xg = ops.gather_rows(tok, perm, k)
+
+    def run():
+        Pre = torch.empty(n, Hd, device=DEV, dtype=bf)
+        Hid = torch.empty(n, Hd, device=DEV, dtype=bf)
+        ops.gemm_grouped(Xg, W1.view(-1), row_off, tile_off, max_tiles, Hd, C, b_gstride=Hd * C, out=Hid, ldb=C,
+                         ep=ops.E(bias=b1, act=L.ACT_GELU, out_pre=Pre, ld_pre=Hd))
+        Y = torch.empty(n, C, device=DEV, dtype=bf)
+        ops.gemm_grouped(Hid, W2.view(-1), row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y, ldb=Hd,
+                         ep=ops.E(bias=b2))
+        gX = torch.empty(n, C, device=DEV, dtype=bf)
+        ops.gemm_grouped(Hid, W1.view(-1), row_off, tile_off, max_tiles, C, Hd, b_kc=False, b_gstride=Hd * C, out=gX,
+                         ldb=C)
+        torch.cuda.synchronize()
+        return Pre, Hid, Y, gX
+    L.call("mg_set_tuning", 3, 128)  # 128^2 tiles everywhere
+    try:
+        ref = run()
+        L.call("mg_set_tuning", 3, 64)  # 64^2 sub-tiles everywhere
+        got = run()
+        L.call("mg_set_tuning", 3, 0)  # the automatic choice (64^2 for K <= 512)
+        auto = run()
+    finally:
+        L.call("mg_set_tuning", 3, 0)
+    for a, b in zip(auto, ref):
+        assert torch.equal(a, b)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)

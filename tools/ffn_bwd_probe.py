@@ -27,6 +27,7 @@ Pre = torch.randn(n, Hd, device=DEV, generator=g).to(bf)
 gP = torch.empty(n, Hd, device=DEV, dtype=bf)
 gX = torch.empty(n, C, device=DEV, dtype=bf)
 gb1 = torch.zeros(E, Hd, device=DEV)
+gb2 = torch.zeros(E, C, device=DEV)
 
 
 def unfused():
@@ -37,7 +38,7 @@ def unfused():
 
 
 def fused():
-    ops.moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1)
+    ops.moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1, gb2)
 
 
 gf = 2 * 2.0 * n * C * Hd / 1e9
