@@ -449,6 +449,32 @@ typedef struct mg_prep_desc {
 } mg_prep_desc;
 int mg_prep_batch(int dtype, int n, const mg_prep_desc* descs, void* stream);
 
+/* Gradient folds: the second pass of the two-pass gradient reductions (split-K weight-gradient slabs, per-image /
+   per-block partial rows), normally one launch each right after its producer.  mg_fold_defer(1, stream): from now
+   on the producers on `stream` (conv weight gradients with split-K slabs, the direct offset-head weight gradient,
+   the fused MTM backward's offset-head rows, the router feature / temperature rows) keep their partials in a
+   per-stream arena that is not reused before the flush and record their folds; mg_fold_flush(stream) runs every
+   recorded fold in one launch per kind and recycles the arena; mg_fold_defer(0, stream) flushes and stops.  The
+   gradients are only final after the flush.  Deferred and immediate folds run the same kernels (bit-identical).
+   The arena grows outside stream capture only (a captured step replays the allocation sequence of its eager warm-up;
+   under capture a producer that finds no room folds immediately). */
+typedef struct mg_fold_rows {
+  const float* src; /* nrows partial rows, row r at src + r * stride */
+  int64_t stride;
+  int32_t nrows, ncols, na; /* out_a[i] += sum_r src[r * stride + i] for i < na, out_b[i - na] for na <= i < ncols */
+  float* out_a;
+  float* out_b;
+} mg_fold_rows;
+typedef struct mg_fold_wgrad {
+  const float* ws; /* splits slabs [splits][Cout][taps * Cin] (tap-major columns) */
+  int32_t splits, Cout, lgCin, taps, lgCC; /* Cin = 1 << lgCin; blocks of CC = 1 << lgCC input channels */
+  float* gw;       /* [Cout][Cin][taps] (reference layout), accumulated */
+} mg_fold_wgrad;
+int mg_fold_defer(int on, void* stream);
+int mg_fold_flush(void* stream);
+/* the rows-fold kernel on caller records (tests / tools) */
+int mg_fold_rows_batch(int n, const mg_fold_rows* recs, void* stream);
+
 /* Multi-tensor column sums (bias gradients of a whole backward in one launch): out[c] += sum_r X[r*ld+c]
    for every descriptor; fp32 atomics across row blocks (at most 32 descriptors per launch). */
 typedef struct mg_colsum_desc {

@@ -125,6 +125,18 @@ inline bool mg_det() { return g_mg_tune[MG_TUNE_DETERMINISTIC].load(std::memory_
 // Device scratch, one block per (device, stream): caller-owned (mg_set_workspace) or library-owned
 // (grown on demand, never shrunk).  NULL when it cannot be provided (mg_last_error says why).
 void* mg_workspace(size_t bytes, hipStream_t stream);
+// Gradient folds (mg_fold.hip).  A producer of fold partials asks mg_fold_alloc first: non-NULL = the stream defers
+// its folds (mg_fold_defer) and the partials live in the deferral arena until the flush, so the fold is recorded
+// (deferred = true); NULL = take mg_workspace and fold now.  Both paths run the same fold kernels.
+void* mg_fold_alloc(size_t bytes, hipStream_t stream);
+int mg_fold_rows_submit(const mg_fold_rows& r, bool deferred, hipStream_t stream);
+int mg_fold_wgrad_submit(const mg_fold_wgrad& r, bool deferred, hipStream_t stream);
+// partials buffer for a fold: the deferral arena when the stream defers, else the stream's workspace
+inline float* mg_fold_partials(size_t bytes, hipStream_t st, bool* deferred) {
+  void* p = mg_fold_alloc(bytes, st);
+  *deferred = p != nullptr;
+  return reinterpret_cast<float*>(p ? p : mg_workspace(bytes, st));
+}
 
 // Fixed-order fold of partial rows (deterministic mode): out_a[i] += sum_r part[r * ncols + i] for i < na,
 // out_b[i - na] += ... for na <= i < ncols (64 columns x 16 row lanes per block, rows folded in lane order).
@@ -179,6 +191,7 @@ bool mg_conv3_direct_ok(int H, int W, int Cin, int Cout, int KH, int KW, int str
 bool mg_conv3_direct(const void* x, int B, int H, int Cin, const void* wpack, int Cout, const mg_epilogue* e, void* y,
                      int64_t ldy, int y_dtype, hipStream_t st);
 bool mg_wgrad3_direct(const void* gy, int64_t ldg, const void* x, int B, int H, int Cin, float** ws_out, int* splits,
+                      bool* deferred,
                       hipStream_t st);
 
 // mg_wgrad_wide.hip: wide split-K weight gradients (bf16 [K][M] x [K][N] -> fp32 C +=), true when handled

@@ -1,0 +1,253 @@
+// Gradient folds: the second pass of every two-pass gradient reduction (split-K weight-gradient slabs, per-image
+// and per-block partial rows), immediate or deferred to one batched launch per backward.
+//
+// The weight gradients of the step are produced in two passes so that no two workgroups add into the same
+// address: the first pass writes partial slabs / rows, the fold sums them in a fixed order into the parameter
+// gradient.  Every fold was its own launch (~5-8 us of mostly launch latency each; ~30 per C2 step: the conv
+// weight-gradient slabs, the MTM offset-head rows, the router feature and temperature rows).  Nothing reads those
+// gradients before the optimizer (or, for the router feature rows, before the batched router-parameter GEMMs at
+// the end of the backward), so with deferral on (mg_fold_defer) a producer writes its partials into a per-stream
+// arena that is not reused until mg_fold_flush, records the fold, and the flush runs all recorded folds as one
+// launch per fold kind.  Immediate folds run through the same kernels with one record, so a gradient is
+// bit-identical whether its fold was deferred or not.
+//
+// Kinds:
+//   rows: out[i] += sum_r src[r * stride + i] for i < ncols (i >= na: out_b[i - na]); 16 row lanes per column,
+//         lanes in order (the order of the per-producer fold kernels it replaced)
+//   wgrad: gw[o][ci][tap] += sum_s ws[s][o][tap * Cin + ci] (split-K slabs of a conv weight gradient folded into the
+//         reference [Cout][Cin][KH][KW] layout, four slabs in flight, fixed order)
+#include <mutex>
+#include <vector>
+
+#include "mg_common.h"
+
+namespace {
+
+constexpr int kFoldMax = 40;  // records per launch (kernel arguments stay below 4 KiB)
+
+struct RowsBatch {
+  mg_fold_rows r[kFoldMax];
+  int blk_off[kFoldMax + 1];
+  int n;
+};
+
+struct WgradBatch {
+  mg_fold_wgrad r[kFoldMax];
+  int blk_off[kFoldMax + 1];
+  int n;
+};
+
+MG_DEV int find_rec(const int* blk_off, int n) {
+  int d = 0;
+  while (d + 1 < n && (int)blockIdx.x >= blk_off[d + 1]) ++d;
+  return d;
+}
+
+// 64 columns x 16 row lanes per block
+__global__ __launch_bounds__(1024) void k_fold_rows_batch(RowsBatch b) {
+  __shared__ float red[16][64];
+  const int d = find_rec(b.blk_off, b.n);
+  const mg_fold_rows& q = b.r[d];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int i = (blockIdx.x - b.blk_off[d]) * 64 + cx;
+  float s = 0.f;
+  if (i < q.ncols)
+    for (int r = ry; r < q.nrows; r += 16) s += q.src[(int64_t)r * q.stride + i];
+  red[ry][cx] = s;
+  __syncthreads();
+  if (ry == 0 && i < q.ncols) {
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) t += red[y][cx];
+    if (i < q.na) q.out_a[i] += t;
+    else q.out_b[i - q.na] += t;
+  }
+}
+
+inline int rows_blocks(const mg_fold_rows& q) { return std::max(1, cdiv(q.ncols, 64)); }
+
+// block (o, chunk of CC input channels) of one record; its slab segments staged in LDS, written in reference order
+__global__ __launch_bounds__(256) void k_fold_wgrad_batch(WgradBatch b) {
+  extern __shared__ float seg[];  // [taps][CC]
+  const int d = find_rec(b.blk_off, b.n);
+  const mg_fold_wgrad& q = b.r[d];
+  const int Cin = 1 << q.lgCin, N = q.taps << q.lgCin, CC = 1 << q.lgCC;
+  const int64_t MN = (int64_t)q.Cout * N;
+  const int lb = blockIdx.x - b.blk_off[d], nch = Cin >> q.lgCC;
+  const int o = lb / nch, c0 = (lb - o * nch) << q.lgCC;
+  const float* src = q.ws + (int64_t)o * N + c0;
+  const int nv = (q.taps << q.lgCC) >> 2;  // 16-B vectors of this block
+  for (int v = threadIdx.x; v < nv; v += 256) {
+    const int tap = (4 * v) >> q.lgCC, ci = (4 * v) & (CC - 1);
+    const float* p = src + ((int64_t)tap << q.lgCin) + ci;
+    f32x4_t acc = *reinterpret_cast<const f32x4_t*>(p);
+    int s = 1;
+    for (; s + 3 < q.splits; s += 4) {
+      const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p + s * MN);
+      const f32x4_t bb = *reinterpret_cast<const f32x4_t*>(p + (s + 1) * MN);
+      const f32x4_t c = *reinterpret_cast<const f32x4_t*>(p + (s + 2) * MN);
+      const f32x4_t e = *reinterpret_cast<const f32x4_t*>(p + (s + 3) * MN);
+      acc += ((a + bb) + (c + e));
+    }
+    for (; s < q.splits; ++s) acc += *reinterpret_cast<const f32x4_t*>(p + s * MN);
+    *reinterpret_cast<f32x4_t*>(seg + 4 * v) = acc;
+  }
+  __syncthreads();
+  float* dst = q.gw + ((int64_t)o * Cin + c0) * q.taps;
+  for (int j = threadIdx.x; j < (q.taps << q.lgCC); j += 256) {  // j = ci_local * taps + tap (reference order)
+    const int ci = j / q.taps, tap = j - ci * q.taps;
+    dst[j] += seg[(tap << q.lgCC) + ci];
+  }
+}
+
+inline int wgrad_blocks(const mg_fold_wgrad& q) { return q.Cout * ((1 << q.lgCin) >> q.lgCC); }
+
+void launch_rows(const mg_fold_rows* recs, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += kFoldMax) {
+    RowsBatch b{};
+    b.n = std::min(kFoldMax, n - i0);
+    for (int j = 0; j < b.n; ++j) {
+      b.r[j] = recs[i0 + j];
+      b.blk_off[j + 1] = b.blk_off[j] + rows_blocks(b.r[j]);
+    }
+    hipLaunchKernelGGL(k_fold_rows_batch, dim3(b.blk_off[b.n]), dim3(1024), 0, st, b);
+  }
+}
+
+void launch_wgrad(const mg_fold_wgrad* recs, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += kFoldMax) {
+    WgradBatch b{};
+    b.n = std::min(kFoldMax, n - i0);
+    size_t lds = 0;
+    for (int j = 0; j < b.n; ++j) {
+      b.r[j] = recs[i0 + j];
+      b.blk_off[j + 1] = b.blk_off[j] + wgrad_blocks(b.r[j]);
+      lds = std::max(lds, (size_t)(b.r[j].taps << b.r[j].lgCC) * sizeof(float));
+    }
+    hipLaunchKernelGGL(k_fold_wgrad_batch, dim3(b.blk_off[b.n]), dim3(256), lds, st, b);
+  }
+}
+
+// ---- per-stream deferral state: pending records and the partials arena ----
+struct Chunk {
+  char* p;
+  size_t bytes;
+};
+struct Defer {
+  int device;
+  hipStream_t stream;
+  bool on;
+  std::vector<mg_fold_rows> rows;
+  std::vector<mg_fold_wgrad> wgrad;
+  std::vector<Chunk> chunks;
+  size_t ci, used;  // current chunk, bytes used in it
+};
+std::mutex g_fold_mu;
+std::vector<Defer> g_defer;
+
+Defer* defer_entry(hipStream_t st, bool create) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  for (auto& d : g_defer)
+    if (d.device == dev && d.stream == st) return &d;
+  if (!create) return nullptr;
+  g_defer.push_back(Defer{dev, st, false, {}, {}, {}, 0, 0});
+  return &g_defer.back();
+}
+
+}  // namespace
+
+void* mg_fold_alloc(size_t bytes, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_fold_mu);
+  Defer* d = defer_entry(st, false);
+  if (!d || !d->on) return nullptr;
+  bytes = (bytes + 255) & ~(size_t)255;
+  while (d->ci < d->chunks.size() && d->used + bytes > d->chunks[d->ci].bytes) {
+    ++d->ci;
+    d->used = 0;
+  }
+  if (d->ci == d->chunks.size()) {
+    // a new chunk: only outside stream capture (the eager warm-up of a captured step sizes the arena, and the
+    // capture then replays the same allocation sequence); under capture the caller folds immediately instead
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    Chunk c{nullptr, std::max(bytes, (size_t)64 << 20)};
+    if (hipMalloc(reinterpret_cast<void**>(&c.p), c.bytes) != hipSuccess) return nullptr;
+    d->chunks.push_back(c);
+    d->used = 0;
+  }
+  void* p = d->chunks[d->ci].p + d->used;
+  d->used += bytes;
+  return p;
+}
+
+int mg_fold_rows_submit(const mg_fold_rows& r, bool deferred, hipStream_t st) {
+  if (deferred) {
+    std::lock_guard<std::mutex> lk(g_fold_mu);
+    Defer* d = defer_entry(st, false);
+    if (d && d->on) {
+      d->rows.push_back(r);
+      return MG_OK;
+    }
+  }
+  launch_rows(&r, 1, st);
+  return MG_OK;
+}
+
+int mg_fold_wgrad_submit(const mg_fold_wgrad& r, bool deferred, hipStream_t st) {
+  if (deferred) {
+    std::lock_guard<std::mutex> lk(g_fold_mu);
+    Defer* d = defer_entry(st, false);
+    if (d && d->on) {
+      d->wgrad.push_back(r);
+      return MG_OK;
+    }
+  }
+  launch_wgrad(&r, 1, st);
+  return MG_OK;
+}
+
+extern "C" int mg_fold_flush(void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  std::vector<mg_fold_rows> rows;
+  std::vector<mg_fold_wgrad> wg;
+  {
+    std::lock_guard<std::mutex> lk(g_fold_mu);
+    Defer* d = defer_entry(st, false);
+    if (!d) return MG_OK;
+    rows.swap(d->rows);
+    wg.swap(d->wgrad);
+    d->ci = 0;  // the arena is reused from the start by the next backward
+    d->used = 0;
+  }
+  if (!wg.empty()) launch_wgrad(wg.data(), (int)wg.size(), st);
+  if (!rows.empty()) launch_rows(rows.data(), (int)rows.size(), st);
+  return mg_check_launch("mg_fold_flush");
+}
+
+extern "C" int mg_fold_defer(int on, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (!on) {
+    const int rc = mg_fold_flush(stream);
+    std::lock_guard<std::mutex> lk(g_fold_mu);
+    Defer* d = defer_entry(st, false);
+    if (d) d->on = false;
+    return rc;
+  }
+  std::lock_guard<std::mutex> lk(g_fold_mu);
+  Defer* d = defer_entry(st, true);
+  MG_REQUIRE(d, "no device");
+  MG_REQUIRE(d->rows.empty() && d->wgrad.empty(), "mg_fold_defer: folds pending (flush first)");
+  d->on = true;
+  return MG_OK;
+}
+
+extern "C" int mg_fold_rows_batch(int n, const mg_fold_rows* recs, void* stream) {
+  MG_REQUIRE(n >= 0 && recs, "bad records");
+  for (int i = 0; i < n; ++i)
+    MG_REQUIRE(recs[i].src && recs[i].out_a && (recs[i].na >= recs[i].ncols || recs[i].out_b) && recs[i].ncols >= 0 &&
+                   recs[i].nrows >= 0,
+               "bad fold record");
+  if (n > 0) launch_rows(recs, n, reinterpret_cast<hipStream_t>(stream));
+  return mg_check_launch("mg_fold_rows_batch");
+}

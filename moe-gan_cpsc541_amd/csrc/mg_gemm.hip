@@ -520,44 +520,8 @@ void run_wgrad(const void* gy, int64_t ldg, const void* x, int B, int H, int W, 
   launch_gemm<T, BM, BN, false, false>(la, lb, ep, Cout, N, P, splits, kNoGroup, 0, st);
 }
 
-// gw[o][ci][tap] += sum_s ws[s][o][tap * Cin + ci]: split-K slabs of a weight gradient folded and moved to the
-// reference [Cout][Cin][KH][KW] layout in one pass.  Block (o, chunk) owns output channel o and input channels
-// [c0, c0 + CC): it reads the `taps` slab segments of CC floats as 16-B vectors with four slabs in flight per
-// step (a fixed summation order: deterministic), stages the sums in LDS and read-modify-writes the contiguous
-// reference-layout range gw[o][c0 .. c0+CC)[*] (the element-per-thread form wrote gw at a stride of `taps`).
-__global__ __launch_bounds__(256) void k_wgrad_fold(const float* __restrict__ ws, int splits, int Cout, int lgCin,
-                                                    int taps, int lgCC, float* __restrict__ gw) {
-  extern __shared__ float seg[];  // [taps][CC]
-  const int Cin = 1 << lgCin, N = taps << lgCin, CC = 1 << lgCC;
-  const int64_t MN = (int64_t)Cout * N;
-  const int o = blockIdx.x, c0 = blockIdx.y << lgCC;
-  const float* src = ws + (int64_t)o * N + c0;
-  const int nv = (taps << lgCC) >> 2;  // 16-B vectors of this block
-  for (int q = threadIdx.x; q < nv; q += 256) {
-    const int tap = (4 * q) >> lgCC, ci = (4 * q) & (CC - 1);
-    const float* p = src + ((int64_t)tap << lgCin) + ci;
-    f32x4_t v = *reinterpret_cast<const f32x4_t*>(p);
-    int s = 1;
-    for (; s + 3 < splits; s += 4) {
-      const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p + s * MN);
-      const f32x4_t b = *reinterpret_cast<const f32x4_t*>(p + (s + 1) * MN);
-      const f32x4_t c = *reinterpret_cast<const f32x4_t*>(p + (s + 2) * MN);
-      const f32x4_t d = *reinterpret_cast<const f32x4_t*>(p + (s + 3) * MN);
-      v += ((a + b) + (c + d));
-    }
-    for (; s < splits; ++s) v += *reinterpret_cast<const f32x4_t*>(p + s * MN);
-    *reinterpret_cast<f32x4_t*>(seg + 4 * q) = v;
-  }
-  __syncthreads();
-  float* dst = gw + ((int64_t)o * Cin + c0) * taps;
-  for (int j = threadIdx.x; j < (taps << lgCC); j += 256) {  // j = ci_local * taps + tap (reference order)
-    const int ci = j / taps, tap = j - ci * taps;
-    dst[j] += seg[(tap << lgCC) + ci];
-  }
-}
-
 // Weight gradient with split-K into fp32 slabs written by the 8-column vector epilogue (coalesced, no atomics),
-// then k_wgrad_fold.  Returns false when the workspace cannot be had (caller falls back to atomics).
+// then the slab fold into the reference layout (mg_fold.hip: immediate, or deferred to the backward's flush).  Returns false when the workspace cannot be had (caller falls back to atomics).
 // stride-1 "same" convolution whose weight gradient can use the cheap-address column loader (LdMCConvS1)
 inline bool wgrad_s1(int H, int W, int KH, int KW, int stride, int pad, int tbk) {
   return stride == 1 && KH == KW && 2 * pad == KH - 1 && W <= tbk && H <= 32 && pow2(H) && pow2(W);
@@ -572,7 +536,8 @@ bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, i
   int kchunk = ((P + splits - 1) / splits + TBK - 1) / TBK * TBK;
   splits = (P + kchunk - 1) / kchunk;
   const int64_t MN = (int64_t)Cout * N;
-  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)splits * MN * sizeof(float), st));
+  bool deferred = false;
+  float* ws = mg_fold_partials((size_t)splits * MN * sizeof(float), st, &deferred);
   if (!ws) return false;
   LdMC<T> la{reinterpret_cast<const T*>(gy), ldg, Cout, P, nullptr, 1, nullptr, 0};
   LdMCConv<T, XF> lb{reinterpret_cast<const T*>(x), H, W, Cin, ilog2(Cin), ilog2(OW), ilog2(OH * OW), P,
@@ -594,8 +559,7 @@ bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, i
   // (Cout x Cin / CC) blocks: enough to spread the slab reads over the chip, >= 8 channels per segment
   int lgCC = ilog2(Cin);
   while (lgCC > 3 && (int64_t)Cout * (Cin >> lgCC) < 1024) --lgCC;
-  hipLaunchKernelGGL(k_wgrad_fold, dim3(Cout, Cin >> lgCC), dim3(256), (size_t)(KH * KW) * sizeof(float) << lgCC, st,
-                     ws, splits, Cout, ilog2(Cin), KH * KW, lgCC, gw);
+  mg_fold_wgrad_submit(mg_fold_wgrad{ws, splits, Cout, ilog2(Cin), KH * KW, lgCC, gw}, deferred, st);
   return true;
 }
 }  // namespace
@@ -642,10 +606,10 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
   if (dtype == MG_BF16 && !in_scale && Cout == 32 && Cin >= 32 && mg_conv3_direct_ok(H, W, Cin, Cout, KH, KW, stride, pad, true)) {
     float* ws = nullptr;
     int ng = 0;
-    if (mg_wgrad3_direct(gy, ldg, x, B, H, Cin, &ws, &ng, st)) {
+    bool deferred = false;
+    if (mg_wgrad3_direct(gy, ldg, x, B, H, Cin, &ws, &ng, &deferred, st)) {
       const int lgCC = 3;  // 32 x Cin / 8 fold blocks
-      hipLaunchKernelGGL(k_wgrad_fold, dim3(Cout, Cin >> lgCC), dim3(256), (size_t)9 * sizeof(float) << lgCC, st, ws,
-                         ng, Cout, ilog2(Cin), 9, lgCC, gw);
+      mg_fold_wgrad_submit(mg_fold_wgrad{ws, ng, Cout, ilog2(Cin), 9, lgCC, gw}, deferred, st);
       return mg_check_launch("mg_conv2d_wgrad (direct 3x3, 32 channels)");
     }
   }

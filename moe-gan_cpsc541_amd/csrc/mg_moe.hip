@@ -530,7 +530,7 @@ __global__ void k_gate_grad(const TG* __restrict__ gout, int64_t ldg, const T* _
 }
 
 // per-token router backward: (g_gate, balance coefficients) -> g_raw [T, E], the per-image sums gsum [B, E] and
-// one temperature-gradient partial per block (tpart; k_fold_partials adds them to the parameter gradient).
+// one temperature-gradient partial per block (tpart; a rows fold, mg_fold.hip, adds them to the parameter gradient).
 // Every reduction runs in a fixed order (segmented butterflies inside a wave, waves of one image folded in wave
 // order, block partials folded by one block), so the results are bit-identical run to run: the image's tokens are
 // contiguous, an image of HW <= 64 tokens lies inside one wave and one of 128 / 256 tokens inside one block.
@@ -664,17 +664,6 @@ __global__ __launch_bounds__(256) void k_router_bwd(const float* __restrict__ pr
   }
 }
 
-// out[0] += sum of part[0 .. n) in a fixed order (one block: strided thread sums, then a butterfly per wave and
-// the waves in order)
-__global__ __launch_bounds__(256) void k_fold_partials(const float* __restrict__ part, int n, float* __restrict__ out) {
-  __shared__ float wsum[4];
-  float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) out[0] += (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
-}
 
 // g_tok[t, c] = sum_j gX[pos_of[t*k+j], c] + sum_e g_raw[t, e] * Wfc[c, e]
 template <typename T, typename TO>
@@ -720,7 +709,7 @@ __global__ void k_router_feat_grad(const T* __restrict__ tok, int64_t ld, int Tn
     }
   }
   if (c < C) {
-    if (part) {  // per-block partial row (no same-address atomics); k_feat_grad_fin folds the rows
+    if (part) {  // per-block partial row (no same-address atomics); a rows fold (mg_fold.hip) sums them
 #pragma unroll
       for (int e = 0; e < E; ++e) part[(int64_t)blockIdx.x * C * E + (int64_t)c * E + e] = acc[e];
     } else {
@@ -732,7 +721,7 @@ __global__ void k_router_feat_grad(const T* __restrict__ tok, int64_t ld, int Tn
 
 // Vector form: a block is TX = C / CV channel lanes (CV channels each, 16-B loads for CV = 8 bf16) x TY = 256 / TX
 // token lanes walking its token chunk; the token lanes of a wave fold with shuffles and each wave-row group
-// writes one partial row [C * E] (k_feat_grad_fin folds them).  The thread-per-channel form issued 2-byte loads
+// writes one partial row [C * E] (folded by a rows fold, mg_fold.hip).  The thread-per-channel form issued 2-byte loads
 // one token at a time (35 us for 65536 tokens x 128 channels).
 template <typename T, int E, int CV>
 __global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict__ tok, int64_t ld, int Tn, int C,
@@ -802,25 +791,6 @@ __global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict_
   }
 }
 
-// out[i] += sum_r part[r * n + i]: 16 columns x 16 row lanes per block (n / 16 blocks: the partial rows of a
-// few-column gradient still spread over the chip), LDS fold in row order
-__global__ __launch_bounds__(256) void k_feat_grad_fin(const float* __restrict__ part, int nparts, int n,
-                                                       float* __restrict__ out) {
-  __shared__ float red[16][16];
-  const int cx = threadIdx.x & 15, ry = threadIdx.x >> 4;
-  const int i = blockIdx.x * 16 + cx;
-  float s = 0.f;
-  if (i < n)
-    for (int r = ry; r < nparts; r += 16) s += part[(int64_t)r * n + i];
-  red[ry][cx] = s;
-  __syncthreads();
-  if (ry == 0 && i < n) {
-    float t = 0.f;
-#pragma unroll
-    for (int y = 0; y < 16; ++y) t += red[y][cx];
-    out[i] += t;
-  }
-}
 
 // out[g][n] += sum_{r in group g} X[src(r)][n] * rs[r]  (grouped bias gradients)
 template <typename T>
@@ -1295,15 +1265,17 @@ extern "C" int mg_router_bwd(const float* probs, const float* zlog, const int32_
   while ((1 << lg) < HW) ++lg;
   dim3 grid(cdiv(T, 256));
   float* tpart = nullptr;
+  bool deferred = false;
   if (g_temp) {
-    tpart = reinterpret_cast<float*>(mg_workspace((size_t)grid.x * sizeof(float), st));
+    tpart = mg_fold_partials((size_t)grid.x * sizeof(float), st, &deferred);
     if (!tpart) return MG_ERR_LAUNCH;
   }
 #define L_(EE) hipLaunchKernelGGL((k_router_bwd<EE>), grid, dim3(256), 0, st, probs, zlog, topi, gate, g_gate, g_probs, g_logits, coef, T, k, lg, \
                                   temperature, anneal, g_raw, gsum, tpart)
   if (E == 4) L_(4); else if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
 #undef L_
-  if (g_temp) hipLaunchKernelGGL(k_fold_partials, dim3(1), dim3(256), 0, st, tpart, (int)grid.x, g_temp);
+  // the temperature partials (one per block) as a one-column rows fold
+  if (g_temp) mg_fold_rows_submit(mg_fold_rows{tpart, 1, (int)grid.x, 1, 1, g_temp, nullptr}, deferred, st);
   return mg_check_launch("mg_router_bwd");
 }
 
@@ -1347,7 +1319,8 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
     const int64_t min_chunk = ((int64_t)T * row / (1 << 20) + TY - 1) / TY * TY;
     if (min_chunk > chunk) chunk = (int)min_chunk;
     const int nb = cdiv(T, chunk);
-    float* part = reinterpret_cast<float*>(mg_workspace((size_t)nb * rows_per_block * C * E * sizeof(float), st));
+    bool deferred = false;
+    float* part = mg_fold_partials((size_t)nb * rows_per_block * C * E * sizeof(float), st, &deferred);
     MG_REQUIRE(part != nullptr, "mg_router_feat_grad: no workspace");
 #define LV_(TT, EE, CC) hipLaunchKernelGGL((k_router_feat_grad_v<TT, EE, CC>), dim3(nb), dim3(256), 0, st, (const TT*)tok, \
                                            ld, T, C, g_raw, chunk, part)
@@ -1356,21 +1329,22 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
     if (dtype == MG_F32) { LVE_(float); } else { LVE_(bf16_t); }
 #undef LVE_
 #undef LV_
-    hipLaunchKernelGGL(k_feat_grad_fin, dim3(cdiv(C * E, 16)), dim3(256), 0, st, part, nb * rows_per_block, C * E,
-                       G1);
+    // the partial rows' fold (mg_fold.hip; the G1 consumers, the router-parameter GEMMs, run after the flush)
+    mg_fold_rows_submit(mg_fold_rows{part, C * E, nb * rows_per_block, C * E, C * E, G1, nullptr}, deferred, st);
     return mg_check_launch("mg_router_feat_grad");
   }
-  // ~512 blocks (a 64-token step per LDS refill); per-block partial rows folded by k_feat_grad_fin
+  // ~512 blocks (a 64-token step per LDS refill); per-block partial rows folded by a rows fold (mg_fold.hip)
   int chunk = std::max(64, std::min(256, (T / 512) / 64 * 64));
   dim3 grid(cdiv(T, chunk));
   int thr = ((C + 63) / 64) * 64;
-  float* part = reinterpret_cast<float*>(mg_workspace((size_t)grid.x * C * E * sizeof(float), st));
+  bool deferred = false;
+  float* part = mg_fold_partials((size_t)grid.x * C * E * sizeof(float), st, &deferred);
 #define L_(TT, EE) hipLaunchKernelGGL((k_router_feat_grad<TT, EE>), grid, dim3(thr), 0, st, (const TT*)tok, ld, T, C, g_raw, chunk, G1, part)
 #define LE_(TT) if (E == 4) L_(TT, 4); else if (E == 8) L_(TT, 8); else if (E == 16) L_(TT, 16); else L_(TT, 32)
   if (dtype == MG_F32) { LE_(float); } else { LE_(bf16_t); }
 #undef LE_
 #undef L_
-  if (part) hipLaunchKernelGGL(k_feat_grad_fin, dim3(cdiv(C * E, 16)), dim3(256), 0, st, part, (int)grid.x, C * E, G1);
+  if (part) mg_fold_rows_submit(mg_fold_rows{part, C * E, (int)grid.x, C * E, C * E, G1, nullptr}, deferred, st);
   return mg_check_launch("mg_router_feat_grad");
 }
 

@@ -569,7 +569,7 @@ inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t -
 //     store: no fp32 atomics, no zero fill, optional accumulate into gx), and dL/dgrid of p = dot products of
 //     gout[p] with x at its corners, reduced over the pixel's C/8 vector lanes with shuffles;
 //  3. offset head (32 -> 2 conv, 3x3) backward fused with the first conv's LeakyReLU: ga1 for the image, and
-//     the image's partial (gw2, gb2) row written to a workspace row (folded over images by k_rows_fin).
+//     the image's partial (gw2, gb2) row written to a workspace row (folded over images by a rows fold, mg_fold.hip).
 template <typename T, typename TG, typename TX>
 __global__ __launch_bounds__(1024) void k_mtm_bwd_img(const TG* __restrict__ gout, const T* __restrict__ x,
                                                       const float* __restrict__ samp, const T* __restrict__ o1,
@@ -778,25 +778,6 @@ __global__ __launch_bounds__(1024) void k_mtm_bwd_img(const TG* __restrict__ gou
   for (int i = tid; i < 578; i += nt) part[(int64_t)b * 578 + i] = red[i];
 }
 
-// out_a[i] += sum_r part[r][i] for i < na, out_b[i - na] += ... for na <= i < ncols  (64 columns x 16 row lanes)
-__global__ __launch_bounds__(1024) void k_rows_fin(const float* __restrict__ part, int nrows, int ncols, int na,
-                                                   float* __restrict__ out_a, float* __restrict__ out_b) {
-  __shared__ float red[16][64];
-  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + cx;
-  float s = 0.f;
-  if (i < ncols)
-    for (int r = ry; r < nrows; r += 16) s += part[(int64_t)r * ncols + i];
-  red[ry][cx] = s;
-  __syncthreads();
-  if (ry == 0 && i < ncols) {
-    float t = 0.f;
-#pragma unroll
-    for (int y = 0; y < 16; ++y) t += red[y][cx];
-    if (i < na) out_a[i] += t;
-    else out_b[i - na] += t;
-  }
-}
 
 }  // namespace
 
@@ -884,7 +865,8 @@ extern "C" int mg_mtm_bwd_fused(int dtype, int gout_dtype, const void* gout, con
   MG_REQUIRE(B > 0 && HW > 0 && HW <= 1024 && C == (8 << lgV) && C <= 512, "needs H*W <= 1024 and C = 8 * 2^k <= 512");
   MG_REQUIRE(mg_al16(gout) && mg_al16(x) && mg_al16(samp) && mg_al16(gx), "16-B aligned gout / x / samp / gx");
   MG_REQUIRE(gx_dtype == dtype || gx_dtype == MG_F32, "gx dtype must be the activation dtype or fp32");
-  float* part = reinterpret_cast<float*>(mg_workspace((size_t)B * 578 * sizeof(float), st));
+  bool deferred = false;
+  float* part = mg_fold_partials((size_t)B * 578 * sizeof(float), st, &deferred);
   if (!part) {
     mg_set_error("mg_mtm_bwd_fused: workspace allocation failed");
     return MG_ERR_LAUNCH;
@@ -902,7 +884,7 @@ extern "C" int mg_mtm_bwd_fused(int dtype, int gout_dtype, const void* gout, con
     if (gout_dtype == MG_F32) L_(bf16_t, float, bf16_t); else L_(bf16_t, bf16_t, bf16_t);
   }
 #undef L_
-  hipLaunchKernelGGL(k_rows_fin, dim3(cdiv(578, 64)), dim3(1024), 0, st, part, B, 578, 576, gw2, gb2);
+  mg_fold_rows_submit(mg_fold_rows{part, 578, B, 578, 576, gw2, gb2}, deferred, st);
   return mg_check_launch("mg_mtm_bwd_fused");
 }
 

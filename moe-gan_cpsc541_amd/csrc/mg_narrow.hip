@@ -20,7 +20,7 @@
 //  * k_wgrad3_direct<S>: dW[o][tap*Cin + c] = sum_p g[p][o] x[p + tap][c] over a block's run of tiles for a
 //    32-channel chunk: the gradient tile [pixels][32] and the halo'd input tile are MC images (pixel rows) read with
 //    the hardware transpose, so the reduction over pixels runs on MFMA; per-block partials are folded by the conv
-//    library's k_wgrad_fold into the reference [Cout][Cin][3][3] layout (fixed order, deterministic).
+//    library's slab fold (mg_fold.hip) into the reference [Cout][Cin][3][3] layout (fixed order, deterministic).
 #include <algorithm>
 
 #include "mg_gemm.h"
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(NT) void k_wgrad3_direct(const bf16_t* __restrict__
       }
     }
   }
-  // partial slab [grp][32][9 Cin] (k_wgrad_fold's layout: column tap * Cin + c)
+  // partial slab [grp][32][9 Cin] (the slab fold's layout, mg_fold.hip: column tap * Cin + c)
   const int N = 9 * Cin;
   float* dst = part + (int64_t)grp * 32 * N + c0 + 16 * cf + (lane & 15);
 #pragma unroll
@@ -369,9 +369,9 @@ bool mg_conv3_direct(const void* x, int B, int H, int Cin, const void* wpack, in
   return conv_dispatch<bf16_t>(x, B, H, Cin, wpack, Cout, e, y, ldy, st);
 }
 
-// partial slabs [ngroups][32][9 Cin] for k_wgrad_fold; false when not handled (shape / workspace)
+// partial slabs [ngroups][32][9 Cin] for the slab fold (mg_fold.hip); false when not handled (shape / workspace)
 bool mg_wgrad3_direct(const void* gy, int64_t ldg, const void* x, int B, int H, int Cin, float** ws_out, int* splits,
-                      hipStream_t st) {
+                      bool* deferred, hipStream_t st) {
   if (ldg % 8 || Cin % WG_CC) return false;
   const int P = B * H * H, ntiles = cdiv(P, TP), chunks = Cin / WG_CC;
   // ~256 blocks (one per CU; each streams its tiles with the next one's loads in flight), >= 4 tiles per group
@@ -379,7 +379,7 @@ bool mg_wgrad3_direct(const void* gy, int64_t ldg, const void* x, int B, int H, 
   int ngroups = std::max(1, std::min(ntiles / 2, target / chunks));
   ngroups = (ngroups + 7) / 8 * 8;  // whole XCD rounds (groups past the last tile exit at once)
   const int tpg = cdiv(ntiles, ngroups);
-  float* ws = reinterpret_cast<float*>(mg_workspace((size_t)ngroups * 32 * 9 * Cin * sizeof(float), st));
+  float* ws = mg_fold_partials((size_t)ngroups * 32 * 9 * Cin * sizeof(float), st, deferred);
   if (!ws) return false;
   const bf16_t* gb = reinterpret_cast<const bf16_t*>(gy);
   const bf16_t* xb = reinterpret_cast<const bf16_t*>(x);

@@ -248,7 +248,9 @@ class DiscriminatorEngine:
         return dict(losses=out, r1=r1, real_pred=real_pred, mism_pred=mism_pred, fake_pred=fake_pred, r1_grad=gx)
 
     def _remap_w0(self):
-        """dW0 was accumulated in the GEMM layout [o][tap*3 + c]; convert to [o][c][kh][kw]."""
+        """dW0 was accumulated in the GEMM layout [o][tap*3 + c]; convert to [o][c][kh][kw].  The remap and
+        finish_grads read the accumulated dW: the deferred conv weight-gradient folds land first."""
+        ops.fold_flush()
         g = self.dW["conv_layers.0."].view(128, 16, 3)
         self.dW["conv_layers.0."] = g.permute(0, 2, 1).contiguous().view(128, 3, 4, 4)
 

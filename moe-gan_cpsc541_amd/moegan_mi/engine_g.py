@@ -496,6 +496,7 @@ class GeneratorEngine:
         items, self._router_bwd = self._router_bwd, []
         if not items:
             return
+        ops.fold_flush()  # the router feature gradients G1 are folds (deferred inside a training step)
         dev = self.dev
         pa, pb, pc, pd = [], [], [], []
         for q in items:
@@ -567,6 +568,7 @@ class GeneratorEngine:
         self.side.run(lambda: (ops.gemm_grouped_wgrad(gP, sv["Xg"], row_off, n, Hd, C, gW1),
                                None if fused else ops.grouped_colsum(gP, row_off, Hd, n, gb1)), gP)
         if self.on_grad_final is not None:  # this block's expert parameters receive no further gradient
+            ops.fold_flush()  # (a weight-gradient fold deferred on this stream lands before the bucket's all-reduce)
             lo = self.st.offsets[ex + "0.net.0.weight"][0]
             o, nl = self.st.offsets[f"{ex}{E-1}.net.2.bias"]
             self.on_grad_final(lo, o + nl)
@@ -679,21 +681,20 @@ class GeneratorEngine:
         t1c = self._p(t1)
         text_seq = ops.linear(t1c, self.Pp("text_projection.3.weight"), bias=self.P("text_projection.3.bias"),
                               out_dtype=torch.float32)
-        # mapping + truncation (:793-808)
-        zt = torch.empty(B, z.shape[1] + text.shape[1], device=dev, dtype=self.pdt)
+        # mapping + truncation (:793-808).  The truncation centre mapping(0) (:802-806, no gradient) rides along as
+        # an extra all-zero row B of the mapping GEMMs instead of its own chain of M = 1 launches; the backward
+        # reads only rows [0, B) of the saved activations
+        trunc = psi < 1.0
+        zt = (ops.zeros(B + 1, z.shape[1] + text.shape[1], device=dev, dtype=self.pdt) if trunc else
+              torch.empty(B, z.shape[1] + text.shape[1], device=dev, dtype=self.pdt))
         ops.copy2d(z, zt, B, z.shape[1], ldo=zt.shape[1])
         ops.copy2d(text, zt[:, z.shape[1]:], B, text.shape[1], ldo=zt.shape[1])
-        h3, hs = self._mapping(zt, save)
-        if psi < 1.0:
-            if self._mean_latent is None:  # mapping(0): depends on the weights only -> once per prep()
-                zeros = torch.zeros(1, zt.shape[1], device=dev, dtype=self.pdt)
-                m3, _ = self._mapping(zeros, False)
-                self._mean_latent = ops.linear(m3, self.Pp("mapping.6.weight"), bias=self.P("mapping.6.bias"),
-                                               out_dtype=torch.float32)
-            mean = self._mean_latent
-            beff = torch.empty(512, device=dev)
-            ops.copy2d(self.P("mapping.6.bias").view(1, -1), beff.view(1, -1), 1, 512, alpha=psi)
-            ops.copy2d(mean, beff.view(1, -1), 1, 512, alpha=1.0 - psi, accumulate=1)
+        h3e, hs = self._mapping(zt, save)
+        h3 = h3e[:B]
+        if trunc:
+            # w = mean + psi (w_full - mean) = psi * h3 W6^T + beff, beff = (1 - psi) * m3 W6^T + b6 (one M = 1 GEMM)
+            beff = ops.linear(h3e[B:B + 1], self.Pp("mapping.6.weight"), bias=self.P("mapping.6.bias"), alpha=1.0 - psi,
+                              out_dtype=torch.float32).view(-1)
             w = ops.linear(h3, self.Pp("mapping.6.weight"), bias=beff, alpha=psi, out_dtype=torch.float32)
         else:
             w = ops.linear(h3, self.Pp("mapping.6.weight"), bias=self.P("mapping.6.bias"), out_dtype=torch.float32)
@@ -839,7 +840,7 @@ class GeneratorEngine:
         # truncation: w = mean + psi (w_full - mean), mean under no_grad
         psi = ctx["psi"]
         g6 = ops.cast(gw, self.pdt, alpha=psi if psi < 1.0 else 1.0)
-        hs = ctx["hs"]
+        hs = [h[:g6.shape[0]] for h in ctx["hs"]]  # (rows past B: the truncation centre's zero row, no gradient)
         ops.linear_wgrad(g6, hs[3], self.G("mapping.6.weight"))
         ops.colsum(g6, self.G("mapping.6.bias"), defer=True)
         g = ops.linear_dgrad(g6, self.Pp("mapping.6.weight"))

@@ -112,6 +112,17 @@ class ZeroArena:
 ARENA = ZeroArena()
 
 
+def fold_defer(on):
+    """Defer (True) the gradient folds of the library's two-pass reductions issued on the current stream until
+    fold_flush(), or flush and stop deferring (False) -- mg_fold_defer."""
+    call("mg_fold_defer", int(bool(on)), S())
+
+
+def fold_flush():
+    """Run every deferred gradient fold of the current stream (one launch per fold kind; mg_fold_flush)."""
+    call("mg_fold_flush", S())
+
+
 def zeros(*shape, device, dtype=torch.float32):
     return ARENA.zeros(tuple(shape), dtype, device)
 

@@ -45,6 +45,8 @@ FAMILIES = {
     "router_aux": ("hbm", ("mg_router_bwd", "mg_moe_gate_grad", "mg_moe_token_grad", "mg_router_feat_grad",
                            "mg_router_param_bwd", "mg_router_param_bwd_batch", "mg_moe_dispatch", "mg_router_kl")),
     "im2col_col2im": ("hbm", ("mg_im2col_4x4s2", "mg_col2im_4x4s2")),
+    # deferred second passes of the two-pass gradient reductions (mg_fold.hip), one batched launch per kind
+    "grad_fold": ("hbm", ("mg_fold_flush", "mg_fold_rows_batch", "mg_fold_defer")),
     "d_conv0": ("hbm", ("mg_d0_fwd", "mg_d0_wgrad", "mg_d0_dgrad")),
     "elementwise": ("hbm", ("mg_cast", "mg_copy2d", "mg_lrelu_mask_mul", "mg_upsample2x_fwd", "mg_upsample2x_bwd",
                             "mg_const_fwd", "mg_gated_axpy", "mg_select_if", "mg_zero_if", "mg_clip_patches")),
@@ -60,6 +62,7 @@ _FAMILY_OF = {e: f for f, (_, es) in FAMILIES.items() for e in es}
 
 # rocprofv3 kernel name (regex, first match wins) -> family, for PMC attribution
 KERNELS = [
+    (r"k_fold_wgrad_batch|k_fold_rows_batch", "grad_fold"),
     (r"k_wgrad_fold|splitk_reduce_kernel<mg::Epi<float>|k_wgrad3_direct", "conv_wgrad+fold"),
     (r"k_conv3_direct", "conv_fwd"),
     (r"k_mx8_conv", "conv_fwd_mx8"),
@@ -73,7 +76,7 @@ KERNELS = [
     (r"k_router_fwd", "router_fwd"),
     (r"k_gather_rows|k_combine", "dispatch_combine"),
     (r"k_warp_fwd", "warp_fwd"),
-    (r"k_mtm_bwd|k_rows_fin", "mtm_bwd"),
+    (r"k_mtm_bwd", "mtm_bwd"),
     (r"k_bwd_in|k_bwd_out|k_scale_bc", "modconv_bwd_io"),
     (r"k_r1", "r1"),
     (r"k_sumsq", "sumsq"),

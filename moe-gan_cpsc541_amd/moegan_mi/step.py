@@ -216,6 +216,9 @@ class TrainStep:
         matters only when the D optimizer has not stepped yet in the window (acc > 1)."""
         ops.ARENA.begin(self.dev)
         ops.COLSUMS.active = True  # bias-gradient column sums batched per backward (flushed below)
+        # the library's gradient folds too: one batched launch per backward (ops.fold_flush); MOEGAN_FOLD_DEFER=0
+        # folds each at its producer (same kernels, bit-identical gradients)
+        ops.fold_defer(os.environ.get("MOEGAN_FOLD_DEFER", "1") == "1")
         # bf16 mode: the fp32-operand GEMMs (prefix, demodulation, router / cross-attention vectors) as split-bf16
         # products (ops.set_f32x3); the fp32 parity mode keeps exact-fp32 MFMA
         x3_prev = ops.set_f32x3(self.cdt == torch.bfloat16 and os.environ.get("MOEGAN_F32X3", "1") == "1")
@@ -223,6 +226,7 @@ class TrainStep:
             return self._step(real, text, z, eps_d, eps_g, perm, anneal, lr_g, lr_d, eff_kl_weight, prep, acc,
                               zero_grads, step_optim)
         finally:
+            ops.fold_defer(False)
             ops.set_f32x3(x3_prev)
             ops.ARENA.end()
             ops.COLSUMS.active = False
@@ -253,6 +257,7 @@ class TrainStep:
                                                         want_kl=False, keep_prefix=True)
         prefix, self.ge.last_prefix = self.ge.last_prefix, None
         dres = self.de.d_phase(real, text, f16, ("nhwc", 8), perm, c.r1_gamma)
+        ops.fold_flush()
         ops.COLSUMS.flush()
         # guard: NaN / Inf d_loss skips the whole batch (t2i_moe_gan.py:1315-1320)
         self._guard(flags, [(dres["losses"][:1], FD), (dres["r1"], FD)],
@@ -281,6 +286,7 @@ class TrainStep:
         if leak:
             ds.zero_grad()
         g_gan, fake_pred, g_img = self.de.g_phase(img16, ("nhwc", 8), text, want_d_params=leak)
+        ops.fold_flush()
         ops.COLSUMS.flush()
         # balance loss on the last MoE layer, over the GLOBAL batch (t2i_moe_gan.py:951-1000)
         last = probs[-1]
@@ -314,6 +320,7 @@ class TrainStep:
             self.ge.backward(ctx, g_img, coef=coef, kl_coef=kl_coef)
         finally:
             self.ge.on_grad_final = None
+        ops.fold_flush()
         ops.COLSUMS.flush()
         if g_finish is not None:  # every bucket reduced and scaled before the guard below rewrites ranges
             g_finish()
