@@ -320,10 +320,11 @@ def main():
     def run_step():
         return ts.step(real, text, z, eps_d, eps_g, perm, anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8)
 
-    # live timing of the roofline kernel: D conv_layers.2 forward on the 64x64 real batch
-    # (implicit GEMM M = B*16*16, N = 256, K = 4*4*128); inactive until the timed region
-    want_dims = (B * (args.res // 4) ** 2, 256, 2048)
-    ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "conv2d:d_conv1" and dims == want_dims, active=False)
+    # live timing of the roofline kernel: the largest kernel of the step's dominant family (expert_gemm), the fused
+    # expert FFN backward of the 16x16 block (mg_moe_ffn_bwd: B*256*k routed rows, C = 128, Hd = 512); inactive until
+    # the timed region
+    want_dims = (B * 256 * k, 128, 512)
+    ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "moe_ffn_bwd" and dims == want_dims, active=False)
 
     graph = None
     if not args.eager:
@@ -453,16 +454,16 @@ def main():
         ms = elapsed / args.steps * 1e3
         kms = [ms_ for _, _, ms_ in kt]
         avg_ms = sum(kms) / max(len(kms), 1)
-        M, N, K = want_dims
-        flop = 2.0 * M * N * K
+        rows, Cx, Hx = want_dims
+        flop = 4.0 * rows * Cx * Hx  # gH = gG W2 (2 rows C Hd) + gX = gP W1 (2 rows Hd C)
         achieved = flop / (avg_ms * 1e-3) / 1e12 if kms else None
         peak = MFMA_PEAK_TFLOPS[args.dtype]
-        traffic = None
+        traffic = alg_bytes = None
         pmc = os.path.join(REPO, "profiles", "pmc_roofline_kernel.json")
         if os.path.exists(pmc):  # HBM bytes per launch from the committed rocprofv3 --pmc passes
-            rec = json.load(open(pmc))
-            if rec.get("batch") == B and args.dtype == "bf16" and not args.fp8 and args.res == 64:
-                traffic = rec["traffic_bytes_per_launch"]
+            rec = json.load(open(pmc)).get("kernels", {}).get("moe_ffn_bwd_16")
+            if rec and B == 256 and args.dtype == "bf16" and not args.fp8 and args.res == 64 and E == 8 and k == 2:
+                traffic, alg_bytes = rec["traffic_bytes_per_launch"], rec["algorithmic_bytes_per_launch"]
         roof = {}
         if families:  # the family that takes the most time in the step leads (rocprof time where committed)
             def _t(f):
@@ -475,11 +476,13 @@ def main():
                 roof["dominant"].update({"ms_per_step": round(_t(dom), 4),
                                          "traffic_mb_per_step": dom.get("traffic_mb_per_step"),
                                          "share_of_step": round(_t(dom) / ms, 4)})
-        roof.update({"bound": "mfma", "kernel": f"mg_conv2d_fwd D conv_layers.2 ({args.res}x{args.res} real), "
-                                                f"implicit GEMM M={M} N={N} K={K}",
+        roof.update({"bound": "mfma", "kernel": f"mg_moe_ffn_bwd: fused expert FFN backward of the 16x16 block "
+                                                f"(largest kernel of the dominant family expert_gemm), {rows} routed "
+                                                f"rows, C={Cx}, Hd={Hx}",
                      "achieved": round(achieved, 2) if achieved else None,
                      "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": traffic, "traffic_unit": "bytes per launch (HBM, PMC)",
+                     "algorithmic_bytes_per_launch": alg_bytes,
                      "algorithmic_flop_per_launch": flop, "launches_timed": len(kms),
                      "avg_launch_ms": round(avg_ms, 4)})
         if args.config == "C4":  # extension: no reference FLOP formula; the executed MFMA work (roofline.py)

@@ -474,6 +474,9 @@ int mg_fold_defer(int on, void* stream);
 int mg_fold_flush(void* stream);
 /* the rows-fold kernel on caller records (tests / tools) */
 int mg_fold_rows_batch(int n, const mg_fold_rows* recs, void* stream);
+/* caller records as folds of the stream: queued behind its pending folds when it defers them (they run after
+   every deferred weight-gradient fold of the flush, so a record may read one's output), else run now */
+int mg_fold_rows_queue(int n, const mg_fold_rows* recs, void* stream);
 
 /* Multi-tensor column sums (bias gradients of a whole backward in one launch): out[c] += sum_r X[r*ld+c]
    for every descriptor; fp32 atomics across row blocks (at most 32 descriptors per launch). */

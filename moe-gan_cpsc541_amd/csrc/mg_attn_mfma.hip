@@ -25,7 +25,7 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 template <int D> struct Pitch;  // LDS row pitch (bf16): rows 0..7 of a tr-read half hit distinct bank octets
-template <> struct Pitch<16> { static constexpr int P = 16; };
+template <> struct Pitch<16> { static constexpr int P = 16; };  // + the chunk swizzle below
 template <> struct Pitch<32> { static constexpr int P = 48; };
 template <> struct Pitch<64> { static constexpr int P = 80; };
 
@@ -34,10 +34,19 @@ template <> struct Frag<16> { s16x4_t a; };
 template <> struct Frag<32> { bf16x8_t a; };
 template <> struct Frag<64> { bf16x8_t a, b; };
 
+// D = 16 images (32-B rows, four 8-B chunks): chunk j of row r is stored at chunk j ^ swz16(r).  A row-operand read
+// (ds_read_b64, lanes 0-31 = rows 0..15 x chunks 0, 1) then puts rows r and r + 8 on different bank quads (unswizzled
+// they share one: the measured 40-61 % bank-conflict share of these kernels), and a transposed read (rows 4g+q of one
+// 8-row half x chunks 0..3) still hits 8 distinct bank octets per lane group.
+MG_DEV constexpr int swz16(int r) { return ((r >> 3) & 1) << 1; }
+template <int D> MG_DEV constexpr int col_off(int r, int c) {  // element offset of column c (a multiple of 4) in row r
+  return D == 16 ? ((((c >> 2) ^ swz16(r))) << 2) + (c & 3) : c;
+}
+
 // row-operand fragment of a [rows][D] LDS image: row r, d-chunk of lane group g
 template <int D> MG_DEV Frag<D> ldfrag(const bf16_t* img, int r, int g);
 template <> MG_DEV Frag<16> ldfrag<16>(const bf16_t* img, int r, int g) {
-  return Frag<16>{*reinterpret_cast<const s16x4_t*>(img + r * Pitch<16>::P + 4 * g)};
+  return Frag<16>{*reinterpret_cast<const s16x4_t*>(img + r * Pitch<16>::P + col_off<16>(r, 4 * g))};
 }
 template <> MG_DEV Frag<32> ldfrag<32>(const bf16_t* img, int r, int g) {
   return Frag<32>{__builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(img + r * Pitch<32>::P + 8 * g))};
@@ -62,12 +71,15 @@ MG_DEV f32x4_t mfma_d(const Frag<64>& x, const Frag<64>& y) {
 
 // acc[m][n] += sum_{k in 32-token chunk} A[m][k] Y[k][n]: A from registers (permuted k order), Y an LDS
 // image [tokens][pitch], rows chunk0 + {4g..4g+3, 16+4g..16+4g+3}, columns c0..c0+15.
+template <int D>
 MG_DEV f32x4_t mfma_tok(bf16x8_t a, const bf16_t* img, int pitch, int chunk0, int c0, int lane, f32x4_t acc) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   auto base = (__attribute__((address_space(3))) char*)(img);
   const int r0 = chunk0 + 4 * g + q;
-  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + ((r0)*pitch + c0 + 4 * p) * 2));
-  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + ((r0 + 16) * pitch + c0 + 4 * p) * 2));
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4_t*)(base + (r0 * pitch + col_off<D>(r0, c0 + 4 * p)) * 2));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4_t*)(base + ((r0 + 16) * pitch + col_off<D>(r0 + 16, c0 + 4 * p)) * 2));
   u16x8_t b;
   b[0] = lo[0]; b[1] = lo[1]; b[2] = lo[2]; b[3] = lo[3];
   b[4] = hi[0]; b[5] = hi[1]; b[6] = hi[2]; b[7] = hi[3];
@@ -102,7 +114,7 @@ MG_DEV void stage(bf16_t* img, const bf16_t* src, int64_t ld, int L, int Lp, int
     int r = e / CV, c = (e - r * CV) * 8;
     u16x8_t v = u16x8_t(0);
     if (r < L) v = *reinterpret_cast<const u16x8_t*>(src + r * ld + c);
-    *reinterpret_cast<u16x8_t*>(img + r * P + c) = v;
+    *reinterpret_cast<u16x8_t*>(img + r * P + col_off<D>(r, c)) = v;  // (the swizzle keeps 16-B pairs whole)
   }
 }
 
@@ -111,7 +123,10 @@ MG_DEV void stage(bf16_t* img, const bf16_t* src, int64_t ld, int L, int Lp, int
 // ---------------------------------------------------------------------------
 // LT: token tile length (a multiple of 16); the sequence length L <= LT is a runtime argument (L = LT for the
 // generator's blocks; CLIP's 50 tokens run on the 64-token tiles with rows >= L masked on load and store)
-template <int D, int LT, int U>  // U units (image, head) per block, WPU waves per unit
+// MASK: L < max(LT, 32) (key / query slots past L masked); false for the generator's blocks (L == LT >= 32), whose softmax runs
+// without the per-score compare / select.  Scores are exponentiated as exp2(s * scale * log2 e - max), one fma and one
+// v_exp per score, and the 1 / sum normalisation is applied to the P V output rather than to every probability.
+template <int D, int LT, int U, bool MASK>  // U units (image, head) per block, WPU waves per unit
 __global__ __launch_bounds__(256) void k_attn_fwd_mfma(const bf16_t* __restrict__ qkv, int B, int L, int C, int heads,
                                                        bf16_t* __restrict__ out, float* __restrict__ lse) {
   constexpr int P = Pitch<D>::P;
@@ -147,7 +162,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(const bf16_t* __restrict_
         qf.b = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(qr + 32 + 8 * g));
       }
     }
-    // pass 1: S^T blocks (lane: key kb*16 + 4g + r, query t*16 + fr)
+    // pass 1: S^T blocks (lane: key kb*16 + 4g + r, query t*16 + fr), raw scores; row max
     f32x4_t s[NKB];
     float m = -INFINITY;
 #pragma unroll
@@ -155,39 +170,46 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(const bf16_t* __restrict_
       s[kb] = mfma_d(ldfrag<D>(Ks, kb * 16 + fr, g), qf);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = (kb * 16 + 4 * g + r < L) ? s[kb][r] * scale : -INFINITY;
-        s[kb][r] = v;
-        m = fmaxf(m, v);
+        if constexpr (MASK)
+          if (kb * 16 + 4 * g + r >= L) s[kb][r] = -INFINITY;
+        m = fmaxf(m, s[kb][r]);
       }
     }
     m = max16x4(m);
+    // p = exp(scale * (s - m)) = exp2(s * k2 - m * k2)
+    const float k2 = scale * 1.4426950408889634f, mk = m * k2;
     float l = 0.f;
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float p = __expf(s[kb][r] - m);
+        float p = __builtin_amdgcn_exp2f(fmaf(s[kb][r], k2, -mk));  // (a masked -inf score gives 0)
         s[kb][r] = p;
         l += p;
       }
     l = sum16x4(l);
-    const float inv = 1.f / l;
-    // pass 2: O = P V  (lane: query t*16 + 4g + r, d = db*16 + fr)
+    // pass 2: O = P V / l  (lane: query t*16 + 4g + r, d = db*16 + fr); the unnormalised probabilities (max 1)
+    // are the bf16 MFMA operand, the row's 1 / l scales the output
     f32x4_t o[D / 16];
 #pragma unroll
     for (int db = 0; db < D / 16; ++db) o[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < NKB / 2; ++c) {
-      bf16x8_t pa = pack8(s[2 * c] * inv, s[2 * c + 1] * inv);
+      bf16x8_t pa = pack8(s[2 * c], s[2 * c + 1]);
 #pragma unroll
-      for (int db = 0; db < D / 16; ++db) o[db] = mfma_tok(pa, Vs, P, 32 * c, db * 16, lane, o[db]);
+      for (int db = 0; db < D / 16; ++db) o[db] = mfma_tok<D>(pa, Vs, P, 32 * c, db * 16, lane, o[db]);
     }
+    // o[db][r] belongs to query t*16 + 4g + r, whose 1 / l lives in lane (4g + r) of every lane group
+    float inv_r[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) inv_r[r] = 1.f / __shfl(l, 4 * g + r, 64);
 #pragma unroll
     for (int db = 0; db < D / 16; ++db)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (t * 16 + 4 * g + r < L) out[((int64_t)b * L + t * 16 + 4 * g + r) * C + h * D + db * 16 + fr] = f2bf(o[db][r]);
-    if (g == 0 && t * 16 + fr < L) lse[((int64_t)b * heads + h) * L + t * 16 + fr] = m + __logf(l);
+        if (!MASK || t * 16 + 4 * g + r < L)
+          out[((int64_t)b * L + t * 16 + 4 * g + r) * C + h * D + db * 16 + fr] = f2bf(o[db][r] * inv_r[r]);
+    if (g == 0 && (!MASK || t * 16 + fr < L)) lse[((int64_t)b * heads + h) * L + t * 16 + fr] = m * scale + __logf(l);
   }
 }
 
@@ -234,7 +256,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_mfma(const bf16_t* __restrict_
 #pragma unroll
           for (int j = 0; j < 8; ++j) dsum += o8[j] * g8[j];
         }
-        lv = lse[((int64_t)b * heads + h) * L + i];
+        lv = lse[((int64_t)b * heads + h) * L + i] * 1.4426950408889634f;  // log2 units: p = exp2(s k2 - lv)
       }
       Ls[i] = lv;
       Ds[i] = dsum;
@@ -242,7 +264,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_mfma(const bf16_t* __restrict_
   }
   __syncthreads();
   if (!live) return;
-  const float scale = rsqrtf((float)D);
+  const float scale = rsqrtf((float)D), k2 = scale * 1.4426950408889634f;
+  constexpr bool MASKK = Lp != L;  // token slots past L exist only when L < 32
   bf16_t* grow = gqkv + (int64_t)b * L * ld + h * D;
   // ---- pass A: dQ = scale * dS K for query tiles
   for (int t = wu; t < L / 16; t += WPU) {
@@ -261,13 +284,15 @@ __global__ __launch_bounds__(256) void k_attn_bwd_mfma(const bf16_t* __restrict_
         f32x4_t dpt = mfma_d(ldfrag<D>(Vs, kb * 16 + fr, g), gf);  // dP^T[key][query]
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = (kb * 16 + 4 * g + r < L) ? __expf(st[r] * scale - li) : 0.f;
+          float p = __builtin_amdgcn_exp2f(fmaf(st[r], k2, -li));
+          if constexpr (MASKK)
+            if (kb * 16 + 4 * g + r >= L) p = 0.f;
           ds[jb][r] = p * (dpt[r] - di);
         }
       }
       bf16x8_t a = pack8(ds[0], ds[1]);
 #pragma unroll
-      for (int db = 0; db < D / 16; ++db) dq[db] = mfma_tok(a, Ks, P, 32 * c, db * 16, lane, dq[db]);
+      for (int db = 0; db < D / 16; ++db) dq[db] = mfma_tok<D>(a, Ks, P, 32 * c, db * 16, lane, dq[db]);
     }
 #pragma unroll
     for (int db = 0; db < D / 16; ++db)
@@ -291,7 +316,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_mfma(const bf16_t* __restrict_
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qi = qb * 16 + 4 * g + r;
-          float p = qi < L ? __expf(sv[r] * scale - Ls[qi]) : 0.f;
+          float p = __builtin_amdgcn_exp2f(fmaf(sv[r], k2, -Ls[qi]));
+          if constexpr (MASKK)
+            if (qi >= L) p = 0.f;
           pp[jb][r] = p;
           ds[jb][r] = p * (dp[r] - Ds[qi]);
         }
@@ -299,8 +326,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_mfma(const bf16_t* __restrict_
       bf16x8_t ap = pack8(pp[0], pp[1]), ad = pack8(ds[0], ds[1]);
 #pragma unroll
       for (int db = 0; db < D / 16; ++db) {
-        dv[db] = mfma_tok(ap, Gs, P, 32 * c, db * 16, lane, dv[db]);
-        dk[db] = mfma_tok(ad, Qs, P, 32 * c, db * 16, lane, dk[db]);
+        dv[db] = mfma_tok<D>(ap, Gs, P, 32 * c, db * 16, lane, dv[db]);
+        dk[db] = mfma_tok<D>(ad, Qs, P, 32 * c, db * 16, lane, dk[db]);
       }
     }
 #pragma unroll
@@ -334,8 +361,12 @@ template <int D, int LT>
 int launch_fwd(const bf16_t* qkv, int B, int C, int heads, bf16_t* out, float* lse, hipStream_t st, int L = LT) {
   constexpr int P = Pitch<D>::P, Lp = LT < 32 ? 32 : LT, WPU = LT / 16 < 4 ? LT / 16 : 4, U = units_fwd<D, LT>();
   size_t sm = (size_t)U * 2 * Lp * P * sizeof(bf16_t);
-  hipLaunchKernelGGL((k_attn_fwd_mfma<D, LT, U>), dim3(cdiv(B * heads, U)), dim3(64 * U * WPU), sm, st, qkv, B, L, C,
-                     heads, out, lse);
+  if (L == Lp)  // (LT = 16 tiles pad the keys to 32 slots: masked)
+    hipLaunchKernelGGL((k_attn_fwd_mfma<D, LT, U, false>), dim3(cdiv(B * heads, U)), dim3(64 * U * WPU), sm, st, qkv, B,
+                       L, C, heads, out, lse);
+  else
+    hipLaunchKernelGGL((k_attn_fwd_mfma<D, LT, U, true>), dim3(cdiv(B * heads, U)), dim3(64 * U * WPU), sm, st, qkv, B,
+                       L, C, heads, out, lse);
   return mg_check_launch("mg_attn_fwd (mfma)");
 }
 template <int D, int L>

@@ -43,28 +43,43 @@ MG_DEV int find_rec(const int* blk_off, int n) {
   return d;
 }
 
-// 64 columns x 16 row lanes per block
+// a record folds 4-column vectors (16-B loads) when its columns, pitch, pointers and split point allow
+__host__ __device__ inline bool rows_vec(const mg_fold_rows& q) {
+  return (q.ncols % 4) == 0 && (q.stride % 4) == 0 && (q.na % 4) == 0 && mg_al16(q.src) && mg_al16(q.out_a) &&
+         (q.na >= q.ncols || mg_al16(q.out_b));
+}
+
+// 64 column lanes x 16 row lanes per block; a lane owns 4 consecutive columns in vector records (each column still
+// summed rows r = lane, lane + 16, ... and then the 16 lanes in order: bit-identical to the scalar form)
 __global__ __launch_bounds__(1024) void k_fold_rows_batch(RowsBatch b) {
-  __shared__ float red[16][64];
+  __shared__ f32x4_t red[16][64];
   const int d = find_rec(b.blk_off, b.n);
   const mg_fold_rows& q = b.r[d];
   const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-  const int i = (blockIdx.x - b.blk_off[d]) * 64 + cx;
-  float s = 0.f;
-  if (i < q.ncols)
-    for (int r = ry; r < q.nrows; r += 16) s += q.src[(int64_t)r * q.stride + i];
+  const bool vec = rows_vec(q);
+  const int w = vec ? 4 : 1;
+  const int i = ((blockIdx.x - b.blk_off[d]) * 64 + cx) * w;
+  f32x4_t s = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  if (i < q.ncols) {
+    if (vec) {
+      for (int r = ry; r < q.nrows; r += 16) s += *reinterpret_cast<const f32x4_t*>(q.src + (int64_t)r * q.stride + i);
+    } else {
+      for (int r = ry; r < q.nrows; r += 16) s[0] += q.src[(int64_t)r * q.stride + i];
+    }
+  }
   red[ry][cx] = s;
   __syncthreads();
   if (ry == 0 && i < q.ncols) {
-    float t = 0.f;
+    f32x4_t t = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int y = 0; y < 16; ++y) t += red[y][cx];
-    if (i < q.na) q.out_a[i] += t;
-    else q.out_b[i - q.na] += t;
+    float* o = i < q.na ? q.out_a + i : q.out_b + (i - q.na);
+    if (vec) *reinterpret_cast<f32x4_t*>(o) += t;
+    else o[0] += t[0];
   }
 }
 
-inline int rows_blocks(const mg_fold_rows& q) { return std::max(1, cdiv(q.ncols, 64)); }
+inline int rows_blocks(const mg_fold_rows& q) { return std::max(1, cdiv(q.ncols, rows_vec(q) ? 256 : 64)); }
 
 // block (o, chunk of CC input channels) of one record; its slab segments staged in LDS, written in reference order
 __global__ __launch_bounds__(256) void k_fold_wgrad_batch(WgradBatch b) {
@@ -102,29 +117,77 @@ __global__ __launch_bounds__(256) void k_fold_wgrad_batch(WgradBatch b) {
 
 inline int wgrad_blocks(const mg_fold_wgrad& q) { return q.Cout * ((1 << q.lgCin) >> q.lgCC); }
 
+// Records of one launch run concurrently and add with plain read-modify-writes, so two records whose outputs
+// overlap (the real, fake and R1 weight gradients of one discriminator conv) must not share a launch: each record
+// goes to level 1 + the highest level of an earlier record it overlaps, and the levels launch in order -- every
+// output still receives its folds in submission order (bit-identical to immediate folds).
+struct Span {
+  uintptr_t lo, hi;
+};
+inline bool overlap(const Span& a, const Span& b) { return a.lo < b.hi && b.lo < a.hi; }
+inline void spans(const mg_fold_rows& q, Span* s, int* ns) {
+  *ns = 0;
+  const int na = std::min(q.na, q.ncols);
+  if (na > 0) s[(*ns)++] = Span{(uintptr_t)q.out_a, (uintptr_t)(q.out_a + na)};
+  if (q.ncols > na) s[(*ns)++] = Span{(uintptr_t)q.out_b, (uintptr_t)(q.out_b + (q.ncols - na))};
+}
+inline void spans(const mg_fold_wgrad& q, Span* s, int* ns) {
+  *ns = 1;
+  s[0] = Span{(uintptr_t)q.gw, (uintptr_t)(q.gw + (int64_t)q.Cout * (q.taps << q.lgCin))};
+}
+template <typename R>
+std::vector<int> levels(const R* recs, int n, int* nlev) {
+  std::vector<int> lev(n, 0);
+  std::vector<Span> sp(2 * n);
+  std::vector<int> ns(n);
+  *nlev = n > 0 ? 1 : 0;
+  for (int i = 0; i < n; ++i) {
+    spans(recs[i], &sp[2 * i], &ns[i]);
+    for (int j = 0; j < i; ++j)
+      for (int a = 0; a < ns[i]; ++a)
+        for (int b = 0; b < ns[j]; ++b)
+          if (overlap(sp[2 * i + a], sp[2 * j + b])) lev[i] = std::max(lev[i], lev[j] + 1);
+    *nlev = std::max(*nlev, lev[i] + 1);
+  }
+  return lev;
+}
+
 void launch_rows(const mg_fold_rows* recs, int n, hipStream_t st) {
-  for (int i0 = 0; i0 < n; i0 += kFoldMax) {
+  int nlev = 0;
+  const std::vector<int> lev = levels(recs, n, &nlev);
+  for (int l = 0; l < nlev; ++l) {
     RowsBatch b{};
-    b.n = std::min(kFoldMax, n - i0);
-    for (int j = 0; j < b.n; ++j) {
-      b.r[j] = recs[i0 + j];
-      b.blk_off[j + 1] = b.blk_off[j] + rows_blocks(b.r[j]);
+    for (int i = 0; i <= n; ++i) {
+      if (b.n == kFoldMax || (i == n && b.n > 0)) {
+        hipLaunchKernelGGL(k_fold_rows_batch, dim3(b.blk_off[b.n]), dim3(1024), 0, st, b);
+        b = RowsBatch{};
+      }
+      if (i == n || lev[i] != l) continue;
+      b.r[b.n] = recs[i];
+      b.blk_off[b.n + 1] = b.blk_off[b.n] + rows_blocks(recs[i]);
+      ++b.n;
     }
-    hipLaunchKernelGGL(k_fold_rows_batch, dim3(b.blk_off[b.n]), dim3(1024), 0, st, b);
   }
 }
 
 void launch_wgrad(const mg_fold_wgrad* recs, int n, hipStream_t st) {
-  for (int i0 = 0; i0 < n; i0 += kFoldMax) {
+  int nlev = 0;
+  const std::vector<int> lev = levels(recs, n, &nlev);
+  for (int l = 0; l < nlev; ++l) {
     WgradBatch b{};
-    b.n = std::min(kFoldMax, n - i0);
     size_t lds = 0;
-    for (int j = 0; j < b.n; ++j) {
-      b.r[j] = recs[i0 + j];
-      b.blk_off[j + 1] = b.blk_off[j] + wgrad_blocks(b.r[j]);
-      lds = std::max(lds, (size_t)(b.r[j].taps << b.r[j].lgCC) * sizeof(float));
+    for (int i = 0; i <= n; ++i) {
+      if (b.n == kFoldMax || (i == n && b.n > 0)) {
+        hipLaunchKernelGGL(k_fold_wgrad_batch, dim3(b.blk_off[b.n]), dim3(256), lds, st, b);
+        b = WgradBatch{};
+        lds = 0;
+      }
+      if (i == n || lev[i] != l) continue;
+      b.r[b.n] = recs[i];
+      b.blk_off[b.n + 1] = b.blk_off[b.n] + wgrad_blocks(recs[i]);
+      lds = std::max(lds, (size_t)(recs[i].taps << recs[i].lgCC) * sizeof(float));
+      ++b.n;
     }
-    hipLaunchKernelGGL(k_fold_wgrad_batch, dim3(b.blk_off[b.n]), dim3(256), lds, st, b);
   }
 }
 
@@ -250,4 +313,23 @@ extern "C" int mg_fold_rows_batch(int n, const mg_fold_rows* recs, void* stream)
                "bad fold record");
   if (n > 0) launch_rows(recs, n, reinterpret_cast<hipStream_t>(stream));
   return mg_check_launch("mg_fold_rows_batch");
+}
+
+extern "C" int mg_fold_rows_queue(int n, const mg_fold_rows* recs, void* stream) {
+  MG_REQUIRE(n >= 0 && (n == 0 || recs), "bad records");
+  for (int i = 0; i < n; ++i)
+    MG_REQUIRE(recs[i].src && recs[i].out_a && (recs[i].na >= recs[i].ncols || recs[i].out_b) && recs[i].ncols >= 0 &&
+                   recs[i].nrows >= 0,
+               "bad fold record");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  {
+    std::lock_guard<std::mutex> lk(g_fold_mu);
+    Defer* d = defer_entry(st, false);
+    if (d && d->on) {
+      d->rows.insert(d->rows.end(), recs, recs + n);
+      return MG_OK;
+    }
+  }
+  if (n > 0) launch_rows(recs, n, st);
+  return mg_check_launch("mg_fold_rows_queue");
 }

@@ -1134,7 +1134,11 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
     int per = ((r1 - r0 + splits - 1) / splits + TBK - 1) / TBK * TBK;
     kbeg = r0 + s * per;
     kend = min(r1, kbeg + per);
-    if (kbeg >= kend) return;
+    ep.zi = s;  // split-K partial slabs: slab s of group g (zstride = one slab of every group)
+    if (kbeg >= kend) {
+      if (ep.zstride == 0) return;  // accumulating epilogue: nothing to add
+      kend = kbeg;                  // a slab is written whole: an empty split stores its zeros
+    }
   }
   A.set_group(g);
   B.set_group(g);

@@ -719,14 +719,31 @@ void run_grouped_wgrad(int M, int N, int ngroups, const int32_t* row_off, int to
              b_gelu};
   mg_epilogue ee{};
   ee.alpha = e ? e->alpha : 1.f;
-  ee.atomic = 1;
-  auto ep = make_epi<float>(C, N, &ee);
-  ep.gstride_c = (int64_t)M * N;
+  const int64_t MN = (int64_t)M * N, GMN = MN * ngroups;
+  // where the K splits meet: fp32 atomics into C; or, when this stream defers its gradient folds (mg_fold.hip),
+  // plain stores of per-split partial slabs [splits][ngroups][M][N] folded later in split order (no atomic traffic:
+  // the ~8 M fp32 atomics per expert weight gradient were a quarter of its time at the C2 shapes, and the fold joins
+  // the backward's one batched flush); one split: a single writer per element, read-modify-write
+  bool deferred = false;
+  float* slabs = nullptr;
+  if (splits > 1 && ee.alpha == 1.f && GMN < (1ll << 31)) {
+    slabs = reinterpret_cast<float*>(mg_fold_alloc((size_t)splits * GMN * sizeof(float), st));
+    deferred = slabs != nullptr;
+  }
+  if (!slabs) {  // (slabs: plain stores of every element, the fold adds them into C)
+    if (splits > 1) ee.atomic = 1;
+    else ee.accumulate = 1;
+  }
+  auto ep = make_epi<float>(slabs ? slabs : C, N, &ee);
+  ep.gstride_c = MN;
+  if (slabs) ep.zstride = GMN;
   Grouping grp{2, ngroups, row_off, nullptr, 0};
   if (sizeof(T) == 2 && M >= 128 && N >= 128 && g_mg_tune[MG_TUNE_GWGRAD_TILE] != 64)
     launch_gemm<T, 128, 128, false, false, 1>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
   else
     launch_gemm<T, 64, 64, false, false, 1>(la, lb, ep, M, N, total_rows, splits, grp, 0, st);
+  if (slabs)  // C[g][m][n] += alpha * sum_s slab[s][g][m][n]
+    mg_fold_rows_submit(mg_fold_rows{slabs, GMN, splits, (int32_t)GMN, (int32_t)GMN, C, nullptr}, deferred, st);
 }
 }  // namespace
 

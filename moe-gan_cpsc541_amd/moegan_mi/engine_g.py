@@ -244,7 +244,7 @@ class GeneratorEngine:
             def wgrad_padded():
                 tmp = ops.zeros(rows, Cin, k, k, device=self.dev)
                 ops.conv2d_wgrad(gyt, xs, rows, k, k, 1, k // 2, tmp)
-                gW.add_(tmp[:Cout])
+                ops.fold_add([(tmp[:Cout], gW)])  # (after tmp's own deferred slab fold)
             self.side.run(wgrad_padded, gyt, xs)
         # demodulation backward
         if batched:  # deferred: all modulated convs' demod + style backward run batched at the end
@@ -408,15 +408,14 @@ class GeneratorEngine:
                     rp(self.P(r + "combined_mu"), self.P(r + "combined_rho"), eps[2]))
         return self.P(r + "feature_mu"), self.P(r + "text_mu"), self.P(r + "combined_mu")
 
-    def _block_vectors(self, w, text_seq, eps, train):
-        """Everything per block that depends only on (w, text_seq, router eps) -- the cross-attention value
-        chain tp -> v -> out_proj (t2i_moe_gan.py:549-556) and the router's text logits and feature-combine
-        matrix (:364-389) -- for all blocks at once: five batched launches instead of eighteen GEMMs."""
-        B = w.shape[0]
+    def _xattn_chain(self, text_seq):
+        """The cross-attention value chain tp -> v -> out_proj of every block (t2i_moe_gan.py:549-556): a
+        function of the text sequence and the weights only, so one step's D-phase and G-phase forwards share it
+        (computed with the prefix); three batched launches, one per level."""
+        B = text_seq.shape[0]
         dev = self.dev
         pres = [name + ".attn_block." for name in self.attn_blocks]
         Cs = [self.P(p + "text_proj.weight").shape[0] for p in pres]
-        bv = {p + "moe.": {} for p in pres}
         chain = {}
         src = [text_seq] * len(pres)
         for key, wname, bname, sl in (("tp", "text_proj.weight", "text_proj.bias", False),
@@ -433,6 +432,17 @@ class GeneratorEngine:
             ops.gemm_batch(probs)
             chain[key] = outs
             src = outs
+        return {p: dict(tp=chain["tp"][i], vv=chain["vv"][i], ca=chain["ca"][i]) for i, p in enumerate(pres)}
+
+    def _block_vectors(self, w, text_seq, eps, train, xchain):
+        """Everything per block that depends only on (w, text_seq, router eps): the cross-attention value chain
+        (``xchain``, _xattn_chain) and the router's text logits and feature-combine matrix (:364-389) -- for all
+        blocks at once in batched launches instead of eighteen GEMMs."""
+        B = w.shape[0]
+        dev = self.dev
+        pres = [name + ".attn_block." for name in self.attn_blocks]
+        Cs = [self.P(p + "text_proj.weight").shape[0] for p in pres]
+        bv = {p + "moe.": {} for p in pres}
         E = self.E
         probs1, probs2 = [], []
         pb = ops.PrepBatch(torch.float32)  # the routers' reparameterisations: one launch
@@ -447,8 +457,8 @@ class GeneratorEngine:
         pb.run()
         ops.gemm_batch(probs1, b_kc=False)
         ops.gemm_batch(probs2, b_kc=False)
-        for i, p in enumerate(pres):
-            bv[p] = dict(tp=chain["tp"][i], vv=chain["vv"][i], ca=chain["ca"][i])
+        for p in pres:
+            bv[p] = xchain[p]
         return bv
 
     def _flush_xattn_bwd(self):
@@ -718,8 +728,10 @@ class GeneratorEngine:
         name0, _, _, _, up0, _ = self.blocks[0]
         assert not up0
         x0, cbsv0 = self.cb_fwd(name0 + ".conv_block.", x, w, save=save)
+        xchain = self._xattn_chain(text_seq) if self.attn_blocks else {}
         return dict(B=B, text=text, text_c=text_c, t0=t0, t1=t1, t1c=t1c, tmu=tmu, trs=trs, text_seq=text_seq,
-                    hs=hs, h3=h3, w=w, w_c=w_c, psi=psi, S=S, S2=S2, D=D, x0=x0, cbsv0=cbsv0, save=save)
+                    hs=hs, h3=h3, w=w, w_c=w_c, psi=psi, S=S, S2=S2, D=D, x0=x0, cbsv0=cbsv0, save=save,
+                    xchain=xchain)
 
     def forward(self, z, text, eps, anneal=1.0, psi=0.7, train=True, save=True, want_img8=False, want_kl=True,
                 keep_prefix=False, prefix=None):
@@ -738,7 +750,7 @@ class GeneratorEngine:
         self.last_prefix = prefix if keep_prefix else None
         B = prefix["B"]
         w, text_seq = prefix["w"], prefix["text_seq"]
-        self._bv = self._block_vectors(w, text_seq, eps, train)
+        self._bv = self._block_vectors(w, text_seq, eps, train, prefix["xchain"])
         probs, kl2s, topis, blocks = [], [], [], []
         img8, rgb8sv = None, None
         x = None

@@ -116,11 +116,36 @@ def fold_defer(on):
     """Defer (True) the gradient folds of the library's two-pass reductions issued on the current stream until
     fold_flush(), or flush and stop deferring (False) -- mg_fold_defer."""
     call("mg_fold_defer", int(bool(on)), S())
+    if not on:
+        _FOLD_KEEP.clear()
+
+
+class _FoldRows(ctypes.Structure):
+    """Mirror of ``mg_fold_rows``."""
+    _fields_ = [("src", ctypes.c_void_p), ("stride", ctypes.c_int64), ("nrows", ctypes.c_int32),
+                ("ncols", ctypes.c_int32), ("na", ctypes.c_int32), ("out_a", ctypes.c_void_p), ("out_b", ctypes.c_void_p)]
+
+
+_FOLD_KEEP = []  # tensors a queued fold reads or writes: held until the flush (the caching allocator must not
+# hand their memory to later work while the fold is still pending)
+
+
+def fold_add(pairs):
+    """dst += src (fp32, contiguous, same size) for every (src, dst) pair as folds of the current stream: queued
+    behind its deferred folds inside a training step (so src may be a deferred fold's output), else run now."""
+    _FOLD_KEEP.extend(t for pair in pairs for t in pair)
+    recs = (_FoldRows * len(pairs))()
+    for i, (src, dst) in enumerate(pairs):
+        assert src.dtype == dst.dtype == torch.float32 and src.is_contiguous() and dst.is_contiguous()
+        assert src.numel() == dst.numel() < 2 ** 31
+        recs[i] = _FoldRows(src.data_ptr(), src.numel(), 1, src.numel(), src.numel(), dst.data_ptr(), None)
+    call("mg_fold_rows_queue", len(pairs), ctypes.addressof(recs), S())
 
 
 def fold_flush():
     """Run every deferred gradient fold of the current stream (one launch per fold kind; mg_fold_flush)."""
     call("mg_fold_flush", S())
+    _FOLD_KEEP.clear()
 
 
 def zeros(*shape, device, dtype=torch.float32):
@@ -307,8 +332,9 @@ def moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1=None,
     """Fused expert FFN backward (mg_moe_ffn_bwd): gP = (gG W2_g) * GELU'(Pre), gX = gP W1_g, gb1 += colsum(gP),
     gb2 += colsum(gG) (per group)."""
     G, Hd, C = W1.shape
-    call("mg_moe_ffn_bwd", L.MG_BF16, gG.shape[0], C, Hd, G, ptr(row_off), ptr(tile_off), max_tiles, ptr(gG),
-         ptr(Pre), ptr(W1), ptr(W2), ptr(gP), ptr(gX), ptr(gb1), ptr(gb2), S())
+    _timed("moe_ffn_bwd", (gG.shape[0], C, Hd),
+           lambda: call("mg_moe_ffn_bwd", L.MG_BF16, gG.shape[0], C, Hd, G, ptr(row_off), ptr(tile_off), max_tiles,
+                        ptr(gG), ptr(Pre), ptr(W1), ptr(W2), ptr(gP), ptr(gX), ptr(gb1), ptr(gb2), S()))
     return gP, gX
 
 

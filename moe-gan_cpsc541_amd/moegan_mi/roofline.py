@@ -46,7 +46,7 @@ FAMILIES = {
                            "mg_router_param_bwd", "mg_router_param_bwd_batch", "mg_moe_dispatch", "mg_router_kl")),
     "im2col_col2im": ("hbm", ("mg_im2col_4x4s2", "mg_col2im_4x4s2")),
     # deferred second passes of the two-pass gradient reductions (mg_fold.hip), one batched launch per kind
-    "grad_fold": ("hbm", ("mg_fold_flush", "mg_fold_rows_batch", "mg_fold_defer")),
+    "grad_fold": ("hbm", ("mg_fold_flush", "mg_fold_rows_batch", "mg_fold_rows_queue", "mg_fold_defer")),
     "d_conv0": ("hbm", ("mg_d0_fwd", "mg_d0_wgrad", "mg_d0_dgrad")),
     "elementwise": ("hbm", ("mg_cast", "mg_copy2d", "mg_lrelu_mask_mul", "mg_upsample2x_fwd", "mg_upsample2x_bwd",
                             "mg_const_fwd", "mg_gated_axpy", "mg_select_if", "mg_zero_if", "mg_clip_patches")),

@@ -7,6 +7,7 @@ import torch
 from goldens import T, check_packed, close, load
 from oracle import aurora_cpu as O
 from oracle.recipe import fill_state
+from steputil import Rounder
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -101,7 +102,9 @@ def test_discriminator_module_bf16_direct_kernel_limits(res):
     """The bf16 discriminator at a size the direct conv_layers.0 / head kernels take (64: W/2 = 32, Hf = 16) and at
     one past their limits (256: W/2 = 128 > 64, Hf = 64 > 32), which falls back to im2col + GEMMs and the GEMM head
     (DiscriminatorEngine._d0_ok / _head_ok; the implicit convs of conv_layers.2 take power-of-two sizes): logits and
-    the image gradient against the fp32 oracle at the bf16 bar (relative L2 <= 2e-2)."""
+    the image gradient against the fp32 oracle: relative L2 within 2e-2, or within 2.5x the bf16 floor of the same
+    oracle (steputil.Rounder.d_round: image, effective weights and the two conv activations rounded to bf16 in value
+    and gradient; root-mean-square over 3 realizations) -- the image gradient sums many cancelling bf16 terms."""
     M = _M()
     from moegan_mi.layout import discriminator_shapes
     D = M.AuroraDiscriminator(dtype="bf16")
@@ -122,8 +125,18 @@ def test_discriminator_module_bf16_direct_kernel_limits(res):
     torch.cuda.synchronize()
     rel = lambda a, b: float((a.detach().double().cpu() - b.double()).norm() / b.double().norm())  # noqa: E731
     assert out.shape == ref.shape
-    assert rel(out, ref.detach()) <= 2e-2, rel(out, ref.detach())
-    assert rel(gimg.grad, ximg.grad) <= 2e-2, rel(gimg.grad, ximg.grad)
+    floors_o, floors_g = [], []
+    for seed in (None, 1, 2):
+        xr = img.clone().requires_grad_(True)
+        fo = O.discriminator(xr, text, PD, Rounder(seed).d_round())
+        (fo * R).sum().backward()
+        floors_o.append(rel(fo, ref.detach()) ** 2)
+        floors_g.append(rel(xr.grad, ximg.grad) ** 2)
+    f_o, f_g = (sum(floors_o) / 3) ** 0.5, (sum(floors_g) / 3) ** 0.5
+    e_o, e_g = rel(out, ref.detach()), rel(gimg.grad, ximg.grad)
+    print(f"res {res}: logits rel {e_o:.3e} (bf16 floor {f_o:.3e}), image gradient rel {e_g:.3e} (floor {f_g:.3e})")
+    assert e_o <= max(2e-2, 2.5 * f_o), (e_o, f_o)
+    assert e_g <= max(2e-2, 2.5 * f_g), (e_g, f_g)
 
 
 def test_sample_and_checkpoint_roundtrip(tmp_path):

@@ -36,7 +36,7 @@ Bar, written per check below (SURVEY.md §8(c) asks 2e-2 on outputs and cosine >
     restatement of its own inputs (1e-5 of the summed magnitudes); the per-token terms and the per-image sums (at
     every batch size) are within FLOOR_X x the floor's relative error; the block's sum has the reference's
     sign wherever the reference exceeds FLOOR_X x the floor's noise on it.  The other single-element tensors (D's
-    head bias / gain) are held to relative error <= max(2e-2, FLOOR_X x floor);
+    head bias / gain) are held to relative error <= max(2e-2, FLOOR_X x the largest floor realization);
   * top-k expert selection: the device picks a top-k of its own probabilities; its sets equal the oracle's own
     fp32 top-k wherever the oracle margin log(p_(k)/p_(k+1)) exceeds DELTA, DELTA bounds the measured drift of
     that margin, flips stay below 10 % of tokens; the oracle then replays the device's selection
@@ -391,7 +391,10 @@ def _run(E, topk, inputs_per_step, lr=2e-4, replay=False):
                 if n.endswith("router.temperature"):
                     pass
                 elif numel == 1:
-                    check(rn <= max(REL, FLOOR_X * fl), f"step{si} grad {which}:{n} rel {rn:.2e} (floor {fl:.2e})")
+                    # (the largest floor realization, as for every other tensor: one cancelling scalar's floor
+                    # realizations spread widely -- see the calibration line)
+                    check(rn <= max(REL, FLOOR_X * fmax),
+                          f"step{si} grad {which}:{n} rel {rn:.2e} (floor {fl:.2e}, largest realization {fmax:.2e})")
                 elif numel < 64:
                     # a few-element sum over every pixel of the batch (the MTM offset heads' biases): its cosine is
                     # as noisy as the sum is cancelling, so it may instead sit within FLOOR_X x its own whole-step
