@@ -157,7 +157,7 @@ struct ColsumArgs {
 
 template <typename T>
 MG_DEV void colsum_block(const mg_colsum_desc& q, int rpb, int lcl, int cb, int rb) {
-  __shared__ float red[256 * 8 + 256];  // RL * (CL*8 + 1) <= 2048 + 256
+  __shared__ float red[256 * 8];  // RL * CL * 8
   const int CL = 1 << lcl, RL = 256 >> lcl;
   const int tx = threadIdx.x & (CL - 1), ty = threadIdx.x >> lcl;
   const T* X = reinterpret_cast<const T*>(q.X);
@@ -191,17 +191,18 @@ MG_DEV void colsum_block(const mg_colsum_desc& q, int rpb, int lcl, int cb, int 
           if (c + j < q.C) acc[j] += ldf(X, (int64_t)r * q.ld + c + j);
     }
   }
-  // red[ty][col] with the row pitch CL*8 + 1 (odd: the fold below walks a column without bank conflicts)
-  const int pitch = CL * 8 + 1;
+  // red[ty][j][tx] (column tx * 8 + j): the stores of one j are consecutive across lanes, and fold thread t reads
+  // word t of every row group -- both conflict-free (the [ty][col] layout put lanes 8 words apart: 8-way)
+  const int pitch = CL * 8;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[ty * pitch + tx * 8 + j] = acc[j];
+  for (int j = 0; j < 8; ++j) red[ty * pitch + j * CL + tx] = acc[j];
   __syncthreads();
   const int cols = CL * 8;
-  for (int col = threadIdx.x; col < cols; col += 256) {
-    const int gc = cb * cols + col;
+  for (int t = threadIdx.x; t < cols; t += 256) {
+    const int gc = cb * cols + (t & (CL - 1)) * 8 + (t >> lcl);
     if (gc < q.C) {
       float s = 0.f;
-      for (int y = 0; y < RL; ++y) s += red[y * pitch + col];
+      for (int y = 0; y < RL; ++y) s += red[y * pitch + t];
       atomicAdd(q.out + gc, s);
     }
   }

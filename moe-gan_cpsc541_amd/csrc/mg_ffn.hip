@@ -214,14 +214,22 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 // so gP is written once and never re-read for gX or gb1 (the unfused path wrote gP, read it for gX, for the bias
 // column sums and for gW1).  GEMM1 / GEMM2 run the MFMA sequence of the two grouped GEMMs they replace, in the
 // same k order: gP and gX are bit-identical to that path; gb1 sums the rows in a fixed order (per-tile partial
-// rows folded per expert in tile order).  LDS: gG tile 32 KiB + W2 chunk 16 + W1 chunk 16 + gP chunk 16 = 80 KiB,
-// two blocks per CU.  bf16, C = 128.
+// rows folded per expert in tile order).  LDS at C = 128: gG tile 32 KiB + W2 chunk 24 + W1 chunk 20 + gP chunk 16 =
+// 92 KiB (padded MC pitches, below), one block per CU.  bf16, C = 128 (256 opt-in).
+// MC image pitches: an odd multiple of 16 dwords, so the transposed fragment reads (k-rows kr0 + q and kr0 + 8 + q,
+// q = 0..3, per lane half) hit 8 distinct bank octets -- the unpadded pitches (64 and 128 bf16: 32 and 64 dwords) put
+// k-rows q and q + 2 (W2) / all four q (W1) on one octet, 2- and 4-way conflicts.  C = 256 keeps W1 unpadded
+// (the padded images would exceed the 160 KiB of LDS).
+template <int C> struct BwdPitch {
+  static constexpr int W2 = FHC + 32;
+  static constexpr int W1 = C == 128 ? C + 32 : C;
+};
 template <int C>
 struct FfnBwdSmem {
-  bf16_t gs[FBM * C];    // gG tile, KC image (A of GEMM1); the bf16 gX tile at the end
-  bf16_t w2[C * FHC];    // W2_e[:, chunk] as an MC image [c][h] (k-rows c), pitch FHC; column sums reuse it
-  bf16_t w1[FHC * C];    // W1_e[chunk, :] as an MC image [h][c] (k-rows h), pitch C
-  bf16_t hs[FBM * FHC];  // gP chunk, KC image (A of GEMM2)
+  bf16_t gs[FBM * C];               // gG tile, KC image (A of GEMM1); the bf16 gX tile at the end
+  bf16_t w2[C * BwdPitch<C>::W2];   // W2_e[:, chunk] as an MC image [c][h] (k-rows c); column sums reuse it
+  bf16_t w1[FHC * BwdPitch<C>::W1]; // W1_e[chunk, :] as an MC image [h][c] (k-rows h)
+  bf16_t hs[FBM * FHC];             // gP chunk, KC image (A of GEMM2)
 };
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
@@ -316,9 +324,9 @@ __device__ __forceinline__ void ffn_bwd_body(
     for (int j = 0; j < WV; ++j) {
       const int v = tid + j * FT;
       const int c = v / (FHC / 8), q = (v % (FHC / 8)) * 8;
-      *reinterpret_cast<u16x8_t*>(sm.w2 + mci(c, q, FHC)) = w2r[j];
+      *reinterpret_cast<u16x8_t*>(sm.w2 + mci(c, q, BwdPitch<C>::W2)) = w2r[j];
       const int hh = v / (C / 8), c1 = (v % (C / 8)) * 8;
-      *reinterpret_cast<u16x8_t*>(sm.w1 + mci(hh, c1, C)) = w1r[j];
+      *reinterpret_cast<u16x8_t*>(sm.w1 + mci(hh, c1, BwdPitch<C>::W1)) = w1r[j];
     }
     __syncthreads();
     if (h0 + FHC < Hd) load_w(h0 + FHC);
@@ -334,7 +342,7 @@ __device__ __forceinline__ void ffn_bwd_body(
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm) a[fm] = frag(sm.gs, kci<FBM>(wm * 32 + fm * 16 + fr, k0 + fk));
 #pragma unroll
-      for (int fn = 0; fn < 2; ++fn) b[fn] = mc_frag(sm.w2, FHC, k0, wn * 32 + fn * 16, lane);
+      for (int fn = 0; fn < 2; ++fn) b[fn] = mc_frag(sm.w2, BwdPitch<C>::W2, k0, wn * 32 + fn * 16, lane);
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
@@ -376,7 +384,7 @@ __device__ __forceinline__ void ffn_bwd_body(
       for (int fm = 0; fm < 2; ++fm) a[fm] = frag(sm.hs, kci<FBM>(wm * 32 + fm * 16 + fr, k0 + fk));
 #pragma unroll
       for (int fn = 0; fn < FN2; ++fn) {
-        const bf16x8_t b = mc_frag(sm.w1, C, k0, wn * (C / 2) + fn * 16, lane);
+        const bf16x8_t b = mc_frag(sm.w1, BwdPitch<C>::W1, k0, wn * (C / 2) + fn * 16, lane);
 #pragma unroll
         for (int fm = 0; fm < 2; ++fm)
           acc2[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fm], b, acc2[fm][fn], 0, 0, 0);
@@ -429,8 +437,8 @@ __device__ __forceinline__ void ffn_bwd_body(
   }
 }
 
-// two blocks per CU (128 VGPRs, a few spilled; A/B only: MG_TUNE_FFN_BWD_OCC = 2) or one with room for the live
-// ranges (the default: 174 vs 220 us at the C2 step's shapes, profiles/round4_ffn_bwd_probe.txt)
+// the 256-VGPR form (one block per CU) is the default: 174 vs 220 us at the C2 step's shapes for the 128-VGPR form,
+// profiles/round4_ffn_bwd_probe.txt, which the padded images (92 KiB) no longer fit twice per CU anyway
 template <int C>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_moe_ffn_bwd(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
@@ -513,7 +521,7 @@ extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngro
   float* part = reinterpret_cast<float*>(mg_workspace((size_t)max_tiles * (Hd + C) * sizeof(float), st));
   if (!part) return MG_ERR_ARG;
   float* part2 = gb2 ? part + (size_t)max_tiles * Hd : nullptr;
-  // C = 256: 144 KiB of LDS, one block per CU, so the 256-VGPR form; C = 128: measured faster too
+  // one block per CU either way (92 / 160 KiB of LDS at C = 128 / 256): the 256-VGPR form unless A/B-tuned
   const bool one_block = C == 256 || g_mg_tune[MG_TUNE_FFN_BWD_OCC] != 2;
 #define L_(K, CC)                                                                                                    \
   hipLaunchKernelGGL(K<CC>, dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),                  \

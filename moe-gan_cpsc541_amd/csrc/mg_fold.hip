@@ -25,17 +25,17 @@ namespace {
 
 constexpr int kFoldMax = 40;  // records per launch (kernel arguments stay below 4 KiB)
 
-struct RowsBatch {
-  mg_fold_rows r[kFoldMax];
+// A launch's records; blk_off: each record's first block (a chained record has no blocks of its own: the blocks of
+// its chain head run it after the head, next[] linking the chain in submission order, -1 ending it)
+template <typename R>
+struct Batch {
+  R r[kFoldMax];
   int blk_off[kFoldMax + 1];
+  int next[kFoldMax];
   int n;
 };
-
-struct WgradBatch {
-  mg_fold_wgrad r[kFoldMax];
-  int blk_off[kFoldMax + 1];
-  int n;
-};
+using RowsBatch = Batch<mg_fold_rows>;
+using WgradBatch = Batch<mg_fold_wgrad>;
 
 MG_DEV int find_rec(const int* blk_off, int n) {
   int d = 0;
@@ -49,16 +49,42 @@ __host__ __device__ inline bool rows_vec(const mg_fold_rows& q) {
          (q.na >= q.ncols || mg_al16(q.out_b));
 }
 
-// 64 column lanes x 16 row lanes per block; a lane owns 4 consecutive columns in vector records (each column still
-// summed rows r = lane, lane + 16, ... and then the 16 lanes in order: bit-identical to the scalar form)
-__global__ __launch_bounds__(1024) void k_fold_rows_batch(RowsBatch b) {
-  __shared__ f32x4_t red[16][64];
-  const int d = find_rec(b.blk_off, b.n);
-  const mg_fold_rows& q = b.r[d];
-  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+// Two block shapes, chosen per record:
+//   thin (nrows <= 16: the split-K slabs of the grouped expert weight gradients, a few rows of up to millions of
+//        columns): 1024 column lanes, each summing its rows in order -- one 16-B load per row, every lane busy;
+//   wide (more rows: the per-image / per-block partial rows): 64 column lanes x 16 row lanes, lane y summing rows
+//        y, y + 16, ..., then the 16 lanes in order.
+// For nrows <= 16 both orders are the same sequential sum 0 + row 0 + row 1 + ... (the wide form only adds zeros
+// after it), so a record folds bit-identically whichever shape it gets.  A lane owns 4 consecutive columns in
+// vector records.
+__host__ __device__ inline bool rows_thin(const mg_fold_rows& q) { return q.nrows <= 16; }
+
+MG_DEV void fold_rows_block(const mg_fold_rows& q, int blk, f32x4_t (*red)[64]) {
   const bool vec = rows_vec(q);
   const int w = vec ? 4 : 1;
-  const int i = ((blockIdx.x - b.blk_off[d]) * 64 + cx) * w;
+  if (rows_thin(q)) {
+    const int i = (blk * 1024 + threadIdx.x) * w;
+    if (i >= q.ncols) return;
+    float* o = i < q.na ? q.out_a + i : q.out_b + (i - q.na);
+    if (vec) {
+      f32x4_t v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (r < q.nrows) v[r] = *reinterpret_cast<const f32x4_t*>(q.src + (int64_t)r * q.stride + i);
+      f32x4_t t = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (r < q.nrows) t += v[r];
+      *reinterpret_cast<f32x4_t*>(o) += t;
+    } else {
+      float t = 0.f;
+      for (int r = 0; r < q.nrows; ++r) t += q.src[(int64_t)r * q.stride + i];
+      o[0] += t;
+    }
+    return;
+  }
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int i = (blk * 64 + cx) * w;
   f32x4_t s = f32x4_t{0.f, 0.f, 0.f, 0.f};
   if (i < q.ncols) {
     if (vec) {
@@ -77,42 +103,85 @@ __global__ __launch_bounds__(1024) void k_fold_rows_batch(RowsBatch b) {
     if (vec) *reinterpret_cast<f32x4_t*>(o) += t;
     else o[0] += t[0];
   }
+  __syncthreads();  // (red is reused by the next record of the chain)
 }
 
-inline int rows_blocks(const mg_fold_rows& q) { return std::max(1, cdiv(q.ncols, rows_vec(q) ? 256 : 64)); }
+__global__ __launch_bounds__(1024) void k_fold_rows_batch(RowsBatch b) {
+  __shared__ f32x4_t red[16][64];
+  int d = find_rec(b.blk_off, b.n);
+  const int blk = blockIdx.x - b.blk_off[d];
+  for (; d >= 0; d = b.next[d]) fold_rows_block(b.r[d], blk, red);
+}
 
-// block (o, chunk of CC input channels) of one record; its slab segments staged in LDS, written in reference order
-__global__ __launch_bounds__(256) void k_fold_wgrad_batch(WgradBatch b) {
-  extern __shared__ float seg[];  // [taps][CC]
-  const int d = find_rec(b.blk_off, b.n);
-  const mg_fold_wgrad& q = b.r[d];
+inline int rows_blocks(const mg_fold_rows& q) {
+  return std::max(1, cdiv(q.ncols, (rows_thin(q) ? 1024 : 64) * (rows_vec(q) ? 4 : 1)));
+}
+
+// block (o, chunk of CC input channels) of one record.  Its taps x CC values are nv 16-B vectors; the 256 threads
+// split as G = 256 / nv split groups (G = 1 when nv >= 128) x nv vectors, group g summing slabs g, g + G, ... in
+// order (eight loads in flight), then the groups folded in order through LDS -- every thread busy even for the
+// narrow chunks (CC = 8 or 16: nv = 18 or 36) whose single-group form left 7 of 8 threads idle behind serial
+// split loads.  The chunk is written in the reference [Cout][Cin][taps] order.
+MG_DEV void fold_wgrad_block(const mg_fold_wgrad& q, int lb, f32x4_t* lds4) {
   const int Cin = 1 << q.lgCin, N = q.taps << q.lgCin, CC = 1 << q.lgCC;
   const int64_t MN = (int64_t)q.Cout * N;
-  const int lb = blockIdx.x - b.blk_off[d], nch = Cin >> q.lgCC;
+  const int nch = Cin >> q.lgCC;
   const int o = lb / nch, c0 = (lb - o * nch) << q.lgCC;
   const float* src = q.ws + (int64_t)o * N + c0;
   const int nv = (q.taps << q.lgCC) >> 2;  // 16-B vectors of this block
-  for (int v = threadIdx.x; v < nv; v += 256) {
+  const int G = nv >= 128 ? 1 : min(256 / nv, q.splits);
+  const int SP = (CC >> 2) + 1;  // seg row pitch in vectors (+1: the transposed reads below walk taps, not banks)
+  f32x4_t* seg4 = lds4 + (G > 1 ? G * nv : 0);
+  const int gi = threadIdx.x / nv;
+  for (int v = threadIdx.x - gi * nv; gi < G && v < nv; v += (G > 1 ? nv : 256)) {
     const int tap = (4 * v) >> q.lgCC, ci = (4 * v) & (CC - 1);
     const float* p = src + ((int64_t)tap << q.lgCin) + ci;
-    f32x4_t acc = *reinterpret_cast<const f32x4_t*>(p);
-    int s = 1;
-    for (; s + 3 < q.splits; s += 4) {
-      const f32x4_t a = *reinterpret_cast<const f32x4_t*>(p + s * MN);
-      const f32x4_t bb = *reinterpret_cast<const f32x4_t*>(p + (s + 1) * MN);
-      const f32x4_t c = *reinterpret_cast<const f32x4_t*>(p + (s + 2) * MN);
-      const f32x4_t e = *reinterpret_cast<const f32x4_t*>(p + (s + 3) * MN);
-      acc += ((a + bb) + (c + e));
+    // slabs gi, gi + G, ... eight loads in flight (past the last slab: zeros), summed as a fixed tree
+    f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int s = gi; s < q.splits; s += 8 * G) {
+      f32x4_t a[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        a[k] = s + k * G < q.splits ? *reinterpret_cast<const f32x4_t*>(p + (int64_t)(s + k * G) * MN)
+                                    : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      acc += ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
-    for (; s < q.splits; ++s) acc += *reinterpret_cast<const f32x4_t*>(p + s * MN);
-    *reinterpret_cast<f32x4_t*>(seg + 4 * v) = acc;
+    if (G > 1) lds4[gi * nv + v] = acc;
+    else seg4[tap * SP + (ci >> 2)] = acc;
+    if (G > 1) break;
+  }
+  if (G > 1) {
+    __syncthreads();
+    for (int v = threadIdx.x; v < nv; v += 256) {
+      f32x4_t t = lds4[v];
+      for (int g = 1; g < G; ++g) t += lds4[g * nv + v];
+      seg4[((4 * v) >> q.lgCC) * SP + (((4 * v) & (CC - 1)) >> 2)] = t;
+    }
   }
   __syncthreads();
+  const float* seg = reinterpret_cast<const float*>(seg4);
   float* dst = q.gw + ((int64_t)o * Cin + c0) * q.taps;
   for (int j = threadIdx.x; j < (q.taps << q.lgCC); j += 256) {  // j = ci_local * taps + tap (reference order)
     const int ci = j / q.taps, tap = j - ci * q.taps;
-    dst[j] += seg[(tap << q.lgCC) + ci];
+    dst[j] += seg[tap * 4 * SP + ci];
   }
+  __syncthreads();  // (the LDS is reused by the next record of the chain)
+}
+
+__global__ __launch_bounds__(256) void k_fold_wgrad_batch(WgradBatch b) {
+  extern __shared__ f32x4_t lds4[];  // [G][nv] group partials, then [nv] folded (seg)
+  int d = find_rec(b.blk_off, b.n);
+  const int lb = blockIdx.x - b.blk_off[d];
+  for (; d >= 0; d = b.next[d]) fold_wgrad_block(b.r[d], lb, lds4);
+}
+
+inline int wgrad_groups(const mg_fold_wgrad& q) {
+  const int nv = (q.taps << q.lgCC) >> 2;
+  return nv >= 128 ? 1 : std::min(256 / nv, q.splits);
+}
+inline size_t wgrad_lds(const mg_fold_wgrad& q) {
+  const int nv = (q.taps << q.lgCC) >> 2, G = wgrad_groups(q);
+  return (size_t)((G > 1 ? G * nv : 0) + nv + q.taps) * 16;
 }
 
 inline int wgrad_blocks(const mg_fold_wgrad& q) { return q.Cout * ((1 << q.lgCin) >> q.lgCC); }
@@ -135,60 +204,83 @@ inline void spans(const mg_fold_wgrad& q, Span* s, int* ns) {
   *ns = 1;
   s[0] = Span{(uintptr_t)q.gw, (uintptr_t)(q.gw + (int64_t)q.Cout * (q.taps << q.lgCin))};
 }
+// records with the same output and block mapping chain (one launch folds them in order, block by block); other
+// overlapping outputs take levels
+inline bool same_target(const mg_fold_rows& a, const mg_fold_rows& b) {
+  return a.out_a == b.out_a && a.out_b == b.out_b && a.ncols == b.ncols && a.na == b.na && rows_vec(a) == rows_vec(b) &&
+         rows_thin(a) == rows_thin(b);
+}
+inline bool same_target(const mg_fold_wgrad& a, const mg_fold_wgrad& b) {
+  return a.gw == b.gw && a.Cout == b.Cout && a.lgCin == b.lgCin && a.taps == b.taps && a.lgCC == b.lgCC;
+}
+inline int nblocks(const mg_fold_rows& q) { return rows_blocks(q); }
+inline int nblocks(const mg_fold_wgrad& q) { return wgrad_blocks(q); }
+inline size_t lds_bytes(const mg_fold_rows&) { return 0; }
+inline size_t lds_bytes(const mg_fold_wgrad& q) { return wgrad_lds(q); }
+constexpr int kChainMax = 8;
+
 template <typename R>
-std::vector<int> levels(const R* recs, int n, int* nlev) {
+void launch_folds(const R* recs, int n, hipStream_t st, void (*kern)(Batch<R>), int threads) {
+  // chains: head[i] = the first earlier record with the same target (or i), at most kChainMax per chain
+  std::vector<int> head(n), len(n, 0);
+  for (int i = 0; i < n; ++i) {
+    head[i] = i;
+    for (int j = 0; j < i; ++j)
+      if (head[j] == j && len[j] < kChainMax && same_target(recs[j], recs[i])) {
+        head[i] = j;
+        break;
+      }
+    ++len[head[i]];
+  }
+  // levels of the chain heads
   std::vector<int> lev(n, 0);
   std::vector<Span> sp(2 * n);
   std::vector<int> ns(n);
-  *nlev = n > 0 ? 1 : 0;
+  int nlev = 0;
   for (int i = 0; i < n; ++i) {
     spans(recs[i], &sp[2 * i], &ns[i]);
-    for (int j = 0; j < i; ++j)
+    if (head[i] != i) continue;
+    for (int j = 0; j < i; ++j) {
+      if (head[j] != j) continue;
       for (int a = 0; a < ns[i]; ++a)
-        for (int b = 0; b < ns[j]; ++b)
-          if (overlap(sp[2 * i + a], sp[2 * j + b])) lev[i] = std::max(lev[i], lev[j] + 1);
-    *nlev = std::max(*nlev, lev[i] + 1);
+        for (int c = 0; c < ns[j]; ++c)
+          if (overlap(sp[2 * i + a], sp[2 * j + c])) lev[i] = std::max(lev[i], lev[j] + 1);
+    }
+    nlev = std::max(nlev, lev[i] + 1);
   }
-  return lev;
+  for (int l = 0; l < nlev; ++l) {
+    Batch<R> b{};
+    size_t lds = 0;
+    auto launch = [&]() {
+      if (b.n > 0) hipLaunchKernelGGL(kern, dim3(b.blk_off[b.n]), dim3(threads), lds, st, b);
+      b = Batch<R>{};
+      lds = 0;
+    };
+    for (int i = 0; i < n; ++i) {
+      if (head[i] != i || lev[i] != l) continue;
+      if (b.n + len[i] > kFoldMax) launch();
+      int prev = -1;
+      for (int k = i; k < n; ++k) {  // the chain, in submission order
+        if (head[k] != i) continue;
+        const int slot = b.n++;
+        b.r[slot] = recs[k];
+        b.next[slot] = -1;
+        b.blk_off[slot + 1] = b.blk_off[slot] + (prev < 0 ? nblocks(recs[k]) : 0);
+        if (prev >= 0) b.next[prev] = slot;
+        prev = slot;
+        lds = std::max(lds, lds_bytes(recs[k]));
+      }
+    }
+    launch();
+  }
 }
 
 void launch_rows(const mg_fold_rows* recs, int n, hipStream_t st) {
-  int nlev = 0;
-  const std::vector<int> lev = levels(recs, n, &nlev);
-  for (int l = 0; l < nlev; ++l) {
-    RowsBatch b{};
-    for (int i = 0; i <= n; ++i) {
-      if (b.n == kFoldMax || (i == n && b.n > 0)) {
-        hipLaunchKernelGGL(k_fold_rows_batch, dim3(b.blk_off[b.n]), dim3(1024), 0, st, b);
-        b = RowsBatch{};
-      }
-      if (i == n || lev[i] != l) continue;
-      b.r[b.n] = recs[i];
-      b.blk_off[b.n + 1] = b.blk_off[b.n] + rows_blocks(recs[i]);
-      ++b.n;
-    }
-  }
+  launch_folds(recs, n, st, k_fold_rows_batch, 1024);
 }
 
 void launch_wgrad(const mg_fold_wgrad* recs, int n, hipStream_t st) {
-  int nlev = 0;
-  const std::vector<int> lev = levels(recs, n, &nlev);
-  for (int l = 0; l < nlev; ++l) {
-    WgradBatch b{};
-    size_t lds = 0;
-    for (int i = 0; i <= n; ++i) {
-      if (b.n == kFoldMax || (i == n && b.n > 0)) {
-        hipLaunchKernelGGL(k_fold_wgrad_batch, dim3(b.blk_off[b.n]), dim3(256), lds, st, b);
-        b = WgradBatch{};
-        lds = 0;
-      }
-      if (i == n || lev[i] != l) continue;
-      b.r[b.n] = recs[i];
-      b.blk_off[b.n + 1] = b.blk_off[b.n] + wgrad_blocks(recs[i]);
-      lds = std::max(lds, (size_t)(recs[i].taps << recs[i].lgCC) * sizeof(float));
-      ++b.n;
-    }
-  }
+  launch_folds(recs, n, st, k_fold_wgrad_batch, 256);
 }
 
 // ---- per-stream deferral state: pending records and the partials arena ----

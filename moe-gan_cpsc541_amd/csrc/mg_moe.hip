@@ -469,7 +469,9 @@ __global__ __launch_bounds__(256) void k_token_grad_v(const T* __restrict__ gX, 
                                                       const float* __restrict__ g_raw, const float* __restrict__ Wfc,
                                                       TO* __restrict__ out, int64_t ldo) {
   extern __shared__ float sW[];  // [E][C]: a lane's 8 channels are contiguous (16-B reads, no bank conflicts)
-  for (int i = threadIdx.x; i < C * E; i += 256) sW[(i % E) * C + i / E] = Wfc[i];
+  // staged in destination order (consecutive lanes, consecutive words: the source-order loop put a lane group's
+  // stores C words apart, one bank: 8-way conflicts); the strided global reads hit L2
+  for (int j = threadIdx.x; j < C * E; j += 256) sW[j] = Wfc[(j % C) * E + j / C];
   __syncthreads();
   const int cv = C >> 3;
   const int n = Tn * cv;

@@ -88,10 +88,16 @@ __global__ __launch_bounds__(256) void k_warp_fwd_v(const T* __restrict__ x, con
   constexpr int VEC = VecOf<T>::N;
   typedef typename VecOf<T>::type vec_t;
   constexpr int OV = 32 / VEC;  // offset-conv input vectors per tap
-  __shared__ float sw[9 * 32 * 2];  // [tap][c][j]
+  // offset-conv weights as [v][NQ] float4s, v = tap * OV + c / VEC (one input vector), float4 k = (e = 2k, j = 0),
+  // (2k, 1), (2k + 1, 0), (2k + 1, 1); chunk k of v stored at slot (k + v / 4) mod NQ, so the 16 distinct vectors a
+  // lane group reads with one ds_read_b128 cover 64 distinct banks (the scalar [tap][c][j] reads were 8-way)
+  constexpr int NQ = VEC / 2;
+  __shared__ f32x4_t sw4[9 * OV * NQ];
+  float* swf = reinterpret_cast<float*>(sw4);
   for (int i = threadIdx.x; i < 576; i += 256) {
     const int j = i / 288, c = (i / 9) % 32, tap = i % 9;
-    sw[(tap * 32 + c) * 2 + j] = w2[i];
+    const int v = tap * OV + c / VEC, e = c % VEC;
+    swf[(v * NQ + (((e >> 1) + (v >> 2)) & (NQ - 1))) * 4 + (e & 1) * 2 + j] = w2[i];
   }
   __syncthreads();
   const int G = 1 << lgG;
@@ -114,9 +120,12 @@ __global__ __launch_bounds__(256) void k_warp_fwd_v(const T* __restrict__ x, con
 #pragma unroll
       for (int e = 0; e < VEC; ++e) t[e] = sizeof(T) == 2 ? bf2f((bf16_t)raw[e]) : (float)raw[e];
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        s0 += t[e] * sw[(tap * 32 + c0 + e) * 2];
-        s1 += t[e] * sw[(tap * 32 + c0 + e) * 2 + 1];
+      for (int k = 0; k < NQ; ++k) {  // (the e order of the scalar form: bit-identical sums)
+        const f32x4_t q = sw4[v * NQ + ((k + (v >> 2)) & (NQ - 1))];
+        s0 += t[2 * k] * q[0];
+        s1 += t[2 * k] * q[1];
+        s0 += t[2 * k + 1] * q[2];
+        s1 += t[2 * k + 1] * q[3];
       }
     }
   }
