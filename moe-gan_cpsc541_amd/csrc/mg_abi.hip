@@ -1,6 +1,7 @@
 // Error plumbing, scratch workspace, tuning switches and version of libmoegan_hip.
 #include <atomic>
 #include <mutex>
+#include <vector>
 #include <string>
 
 #include "mg_common.h"
@@ -74,6 +75,39 @@ void* mg_workspace(size_t bytes, hipStream_t stream) {
   }
   e->bytes = want;
   return e->ptr;
+}
+
+namespace {
+struct CntEntry {
+  int device;
+  hipStream_t stream;
+  int* ptr;
+  int n;
+};
+std::vector<CntEntry> g_cnt;
+std::mutex g_cnt_mu;
+}  // namespace
+
+int* mg_tile_counters(int n, hipStream_t stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_cnt_mu);
+  for (auto& e : g_cnt)
+    if (e.device == dev && e.stream == stream && e.n >= n) return e.ptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  const int want = std::max(n, 8192);
+  int* p = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&p), (size_t)want * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, (size_t)want * sizeof(int), stream) != hipSuccess) return nullptr;
+  for (auto& e : g_cnt)
+    if (e.device == dev && e.stream == stream) {  // a larger set replaces the old one (kept: in-flight launches)
+      e.ptr = p;
+      e.n = want;
+      return p;
+    }
+  g_cnt.push_back(CntEntry{dev, stream, p, want});
+  return p;
 }
 
 extern "C" int mg_set_workspace(void* ptr, size_t bytes, void* stream) {

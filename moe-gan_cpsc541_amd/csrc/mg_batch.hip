@@ -157,7 +157,7 @@ struct ColsumArgs {
 
 template <typename T>
 MG_DEV void colsum_block(const mg_colsum_desc& q, int rpb, int lcl, int cb, int rb) {
-  __shared__ float red[256 * 8];  // RL * CL * 8
+  __shared__ float red[4096];  // RL * 8 * (CL + PAD) <= 2048 + 32 * 64
   const int CL = 1 << lcl, RL = 256 >> lcl;
   const int tx = threadIdx.x & (CL - 1), ty = threadIdx.x >> lcl;
   const T* X = reinterpret_cast<const T*>(q.X);
@@ -191,18 +191,21 @@ MG_DEV void colsum_block(const mg_colsum_desc& q, int rpb, int lcl, int cb, int 
           if (c + j < q.C) acc[j] += ldf(X, (int64_t)r * q.ld + c + j);
     }
   }
-  // red[ty][j][tx] (column tx * 8 + j): the stores of one j are consecutive across lanes, and fold thread t reads
-  // word t of every row group -- both conflict-free (the [ty][col] layout put lanes 8 words apart: 8-way)
-  const int pitch = CL * 8;
+  // red[ty][j][tx] (column tx * 8 + j), j rows padded by 4 words: a lane group's stores of one j are consecutive
+  // words, and fold thread col (consecutive columns, so the atomics below stay coalesced) reads word
+  // j * (CL + 4) + tx -- 4j + tx distinct mod 32 over 32 consecutive columns, conflict-free both ways (the plain
+  // [ty][col] layout put the stores 8 words apart: 8-way)
+  const int PAD = CL >= 4 ? 4 : 0, pitch = 8 * (CL + PAD);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[ty * pitch + j * CL + tx] = acc[j];
+  for (int j = 0; j < 8; ++j) red[ty * pitch + j * (CL + PAD) + tx] = acc[j];
   __syncthreads();
   const int cols = CL * 8;
-  for (int t = threadIdx.x; t < cols; t += 256) {
-    const int gc = cb * cols + (t & (CL - 1)) * 8 + (t >> lcl);
+  for (int col = threadIdx.x; col < cols; col += 256) {
+    const int gc = cb * cols + col;
     if (gc < q.C) {
       float s = 0.f;
-      for (int y = 0; y < RL; ++y) s += red[y * pitch + t];
+      const int w = (col & 7) * (CL + PAD) + (col >> 3);
+      for (int y = 0; y < RL; ++y) s += red[y * pitch + w];
       atomicAdd(q.out + gc, s);
     }
   }

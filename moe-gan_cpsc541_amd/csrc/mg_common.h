@@ -116,7 +116,8 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_GWGRAD_BLOCKS = 20,  // mg_gemm_grouped_wgrad split target (blocks of 128^2 tiles): 0 automatic (512)
        MG_TUNE_BATCH_SPLIT = 21,  // mg_gemm_batch split-K slabs, > 1: on, that block target (A/B; 0 / 1 off: neutral in the step)
        MG_TUNE_GROUPED_SHORTK = 22,  // grouped expert GEMMs with K <= this on 64^2 tiles (0: 512, -1: never)
-       MG_TUNE_COUNT = 23 };
+       MG_TUNE_SPLITK_FUSED = 23,    // 1: split-K slabs reduced inside the launch (measured slower at C2: off)
+       MG_TUNE_COUNT = 24 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 // Deterministic mode (mg_set_tuning(MG_TUNE_DETERMINISTIC, 1)): every reduction that crosses workgroups runs in
 // a fixed order -- per-block partial rows in the stream's workspace folded by one pass, or one writer per
@@ -125,6 +126,9 @@ inline bool mg_det() { return g_mg_tune[MG_TUNE_DETERMINISTIC].load(std::memory_
 // Device scratch, one block per (device, stream): caller-owned (mg_set_workspace) or library-owned
 // (grown on demand, never shrunk).  NULL when it cannot be provided (mg_last_error says why).
 void* mg_workspace(size_t bytes, hipStream_t stream);
+// per-stream zeroed int counters for in-launch split-K reductions (mg_gemm.h gemm_splitk_fused_kernel): at least n,
+// allocated and zeroed outside stream capture only (NULL otherwise: the caller takes the two-launch form)
+int* mg_tile_counters(int n, hipStream_t stream);
 // Gradient folds (mg_fold.hip).  A producer of fold partials asks mg_fold_alloc first: non-NULL = the stream defers
 // its folds (mg_fold_defer) and the partials live in the deferral arena until the flush, so the fold is recorded
 // (deferred = true); NULL = take mg_workspace and fold now.  Both paths run the same fold kernels.

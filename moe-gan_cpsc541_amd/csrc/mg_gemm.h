@@ -1190,6 +1190,71 @@ __global__ __launch_bounds__(NTHREADS) void gemm_batch_kernel(BatchArgs<TO, AL, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split-K with the reduction in the same launch.  Every K-split block writes its fp32 slab as before; then it
+// publishes (every wave drains its stores, barrier, one lane: agent-scope release, drain, relaxed agent-scope
+// ticket on the tile's counter) and the block that draws the last ticket resets the counter, acquires at agent
+// scope and reduces the tile's slabs in split order through the real epilogue -- the reduction kernel's order,
+// so the outputs are bit-identical to the two-launch form (cdna_hip_programming.md, "In-launch split-K
+// reduction").  Counters live per stream (mg_tile_counters), zeroed once at allocation and by every last arriver.
+// ---------------------------------------------------------------------------
+template <int BM, int BN, class EP>
+MG_DEV void splitk_tile_fixup(const float* __restrict__ ws, int splits, int M, int N, const EP& ep, int m0, int n0,
+                              int* cnt) {
+  __shared__ int last_flag;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int is_last = old == splits - 1;
+    if (is_last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    last_flag = is_last;
+  }
+  __syncthreads();
+  if (!last_flag) return;
+  const int64_t MN = (int64_t)M * N;
+  for (int e = threadIdx.x; e < BM * BN / 8; e += NTHREADS) {
+    const int r = e / (BN / 8), c = (e - r * (BN / 8)) * 8;
+    const int m = m0 + r, n = n0 + c;
+    if (m >= M || n >= N) continue;
+    const float* p = ws + (int64_t)m * N + n;
+    if (ep.vec_ok && (N & 7) == 0) {
+      float v[8], t[8];
+      ld8(p, v);
+#pragma unroll 4
+      for (int sp = 1; sp < splits; ++sp) {
+        ld8(p + sp * MN, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += t[j];
+      }
+      ep.vec8(m, n, v);
+    } else {
+      for (int j = 0; j < 8 && n + j < N; ++j) {
+        float v = 0.f;
+        for (int sp = 0; sp < splits; ++sp) v += p[sp * MN + j];
+        ep(m, n + j, v);
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, typename TO, bool X3 = false>
+__global__ __launch_bounds__(NTHREADS) void gemm_splitk_fused_kernel(AL A, BL B, Epi<float> slab, Epi<TO> ep, int M,
+                                                                      int N, int K, int kchunk, int* cnt) {
+  const int s = blockIdx.z;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  slab.zi = s;
+  const int kbeg = s * kchunk, kend = min(K, kbeg + kchunk);
+  gemm_tile<T, BM, BN, A_KC, B_KC, AL, BL, Epi<float>, X3>(A, B, slab, m0, n0, M, N, kbeg, kend, 0);
+  splitk_tile_fixup<BM, BN>(slab.C, gridDim.z, M, N, ep, m0, n0, cnt + blockIdx.x * gridDim.y + blockIdx.y);
+}
+
 // launch helper: picks the grid; grouped-M launches an upper bound of tiles.
 template <typename T, int BM, int BN, bool A_KC, bool B_KC, int TAG = 0, bool X3 = false, class AL, class BL, class EP>
 inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, int K, int splits, Grouping grp,

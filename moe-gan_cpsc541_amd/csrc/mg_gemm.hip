@@ -130,11 +130,22 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
   Epi<float> slab = make_epi<float>(ws, N, &raw);
   slab.zstride = MN;
   slab.vec_ok = slab.host_vec_ok() ? 1 : 0;
+  auto ep = make_epi<TO>(C, ldc, e);
+  ep.vec_ok = ep.host_vec_ok() ? 1 : 0;
+  // the reduction inside the launch (last-arriving split of each tile; A/B slot MG_TUNE_SPLITK_FUSED): measured at
+  // C2 no faster on the few-tile GEMMs (the agent-scope release / acquire cost what the second launch did) and
+  // 30-70 % slower on the many-tile conv slabs (every block's release writes back its XCD's dirty L2 lines)
+  int* cnt = g_mg_tune[MG_TUNE_SPLITK_FUSED] == 1 ? mg_tile_counters((int)tiles, st) : nullptr;
   auto go = [&](auto la, auto lb, auto akc, auto bkc) {
     dim3 grid(cdiv(M, 64), cdiv(N, 64), splits);
-    hipLaunchKernelGGL((gemm_kernel<T, 64, 64, decltype(akc)::value, decltype(bkc)::value, decltype(la),
-                                    decltype(lb), Epi<float>, 0, X3>),
-                       grid, dim3(NTHREADS), 0, st, la, lb, slab, M, N, K, kchunk, xcd_group());
+    if (cnt)
+      hipLaunchKernelGGL((gemm_splitk_fused_kernel<T, 64, 64, decltype(akc)::value, decltype(bkc)::value,
+                                                  decltype(la), decltype(lb), TO, X3>),
+                         grid, dim3(NTHREADS), 0, st, la, lb, slab, ep, M, N, K, kchunk, cnt);
+    else
+      hipLaunchKernelGGL((gemm_kernel<T, 64, 64, decltype(akc)::value, decltype(bkc)::value, decltype(la),
+                                      decltype(lb), Epi<float>, 0, X3>),
+                         grid, dim3(NTHREADS), 0, st, la, lb, slab, M, N, K, kchunk, xcd_group());
   };
   const T* Ap = reinterpret_cast<const T*>(A);
   const T* Bp = reinterpret_cast<const T*>(B);
@@ -149,8 +160,7 @@ bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, in
     if (b_kc) go(la, LdKC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, FF{}, TT{});
     else go(la, LdMC<T>{Bp, ldb, N, K, nullptr, 1, nullptr, 0}, FF{}, FF{});
   }
-  auto ep = make_epi<TO>(C, ldc, e);
-  ep.vec_ok = ep.host_vec_ok() ? 1 : 0;
+  if (cnt) return true;
   int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
   hipLaunchKernelGGL((splitk_reduce_kernel<Epi<TO>>), dim3(blocks), dim3(256), 0, st, ws, splits, M, N, ep);
   return true;
@@ -396,10 +406,16 @@ bool conv_slabs_t(const void* x, int B, int H, int W, int Cin, const void* wpack
                             KW, stride, pad, K, sc, kwinv(KW)};
   LdKC<T> lb{reinterpret_cast<const T*>(wpack), K, Cout, K, nullptr, 1, nullptr, 0};
   dim3 grid(cdiv(M, BM), cdiv(Cout, BN), splits);
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, true, LdKCConv<T, false, SC>, LdKC<T>, Epi<float>>), grid,
-                     dim3(NTHREADS), 0, st, la, lb, slab, M, Cout, K, kchunk, xcd_group());
   auto ep = make_epi<TO>(y, ldy, e);
   ep.vec_ok = ep.host_vec_ok() ? 1 : 0;
+  int* cnt = g_mg_tune[MG_TUNE_SPLITK_FUSED] == 1 ? mg_tile_counters((int)tiles, st) : nullptr;
+  if (cnt) {  // the reduction inside the launch (gemm_splitk_fused_kernel; A/B only, see run_splitk_slabs)
+    hipLaunchKernelGGL((gemm_splitk_fused_kernel<T, BM, BN, true, true, LdKCConv<T, false, SC>, LdKC<T>, TO>), grid,
+                       dim3(NTHREADS), 0, st, la, lb, slab, ep, M, Cout, K, kchunk, cnt);
+    return true;
+  }
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, true, LdKCConv<T, false, SC>, LdKC<T>, Epi<float>>), grid,
+                     dim3(NTHREADS), 0, st, la, lb, slab, M, Cout, K, kchunk, xcd_group());
   int blocks = (int)std::min<int64_t>(cdiv(MN, 256), 2048);
   hipLaunchKernelGGL((splitk_reduce_kernel<Epi<TO>>), dim3(blocks), dim3(256), 0, st, ws, splits, M, Cout, ep);
   return true;

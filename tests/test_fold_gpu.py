@@ -109,3 +109,52 @@ def test_fold_add_keeps_tensors_until_flush():
         ops.fold_defer(False)
     torch.cuda.synchronize()
     assert torch.equal(dst, torch.full((4096,), 2.0, device=DEV))
+
+
+def _splitk_modes(fn):
+    """fn() under the two-launch split-K reduction (the default) and the in-launch one (tuning slot 23 = 1, A/B),
+    the latter twice (the tile counters reset themselves)."""
+    from moegan_mi import _lib as L
+    two = fn()
+    L.call("mg_set_tuning", 23, 1)
+    try:
+        one, again = fn(), fn()
+    finally:
+        L.call("mg_set_tuning", 23, 0)
+    torch.cuda.synchronize()
+    return two, one, again
+
+
+@pytest.mark.parametrize("dtype,M,N,K", [(torch.bfloat16, 256, 512, 1024), (torch.float32, 257, 512, 512),
+                                         (torch.bfloat16, 100, 72, 4096), (torch.float32, 64, 1024, 2048)])
+def test_splitk_in_launch_reduction_bit_identical(dtype, M, N, K):
+    """Few-tile GEMMs split K into fp32 slabs; the last-arriving split of each tile reduces them through the real
+    epilogue (bias + leaky ReLU here) inside the launch: bit-identical to the separate reduction launch, and the
+    per-stream tile counters come back to zero (a repeat gives the same bits)."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=DEV, generator=g).to(dtype)
+    B = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(dtype)
+    bias = torch.randn(N, device=DEV, generator=g)
+    ep = ops.E(bias=bias, act=1)  # ACT_LRELU
+    out_dtype = torch.float32 if dtype == torch.float32 else torch.bfloat16
+    two, one, again = _splitk_modes(lambda: ops.gemm(A, B, M, N, K, ep=ep, out_dtype=out_dtype))
+    assert torch.equal(two, one) and torch.equal(one, again)
+    ref = torch.nn.functional.leaky_relu(A.double() @ B.double().T + bias.double(), 0.2)
+    err = ((one.double() - ref).norm() / ref.norm()).item()
+    assert err < (2e-2 if dtype == torch.bfloat16 else 2e-3), err
+
+
+def test_splitk_in_launch_reduction_conv():
+    """A few-tile implicit conv (16 output tiles, K = 2304) with K split into slabs: in-launch reduction
+    bit-identical to the two-launch form."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(4, 16, 16, 256, device=DEV, generator=g).bfloat16()
+    W = torch.randn(64, 256, 3, 3, device=DEV, generator=g) * (9 * 256) ** -0.5
+    wp = ops.pack_conv(W, torch.bfloat16)
+    bias = torch.randn(64, device=DEV, generator=g)
+    two, one, again = _splitk_modes(lambda: ops.conv2d(x, wp, 64, 3, 3, 1, 1, ep=ops.E(bias=bias, act=1)))
+    assert torch.equal(two, one) and torch.equal(one, again)
+    ref = torch.nn.functional.leaky_relu(torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), W.double(),
+                                                                     bias.double(), padding=1), 0.2)
+    err = ((one.double().permute(0, 3, 1, 2) - ref).norm() / ref.norm()).item()
+    assert err < 2e-2, err
