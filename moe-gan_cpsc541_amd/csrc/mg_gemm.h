@@ -1089,7 +1089,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
   constexpr int TBK = tile_bk<T, X3>();
   // ---- resolve tile / group ----
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if ((grp.mode == 0 || grp.mode == 1) && grp.swz && (grp.swz == 1 || gridDim.z > 1)) {
+  if (((grp.mode == 0 || grp.mode == 1) && grp.swz && (grp.swz == 1 || gridDim.z > 1)) || (grp.mode == 2 && grp.swz)) {
     // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs by linear id, so blocks that
     // share an XCD (linear id % 8) take a contiguous run of (split, m-tile, n-tile) work items, n fastest --
     // all tiles of one K split (which read the same operand rows: a split-K weight gradient re-reads its
@@ -1128,8 +1128,8 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M
     m0 = (blockIdx.x - g * tpg) * BM;
   } else if (grp.mode == 2) {
     int splits = gridDim.z / grp.ngroups;
-    g = blockIdx.z / splits;
-    int s = blockIdx.z - g * splits;
+    g = bz / splits;  // (bz: the XCD-ordered z index, so the tiles of one group's K split share an XCD's L2)
+    int s = bz - g * splits;
     int r0 = grp.row_off[g], r1 = grp.row_off[g + 1];
     int per = ((r1 - r0 + splits - 1) / splits + TBK - 1) / TBK * TBK;
     kbeg = r0 + s * per;
@@ -1274,6 +1274,11 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   // re-read per column tile already hit in L2: profiles/round4_xcd_probe.txt), so off by default.
   const int xcd = g_mg_tune[MG_TUNE_XCD];
   if (grp.mode == 0 || grp.mode == 1) grp.swz = xcd == 3 ? 0 : xcd;
+  // grouped weight gradients (mode 2): on by default (slot value 3 turns it off).  Their (group, K split) slices
+  // are read by every output tile of the slice; in dispatch order those tiles land on different XCDs, and the
+  // PMC passes showed the narrow operand fetched once per tile (a 16x16 block's gW1 read 270 MB for 168 MB of
+  // operands)
+  if (grp.mode == 2) grp.swz = xcd == 3 ? 0 : 1;
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, A_KC, B_KC, AL, BL, EP, TAG, X3>), grid, dim3(NTHREADS), 0, st, A, B, e2, M, N,
                      K, kchunk, grp);
 }

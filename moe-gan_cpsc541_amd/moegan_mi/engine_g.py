@@ -855,20 +855,25 @@ class GeneratorEngine:
         hs = [h[:g6.shape[0]] for h in ctx["hs"]]  # (rows past B: the truncation centre's zero row, no gradient)
         ops.linear_wgrad(g6, hs[3], self.G("mapping.6.weight"))
         ops.colsum(g6, self.G("mapping.6.bias"), defer=True)
-        g = ops.linear_dgrad(g6, self.Pp("mapping.6.weight"))
+        # each data gradient leaves its GEMM already times lrelu'(the layer output below it) (the epilogue's
+        # MUL_LRELU_GRAD; the input rows of the first layer take none)
+        g = ops.linear_dgrad(g6, self.Pp("mapping.6.weight"), lrelu_out=hs[3])
         for j, i in enumerate((4, 2, 0)):
-            ops.lrelu_mask_mul(g, hs[3 - j], g)
             ops.linear_wgrad(g, hs[2 - j], self.G(f"mapping.{i}.weight"))
             ops.colsum(g, self.G(f"mapping.{i}.bias"), defer=True)
             if i != 0 or want_input_grads:
-                g = ops.linear_dgrad(g, self.Pp(f"mapping.{i}.weight"))
+                g = ops.linear_dgrad(g, self.Pp(f"mapping.{i}.weight"), lrelu_out=hs[2 - j] if i != 0 else None)
         g_zt = g if want_input_grads else None
         # text projection backward
         g_tsc = self._p(g_ts)
         ops.linear_wgrad(g_tsc, ctx["t1c"], self.G("text_projection.3.weight"))
         ops.colsum(g_ts, self.G("text_projection.3.bias"), defer=True)
-        g_t1 = ops.linear_dgrad(g_tsc, self.Pp("text_projection.3.weight"), out_dtype=torch.float32)
-        ops.lrelu_mask_mul(g_t1, ctx["t1"], g_t1)
+        if ctx["t1"].dtype == torch.float32 and ctx["t1"].is_contiguous():
+            g_t1 = ops.linear_dgrad(g_tsc, self.Pp("text_projection.3.weight"), out_dtype=torch.float32,
+                                    lrelu_out=ctx["t1"])
+        else:
+            g_t1 = ops.linear_dgrad(g_tsc, self.Pp("text_projection.3.weight"), out_dtype=torch.float32)
+            ops.lrelu_mask_mul(g_t1, ctx["t1"], g_t1)
         g_t0 = torch.empty_like(g_t1)
         ops.layernorm_bwd(g_t1, ctx["t0"], ctx["tmu"], ctx["trs"], self.P("text_projection.1.weight"), g_t0,
                           self.G("text_projection.1.weight"), self.G("text_projection.1.bias"))

@@ -214,11 +214,18 @@ def linear(x, W, bias=None, act=0, out=None, out_dtype=None, **epk):
     return gemm(x, W, M, N, K, out=out, out_dtype=out_dtype, ep=E(bias=bias, act=act, **epk))
 
 
-def linear_dgrad(g, W, out=None, accumulate=0, out_dtype=None):
-    """gx = g @ W for g [M,N], W [N,K] -> [M,K]."""
+def linear_dgrad(g, W, out=None, accumulate=0, out_dtype=None, lrelu_out=None):
+    """gx = g @ W for g [M,N], W [N,K] -> [M,K]; ``lrelu_out`` (the leaky-ReLU output y of the layer below, same
+    dtype and shape as gx): gx *= lrelu'(y) in the epilogue."""
     M, N = g.shape
     K = W.shape[1]
-    return gemm(g, W, M, K, N, b_kc=False, out=out, out_dtype=out_dtype, ep=E(accumulate=accumulate))
+    if lrelu_out is not None:
+        odt = out_dtype or g.dtype
+        assert lrelu_out.dtype == odt and tuple(lrelu_out.shape) == (M, K) and lrelu_out.stride(1) == 1
+        ep = E(accumulate=accumulate, act=L.ACT_MUL_LRELU_GRAD, aux=lrelu_out, ld_aux=lrelu_out.stride(0))
+    else:
+        ep = E(accumulate=accumulate)
+    return gemm(g, W, M, K, N, b_kc=False, out=out, out_dtype=out_dtype, ep=ep)
 
 
 def linear_wgrad(g, x, gW, alpha=1.0):

@@ -51,11 +51,12 @@ for step in "$@"; do
       cut -c1-600 ${O}_fullbench.json ;;
     prof|c5prof)
       extra=""
-      [ "$step" = c5prof ] && extra="--config C5"
+      fargs=""
+      [ "$step" = c5prof ] && extra="--config C5" && fargs="256 32 bf16 fp8"
       run 400 ${O}_${step}.log rocprofv3 --kernel-trace --stats -d ${O}_${step} -o run --output-format csv -- \
         python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-families --secondary "" $extra
       python3 tools/prof_summary.py ${O}_${step}/run_kernel_stats.csv > ${O}_${step}_stats.txt
-      python3 tools/family_time.py ${O}_${step}/run_kernel_trace.csv ${O}_${step}_family.json > ${O}_${step}_family.txt
+      FAMILY_LAST=9 python3 tools/family_time.py ${O}_${step}/run_kernel_trace.csv ${O}_${step}_family.json $fargs > ${O}_${step}_family.txt
       cat ${O}_${step}_family.txt ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
