@@ -491,10 +491,14 @@ __global__ __launch_bounds__(256) void k_token_grad_v(const T* __restrict__ gX, 
 #pragma unroll
         for (int q = 0; q < 8; ++q) s[q] += v[q];
       }
+    // a lane's two 16-B weight reads, 32 B apart across lanes, put lanes l and l + 8 of a ds_read_b128 lane group on
+    // one bank quad; lanes with bit 3 set read their second half first (both halves land, order only)
+    const int hsw = (threadIdx.x >> 3) & 1;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const f32x4_t w0 = *reinterpret_cast<const f32x4_t*>(sW + e * C + c);
-      const f32x4_t w1 = *reinterpret_cast<const f32x4_t*>(sW + e * C + c + 4);
+      const f32x4_t wa = *reinterpret_cast<const f32x4_t*>(sW + e * C + c + 4 * hsw);
+      const f32x4_t wb = *reinterpret_cast<const f32x4_t*>(sW + e * C + c + 4 - 4 * hsw);
+      const f32x4_t w0 = hsw ? wb : wa, w1 = hsw ? wa : wb;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         s[q] += gr[e] * w0[q];
@@ -767,8 +771,8 @@ __global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict_
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[j][e] += __shfl_xor(acc[j][e], o, 64);
   const int R = TY / tyw;  // partial rows of this block (one per wave-row group)
-  if (R > 1 && (int64_t)R * C * E <= 8192) {  // fold them in LDS (fixed order): one row per block
-    __shared__ float red[8192];
+  if (R > 1 && (int64_t)R * C * E <= 16384) {  // fold them in LDS (fixed order): one row per block
+    __shared__ float red[16384];
     if (ty % tyw == 0) {
 #pragma unroll
       for (int j = 0; j < CV; ++j)
@@ -1315,10 +1319,12 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
   if (C % CV == 0 && C / CV <= 256 && (256 % (C / CV)) == 0 && ld % 8 == 0 && mg_al16(tok) && mg_al16(g_raw) &&
       T > 0) {
     const int TX = C / CV, TY = 256 / TX, R = TY / (TX < 64 ? 64 / TX : 1);
-    const int rows_per_block = (R > 1 && (int64_t)R * C * E <= 8192) ? 1 : R;  // in-block LDS fold (kernel)
-    int chunk = std::max(TY, (T / 256 + TY - 1) / TY * TY);  // ~256 blocks ...
-    const int64_t row = (int64_t)rows_per_block * C * E;      // ... with at most 1 M floats of partial rows
-    const int64_t min_chunk = ((int64_t)T * row / (1 << 20) + TY - 1) / TY * TY;
+    const int rows_per_block = (R > 1 && (int64_t)R * C * E <= 16384) ? 1 : R;  // in-block LDS fold (kernel)
+    // ~1024 blocks with at most 4 M floats of partial rows (at 32 experts the old 256-block / 1 M-float budget
+    // left 64 blocks walking 1024 tokens each: 175 us for the 16x16 block's 65536 tokens at C5)
+    int chunk = std::max(TY, (T / 1024 + TY - 1) / TY * TY);
+    const int64_t row = (int64_t)rows_per_block * C * E;
+    const int64_t min_chunk = ((int64_t)T * row / (4 << 20) + TY - 1) / TY * TY;
     if (min_chunk > chunk) chunk = (int)min_chunk;
     const int nb = cdiv(T, chunk);
     bool deferred = false;

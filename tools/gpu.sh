@@ -5,6 +5,7 @@
 #   suite        the whole `pytest -m gpu` suite in one process + smoke()          -> gpurun_out/TAG_suite.log
 #   tests=F,G    the named test files only (tests/F.py ...)                        -> gpurun_out/TAG_tests.log
 #   bench        default C2 bench line (no CPU leg, no secondary configs)          -> gpurun_out/TAG_bench.json
+#   c5bench      the C5 bench line (32 experts top-4, MX-fp8 convs)                -> gpurun_out/TAG_c5bench.json
 #   fullbench    the driver's default bench (CPU leg + secondary configs)          -> gpurun_out/TAG_fullbench.json
 #   prof         rocprofv3 --kernel-trace --stats of a short replayed bench, the family split and the top kernels
 #                                                                                  -> gpurun_out/TAG_prof/, TAG_family.*
@@ -45,6 +46,10 @@ for step in "$@"; do
       run 300 ${O}_bench.log python bench.py --no-cpu-baseline --secondary ""
       grep '^{' ${O}_bench.log > ${O}_bench.json
       cut -c1-400 ${O}_bench.json ;;
+    c5bench)
+      run 300 ${O}_c5bench.log python bench.py --config C5 --no-cpu-baseline --secondary ""
+      grep '^{' ${O}_c5bench.log > ${O}_c5bench.json
+      cut -c1-400 ${O}_c5bench.json ;;
     fullbench)
       run 600 ${O}_fullbench.log python bench.py
       grep '^{' ${O}_fullbench.log > ${O}_fullbench.json
