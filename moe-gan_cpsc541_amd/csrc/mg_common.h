@@ -69,23 +69,52 @@ MG_DEV float gelu_erf_grad(float x) {
 }
 // bf16-output forms: erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the 2^-9 bf16
 // rounding of the result) -- one reciprocal, one exp and five FMAs instead of the piecewise erff; the
-// GELU gradient reuses that exp(-x^2/2) for the Gaussian density.
-MG_DEV float erfc_poly(float t) {
-  return t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+// GELU gradient reuses that exp(-x^2/2) for the Gaussian density.  One explicit operation sequence (every FMA
+// spelled out, so no contraction choice differs between forms) instantiated for a scalar and for a pair: the pair
+// form runs its multiplies and FMAs as packed-fp32 instructions (v_pk_fma_f32 / v_pk_mul_f32, two elements per
+// instruction; rcp / exp stay per element) and gives the same bits per element.  The fused expert kernels spend
+// most of their VALU issue here (the backward's GELU' per hidden unit was ~30 instructions per element).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+MG_DEV float gfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+MG_DEV f32x2_t gfma(f32x2_t a, f32x2_t b, f32x2_t c) { return __builtin_elementwise_fma(a, b, c); }
+MG_DEV float gabs(float a) { return __builtin_fabsf(a); }
+MG_DEV f32x2_t gabs(f32x2_t a) { return __builtin_elementwise_abs(a); }
+MG_DEV float gcopysign(float a, float b) { return __builtin_copysignf(a, b); }
+MG_DEV f32x2_t gcopysign(f32x2_t a, f32x2_t b) { return __builtin_elementwise_copysign(a, b); }
+MG_DEV float grcp(float a) { return __builtin_amdgcn_rcpf(a); }
+MG_DEV f32x2_t grcp(f32x2_t a) { return f32x2_t{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)}; }
+MG_DEV float gexp(float a) { return __expf(a); }
+MG_DEV f32x2_t gexp(f32x2_t a) { return f32x2_t{__expf(a.x), __expf(a.y)}; }
+template <typename V> MG_DEV V gsplat(float c) { return V(c); }
+// (t, g) of the erf approximation: t = 1 / (1 + p a), g = exp(-a^2), a = |x| / sqrt 2; returns erf(|x| / sqrt 2)
+// with the sign of x
+template <typename V> MG_DEV V gelu_erf_core(V x, V& g) {
+  const V a = gabs(x) * gsplat<V>(0.70710678118654752f);
+  const V t = grcp(gfma(gsplat<V>(0.3275911f), a, gsplat<V>(1.f)));
+  g = gexp(-(a * a));  // exp(-x^2 / 2)
+  V q = gfma(t, gsplat<V>(1.061405429f), gsplat<V>(-1.453152027f));
+  q = gfma(t, q, gsplat<V>(1.421413741f));
+  q = gfma(t, q, gsplat<V>(-0.284496736f));
+  q = gfma(t, q, gsplat<V>(0.254829592f));
+  const V p = t * q;
+  return gcopysign(gfma(-p, g, gsplat<V>(1.f)), x);
 }
-MG_DEV float gelu_fast(float x) {
-  const float a = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
-  const float e = copysignf(1.f - erfc_poly(t) * __expf(-a * a), x);
-  return 0.5f * x * (1.f + e);
+template <typename V> MG_DEV V gelu_fast_t(V x) {
+  V g;
+  const V e = gelu_erf_core(x, g);
+  const V hx = x * gsplat<V>(0.5f);
+  return gfma(hx, e, hx);  // 0.5 x (1 + e)
 }
-MG_DEV float gelu_fast_grad(float x) {
-  const float a = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
-  const float g = __expf(-a * a);  // exp(-x^2 / 2)
-  const float e = copysignf(1.f - erfc_poly(t) * g, x);
-  return 0.5f * (1.f + e) + x * 0.3989422804014327f * g;
+template <typename V> MG_DEV V gelu_fast_grad_t(V x) {
+  V g;
+  const V e = gelu_erf_core(x, g);
+  // 0.5 (1 + e) + x phi(x), phi(x) = exp(-x^2 / 2) / sqrt(2 pi)
+  return gfma(x * gsplat<V>(0.3989422804014327f), g, gfma(gsplat<V>(0.5f), e, gsplat<V>(0.5f)));
 }
+MG_DEV float gelu_fast(float x) { return gelu_fast_t<float>(x); }
+MG_DEV float gelu_fast_grad(float x) { return gelu_fast_grad_t<float>(x); }
+MG_DEV f32x2_t gelu_fast2(f32x2_t x) { return gelu_fast_t<f32x2_t>(x); }
+MG_DEV f32x2_t gelu_fast_grad2(f32x2_t x) { return gelu_fast_grad_t<f32x2_t>(x); }
 
 MG_DEV float wave_sum(float v) {
 #pragma unroll

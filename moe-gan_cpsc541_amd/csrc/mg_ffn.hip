@@ -152,10 +152,13 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         const f32x4_t bias = *reinterpret_cast<const f32x4_t*>(b1g + h0 + col);
         u16x4_t pv, gv;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v = acc1[fm][fn][j] + bias[j];
-          pv[j] = __builtin_bit_cast(unsigned short, f2bf(v));
-          gv[j] = __builtin_bit_cast(unsigned short, f2bf(gelu_fast(v)));
+        for (int j = 0; j < 4; j += 2) {  // element pairs on packed fp32 (mg_common.h gelu_fast2)
+          const float v0 = acc1[fm][fn][j] + bias[j], v1 = acc1[fm][fn][j + 1] + bias[j + 1];
+          const f32x2_t y = gelu_fast2(f32x2_t{v0, v1});
+          pv[j] = __builtin_bit_cast(unsigned short, f2bf(v0));
+          pv[j + 1] = __builtin_bit_cast(unsigned short, f2bf(v1));
+          gv[j] = __builtin_bit_cast(unsigned short, f2bf(y.x));
+          gv[j + 1] = __builtin_bit_cast(unsigned short, f2bf(y.y));
         }
         if (row < nrows) {
           const int o = row * Hd + h0 + col;
@@ -359,8 +362,11 @@ __device__ __forceinline__ void ffn_bwd_body(
         const u16x4_t pv = pre_r[fm][fn];
         u16x4_t gv;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          gv[j] = __builtin_bit_cast(unsigned short, f2bf(acc1[fm][fn][j] * gelu_fast_grad(bf2f(pv[j]))));
+        for (int j = 0; j < 4; j += 2) {  // element pairs on packed fp32 (mg_common.h gelu_fast_grad2)
+          const f32x2_t d = gelu_fast_grad2(f32x2_t{bf2f(pv[j]), bf2f(pv[j + 1])});
+          gv[j] = __builtin_bit_cast(unsigned short, f2bf(acc1[fm][fn][j] * d.x));
+          gv[j + 1] = __builtin_bit_cast(unsigned short, f2bf(acc1[fm][fn][j + 1] * d.y));
+        }
         if (row < nrows) *reinterpret_cast<u16x4_t*>(gpb + (int64_t)row * Hd + h0 + col) = gv;
         *reinterpret_cast<u16x4_t*>(sm.hs + kci<FBM>(row, col)) = gv;  // rows past the group: gG = 0, so gP = 0
       }

@@ -84,7 +84,11 @@ MG_DEV f32x4_t vgelu(f32x4_t v) { return f32x4_t{gelu_erf(v[0]), gelu_erf(v[1]),
 MG_DEV u16x8_t vgelu(u16x8_t v) {
   u16x8_t r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = f2bf(gelu_fast(bf2f(v[j])));
+  for (int j = 0; j < 8; j += 2) {  // element pairs on packed fp32
+    const f32x2_t y = gelu_fast2(f32x2_t{bf2f(v[j]), bf2f(v[j + 1])});
+    r[j] = f2bf(y.x);
+    r[j + 1] = f2bf(y.y);
+  }
   return r;
 }
 
@@ -526,13 +530,31 @@ struct Epi {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = lrelu(v[j]);
     } else if (act == ACT_GELU) {
+      if constexpr (sizeof(TO) == 2) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = sizeof(TO) == 2 ? gelu_fast(v[j]) : gelu_erf(v[j]);
+        for (int j = 0; j < 8; j += 2) {  // element pairs on packed fp32
+          const f32x2_t y = gelu_fast2(f32x2_t{v[j], v[j + 1]});
+          v[j] = y.x;
+          v[j + 1] = y.y;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+      }
     } else if (act == ACT_MUL_GELU_GRAD) {
       if (pf) pf_unpack(*pf, t);
       else ld8(aux + (int64_t)m * ld_aux + n, t);
+      if constexpr (sizeof(TO) == 2) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= sizeof(TO) == 2 ? gelu_fast_grad(t[j]) : gelu_erf_grad(t[j]);
+        for (int j = 0; j < 8; j += 2) {
+          const f32x2_t d = gelu_fast_grad2(f32x2_t{t[j], t[j + 1]});
+          v[j] *= d.x;
+          v[j + 1] *= d.y;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_erf_grad(t[j]);
+      }
     } else if (act == ACT_MUL_LRELU_GRAD) {
       if (pf) pf_unpack(*pf, t);
       else ld8(aux + (int64_t)m * ld_aux + n, t);

@@ -416,9 +416,10 @@ __global__ __launch_bounds__(256) void k_adamw_dev_v(float* __restrict__ p, cons
     adamw_elem(gi, pi, mi, vi, coef, lr, b1, b2, eps, wd, step_size, bc2_sqrt);
   };
   const int64_t n4 = n >> 2;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    f32x4_t pv = reinterpret_cast<const f32x4_t*>(p)[i], gv = reinterpret_cast<const f32x4_t*>(g)[i];
-    f32x4_t mv = reinterpret_cast<const f32x4_t*>(m)[i], vv = reinterpret_cast<const f32x4_t*>(v)[i];
+  // two 4-parameter vectors per thread and iteration, all eight 16-B loads issued before the math (one vector per
+  // iteration left one set of loads in flight per thread: ~4.2 TB/s on the C5 generator's 95 M parameters)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  auto upd4 = [&](int64_t i, f32x4_t pv, f32x4_t gv, f32x4_t mv, f32x4_t vv) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float pj = pv[j], mj = mv[j], vj = vv[j];
@@ -436,7 +437,20 @@ __global__ __launch_bounds__(256) void k_adamw_dev_v(float* __restrict__ p, cons
       for (int j = 0; j < 4; ++j) h[j] = f2bf(pv[j]);
       reinterpret_cast<u16x4_t*>(shadow)[i] = h;
     }
+  };
+  const f32x4_t* p4 = reinterpret_cast<const f32x4_t*>(p);
+  const f32x4_t* g4 = reinterpret_cast<const f32x4_t*>(g);
+  const f32x4_t* m4 = reinterpret_cast<const f32x4_t*>(m);
+  const f32x4_t* v4 = reinterpret_cast<const f32x4_t*>(v);
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const int64_t i2 = i + stride;
+    const f32x4_t pa = p4[i], ga = g4[i], ma = m4[i], va = v4[i];
+    const f32x4_t pb = p4[i2], gb = g4[i2], mb = m4[i2], vb = v4[i2];
+    upd4(i, pa, ga, ma, va);
+    upd4(i2, pb, gb, mb, vb);
   }
+  if (i < n4) upd4(i, p4[i], g4[i], m4[i], v4[i]);
   for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float pi = p[i], mi = m[i], vi = v[i];

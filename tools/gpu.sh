@@ -14,6 +14,7 @@
 #   issue        SQ issue profile of one eager step (tools/pmc_step_issue.py)      -> gpurun_out/TAG_issue.txt
 #   probe=NAME   python tools/NAME.py (isolated kernel probes)                     -> gpurun_out/TAG_NAME.txt
 #   tune=SPEC    bench with MOEGAN_TUNE=SPEC (slot=value[,slot=value])             -> gpurun_out/TAG_tune_SPEC.json
+#   c5tune=SPEC  the same on the C5 config                                         -> gpurun_out/TAG_c5tune_SPEC.json
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=$1
@@ -86,11 +87,13 @@ for step in "$@"; do
       name=${step#probe=}
       run 300 ${O}_${name}.txt python3 tools/${name}.py
       cat ${O}_${name}.txt ;;
-    tune=*)
-      spec=${step#tune=}
-      run 300 ${O}_tune.log env MOEGAN_TUNE="$spec" python bench.py --no-cpu-baseline --secondary ""
-      grep '^{' ${O}_tune.log > "${O}_tune_${spec//[,=]/_}.json"
-      echo "tune $spec: $(cut -c1-200 "${O}_tune_${spec//[,=]/_}.json")" ;;
+    tune=*|c5tune=*)
+      spec=${step#*tune=}
+      cfg=""
+      [ "${step%%tune=*}" = c5 ] && cfg="--config C5"
+      run 300 ${O}_tune.log env MOEGAN_TUNE="$spec" python bench.py --no-cpu-baseline --secondary "" $cfg
+      grep '^{' ${O}_tune.log > "${O}_${step%%=*}_${spec//[,=]/_}.json"
+      echo "${step%%=*} $spec: $(cut -c1-200 "${O}_${step%%=*}_${spec//[,=]/_}.json")" ;;
     *)
       echo "[gpu.sh] unknown step $step"; exit 2 ;;
   esac
