@@ -7,7 +7,7 @@ on the stream it is enqueued on.  A family's achieved rate is its total work ove
 
 A call's event time includes every kernel that entry point launches (e.g. ``mg_conv2d_wgrad`` = GEMM +
 ``k_wgrad_fold`` / split-K reduce), so the wgrad family carries its fold.  ``KERNELS`` maps the rocprofv3
-kernel names to the same families so the PMC traffic of a ``--pmc`` pass (tools/family_pmc.py) can be
+kernel names to the same families so the PMC traffic of a ``--pmc`` pass (tools/family_traffic.py) can be
 attributed per family too.
 """
 import re
