@@ -268,7 +268,7 @@ class DiscriminatorEngine:
         ops.copy2d(f["img_part"], fake_pred, B, No)
         ops.copy2d(tb.view(B, 1).expand(B, No).contiguous() if No > 1 else tb.view(B, 1), fake_pred, B, No,
                    accumulate=1)
-        loss = torch.zeros(1, device=self.dev)
+        loss = torch.empty(1, device=self.dev)  # (mg_g_loss writes it)
         g = torch.empty(B, No, device=self.dev)
         ops.g_loss(fake_pred.view(-1), loss, g.view(-1), scale)
         g_img = ops.zeros(*fake_img.shape, device=self.dev, dtype=self.cdt)

@@ -79,6 +79,7 @@ class GeneratorEngine:
         self._defer = False
         self._mean_latent = None
         self._want_kl = True
+        self.last_klbuf = None
         self._bv = None  # per-block vectors of the running forward (_block_vectors)
         self.guard_flags = None  # the training step's loss-guard word (step.py), read by the router backward
         # called with (lo, hi) when a contiguous range of the flat gradient is final during backward (a block's
@@ -334,7 +335,7 @@ class GeneratorEngine:
     # ------------------------------------------------------------------
     # SparseMoE + BayesianRouter  (t2i_moe_gan.py:265-491)
     # ------------------------------------------------------------------
-    def moe_fwd(self, pre, tok, resid, w, HW, eps, anneal, train=True, save=True):
+    def moe_fwd(self, pre, tok, resid, w, HW, eps, anneal, train=True, save=True, kl_out=None):
         r = pre + "router."
         T, C = tok.shape
         B = w.shape[0]
@@ -388,7 +389,7 @@ class GeneratorEngine:
         ops.moe_combine(Y, pos_of, gate, resid, out)  # x_spatial + moe_out (:571)
         kl2 = None
         if train and self._want_kl:
-            kl2 = torch.empty(2, device=self.dev, dtype=torch.float32)
+            kl2 = kl_out if kl_out is not None else torch.empty(2, device=self.dev, dtype=torch.float32)
             ops.router_kl(self.P(r + "feature_mu"), self.P(r + "feature_rho"), self.P(r + "text_mu"),
                           self.P(r + "text_rho"), self.P(r + "combined_mu"), self.P(r + "combined_rho"), kl2)
         sv = None
@@ -597,7 +598,7 @@ class GeneratorEngine:
     # ------------------------------------------------------------------
     # AttentionBlock  (t2i_moe_gan.py:493-576)
     # ------------------------------------------------------------------
-    def attn_fwd(self, pre, x, w, text_seq, eps, anneal, train=True, save=True):
+    def attn_fwd(self, pre, x, w, text_seq, eps, anneal, train=True, save=True, kl_out=None):
         B, H, W, C = x.shape
         L_ = H * W
         T = B * L_
@@ -620,7 +621,8 @@ class GeneratorEngine:
         xf1 = ops.linear(att, self.Pc(pre + "self_attn.out_proj.weight"), bias=self.P(pre + "self_attn.out_proj.bias"),
                          resid=xf0, ld_res=C, addvec=ca, add_shift=ops.ilog2(L_), add_ld=C)
         n3, mu3, rs3 = ops.layernorm_fwd(xf1, self.P(pre + "norm3.weight"), self.P(pre + "norm3.bias"))
-        xpre, probs, kl2, topi, sv_moe = self.moe_fwd(pre + "moe.", n3, xf1, w, L_, eps, anneal, train, save)
+        xpre, probs, kl2, topi, sv_moe = self.moe_fwd(pre + "moe.", n3, xf1, w, L_, eps, anneal, train, save,
+                                                      kl_out=kl_out)
         out, sv_out = self.mc_fwd(pre + "proj_out.", xpre.view(B, H, W, C), w, save=save)
         sv = None
         if save:
@@ -649,7 +651,9 @@ class GeneratorEngine:
         # self-attention
         g_att = ops.linear_dgrad(g_xf1, self.Pc(pre + "self_attn.out_proj.weight"))
         ops.linear_wgrad(g_xf1, sv["att"], self.G(pre + "self_attn.out_proj.weight"))
-        ops.colsum(g_xf1, self.G(pre + "self_attn.out_proj.bias"))
+        # out_proj bias gradient = column sums of g_xf1 = the sum over images of g_ca (deferred: g_xf1 itself is
+        # accumulated into below, g_ca is not)
+        ops.colsum(g_ca, self.G(pre + "self_attn.out_proj.bias"), defer=True)
         g_qkv = ops.attn_bwd(sv["qkv"], sv["att"], g_att, sv["lse"], B, L_, C)
         g_n1 = ops.linear_dgrad(g_qkv, self.Pc(pre + "self_attn.in_proj_weight"))
         gWqkv, gbqkv = self.G(pre + "self_attn.in_proj_weight"), self.G(pre + "self_attn.in_proj_bias")
@@ -752,6 +756,9 @@ class GeneratorEngine:
         w, text_seq = prefix["w"], prefix["text_seq"]
         self._bv = self._block_vectors(w, text_seq, eps, train, prefix["xchain"])
         probs, kl2s, topis, blocks = [], [], [], []
+        # every block's two KL terms in one [blocks, 2] buffer (no stack of per-block results afterwards)
+        klbuf = (torch.empty(len(self.attn_blocks), 2, device=self.dev, dtype=torch.float32)
+                 if train and self._want_kl else None)
         img8, rgb8sv = None, None
         x = None
         ai = 0
@@ -765,7 +772,8 @@ class GeneratorEngine:
             asv = None
             if attn:
                 x, p, kl2, topi, asv = self.attn_fwd(name + ".attn_block.", x, w, text_seq,
-                                                     None if eps is None else eps[ai], anneal, train, save)
+                                                     None if eps is None else eps[ai], anneal, train, save,
+                                                     kl_out=None if klbuf is None else klbuf[ai])
                 ai += 1
                 probs.append(p)
                 kl2s.append(kl2)
@@ -781,6 +789,7 @@ class GeneratorEngine:
             ctx = {k: prefix[k] for k in ("B", "text", "text_c", "t0", "t1", "t1c", "tmu", "trs", "text_seq", "hs",
                                           "h3", "w", "w_c", "psi")}
             ctx.update(z=z, blocks=blocks, rgbsv=rgbsv, rgb8sv=rgb8sv)
+        self.last_klbuf = klbuf  # kl2s are its rows (TrainStep reads the buffer instead of stacking them)
         return img16, img8, kl2s, probs, topis, ctx
 
     def backward(self, ctx, g_img16, coef=None, kl_coef=None, want_input_grads=False, g_probs=None, g_img8=None):

@@ -293,7 +293,7 @@ class TrainStep:
         load = ops.zeros(c.E, device=self.dev)
         ops.colsum(last, load)
         self._allreduce_sum(load)
-        bal = torch.zeros(1, device=self.dev)
+        bal = torch.empty(1, device=self.dev)  # (mg_balance writes it)
         coef = torch.empty(c.E, device=self.dev)
         ops.balance(load, c.E, last.shape[0] * self.world, c.balance_weight, float(self.world), bal, coef)
         # CLIP terms (t2i_moe_gan.py:1385-1387): forward only, they enter g_loss's value but no gradient
@@ -302,7 +302,8 @@ class TrainStep:
             clip16 = clip_loss(img16[..., :3].permute(0, 3, 1, 2), text, self.clip_encoder, images_nhwc=img16)
             clip8 = clip_loss(img8[..., :3].permute(0, 3, 1, 2), text, self.clip_encoder, images_nhwc=img8)
         # KL (t2i_moe_gan.py:846, :1367-1376, :1402-1404)
-        kl2 = torch.stack(kl2s)
+        kb = self.ge.last_klbuf  # the forward's [blocks, 2] KL buffer, whose rows kl2s are
+        kl2 = kb if kb is not None and kb.shape[0] == len(kl2s) else torch.stack(kl2s)
         kl_coef = torch.empty(len(kl2s), device=self.dev)
         kl_total = torch.empty(1, device=self.dev)
         ops.kl_coefs(kl2, len(kl2s), eff_kl_weight, kl_coef, kl_total)
