@@ -132,7 +132,7 @@ void mg_set_error(const std::string& msg);
 int mg_check_launch(const char* what);
 // Tuning overrides (0 = automatic), set through mg_set_tuning for A/B measurements.
 enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, MG_TUNE_GEMM_TILE = 3,
-       MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_XCD = 6 /* 0 none, 1 all, 2 split-K */, MG_TUNE_WGRAD_MODE = 7,
+       MG_TUNE_WGRAD_SPLITS = 4, MG_TUNE_NO_SLABS = 5, MG_TUNE_XCD = 6 /* 0 auto (= all), 1 all, 2 split-K, 3 none */, MG_TUNE_WGRAD_MODE = 7,
        MG_TUNE_WARP_LDS = 8, MG_TUNE_SHORTK = 9, MG_TUNE_ATOMIC_BLOCKS = 10, MG_TUNE_DETERMINISTIC = 11,
        MG_TUNE_S1_OFF = 12,  // 1: weight gradients of stride-1 convs through the generic LdMCConv (A/B)
        MG_TUNE_D0_STORE = 13,  // mg_d0_fwd output path: 0 automatic, 1 straight from the accumulators, 2 LDS-staged rows

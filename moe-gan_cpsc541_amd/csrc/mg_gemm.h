@@ -1291,11 +1291,12 @@ inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, in
   dim3 grid(gx, cdiv(N, BN), gz);
   EP e2 = ep;
   e2.vec_ok = e2.host_vec_ok() ? 1 : 0;
-  // XCD-aware order (gemm_kernel), A/B only: tuning slot MG_TUNE_XCD 1 every launch (dense or grouped), 2 split-K
-  // launches.  Measured neutral-to-worse on the short-K token projections and the expert GEMMs (their row tiles
-  // re-read per column tile already hit in L2: profiles/round4_xcd_probe.txt), so off by default.
+  // XCD-aware order (gemm_kernel): tuning slot MG_TUNE_XCD 0 (default) / 1 every launch (dense or grouped), 2 split-K
+  // launches only, 3 none.  Round 4 measured it neutral-to-worse in isolation (profiles/round4_xcd_probe.txt); in
+  // the round-5 step it is a steady win: C2 8.51 / 8.51 -> 8.39 / 8.39 ms, C5 11.21 -> 11.02 ms (same-box A/B,
+  // tools/gpu.sh tune=6=0 / tune=6=1), so on by default.
   const int xcd = g_mg_tune[MG_TUNE_XCD];
-  if (grp.mode == 0 || grp.mode == 1) grp.swz = xcd == 3 ? 0 : xcd;
+  if (grp.mode == 0 || grp.mode == 1) grp.swz = xcd == 0 ? 1 : xcd == 3 ? 0 : xcd;
   // grouped weight gradients (mode 2): on by default (slot value 3 turns it off).  Their (group, K split) slices
   // are read by every output tile of the slice; in dispatch order those tiles land on different XCDs, and the
   // PMC passes showed the narrow operand fetched once per tile (a 16x16 block's gW1 read 270 MB for 168 MB of

@@ -13,10 +13,10 @@ namespace {
 
 constexpr Grouping kNoGroup{0, 1, nullptr, nullptr, 0};
 // plain (ungrouped) launch with the tuned XCD tile order (MG_TUNE_XCD), for the direct split-K slab launches
-inline Grouping xcd_group() {
+inline Grouping xcd_group() {  // XCD-aware block order (gemm_kernel): on unless tuning slot MG_TUNE_XCD says otherwise
   Grouping g = kNoGroup;
   const int x = g_mg_tune[MG_TUNE_XCD];
-  g.swz = x == 3 ? 0 : x;
+  g.swz = x == 0 ? 1 : x == 3 ? 0 : x;
   return g;
 }
 
