@@ -648,13 +648,23 @@ template <> struct Tile<float> { static constexpr int BK = 32, PADK = 4, PADM = 
 
 // K step of a GEMM instantiation: X3 (fp32 operands multiplied as split bf16, hi*hi + hi*lo + lo*hi) stages its
 // tiles as bf16 images, so it takes the bf16 step
-template <typename T, bool X3> constexpr int tile_bk() { return X3 ? Tile<bf16_t>::BK : Tile<T>::BK; }
+// MG_BK_SMALL: the K step of bf16 tiles of at most 64 x 64 outputs (A/B build switch; 64 = the common step).  A
+// 128-deep step doubles the bytes each of those latency-bound blocks keeps in flight per barrier.
+#ifndef MG_BK_SMALL
+#define MG_BK_SMALL 64
+#endif
+template <typename T, bool X3, int BM = 128, int BN = 128> constexpr int tile_bk() {
+  return X3 ? Tile<bf16_t>::BK : (sizeof(T) == 2 && BM * BN <= 64 * 64) ? MG_BK_SMALL : Tile<T>::BK;
+}
+// the largest K step any bf16 tile uses (the implicit-conv loaders' "one tap per K step" test needs Cin >= it)
+template <typename T> constexpr int max_tile_bk() { return tile_bk<T, false, 64, 64>() > Tile<T>::BK ? tile_bk<T, false, 64, 64>() : Tile<T>::BK; }
 
 template <typename T> MG_DEV constexpr int mc_swz(int k) { return sizeof(T) == 2 ? ((k >> 3) & 1) << 4 : 0; }
 // KC image element offset of (row r, k) for bf16: 16-B chunk (k / 8) stored at chunk (k / 8) ^ (r & 7)
 // of an unpadded 128-B row -- conflict-free ds_read_b128 fragment reads and ds_write_b128 stores.
 template <typename T> MG_DEV constexpr int kc_off(int r, int k, int ldk) {
-  return sizeof(T) == 2 ? r * ldk + ((((k >> 3) ^ (r & 7))) << 3) + (k & 7) : r * ldk + k;
+  // (a 256-B row -- a 128-deep step -- swizzles its 16 chunks by row & 15: rows 256 B apart share their banks)
+  return sizeof(T) == 2 ? r * ldk + ((((k >> 3) ^ (r & ((ldk >> 3) - 1) & 15))) << 3) + (k & 7) : r * ldk + k;
 }
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
@@ -779,7 +789,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   typedef typename VecOf<T>::type vec_t;
   // LT: element type of the LDS images (X3: bf16 hi / lo images of the fp32 operands, bf16 tile geometry)
   typedef typename std::conditional<X3, bf16_t, T>::type LT;
-  constexpr int TBK = tile_bk<T, X3>();
+  constexpr int TBK = tile_bk<T, X3, BM, BN>();
   constexpr int LDK = TBK + Tile<LT>::PADK;
   constexpr int LDA = A_KC ? LDK : BM + Tile<LT>::PADM;
   constexpr int LDB = B_KC ? LDK : BN + Tile<LT>::PADM;
@@ -1108,7 +1118,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 // TAG only names the instantiation (1 = MoE expert GEMMs) so profiles can attribute its dispatches.
 template <typename T, int BM, int BN, bool A_KC, bool B_KC, class AL, class BL, class EP, int TAG = 0, bool X3 = false>
 __global__ __launch_bounds__(NTHREADS) void gemm_kernel(AL A, BL B, EP ep, int M, int N, int K, int kchunk, Grouping grp) {
-  constexpr int TBK = tile_bk<T, X3>();
+  constexpr int TBK = tile_bk<T, X3, BM, BN>();
   // ---- resolve tile / group ----
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (((grp.mode == 0 || grp.mode == 1) && grp.swz && (grp.swz == 1 || gridDim.z > 1)) || (grp.mode == 2 && grp.swz)) {
@@ -1281,7 +1291,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_splitk_fused_kernel(AL A, BL B,
 template <typename T, int BM, int BN, bool A_KC, bool B_KC, int TAG = 0, bool X3 = false, class AL, class BL, class EP>
 inline void launch_gemm(const AL& A, const BL& B, const EP& ep, int M, int N, int K, int splits, Grouping grp,
                         int max_tiles_m, hipStream_t st) {
-  constexpr int TBK = tile_bk<T, X3>();
+  constexpr int TBK = tile_bk<T, X3, BM, BN>();
   int kchunk = K;
   if (grp.mode != 2 && splits > 1) kchunk = ((K + splits - 1) / splits + TBK - 1) / TBK * TBK;
   if (grp.mode != 2) splits = (K + kchunk - 1) / kchunk;

@@ -109,7 +109,7 @@ void run_plain_tiles(int a_kc, int b_kc, int M, int N, int K, const void* A, int
 template <typename T, typename TO, bool X3 = false>
 bool run_splitk_slabs(int a_kc, int b_kc, int M, int N, int K, const void* A, int64_t lda, const void* B,
                       int64_t ldb, void* C, int64_t ldc, const mg_epilogue* e, hipStream_t st, int want_splits = 0) {
-  constexpr int TBK = tile_bk<T, X3>();
+  constexpr int TBK = tile_bk<T, X3, 64, 64>();
   int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
   if (a_xf(e)) return false;
   int splits;
@@ -278,7 +278,7 @@ int run_batch(int n, const mg_gemm_desc* d, hipStream_t st) {
     // blocks.  Opt-in (tuning slot 21 = block target): split K into fp32 slabs, then one batched reduction applies
     // each real epilogue.  The batched GEMMs halve (12.9 -> 7.1 us average) but the reduction launches cost what
     // that saves: 8.844 / 8.826 ms per step with / without at 512 blocks (same box, three rounds), so off.
-    constexpr int TBK = tile_bk<T, X3>();
+    constexpr int TBK = tile_bk<T, X3, 64, 64>();
     const int bs = g_mg_tune[MG_TUNE_BATCH_SPLIT];
     int S = 1;
     if (bs > 1) {
@@ -384,7 +384,7 @@ void run_conv(const void* x, int B, int H, int W, int Cin, const void* wpack, in
 template <typename T, typename TO, bool SC, int BM, int BN>
 bool conv_slabs_t(const void* x, int B, int H, int W, int Cin, const void* wpack, int Cout, int KH, int KW,
                   int stride, int pad, const float* sc, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
-  constexpr int TBK = Tile<T>::BK;
+  constexpr int TBK = tile_bk<T, false, BM, BN>();
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int M = B * OH * OW, K = KH * KW * Cin;
   int64_t tiles = (int64_t)cdiv(M, BM) * cdiv(Cout, BN);
@@ -440,7 +440,7 @@ void run_conv_tiles(const void* x, int B, int H, int W, int Cin, const void* wpa
         mg_conv3_direct(x, B, H, Cin, wpack, Cout, e, y, ldy, std::is_same<TO, float>::value ? MG_F32 : MG_BF16, st))
       return;
   }
-  const bool small_c = Cin < Tile<T>::BK;  // a K step spans several taps: per-lane tap decode
+  const bool small_c = Cin < max_tile_bk<T>();  // a K step spans several taps: per-lane tap decode
   if (small_c ? conv_slabs<T, TO, true>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st)
               : conv_slabs<T, TO, false>(x, B, H, W, Cin, wpack, Cout, KH, KW, stride, pad, sc, y, ldy, e, st))
     return;
@@ -546,7 +546,7 @@ inline bool wgrad_s1(int H, int W, int KH, int KW, int stride, int pad, int tbk)
 template <typename T, int BM, int BN, bool XF = false>
 bool run_wgrad_slabs(const void* gy, int64_t ldg, const void* x, int B, int H, int W, int Cin, const float* sc,
                      int Cout, int KH, int KW, int stride, int pad, float* gw, int splits, hipStream_t st) {
-  constexpr int TBK = Tile<T>::BK;
+  constexpr int TBK = tile_bk<T, false, BM, BN>();
   int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   int P = B * OH * OW, N = KH * KW * Cin;
   int kchunk = ((P + splits - 1) / splits + TBK - 1) / TBK * TBK;
@@ -861,11 +861,11 @@ extern "C" int mg_conv2d_dgrad_s2(int dtype, const void* g, int B, int OH, int O
   if (B == 0) return MG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == MG_F32) {
-    if (out_dtype == MG_F32) (Cg < Tile<float>::BK ? run_dgrad_s2<float, float, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<float, float, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
-    else (Cg < Tile<float>::BK ? run_dgrad_s2<float, bf16_t, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<float, bf16_t, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
+    if (out_dtype == MG_F32) (Cg < max_tile_bk<float>() ? run_dgrad_s2<float, float, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<float, float, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
+    else (Cg < max_tile_bk<float>() ? run_dgrad_s2<float, bf16_t, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<float, bf16_t, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
   } else {
-    if (out_dtype == MG_F32) (Cg < Tile<bf16_t>::BK ? run_dgrad_s2<bf16_t, float, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<bf16_t, float, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
-    else (Cg < Tile<bf16_t>::BK ? run_dgrad_s2<bf16_t, bf16_t, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<bf16_t, bf16_t, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
+    if (out_dtype == MG_F32) (Cg < max_tile_bk<bf16_t>() ? run_dgrad_s2<bf16_t, float, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<bf16_t, float, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
+    else (Cg < max_tile_bk<bf16_t>() ? run_dgrad_s2<bf16_t, bf16_t, true>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st) : run_dgrad_s2<bf16_t, bf16_t, false>(g, B, OH, OW, Cg, wcls, Cin, out, ldo, ep, st));
   }
   return mg_check_launch("mg_conv2d_dgrad_s2");
 }
