@@ -214,7 +214,7 @@ int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngroups, const 
    gX[r] = gP[r] W1_g ([total_rows, C] bf16), and gb1[g] (fp32 [ngroups, Hd], accumulated; NULL skips it) +=
    sum over the group's rows of gP (the bf16 values), folded in a fixed order.  gP and gX are bit-identical to
    mg_gemm_grouped (gG x W2 with the GELU' epilogue, then gP x W1).  bf16, C = 128 or 256 (256: 144 KiB of LDS,
-   one block per CU, gfx950), Hd % 64 == 0; gb2 (fp32 [ngroups, C], accumulated; NULL skips it) += the column
+   one block per CU, gfx950), Hd % 128 == 0; gb2 (fp32 [ngroups, C], accumulated; NULL skips it) += the column
    sums of gG over the group's rows (the layer-2 bias gradient, from the gG tile the pass holds in LDS, per-tile
    partial rows folded in tile order); W1 [G, Hd, C],
    W2 [G, C, Hd]; grid = max_tiles blocks of 128 rows. */

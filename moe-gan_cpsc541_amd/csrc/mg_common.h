@@ -136,7 +136,7 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_WARP_LDS = 8, MG_TUNE_SHORTK = 9, MG_TUNE_ATOMIC_BLOCKS = 10, MG_TUNE_DETERMINISTIC = 11,
        MG_TUNE_S1_OFF = 12,  // 1: weight gradients of stride-1 convs through the generic LdMCConv (A/B)
        MG_TUNE_D0_STORE = 13,  // mg_d0_fwd output path: 0 automatic, 1 straight from the accumulators, 2 LDS-staged rows
-       MG_TUNE_FFN_BWD_OCC = 14,  // mg_moe_ffn_bwd: 0 automatic (one block per CU, 256 VGPRs), 2 two blocks (128 VGPRs)
+       MG_TUNE_FFN_BWD_OCC = 14,  // mg_moe_ffn_bwd: 0 automatic (one block per CU, 256 VGPRs, 128-unit chunks), 2 two blocks (128 VGPRs), 3 64-unit chunks
        MG_TUNE_WIDE_WGRAD = 15,   // 1: linear-layer weight gradients through the generic split-K GEMM (A/B), 2: wide kernel on every eligible shape
        MG_TUNE_NARROW = 16,  // the 32-channel 3x3 convs (offset heads) through the implicit GEMM: 1 all, 2 fwd, 3 dgrad, 4 wgrad
        MG_TUNE_NARROW_BLOCKS = 17,  // mg_narrow.hip grid target (blocks): 0 automatic

@@ -223,16 +223,16 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 // q = 0..3, per lane half) hit 8 distinct bank octets -- the unpadded pitches (64 and 128 bf16: 32 and 64 dwords) put
 // k-rows q and q + 2 (W2) / all four q (W1) on one octet, 2- and 4-way conflicts.  C = 256 keeps W1 unpadded
 // (the padded images would exceed the 160 KiB of LDS).
-template <int C> struct BwdPitch {
-  static constexpr int W2 = FHC + 32;
+template <int C, int FH> struct BwdPitch {
+  static constexpr int W2 = FH + 32;
   static constexpr int W1 = C == 128 ? C + 32 : C;
 };
-template <int C>
+template <int C, int FH>
 struct FfnBwdSmem {
   bf16_t gs[FBM * C];               // gG tile, KC image (A of GEMM1); the bf16 gX tile at the end
-  bf16_t w2[C * BwdPitch<C>::W2];   // W2_e[:, chunk] as an MC image [c][h] (k-rows c); column sums reuse it
-  bf16_t w1[FHC * BwdPitch<C>::W1]; // W1_e[chunk, :] as an MC image [h][c] (k-rows h)
-  bf16_t hs[FBM * FHC];             // gP chunk, KC image (A of GEMM2)
+  bf16_t w2[C * BwdPitch<C, FH>::W2];   // W2_e[:, chunk] as an MC image [c][h] (k-rows c); column sums reuse it
+  bf16_t w1[FH * BwdPitch<C, FH>::W1]; // W1_e[chunk, :] as an MC image [h][c] (k-rows h)
+  bf16_t hs[FBM * FH];              // gP chunk, KC image (A of GEMM2)
 };
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
@@ -253,12 +253,12 @@ MG_DEV bf16x8_t mc_frag(const bf16_t* img, int ld, int kr0, int c0, int lane) {
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
-template <int C>
+template <int C, int FH>
 __device__ __forceinline__ void ffn_bwd_body(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
     bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
-  __shared__ FfnBwdSmem<C> sm;
+  __shared__ FfnBwdSmem<C, FH> sm;
   const int t = blockIdx.x;
   int g = -1;
   for (int i = 0; i < ngroups; ++i)
@@ -287,7 +287,8 @@ __device__ __forceinline__ void ffn_bwd_body(
     if (r < nrows) val = *reinterpret_cast<const u16x8_t*>(gG + (int64_t)(r0 + r) * C + k);
     *reinterpret_cast<u16x8_t*>(sm.gs + kci<FBM>(r, k)) = val;
   }
-  constexpr int WV = FHC * C / 8 / FT;
+  constexpr int WV = FH * C / 8 / FT;
+  constexpr int FN1 = FH / 32;  // GEMM1 hidden-unit fragments per wave (FH / 2 units)
   constexpr int FN2 = C / 32;  // GEMM2 column fragments per wave (C / 2 columns)
   f32x4_t acc2[2][FN2];
 #pragma unroll
@@ -298,12 +299,12 @@ __device__ __forceinline__ void ffn_bwd_body(
   // register ring (distance one chunk): the next chunk's weights are loaded right after this chunk's are stored to
   // LDS, and its GELU' operand right after this chunk's epilogue used it, so both latencies overlap the products
   u16x8_t w1r[WV], w2r[WV];
-  u16x4_t pre_r[2][2];
+  u16x4_t pre_r[2][FN1];
   auto load_w = [&](int h0) {
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
       const int v = tid + j * FT;
-      const int c = v / (FHC / 8), q = (v % (FHC / 8)) * 8;   // W2_e[c][h0 + q .. +8]
+      const int c = v / (FH / 8), q = (v % (FH / 8)) * 8;   // W2_e[c][h0 + q .. +8]
       w2r[j] = *reinterpret_cast<const u16x8_t*>(W2g + (int64_t)c * Hd + h0 + q);
       const int hh = v / (C / 8), c1 = (v % (C / 8)) * 8;     // W1_e[h0 + hh][c1 .. +8]
       w1r[j] = *reinterpret_cast<const u16x8_t*>(W1g + (int64_t)(h0 + hh) * C + c1);
@@ -313,52 +314,52 @@ __device__ __forceinline__ void ffn_bwd_body(
 #pragma unroll
     for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < 2; ++fn) {
+      for (int fn = 0; fn < FN1; ++fn) {
         const int row = wm * 32 + fm * 16 + fr;
-        const int col = wn * 32 + fn * 16 + 4 * (lane >> 4);
+        const int col = wn * (FH / 2) + fn * 16 + 4 * (lane >> 4);
         pre_r[fm][fn] = row < nrows ? *reinterpret_cast<const u16x4_t*>(preb + (int64_t)row * Hd + h0 + col) : u16x4_t(0);
       }
   };
   load_w(0);
   load_pre(0);
-  for (int h0 = 0; h0 < Hd; h0 += FHC) {
+  for (int h0 = 0; h0 < Hd; h0 += FH) {
     __syncthreads();  // the previous chunk's GEMM2 / column sums are done with w1, w2 and hs
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
       const int v = tid + j * FT;
-      const int c = v / (FHC / 8), q = (v % (FHC / 8)) * 8;
-      *reinterpret_cast<u16x8_t*>(sm.w2 + mci(c, q, BwdPitch<C>::W2)) = w2r[j];
+      const int c = v / (FH / 8), q = (v % (FH / 8)) * 8;
+      *reinterpret_cast<u16x8_t*>(sm.w2 + mci(c, q, BwdPitch<C, FH>::W2)) = w2r[j];
       const int hh = v / (C / 8), c1 = (v % (C / 8)) * 8;
-      *reinterpret_cast<u16x8_t*>(sm.w1 + mci(hh, c1, BwdPitch<C>::W1)) = w1r[j];
+      *reinterpret_cast<u16x8_t*>(sm.w1 + mci(hh, c1, BwdPitch<C, FH>::W1)) = w1r[j];
     }
     __syncthreads();
-    if (h0 + FHC < Hd) load_w(h0 + FHC);
-    // ---- GEMM1: gH[128 x 64] = gG[128 x C] . W2c[C x 64]; wave (wm, wn): rows wm*32, hidden units wn*32 ----
-    f32x4_t acc1[2][2];
+    if (h0 + FH < Hd) load_w(h0 + FH);
+    // ---- GEMM1: gH[128 x FH] = gG[128 x C] . W2c[C x FH]; wave (wm, wn): rows wm*32, hidden units wn*FH/2 ----
+    f32x4_t acc1[2][FN1];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc1[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < FN1; ++b) acc1[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
     for (int k0 = 0; k0 < C; k0 += 32) {
-      bf16x8_t a[2], b[2];
+      bf16x8_t a[2], b[FN1];
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm) a[fm] = frag(sm.gs, kci<FBM>(wm * 32 + fm * 16 + fr, k0 + fk));
 #pragma unroll
-      for (int fn = 0; fn < 2; ++fn) b[fn] = mc_frag(sm.w2, BwdPitch<C>::W2, k0, wn * 32 + fn * 16, lane);
+      for (int fn = 0; fn < FN1; ++fn) b[fn] = mc_frag(sm.w2, BwdPitch<C, FH>::W2, k0, wn * (FH / 2) + fn * 16, lane);
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
-        for (int fn = 0; fn < 2; ++fn)  // transposed product: lane holds 4 consecutive hidden units of one row
+        for (int fn = 0; fn < FN1; ++fn)  // transposed product: lane holds 4 consecutive hidden units of one row
           acc1[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[fn], a[fm], acc1[fm][fn], 0, 0, 0);
     }
     // ---- gP = gH * GELU'(Pre): HBM (8-B runs) and the LDS image for GEMM2 ----
 #pragma unroll
     for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < 2; ++fn) {
+      for (int fn = 0; fn < FN1; ++fn) {
         const int row = wm * 32 + fm * 16 + fr;
-        const int col = wn * 32 + fn * 16 + 4 * (lane >> 4);
+        const int col = wn * (FH / 2) + fn * 16 + 4 * (lane >> 4);
         const u16x4_t pv = pre_r[fm][fn];
         u16x4_t gv;
 #pragma unroll
@@ -370,37 +371,37 @@ __device__ __forceinline__ void ffn_bwd_body(
         if (row < nrows) *reinterpret_cast<u16x4_t*>(gpb + (int64_t)row * Hd + h0 + col) = gv;
         *reinterpret_cast<u16x4_t*>(sm.hs + kci<FBM>(row, col)) = gv;  // rows past the group: gG = 0, so gP = 0
       }
-    if (h0 + FHC < Hd) load_pre(h0 + FHC);
+    if (h0 + FH < Hd) load_pre(h0 + FH);
     __syncthreads();  // hs complete; every GEMM1 read of w2 done
     // column sums of the bf16 gP chunk (what the weight gradient reads): 8 row groups of 16 per column, in order,
     // into the free w2 buffer
-    float* red = reinterpret_cast<float*>(sm.w2);  // [8 row groups][64 columns]
-    {
-      const int col = tid & (FHC - 1), rg = tid >> 6;
+    float* red = reinterpret_cast<float*>(sm.w2);  // [8 row groups][FH columns]
+    for (int col = tid & 63; col < FH; col += 64) {
+      const int rg = tid >> 6;
       float cs = 0.f;
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) cs += bf2f(sm.hs[kci<FBM>(rg * 16 + rr, col)]);
-      red[rg * FHC + col] = cs;
+      red[rg * FH + col] = cs;
     }
-    // ---- GEMM2: gX[128 x C] += hs[128 x 64] . W1c[64 x C]; wave (wm, wn): rows wm*32, cols wn*C/2 ----
+    // ---- GEMM2: gX[128 x C] += hs[128 x FH] . W1c[FH x C]; wave (wm, wn): rows wm*32, cols wn*C/2 ----
 #pragma unroll 1
-    for (int k0 = 0; k0 < FHC; k0 += 32) {
+    for (int k0 = 0; k0 < FH; k0 += 32) {
       bf16x8_t a[2];
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm) a[fm] = frag(sm.hs, kci<FBM>(wm * 32 + fm * 16 + fr, k0 + fk));
 #pragma unroll
       for (int fn = 0; fn < FN2; ++fn) {
-        const bf16x8_t b = mc_frag(sm.w1, BwdPitch<C>::W1, k0, wn * (C / 2) + fn * 16, lane);
+        const bf16x8_t b = mc_frag(sm.w1, BwdPitch<C, FH>::W1, k0, wn * (C / 2) + fn * 16, lane);
 #pragma unroll
         for (int fm = 0; fm < 2; ++fm)
           acc2[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fm], b, acc2[fm][fn], 0, 0, 0);
       }
     }
     __syncthreads();  // red complete
-    if (tid < FHC) {
+    if (tid < FH) {
       float cs = 0.f;
 #pragma unroll
-      for (int rg = 0; rg < FT / FHC; ++rg) cs += red[rg * FHC + tid];
+      for (int rg = 0; rg < FT / 64; ++rg) cs += red[rg * FH + tid];
       partb[h0 + tid] = cs;
     }
   }
@@ -450,14 +451,14 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
     bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
-  ffn_bwd_body<C>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2);
+  ffn_bwd_body<C, 64>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2);
 }
-template <int C>
+template <int C, int FH>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_moe_ffn_bwd_w2(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
     bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
-  ffn_bwd_body<C>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2);
+  ffn_bwd_body<C, FH>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2);
 }
 
 // gb1[g][h] += sum over the tiles of group g (tile order) of part[tile][h]: 64 columns x 4 tile lanes per block,
@@ -517,7 +518,7 @@ extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngro
                               const void* W2, void* gP, void* gX, float* gb1, float* gb2, void* stream) {
   MG_REQUIRE(dtype == MG_BF16, "bf16 only");
   MG_REQUIRE(C == 128 || C == 256, "C must be 128 or 256");
-  MG_REQUIRE(Hd > 0 && Hd % FHC == 0, "Hd must be a multiple of 64");
+  MG_REQUIRE(Hd > 0 && Hd % 128 == 0, "Hd must be a multiple of 128");
   MG_REQUIRE(ngroups >= 1 && ngroups <= 64, "1 <= ngroups <= 64");
   MG_REQUIRE(mg_al16(gG) && mg_al16(pre) && mg_al16(W1) && mg_al16(W2) && mg_al16(gP) && mg_al16(gX),
              "operands must be 16-byte aligned");
@@ -529,14 +530,17 @@ extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngro
   float* part2 = gb2 ? part + (size_t)max_tiles * Hd : nullptr;
   // one block per CU either way (92 / 160 KiB of LDS at C = 128 / 256): the 256-VGPR form unless A/B-tuned
   const bool one_block = C == 256 || g_mg_tune[MG_TUNE_FFN_BWD_OCC] != 2;
-#define L_(K, CC)                                                                                                    \
-  hipLaunchKernelGGL(K<CC>, dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),                  \
+#define L_(K, ...)                                                                                                   \
+  hipLaunchKernelGGL((K<__VA_ARGS__>), dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),       \
                      reinterpret_cast<const bf16_t*>(pre), ngroups, row_off, tile_off, Hd,                            \
                      reinterpret_cast<const bf16_t*>(W1), reinterpret_cast<const bf16_t*>(W2),                        \
                      reinterpret_cast<bf16_t*>(gP), reinterpret_cast<bf16_t*>(gX), part, part2)
-  if (C == 256) L_(k_moe_ffn_bwd_w2, 256);
-  else if (one_block) L_(k_moe_ffn_bwd_w2, 128);
-  else L_(k_moe_ffn_bwd, 128);
+  // C = 128: 128-unit hidden chunks by default (half the chunk barriers, twice the MFMA work between them; 144 KiB of
+  // LDS); tuning slot MG_TUNE_FFN_BWD_OCC = 3 keeps the 64-unit chunks of rounds 4-5 (A/B)
+  if (C == 256) L_(k_moe_ffn_bwd_w2, 256, 64);
+  else if (!one_block) L_(k_moe_ffn_bwd, 128);
+  else if (g_mg_tune[MG_TUNE_FFN_BWD_OCC] == 3) L_(k_moe_ffn_bwd_w2, 128, 64);
+  else L_(k_moe_ffn_bwd_w2, 128, 128);
 #undef L_
   if (gb1) hipLaunchKernelGGL(k_ffn_bias_fold, dim3(cdiv(Hd, 64), ngroups), dim3(256), 0, st, part, tile_off, Hd, gb1);
   if (gb2) hipLaunchKernelGGL(k_ffn_bias_fold, dim3(cdiv(C, 64), ngroups), dim3(256), 0, st, part2, tile_off, C, gb2);
