@@ -31,52 +31,18 @@ __global__ void k_reparam(const float* __restrict__ mu, const float* __restrict_
 
 MG_DEV float teff_of(const float* temp, float anneal) { return fminf(fmaxf(temp[0] * anneal, 0.5f), 5.f); }
 
-// TEAM lanes per token; block = 256 threads = 256/TEAM tokens
-template <typename T, int E>
-__global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int C, const float* __restrict__ Wfc,
-                             const float* __restrict__ Lt, int lgHW, const float* __restrict__ temp, float anneal,
-                             int k, int eval_mode, float* __restrict__ probs, float* __restrict__ zlog,
-                             int* __restrict__ topi, float* __restrict__ gate) {
-  constexpr int TEAM = 8;
-  constexpr int VEC = VecOf<T>::N;
-  // Wfc [C][E] in LDS with element e of row c at (e + c / VEC) mod E: the 8 lanes of a team read rows
-  // VEC apart, which the rotation puts on distinct banks
-  extern __shared__ float wsm[];
-  for (int i = threadIdx.x; i < C * E; i += blockDim.x) {
-    const int c = i / E, e = i - c * E;
-    wsm[c * E + ((e + c / VEC) & (E - 1))] = Wfc[i];
-  }
-  __syncthreads();
-  int team = threadIdx.x / TEAM, tl = threadIdx.x % TEAM;
-  // grid-stride over tokens: each block stages Wfc once for many tokens
-  for (int t = blockIdx.x * (blockDim.x / TEAM) + team; t - team < Tn; t += gridDim.x * (blockDim.x / TEAM)) {
-  bool ok = t < Tn;
-  float acc[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) acc[e] = 0.f;
-  if (ok) {
-    for (int c0 = tl * VEC; c0 < C; c0 += TEAM * VEC) {
-      auto v = *reinterpret_cast<const typename VecOf<T>::type*>(tok + (int64_t)t * ld + c0);
-      const int rot = c0 / VEC;
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        float x;
-        if constexpr (sizeof(T) == 4) x = v[j]; else x = bf2f(v[j]);
-        const float* wr = wsm + (c0 + j) * E;
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] += x * wr[(e + rot) & (E - 1)];
-      }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    acc[e] += __shfl_xor(acc[e], 1, 64);
-    acc[e] += __shfl_xor(acc[e], 2, 64);
-    acc[e] += __shfl_xor(acc[e], 4, 64);
-  }
-  // softmax / top-k spread over the team: after the butterfly every lane holds all E logits; lane tl owns
-  // experts tl, tl + 8, ... and the team reduces max / sums / arg-max with shuffles, so probs and zlog leave as
-  // 32-byte runs per token instead of one lane's scalar stores (the team-serial epilogue ran at ~9 % of HBM)
+constexpr int RTEAM = 8;  // lanes per token in the router's softmax / top-k
+
+// Softmax / top-k of one token spread over its team of RTEAM lanes: lane tl owns experts tl, tl + 8, ... and
+// holds their raw logits x . Wfc in araw[]; the team reduces max / sums / arg-max with shuffles, so probs and
+// zlog leave as 32-byte runs per token instead of one lane's scalar stores (the team-serial epilogue ran at
+// ~9 % of HBM).  Every lane of the wave calls it (shuffles); ok = false for a team past the last token.
+template <int E>
+MG_DEV void router_token(const float* araw, bool ok, int t, int tl, int lgHW, const float* __restrict__ Lt,
+                         const float* __restrict__ temp, float anneal, int k, int eval_mode,
+                         float* __restrict__ probs, float* __restrict__ zlog, int* __restrict__ topi,
+                         float* __restrict__ gate) {
+  constexpr int TEAM = RTEAM;
   constexpr int NE = E >= TEAM ? E / TEAM : 1;
   const int b = (ok ? t : 0) >> lgHW;
   const float te = teff_of(temp, anneal);
@@ -86,11 +52,7 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
   for (int j = 0; j < NE; ++j) {
     const int e = tl + TEAM * j;
     const bool own = e < E;
-    float a = 0.f;
-#pragma unroll
-    for (int q = 0; q < E; ++q)
-      if (q == e) a = acc[q];
-    z[j] = own && ok ? (a + Lt[(int64_t)b * E + e]) / te : 0.f;
+    z[j] = own && ok ? (araw[j] + Lt[(int64_t)b * E + e]) / te : 0.f;
     p[j] = own ? clampf(z[j], -20.f, 20.f) : -INFINITY;
     mx = fmaxf(mx, p[j]);
   }
@@ -178,7 +140,182 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
       }
     }
   }
+}
+
+// TEAM lanes per token; block = 256 threads = 256/TEAM tokens
+template <typename T, int E>
+__global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int C, const float* __restrict__ Wfc,
+                             const float* __restrict__ Lt, int lgHW, const float* __restrict__ temp, float anneal,
+                             int k, int eval_mode, float* __restrict__ probs, float* __restrict__ zlog,
+                             int* __restrict__ topi, float* __restrict__ gate) {
+  constexpr int TEAM = RTEAM;
+  constexpr int VEC = VecOf<T>::N;
+  // Wfc [C][E] in LDS with element e of row c at (e + c / VEC) mod E: the 8 lanes of a team read rows
+  // VEC apart, which the rotation puts on distinct banks
+  extern __shared__ float wsm[];
+  for (int i = threadIdx.x; i < C * E; i += blockDim.x) {
+    const int c = i / E, e = i - c * E;
+    wsm[c * E + ((e + c / VEC) & (E - 1))] = Wfc[i];
+  }
+  __syncthreads();
+  int team = threadIdx.x / TEAM, tl = threadIdx.x % TEAM;
+  // grid-stride over tokens: each block stages Wfc once for many tokens
+  for (int t = blockIdx.x * (blockDim.x / TEAM) + team; t - team < Tn; t += gridDim.x * (blockDim.x / TEAM)) {
+  bool ok = t < Tn;
+  float acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = 0.f;
+  if (ok) {
+    for (int c0 = tl * VEC; c0 < C; c0 += TEAM * VEC) {
+      auto v = *reinterpret_cast<const typename VecOf<T>::type*>(tok + (int64_t)t * ld + c0);
+      const int rot = c0 / VEC;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        float x;
+        if constexpr (sizeof(T) == 4) x = v[j]; else x = bf2f(v[j]);
+        const float* wr = wsm + (c0 + j) * E;
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += x * wr[(e + rot) & (E - 1)];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    acc[e] += __shfl_xor(acc[e], 1, 64);
+    acc[e] += __shfl_xor(acc[e], 2, 64);
+    acc[e] += __shfl_xor(acc[e], 4, 64);
+  }
+  constexpr int NE = E >= TEAM ? E / TEAM : 1;
+  float araw[NE];
+#pragma unroll
+  for (int j = 0; j < NE; ++j) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < E; ++q)
+      if (q == tl + TEAM * j) v = acc[q];
+    araw[j] = v;
+  }
+  router_token<E>(araw, ok, t, tl, lgHW, Lt, temp, anneal, k, eval_mode, probs, zlog, topi, gate);
   }  // token loop
+}
+
+// Router logits on the matrix cores (bf16 tokens, E >= 8): a wave computes z[16 x E] = tok[16 x C] . Wfc[C x E]
+// for each of its (up to RTPW) 16-token tiles with v_mfma_f32_16x16x32_bf16, Wfc split into bf16 hi + lo halves
+// (w = hi + lo + O(2^-18 |w|), below the fp32 rounding of a C-term sum; tokens are bf16 already), then each tile
+// goes through LDS to the team softmax / top-k.  The team kernel above spends one lane-FMA plus one LDS read per
+// token-channel-expert and at few tokens per layer (4x4: 4096 tokens of C = 512) is latency bound at ~55 us;
+// here the contraction is C/32 x EP/16 x 2 MFMAs per 16 tokens.
+// LDS: Wfc^T in channel chunks of RKC as hi / lo bf16 [EP][RKC + 8] (rows 16 B apart mod 128 B, so the 16
+// columns of a B fragment read distinct banks) + a [16][EP + 1] fp32 logit tile per wave: <= 42 KiB at E = 32.
+constexpr int RKC = 256;  // channels per staged chunk
+constexpr int RTPW = 4;   // most tiles per wave
+template <int E>
+__global__ __launch_bounds__(256) void k_router_fwd_mfma(const bf16_t* __restrict__ tok, int64_t ld, int Tn, int C,
+                                                         int tpw, const float* __restrict__ Wfc,
+                                                         const float* __restrict__ Lt, int lgHW,
+                                                         const float* __restrict__ temp, float anneal, int k,
+                                                         int eval_mode, float* __restrict__ probs,
+                                                         float* __restrict__ zlog, int* __restrict__ topi,
+                                                         float* __restrict__ gate) {
+  constexpr int EP = E < 16 ? 16 : E;  // experts padded to the 16-column MFMA tile
+  constexpr int NH = EP / 16;
+  constexpr int ZP = EP + 1;
+  constexpr int P = RKC + 8;
+  __shared__ __align__(16) bf16_t whi[EP * P];
+  __shared__ __align__(16) bf16_t wlo[EP * P];
+  __shared__ float ztile[4 * 16 * ZP];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int team = lane / RTEAM, tl = lane % RTEAM;
+  const int ntile = (Tn + 15) / 16;
+  const int tile0 = (blockIdx.x * 4 + wave) * tpw;  // this wave's tiles: tile0 .. tile0 + tpw - 1
+  f32x4_t acc[RTPW][NH];
+#pragma unroll
+  for (int j = 0; j < RTPW; ++j)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc[j][h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < C; c0 += RKC) {
+    const int kc = min(RKC, C - c0);
+    if (c0 > 0) __syncthreads();  // the previous chunk's fragments are read
+    // stage the chunk: float4 runs of Wfc rows, 8 loads in flight per thread (a load-then-store loop is one
+    // L2 round trip per element group)
+    const int n4 = kc * E / 4;
+    const f32x4_t* src = reinterpret_cast<const f32x4_t*>(Wfc + (int64_t)c0 * E);
+    for (int i0 = threadIdx.x; i0 < n4; i0 += 256 * 8) {
+      f32x4_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 256;
+        v[u] = i < n4 ? src[i] : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 256;
+        if (i < n4) {
+          const int c = (i * 4) / E, e0 = (i * 4) % E;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const bf16_t h = f2bf(v[u][q]);
+            whi[(e0 + q) * P + c] = h;
+            wlo[(e0 + q) * P + c] = f2bf(v[u][q] - bf2f(h));
+          }
+        }
+      }
+    }
+    if constexpr (E < EP) {
+      if (c0 == 0)
+        for (int i = threadIdx.x; i < (EP - E) * P; i += 256) {
+          whi[E * P + i] = 0;
+          wlo[E * P + i] = 0;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RTPW; ++j) {
+      const int tile = tile0 + j;
+      if (j < tpw && tile < ntile) {  // wave-uniform
+        // rows past the last token re-read the last token; their logits are never used
+        const bf16_t* arow = tok + (int64_t)min(tile * 16 + fr, Tn - 1) * ld + c0 + fq * 8;
+#pragma unroll 4
+        for (int ks = 0; ks < kc; ks += 32) {
+          const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(arow + ks));
+#pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            const int off = (h * 16 + fr) * P + ks + fq * 8;
+            const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(wlo + off));
+            const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(whi + off));
+            acc[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[j][h], 0, 0, 0);
+            acc[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[j][h], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  float* zw = ztile + wave * 16 * ZP;
+#pragma unroll
+  for (int j = 0; j < RTPW; ++j) {
+    const int tile = tile0 + j;
+    if (j < tpw && tile < ntile) {  // wave-uniform
+      // D[token fq*4 + r][expert h*16 + fr] -> the wave's logit tile -> teams of 8 lanes, 8 tokens per pass
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zw[(fq * 4 + r) * ZP + h * 16 + fr] = acc[j][h][r];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      constexpr int NE = E / RTEAM;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int row = half * 8 + team, t = tile * 16 + row;
+        float araw[NE];
+#pragma unroll
+        for (int q = 0; q < NE; ++q) araw[q] = zw[row * ZP + tl + RTEAM * q];
+        router_token<E>(araw, t < Tn, t, tl, lgHW, Lt, temp, anneal, k, eval_mode, probs, zlog, topi, gate);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
 }
 
 // ---- dispatch: deterministic per-expert position lists ----
@@ -1181,6 +1318,20 @@ extern "C" int mg_router_fwd(int dtype, const void* tok, int64_t ld, int T, int 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int lg = 0;
   while ((1 << lg) < HW) ++lg;
+  if (T <= 0) return 0;
+  if (dtype != MG_F32 && E >= 8 && C % 32 == 0 && ld % 8 == 0 && mg_al16(tok) && mg_al16(Wfc) &&
+      g_mg_tune[MG_TUNE_ROUTER_TEAM] == 0) {
+    // tiles per wave: enough blocks to spread over the CUs (>= 512 where there are tokens for it), then up to
+    // RTPW tiles per wave so each block stages Wfc for more tokens
+    const int ntile = cdiv(T, 16);
+    const int tpw = std::max(1, std::min(RTPW, ntile / (4 * 512)));
+    dim3 gm(cdiv(ntile, 4 * tpw));
+#define L_(EE) hipLaunchKernelGGL((k_router_fwd_mfma<EE>), gm, dim3(256), 0, st, (const bf16_t*)tok, ld, T, C, tpw, \
+                                  Wfc, Lt, lg, temperature, anneal, k, eval_mode, probs, zlog, topi, gate)
+    if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
+#undef L_
+    return mg_check_launch("mg_router_fwd");
+  }
   dim3 grid(std::min(cdiv(T, 32), 1024));
   size_t sm = (size_t)C * E * sizeof(float);
 #define L_(TT, EE) hipLaunchKernelGGL((k_router_fwd<TT, EE>), grid, dim3(256), sm, st, (const TT*)tok, ld, T, C, Wfc, Lt, lg, \

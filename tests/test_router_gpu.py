@@ -52,6 +52,37 @@ def test_router_fwd_across_experts(E, k, dtype):
     assert rel(torch.sort(gate, dim=1).values[clear], torch.sort(gt, dim=1).values.float()[clear]) < 1e-5
 
 
+@pytest.mark.parametrize("T,C,E,k,HW", [(4096 - 5, 512, 32, 4, 16), (65536 + 3, 128, 32, 4, 256),
+                                        (1000, 256, 8, 2, 8), (70000, 128, 16, 2, 1024), (48, 192, 8, 8, 16)])
+def test_router_fwd_mfma_shapes(T, C, E, k, HW):
+    """bf16 router logits on the matrix cores (Wfc as bf16 hi + lo): several channel chunks (C = 512), ragged
+    token counts, several tiles per wave (T > 65536), C not a multiple of the chunk; against fp64 and against the
+    lane-FMA team kernel (tuning slot 24 = 1)."""
+    from moegan_mi import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(T + C + E)
+    B = (T + HW - 1) // HW
+    tok = torch.randn(T, C, device=DEV, generator=g).to(torch.bfloat16)
+    Wfc = torch.randn(C, E, device=DEV, generator=g) * (2.0 / C ** 0.5)
+    Lt = torch.randn(B, E, device=DEV, generator=g)
+    temp = torch.tensor([1.1], device=DEV)
+    probs, zlog, topi, gate = ops.router_fwd(tok, Wfc, Lt, E, k, HW, temp, 1.0)
+    L.call("mg_set_tuning", 24, 1)
+    try:
+        probs_t, zlog_t, topi_t, gate_t = ops.router_fwd(tok, Wfc, Lt, E, k, HW, temp, 1.0)
+    finally:
+        L.call("mg_set_tuning", 24, 0)
+    p, z, ti, gt = ref_router(tok.float(), Wfc, Lt, HW, 1.1, 1.0, k)
+    assert rel(zlog, z) < 1e-5 and rel(zlog, zlog_t) < 1e-5
+    assert rel(probs, p) < 1e-5
+    srt = torch.sort(p, dim=1, descending=True).values
+    clear = (srt[:, k - 1] - srt[:, k]).abs() > 1e-6 if k < E else torch.ones(T, dtype=torch.bool, device=DEV)
+    order = torch.sort(topi.long(), dim=1).values
+    assert torch.equal(order[clear], torch.sort(ti, dim=1).values[clear])
+    assert torch.equal(order[clear], torch.sort(topi_t.long(), dim=1).values[clear])
+    assert clear.float().mean() > 0.95
+    assert rel(torch.sort(gate, dim=1).values[clear], torch.sort(gt, dim=1).values.float()[clear]) < 1e-5
+
+
 @pytest.mark.parametrize("E", [4, 8, 16, 32])
 def test_token_and_feature_grad_across_experts(E):
     g = torch.Generator(device=DEV).manual_seed(100 + E)
