@@ -146,7 +146,8 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_BATCH_SPLIT = 21,  // mg_gemm_batch split-K slabs, > 1: on, that block target (A/B; 0 / 1 off: neutral in the step)
        MG_TUNE_GROUPED_SHORTK = 22,  // grouped expert GEMMs with K <= this on 64^2 tiles (0: 512, -1: never)
        MG_TUNE_SPLITK_FUSED = 23,    // 1: split-K slabs reduced inside the launch (measured slower at C2: off)
-       MG_TUNE_ROUTER_TEAM = 24,     // 1: router logits on the lane-FMA team kernel instead of the MFMA one (A/B)
+       MG_TUNE_ROUTER_TEAM = 24,     // A/B bitmask, lane-FMA forms instead of the MFMA / team ones: 1 router
+                                     // logits, 2 router backward (thread per token), 4 token gradient
        MG_TUNE_COUNT = 25 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 // Deterministic mode (mg_set_tuning(MG_TUNE_DETERMINISTIC, 1)): every reduction that crosses workgroups runs in

@@ -199,19 +199,18 @@ __global__ void k_router_fwd(const T* __restrict__ tok, int64_t ld, int Tn, int 
   }  // token loop
 }
 
-// Router logits on the matrix cores (bf16 tokens, E >= 8): a wave computes z[16 x E] = tok[16 x C] . Wfc[C x E]
-// for each of its (up to RTPW) 16-token tiles with v_mfma_f32_16x16x32_bf16, Wfc split into bf16 hi + lo halves
-// (w = hi + lo + O(2^-18 |w|), below the fp32 rounding of a C-term sum; tokens are bf16 already), then each tile
-// goes through LDS to the team softmax / top-k.  The team kernel above spends one lane-FMA plus one LDS read per
-// token-channel-expert and at few tokens per layer (4x4: 4096 tokens of C = 512) is latency bound at ~55 us;
-// here the contraction is C/32 x EP/16 x 2 MFMAs per 16 tokens.
-// LDS: Wfc^T in channel chunks of RKC as hi / lo bf16 [EP][RKC + 8] (rows 16 B apart mod 128 B, so the 16
-// columns of a B fragment read distinct banks) + a [16][EP + 1] fp32 logit tile per wave: <= 42 KiB at E = 32.
-constexpr int RKC = 256;  // channels per staged chunk
-constexpr int RTPW = 4;   // most tiles per wave
-template <int E>
+// Router logits on the matrix cores (bf16 tokens, E >= 8, C = 128 / 256 / 384 / 512): z[T x E] = tok . Wfc with
+// v_mfma_f32_16x16x32_bf16, Wfc split into bf16 hi + lo halves (w = hi + lo + O(2^-18 |w|), below the fp32
+// rounding of a C-term sum; tokens are bf16 already).  A block takes nt 16-token tiles; its 4 waves split the
+// channels in quarters, each holding its quarter of Wfc as B fragments in registers (read straight from L2, no
+// LDS staging) and loading every A fragment it needs up front, so a block is one load latency, a few MFMAs,
+// one LDS fold of the 4 partial tiles (fixed wave order) and the team softmax / top-k.  The lane-FMA team kernel
+// above spends one FMA plus one LDS read per token-channel-expert and, at few tokens per layer, is latency bound
+// (C5: 40 / 33 / 53 us at 4096 / 16384 / 65536 tokens).
+constexpr int RNT = 4;  // most 16-token tiles per block: NT = 4 / NKS (the A fragments a lane holds)
+template <int E, int NKS>
 __global__ __launch_bounds__(256) void k_router_fwd_mfma(const bf16_t* __restrict__ tok, int64_t ld, int Tn, int C,
-                                                         int tpw, const float* __restrict__ Wfc,
+                                                         int nt, const float* __restrict__ Wfc,
                                                          const float* __restrict__ Lt, int lgHW,
                                                          const float* __restrict__ temp, float anneal, int k,
                                                          int eval_mode, float* __restrict__ probs,
@@ -220,101 +219,77 @@ __global__ __launch_bounds__(256) void k_router_fwd_mfma(const bf16_t* __restric
   constexpr int EP = E < 16 ? 16 : E;  // experts padded to the 16-column MFMA tile
   constexpr int NH = EP / 16;
   constexpr int ZP = EP + 1;
-  constexpr int P = RKC + 8;
-  __shared__ __align__(16) bf16_t whi[EP * P];
-  __shared__ __align__(16) bf16_t wlo[EP * P];
-  __shared__ float ztile[4 * 16 * ZP];
+  constexpr int NT = RNT / NKS;
+  constexpr int ZW = NT * 16 * ZP;  // one wave's partial logits
+  __shared__ float zpart[4 * ZW];   // [wave][token of the block][expert]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int fr = lane & 15, fq = lane >> 4;
-  const int team = lane / RTEAM, tl = lane % RTEAM;
-  const int ntile = (Tn + 15) / 16;
-  const int tile0 = (blockIdx.x * 4 + wave) * tpw;  // this wave's tiles: tile0 .. tile0 + tpw - 1
-  f32x4_t acc[RTPW][NH];
+  const int tb0 = blockIdx.x * nt * 16;
+  const int c0 = wave * (NKS * 32) + fq * 8;  // this wave's channel quarter (C = 128 NKS)
+  // A fragments, all loaded up front; rows past the last token re-read it
+  bf16x8_t af[NT][NKS];
 #pragma unroll
-  for (int j = 0; j < RTPW; ++j)
+  for (int j = 0; j < NT; ++j)
 #pragma unroll
-    for (int h = 0; h < NH; ++h) acc[j][h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < C; c0 += RKC) {
-    const int kc = min(RKC, C - c0);
-    if (c0 > 0) __syncthreads();  // the previous chunk's fragments are read
-    // stage the chunk: float4 runs of Wfc rows, 8 loads in flight per thread (a load-then-store loop is one
-    // L2 round trip per element group)
-    const int n4 = kc * E / 4;
-    const f32x4_t* src = reinterpret_cast<const f32x4_t*>(Wfc + (int64_t)c0 * E);
-    for (int i0 = threadIdx.x; i0 < n4; i0 += 256 * 8) {
-      f32x4_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + u * 256;
-        v[u] = i < n4 ? src[i] : f32x4_t{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + u * 256;
-        if (i < n4) {
-          const int c = (i * 4) / E, e0 = (i * 4) % E;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const bf16_t h = f2bf(v[u][q]);
-            whi[(e0 + q) * P + c] = h;
-            wlo[(e0 + q) * P + c] = f2bf(v[u][q] - bf2f(h));
-          }
-        }
-      }
+    for (int st = 0; st < NKS; ++st) {
+      const int64_t row = min(tb0 + j * 16 + fr, Tn - 1);
+      af[j][st] = __builtin_bit_cast(bf16x8_t, j < nt ? *reinterpret_cast<const u16x8_t*>(tok + row * ld + c0 + st * 32)
+                                                      : u16x8_t{0, 0, 0, 0, 0, 0, 0, 0});
     }
-    if constexpr (E < EP) {
-      if (c0 == 0)
-        for (int i = threadIdx.x; i < (EP - E) * P; i += 256) {
-          whi[E * P + i] = 0;
-          wlo[E * P + i] = 0;
-        }
-    }
-    __syncthreads();
+  // B fragments of the quarter: expert h * 16 + fr, channels c0 + 32 st .. + 8, as bf16 hi / lo
+  bf16x8_t bh[NKS][NH], bl[NKS][NH];
 #pragma unroll
-    for (int j = 0; j < RTPW; ++j) {
-      const int tile = tile0 + j;
-      if (j < tpw && tile < ntile) {  // wave-uniform
-        // rows past the last token re-read the last token; their logits are never used
-        const bf16_t* arow = tok + (int64_t)min(tile * 16 + fr, Tn - 1) * ld + c0 + fq * 8;
-#pragma unroll 4
-        for (int ks = 0; ks < kc; ks += 32) {
-          const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(arow + ks));
+  for (int st = 0; st < NKS; ++st)
 #pragma unroll
-          for (int h = 0; h < NH; ++h) {
-            const int off = (h * 16 + fr) * P + ks + fq * 8;
-            const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(wlo + off));
-            const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(whi + off));
-            acc[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl, acc[j][h], 0, 0, 0);
-            acc[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh, acc[j][h], 0, 0, 0);
-          }
-        }
+    for (int h = 0; h < NH; ++h) {
+      const int e = h * 16 + fr;
+      float w[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w[q] = e < E ? Wfc[(int64_t)(c0 + st * 32 + q) * E + e] : 0.f;
+      u16x8_t hv, lv;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        hv[q] = f2bf(w[q]);
+        lv[q] = f2bf(w[q] - bf2f(hv[q]));
       }
+      bh[st][h] = __builtin_bit_cast(bf16x8_t, hv);
+      bl[st][h] = __builtin_bit_cast(bf16x8_t, lv);
     }
-  }
-  float* zw = ztile + wave * 16 * ZP;
+  float* zw = zpart + wave * ZW;
 #pragma unroll
-  for (int j = 0; j < RTPW; ++j) {
-    const int tile = tile0 + j;
-    if (j < tpw && tile < ntile) {  // wave-uniform
-      // D[token fq*4 + r][expert h*16 + fr] -> the wave's logit tile -> teams of 8 lanes, 8 tokens per pass
+  for (int j = 0; j < NT; ++j) {
+    if (j < nt) {  // block-uniform
+      f32x4_t acc[NH];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) acc[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < NKS; ++st)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j][st], bl[st][h], acc[h], 0, 0, 0);
+          acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[j][st], bh[st][h], acc[h], 0, 0, 0);
+        }
+      // D[token fq*4 + r][expert h*16 + fr]
 #pragma unroll
       for (int h = 0; h < NH; ++h)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) zw[(fq * 4 + r) * ZP + h * 16 + fr] = acc[j][h][r];
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      constexpr int NE = E / RTEAM;
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int row = half * 8 + team, t = tile * 16 + row;
-        float araw[NE];
-#pragma unroll
-        for (int q = 0; q < NE; ++q) araw[q] = zw[row * ZP + tl + RTEAM * q];
-        router_token<E>(araw, t < Tn, t, tl, lgHW, Lt, temp, anneal, k, eval_mode, probs, zlog, topi, gate);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+        for (int r = 0; r < 4; ++r) zw[(j * 16 + fq * 4 + r) * ZP + h * 16 + fr] = acc[h][r];
     }
+  }
+  __syncthreads();
+  // teams of 8 lanes, 32 tokens per pass (a pass's active teams fill whole waves: nt * 16 is a multiple of 16);
+  // the four channel quarters fold in wave order
+  const int team = threadIdx.x / RTEAM, tl = threadIdx.x % RTEAM;
+  constexpr int NE = E / RTEAM;
+  for (int row = team; row < nt * 16; row += 256 / RTEAM) {
+    const int t = tb0 + row;
+    float araw[NE];
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+      const int o = row * ZP + tl + RTEAM * q;
+      araw[q] = ((zpart[o] + zpart[ZW + o]) + zpart[2 * ZW + o]) + zpart[3 * ZW + o];
+    }
+    router_token<E>(araw, t < Tn, t, tl, lgHW, Lt, temp, anneal, k, eval_mode, probs, zlog, topi, gate);
   }
 }
 
@@ -646,6 +621,108 @@ __global__ __launch_bounds__(256) void k_token_grad_v(const T* __restrict__ gX, 
   }
 }
 
+// Token gradient with the router term on the matrix cores: out[t] = sum_j gX[pos_of[t*k+j]] + g_raw[t] . Wfc^T.
+// The [16 x E] . [E x C] products run as v_mfma_f32_16x16x32_bf16 with both fp32 operands split into bf16 hi + lo
+// (three products, lo * lo dropped: relative error ~2^-16 per term); experts past E (E = 8, 16) are zero k-rows.
+// A block takes nt 16-token tiles; wave w owns output channels [16 NB w, 16 NB (w + 1)) and holds their Wfc
+// fragments in registers (straight from L2, no staging); the product tile goes through LDS ([16 nt][C + 4] fp32)
+// to a coalesced pass that adds the k gathered expert-output gradients and stores 16-B vectors.  The lane-FMA
+// kernel above spends 2 LDS reads + 8 FMAs per token-8-channel-expert and staged C x E floats per block
+// (C5: 48 - 57 us per call against ~4 - 18 us of HBM traffic).
+template <typename T, typename TO, int E, int NB>
+__global__ __launch_bounds__(256) void k_token_grad_mfma(const T* __restrict__ gX, int64_t ldx,
+                                                         const int* __restrict__ pos_of, int Tn, int k, int nt,
+                                                         const float* __restrict__ g_raw,
+                                                         const float* __restrict__ Wfc, TO* __restrict__ out,
+                                                         int64_t ldo) {
+  constexpr int C = 64 * NB;
+  constexpr int CP = C + 4;
+  extern __shared__ __align__(16) float gtile[];  // [nt * 16][CP]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  const bool kin = fq * 8 < E;  // this lane's 8 k-rows (experts) exist
+  const int tb0 = blockIdx.x * nt * 16;
+  auto split = [](const float* w, bf16x8_t& hi, bf16x8_t& lo) {
+    u16x8_t hv, lv;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      hv[q] = f2bf(w[q]);
+      lv[q] = f2bf(w[q] - bf2f(hv[q]));
+    }
+    hi = __builtin_bit_cast(bf16x8_t, hv);
+    lo = __builtin_bit_cast(bf16x8_t, lv);
+  };
+  // B fragments: Wfc^T[e][c] for channel c = 16 (NB w + b) + fr, experts fq*8 .. +8 (a Wfc row run)
+  bf16x8_t bh[NB], bl[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int c = (wave * NB + b) * 16 + fr;
+    float w[8];
+    if (kin) {
+      const f32x4_t w0 = *reinterpret_cast<const f32x4_t*>(Wfc + (int64_t)c * E + fq * 8);
+      const f32x4_t w1 = *reinterpret_cast<const f32x4_t*>(Wfc + (int64_t)c * E + fq * 8 + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[q] = w0[q];
+        w[q + 4] = w1[q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w[q] = 0.f;
+    }
+    split(w, bh[b], bl[b]);
+  }
+  for (int j = 0; j < nt; ++j) {
+    const int64_t row = min(tb0 + j * 16 + fr, Tn - 1);  // rows past the last token: never stored
+    float a[8];
+    if (kin) {
+      const f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(g_raw + row * E + fq * 8);
+      const f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(g_raw + row * E + fq * 8 + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[q] = a0[q];
+        a[q + 4] = a1[q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = 0.f;
+    }
+    bf16x8_t ah, al;
+    split(a, ah, al);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[b], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[b], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[b], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gtile[(j * 16 + fq * 4 + r) * CP + (wave * NB + b) * 16 + fr] = acc[r];
+    }
+  }
+  __syncthreads();
+  constexpr int CV = C / 8;
+  const int n = nt * 16 * CV;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int r = i / CV, c = (i - r * CV) * 8, t = tb0 + r;
+    if (t >= Tn) continue;
+    float sv[8], v[8];
+    const f32x4_t s0 = *reinterpret_cast<const f32x4_t*>(gtile + r * CP + c);
+    const f32x4_t s1 = *reinterpret_cast<const f32x4_t*>(gtile + r * CP + c + 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      sv[q] = s0[q];
+      sv[q + 4] = s1[q];
+    }
+    if (gX)
+      for (int j = 0; j < k; ++j) {
+        ld8(gX + (int64_t)pos_of[t * k + j] * ldx + c, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sv[q] += v[q];
+      }
+    st8(out + (int64_t)t * ldo + c, sv);
+  }
+}
+
 // g_gate[a] = <gout[t], Y[pos_of[a]]>, one wave per assignment
 template <typename T, typename TG>
 __global__ void k_gate_grad(const TG* __restrict__ gout, int64_t ldg, const T* __restrict__ Y, int64_t ldy,
@@ -807,6 +884,159 @@ __global__ __launch_bounds__(256) void k_router_bwd(const float* __restrict__ pr
   }
 }
 
+
+MG_DEV float team_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  return v;
+}
+
+// Team form of k_router_bwd (E >= 8, the same math): RTEAM lanes per token, lane tl owning experts tl, tl + 8, ...,
+// the per-token reductions over experts as team butterflies.  A block of 256 threads (32 teams) covers
+// TB = max(32, HW) consecutive tokens, each team TB / 32 of them in turn, so every image lies inside one block;
+// per-image sums and the block's temperature partial fold the team partials in team order (fixed order:
+// bit-identical run to run).  The thread-per-token kernel ran 16 blocks for the 4096 tokens of a 4x4 layer and
+// read each token's rows as scattered 4-B loads (C5: 39 us per call); here a wave reads 8 tokens' rows whole.
+template <int E>
+__global__ __launch_bounds__(256) void k_router_bwd_team(const float* __restrict__ probs,
+                                                         const float* __restrict__ zlog, const int* __restrict__ topi,
+                                                         const float* __restrict__ gate,
+                                                         const float* __restrict__ g_gate,
+                                                         const float* __restrict__ g_probs,
+                                                         const float* __restrict__ g_logits,
+                                                         const float* __restrict__ coef, int Tn, int k, int lgHW,
+                                                         const float* __restrict__ temp, float anneal,
+                                                         float* __restrict__ g_raw, float* __restrict__ gsum,
+                                                         float* __restrict__ tpart) {
+  constexpr int NE = E / RTEAM;
+  constexpr int NT = 256 / RTEAM;  // teams per block
+  __shared__ float red[NT * E];
+  __shared__ float tred[NT];
+  const int team = threadIdx.x / RTEAM, tl = threadIdx.x % RTEAM;
+  const int HW = 1 << lgHW;
+  const int TB = HW > NT ? HW : NT;
+  const int t0 = blockIdx.x * TB;
+  const float te = teff_of(temp, anneal);
+  float acc[NE];
+#pragma unroll
+  for (int j = 0; j < NE; ++j) acc[j] = 0.f;
+  float gt_part = 0.f;
+  for (int tt = team; tt < TB; tt += NT) {
+    const int t = t0 + tt;
+    const bool ok = t < Tn;  // team-uniform; a dead team computes on zeros (the shuffles stay wave-wide)
+    const int64_t r = (int64_t)(ok ? t : 0) * E;
+    float p[NE], gp[NE], z[NE];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int e = tl + RTEAM * j;
+      p[j] = probs[r + e];
+      z[j] = zlog[r + e];
+      gp[j] = (coef ? coef[e] : 0.f) + (g_probs ? g_probs[r + e] : 0.f);
+    }
+    if (g_gate) {
+      const int64_t rk = (int64_t)(ok ? t : 0) * k;
+      if (k == E) {
+        for (int i = 0; i < k; ++i) {
+          const int ex = topi[rk + i];
+          const float gg = g_gate[rk + i];
+#pragma unroll
+          for (int j = 0; j < NE; ++j)
+            if (tl + RTEAM * j == ex) gp[j] += gg;
+        }
+      } else {
+        float S = 0.f, dot = 0.f;
+        for (int i = 0; i < k; ++i) {
+          const int ex = topi[rk + i];
+#pragma unroll
+          for (int j = 0; j < NE; ++j)
+            if (tl + RTEAM * j == ex) S += p[j];
+          dot += g_gate[rk + i] * gate[rk + i];
+        }
+        S = team_sum(S);
+        for (int i = 0; i < k; ++i) {
+          const int ex = topi[rk + i];
+          const float v = (g_gate[rk + i] - dot) / S;
+#pragma unroll
+          for (int j = 0; j < NE; ++j)
+            if (tl + RTEAM * j == ex) gp[j] += v;
+        }
+      }
+    }
+    // recompute softmax s and clamped q
+    float l[NE], sv[NE], q[NE];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      l[j] = fminf(fmaxf(z[j], -20.f), 20.f);
+      mx = fmaxf(mx, l[j]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+    float den = 0.f;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      sv[j] = expf(l[j] - mx);
+      den += sv[j];
+    }
+    den = team_sum(den);
+    float Sq = 0.f;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      sv[j] /= den;
+      q[j] = fminf(fmaxf(sv[j], 1e-6f), 1.f);
+      Sq += q[j];
+    }
+    Sq = team_sum(Sq);
+    float d1 = 0.f;  // p = q / Sq
+#pragma unroll
+    for (int j = 0; j < NE; ++j) d1 += gp[j] * (q[j] / Sq);
+    d1 = team_sum(d1);
+    float gs_[NE], d2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const float gq = (gp[j] - d1) / Sq;
+      gs_[j] = (sv[j] >= 1e-6f && sv[j] <= 1.f) ? gq : 0.f;
+      d2 += gs_[j] * sv[j];
+    }
+    d2 = team_sum(d2);
+    if (ok) {
+#pragma unroll
+      for (int j = 0; j < NE; ++j) {
+        const int e = tl + RTEAM * j;
+        float gl = sv[j] * (gs_[j] - d2);
+        if (g_logits) gl += g_logits[r + e];  // the router's second output, logits (:378-381)
+        gl = (z[j] >= -20.f && z[j] <= 20.f) ? gl : 0.f;
+        gt_part += -gl * z[j] / te;
+        acc[j] += gl / te;
+        g_raw[r + e] = gl / te;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NE; ++j) red[team * E + tl + RTEAM * j] = acc[j];
+  gt_part = team_sum(gt_part);
+  if (tl == 0) tred[team] = gt_part;
+  __syncthreads();
+  // per-image sums over the image's teams, in team order
+  const int nimg = TB >> lgHW;
+  const int tpi = HW < NT ? HW : NT;  // teams per image
+  for (int i = threadIdx.x; i < nimg * E; i += 256) {
+    const int bl = i / E, e = i - bl * E;
+    if (t0 + bl * HW < Tn) {
+      float v = 0.f;
+      for (int w = bl * tpi; w < bl * tpi + tpi; ++w) v += red[w * E + e];
+      gsum[(int64_t)((t0 >> lgHW) + bl) * E + e] = v;
+    }
+  }
+  if (threadIdx.x == 0 && tpart) {
+    float tt = 0.f;
+    for (int i = 0; i < NT; ++i) tt += tred[i];
+    const float raw = temp[0] * anneal;
+    tpart[blockIdx.x] = (raw >= 0.5f && raw <= 5.f) ? tt * anneal : 0.f;
+  }
+}
 
 // g_tok[t, c] = sum_j gX[pos_of[t*k+j], c] + sum_e g_raw[t, e] * Wfc[c, e]
 template <typename T, typename TO>
@@ -1319,16 +1549,18 @@ extern "C" int mg_router_fwd(int dtype, const void* tok, int64_t ld, int T, int 
   int lg = 0;
   while ((1 << lg) < HW) ++lg;
   if (T <= 0) return 0;
-  if (dtype != MG_F32 && E >= 8 && C % 32 == 0 && ld % 8 == 0 && mg_al16(tok) && mg_al16(Wfc) &&
-      g_mg_tune[MG_TUNE_ROUTER_TEAM] == 0) {
-    // tiles per wave: enough blocks to spread over the CUs (>= 512 where there are tokens for it), then up to
-    // RTPW tiles per wave so each block stages Wfc for more tokens
+  if (dtype != MG_F32 && E >= 8 && C % 128 == 0 && C <= 512 && ld % 8 == 0 && mg_al16(tok) &&
+      (g_mg_tune[MG_TUNE_ROUTER_TEAM] & 1) == 0) {
+    // tiles per block: up to 4 / (C / 128) (the A fragments a lane holds) once there are >= 1024 blocks' worth
     const int ntile = cdiv(T, 16);
-    const int tpw = std::max(1, std::min(RTPW, ntile / (4 * 512)));
-    dim3 gm(cdiv(ntile, 4 * tpw));
-#define L_(EE) hipLaunchKernelGGL((k_router_fwd_mfma<EE>), gm, dim3(256), 0, st, (const bf16_t*)tok, ld, T, C, tpw, \
-                                  Wfc, Lt, lg, temperature, anneal, k, eval_mode, probs, zlog, topi, gate)
-    if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
+    const int nks = C / 128;
+    const int nt = std::max(1, std::min(RNT / nks, ntile / 1024));
+    dim3 gm(cdiv(ntile, nt));
+#define L_(EE, NK) hipLaunchKernelGGL((k_router_fwd_mfma<EE, NK>), gm, dim3(256), 0, st, (const bf16_t*)tok, ld, T, C, \
+                                      nt, Wfc, Lt, lg, temperature, anneal, k, eval_mode, probs, zlog, topi, gate)
+#define LK_(EE) if (nks == 1) L_(EE, 1); else if (nks == 2) L_(EE, 2); else if (nks == 3) L_(EE, 3); else L_(EE, 4)
+    if (E == 8) { LK_(8); } else if (E == 16) { LK_(16); } else { LK_(32); }
+#undef LK_
 #undef L_
     return mg_check_launch("mg_router_fwd");
   }
@@ -1420,16 +1652,21 @@ extern "C" int mg_router_bwd(const float* probs, const float* zlog, const int32_
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int lg = 0;
   while ((1 << lg) < HW) ++lg;
-  dim3 grid(cdiv(T, 256));
+  const bool team = E >= 8 && (g_mg_tune[MG_TUNE_ROUTER_TEAM] & 2) == 0;
+  dim3 grid(team ? cdiv(T, std::max(HW, 256 / RTEAM)) : cdiv(T, 256));
   float* tpart = nullptr;
   bool deferred = false;
   if (g_temp) {
     tpart = mg_fold_partials((size_t)grid.x * sizeof(float), st, &deferred);
     if (!tpart) return MG_ERR_LAUNCH;
   }
-#define L_(EE) hipLaunchKernelGGL((k_router_bwd<EE>), grid, dim3(256), 0, st, probs, zlog, topi, gate, g_gate, g_probs, g_logits, coef, T, k, lg, \
-                                  temperature, anneal, g_raw, gsum, tpart)
-  if (E == 4) L_(4); else if (E == 8) L_(8); else if (E == 16) L_(16); else L_(32);
+#define L_(KN, EE) hipLaunchKernelGGL((KN<EE>), grid, dim3(256), 0, st, probs, zlog, topi, gate, g_gate, g_probs, g_logits, coef, T, k, lg, \
+                                      temperature, anneal, g_raw, gsum, tpart)
+  if (team) {
+    if (E == 8) L_(k_router_bwd_team, 8); else if (E == 16) L_(k_router_bwd_team, 16); else L_(k_router_bwd_team, 32);
+  } else {
+    if (E == 4) L_(k_router_bwd, 4); else if (E == 8) L_(k_router_bwd, 8); else if (E == 16) L_(k_router_bwd, 16); else L_(k_router_bwd, 32);
+  }
 #undef L_
   // the temperature partials (one per block) as a one-column rows fold
   if (g_temp) mg_fold_rows_submit(mg_fold_rows{tpart, 1, (int)grid.x, 1, 1, g_temp, nullptr}, deferred, st);
@@ -1441,6 +1678,25 @@ extern "C" int mg_moe_token_grad(int dtype, const void* gX, int64_t ldx, const i
                                  void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t n = (int64_t)T * C;
+  if (T <= 0) return 0;
+  if ((C == 128 || C == 256 || C == 512) && (E == 8 || E == 16 || E == 32) && (!gX || (ldx % 8 == 0 && mg_al16(gX))) &&
+      ldo % 8 == 0 && mg_al16(out) && mg_al16(g_raw) && mg_al16(Wfc) && (g_mg_tune[MG_TUNE_ROUTER_TEAM] & 4) == 0) {
+    // tiles per block: the product tile [16 nt][C + 4] fp32 within ~33 KiB, once there are >= 1024 blocks' worth
+    const int ntile = cdiv(T, 16);
+    const int nt = std::max(1, std::min(512 / C, ntile / 1024));
+    const size_t lds = (size_t)nt * 16 * (C + 4) * sizeof(float);
+    dim3 gm(cdiv(ntile, nt));
+#define LM_(TT, TO, EE, NB) hipLaunchKernelGGL((k_token_grad_mfma<TT, TO, EE, NB>), gm, dim3(256), lds, st, (const TT*)gX, \
+                                            ldx, pos_of, T, k, nt, g_raw, Wfc, (TO*)out, ldo)
+#define LMC_(TT, TO, EE) if (C == 128) LM_(TT, TO, EE, 2); else if (C == 256) LM_(TT, TO, EE, 4); else LM_(TT, TO, EE, 8)
+#define LME_(TT, TO) if (E == 8) { LMC_(TT, TO, 8); } else if (E == 16) { LMC_(TT, TO, 16); } else { LMC_(TT, TO, 32); }
+    if (dtype == MG_F32) { if (out_dtype == MG_F32) { LME_(float, float); } else { LME_(float, bf16_t); } }
+    else { if (out_dtype == MG_F32) { LME_(bf16_t, float); } else { LME_(bf16_t, bf16_t); } }
+#undef LME_
+#undef LMC_
+#undef LM_
+    return mg_check_launch("mg_moe_token_grad");
+  }
   if (C % 8 == 0 && (!gX || (ldx % 8 == 0 && mg_al16(gX))) && ldo % 8 == 0 && mg_al16(out) && n / 8 < (1LL << 31) &&
       (E == 4 || E == 8 || E == 16 || E == 32) && mg_al16(g_raw) && (size_t)C * E * 4 <= 65536) {
     const size_t lds = (size_t)C * E * sizeof(float);

@@ -83,6 +83,59 @@ def test_router_fwd_mfma_shapes(T, C, E, k, HW):
     assert rel(torch.sort(gate, dim=1).values[clear], torch.sort(gt, dim=1).values.float()[clear]) < 1e-5
 
 
+@pytest.mark.parametrize("E,k,HW,B", [(32, 4, 16, 64), (32, 4, 256, 9), (8, 2, 64, 17), (16, 16, 1, 300),
+                                      (8, 2, 4, 33), (4, 2, 16, 8)])
+def test_router_bwd_against_autograd(E, k, HW, B):
+    """mg_router_bwd (8-lane teams for E >= 8, thread per token for E = 4) against fp64 autograd of the router's
+    softmax / clamp / renormalise / top-k gate (t2i_moe_gan.py:375-402): the raw-logit gradient, the per-image
+    sums and the temperature gradient; and against the thread-per-token kernel (tuning slot 24 = 2)."""
+    from moegan_mi import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(E * 1000 + HW + B)
+    T, C = B * HW, 128
+    tok = torch.randn(T, C, device=DEV, generator=g).to(torch.bfloat16)
+    Wfc = torch.randn(C, E, device=DEV, generator=g) * 0.3
+    Lt = torch.randn(B, E, device=DEV, generator=g)
+    temp = torch.tensor([1.3], device=DEV)
+    probs, zlog, topi, gate = ops.router_fwd(tok, Wfc, Lt, E, k, HW, temp, 0.9)
+    g_gate = torch.randn(T, k, device=DEV, generator=g)
+    g_probs = torch.randn(T, E, device=DEV, generator=g)
+    g_logits = torch.randn(T, E, device=DEV, generator=g) * 0.1
+    coef = torch.randn(E, device=DEV, generator=g)
+
+    def run():
+        gt = torch.zeros(1, device=DEV)
+        g_raw, gsum = ops.router_bwd(probs, zlog, topi, gate, g_gate, g_probs, coef, HW, temp, 0.9, gt, B,
+                                     g_logits=g_logits)
+        ops.fold_flush()
+        torch.cuda.synchronize()
+        return g_raw, gsum, gt
+
+    g_raw, gsum, gt = run()
+    L.call("mg_set_tuning", 24, 2)
+    try:
+        g_raw2, gsum2, gt2 = run()
+    finally:
+        L.call("mg_set_tuning", 24, 0)
+    te = min(max(1.3 * 0.9, 0.5), 5.0)
+    raw = (zlog.double() * te).requires_grad_(True)
+    tp = torch.tensor([1.3], dtype=torch.float64, device=DEV, requires_grad=True)
+    z = raw / (tp * 0.9).clamp(0.5, 5.0)
+    lz = z.clamp(-20.0, 20.0)
+    q = torch.softmax(lz, dim=1).clamp(1e-6, 1.0)
+    p = q / q.sum(dim=1, keepdim=True)
+    pk = p.gather(1, topi.long())
+    gk = pk if k == E else pk / pk.sum(dim=1, keepdim=True)
+    loss = (p * (coef.double() + g_probs.double())).sum() + (gk * g_gate.double()).sum() + \
+        (lz * g_logits.double()).sum()
+    ref_raw, ref_t = torch.autograd.grad(loss, (raw, tp))
+    assert rel(g_raw, ref_raw) < 1e-5
+    assert rel(gsum, ref_raw.view(B, HW, E).sum(1)) < 1e-5
+    assert abs(gt.item() - ref_t.item()) <= 1e-5 * max(1.0, abs(ref_t.item()))
+    assert rel(g_raw, g_raw2) < 1e-6 and rel(gsum, gsum2) < 1e-5
+    again = run()
+    assert all(torch.equal(a, b) for a, b in zip((g_raw, gsum, gt), again))  # fixed reduction order
+
+
 @pytest.mark.parametrize("E", [4, 8, 16, 32])
 def test_token_and_feature_grad_across_experts(E):
     g = torch.Generator(device=DEV).manual_seed(100 + E)
@@ -99,6 +152,32 @@ def test_token_and_feature_grad_across_experts(E):
     G1 = torch.zeros(C, E, device=DEV)
     ops.router_feat_grad(tok, g_raw, G1)
     assert rel(G1, tok.float().T @ g_raw) < 1e-5
+
+
+@pytest.mark.parametrize("T,C,E,k,out_dtype", [(4096 - 3, 512, 32, 4, torch.float32), (16384, 256, 32, 4, torch.bfloat16),
+                                               (65536 + 5, 128, 32, 4, torch.float32), (1000, 128, 8, 2, torch.float32),
+                                               (3000, 256, 16, 2, torch.bfloat16)])
+def test_token_grad_mfma_shapes(T, C, E, k, out_dtype):
+    """Token gradient with the router term on the matrix cores (both fp32 operands as bf16 hi + lo): one and
+    several tiles per block, ragged token counts, E = 8 / 16 (zero k-rows); against fp64 and against the lane-FMA
+    kernel (tuning slot 24 = 4)."""
+    from moegan_mi import _lib as L
+    g = torch.Generator(device=DEV).manual_seed(T + C * 3 + E)
+    gX = torch.randn(T * k, C, device=DEV, generator=g).to(torch.bfloat16)
+    pos_of = torch.randperm(T * k, device=DEV, generator=g).to(torch.int32)
+    g_raw = torch.randn(T, E, device=DEV, generator=g)
+    Wfc = torch.randn(C, E, device=DEV, generator=g) * 0.5
+    out = ops.moe_token_grad(gX, pos_of, g_raw, Wfc, torch.empty(T, C, device=DEV, dtype=out_dtype), k)
+    L.call("mg_set_tuning", 24, 4)
+    try:
+        out_l = ops.moe_token_grad(gX, pos_of, g_raw, Wfc, torch.empty(T, C, device=DEV, dtype=out_dtype), k)
+    finally:
+        L.call("mg_set_tuning", 24, 0)
+    ref = gX.double()[pos_of.long().view(T, k)].sum(1) + g_raw.double() @ Wfc.double().T
+    tol = 1e-5 if out_dtype == torch.float32 else 8e-3
+    assert rel(out, ref) < tol and rel(out_l, ref) < tol
+    if out_dtype == torch.float32:
+        assert rel(out, out_l) < 1e-5
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
