@@ -893,13 +893,14 @@ MG_DEV float team_sum(float v) {
 }
 
 // Team form of k_router_bwd (E >= 8, the same math): RTEAM lanes per token, lane tl owning experts tl, tl + 8, ...,
-// the per-token reductions over experts as team butterflies.  A block of 256 threads (32 teams) covers
-// TB = max(32, HW) consecutive tokens, each team TB / 32 of them in turn, so every image lies inside one block;
+// the per-token reductions over experts as team butterflies.  A block of NT teams (32 / 64 / 128: one team per
+// token up to 128-token images) covers TB = max(NT, HW) consecutive tokens, each team TB / NT of them in turn, so
+// every image lies inside one block;
 // per-image sums and the block's temperature partial fold the team partials in team order (fixed order:
 // bit-identical run to run).  The thread-per-token kernel ran 16 blocks for the 4096 tokens of a 4x4 layer and
 // read each token's rows as scattered 4-B loads (C5: 39 us per call); here a wave reads 8 tokens' rows whole.
-template <int E>
-__global__ __launch_bounds__(256) void k_router_bwd_team(const float* __restrict__ probs,
+template <int E, int NT>
+__global__ __launch_bounds__(NT * RTEAM) void k_router_bwd_team(const float* __restrict__ probs,
                                                          const float* __restrict__ zlog, const int* __restrict__ topi,
                                                          const float* __restrict__ gate,
                                                          const float* __restrict__ g_gate,
@@ -909,8 +910,7 @@ __global__ __launch_bounds__(256) void k_router_bwd_team(const float* __restrict
                                                          const float* __restrict__ temp, float anneal,
                                                          float* __restrict__ g_raw, float* __restrict__ gsum,
                                                          float* __restrict__ tpart) {
-  constexpr int NE = E / RTEAM;
-  constexpr int NT = 256 / RTEAM;  // teams per block
+  constexpr int NE = E / RTEAM;  // NT: teams per block
   __shared__ float red[NT * E];
   __shared__ float tred[NT];
   const int team = threadIdx.x / RTEAM, tl = threadIdx.x % RTEAM;
@@ -1022,7 +1022,7 @@ __global__ __launch_bounds__(256) void k_router_bwd_team(const float* __restrict
   // per-image sums over the image's teams, in team order
   const int nimg = TB >> lgHW;
   const int tpi = HW < NT ? HW : NT;  // teams per image
-  for (int i = threadIdx.x; i < nimg * E; i += 256) {
+  for (int i = threadIdx.x; i < nimg * E; i += NT * RTEAM) {
     const int bl = i / E, e = i - bl * E;
     if (t0 + bl * HW < Tn) {
       float v = 0.f;
@@ -1477,29 +1477,27 @@ __global__ __launch_bounds__(256) void k_router_param_bwd_batch(RpbBatch b, cons
 
 // balance loss (t2i_moe_gan.py:951-1000) from the global per-expert prob sums:
 // out[0] = loss; coef[e] = d loss / d probs[t, e] (* grad_scale)
+// one lane per expert (E <= 64), mean / variance as wave butterflies (fixed order); the serial single-lane form
+// walked its E loads one round trip at a time (C5: 18 us for 32 experts)
 __global__ void k_balance(const float* __restrict__ load, int E, float T, float weight, float grad_scale,
                           float* __restrict__ out, float* __restrict__ coef) {
-  if (threadIdx.x != 0) return;
-  float frac[64];
-  float mean = 0.f;
-  for (int e = 0; e < E; ++e) {
-    frac[e] = (load[e] + 1e-6f) / T;
-    mean += frac[e];
-  }
-  mean /= E;
-  float var = 0.f;
-  for (int e = 0; e < E; ++e) var += (frac[e] - mean) * (frac[e] - mean);
-  float sd = sqrtf(var / (E - 1));
-  float den = mean + 1e-6f;
-  float cv = sd / den;
-  float raw = E * cv;
-  float L = isnan(raw) ? 0.f : fminf(fmaxf(raw, 0.f), 10.f);
-  out[0] = weight * L;
-  bool pass = !isnan(raw) && raw >= 0.f && raw <= 10.f;
-  for (int e = 0; e < E; ++e) {
+  const int e = threadIdx.x;
+  const bool own = e < E;
+  const float frac = own ? (load[e] + 1e-6f) / T : 0.f;
+  const float mean = wave_sum(frac) / E;
+  const float dv = own ? frac - mean : 0.f;
+  const float var = wave_sum(dv * dv);
+  const float sd = sqrtf(var / (E - 1));
+  const float den = mean + 1e-6f;
+  const float cv = sd / den;
+  const float raw = E * cv;
+  const float L = isnan(raw) ? 0.f : fminf(fmaxf(raw, 0.f), 10.f);
+  if (e == 0) out[0] = weight * L;
+  const bool pass = !isnan(raw) && raw >= 0.f && raw <= 10.f;
+  if (own) {
     float dcv = 0.f;
     if (pass && sd > 0.f) {
-      float dsd = (frac[e] - mean) / ((E - 1) * sd);
+      const float dsd = dv / ((E - 1) * sd);
       dcv = (dsd * den - sd / E) / (den * den);
     }
     coef[e] = pass ? weight * E * dcv / T * grad_scale : 0.f;
@@ -1653,20 +1651,24 @@ extern "C" int mg_router_bwd(const float* probs, const float* zlog, const int32_
   int lg = 0;
   while ((1 << lg) < HW) ++lg;
   const bool team = E >= 8 && (g_mg_tune[MG_TUNE_ROUTER_TEAM] & 2) == 0;
-  dim3 grid(team ? cdiv(T, std::max(HW, 256 / RTEAM)) : cdiv(T, 256));
+  const int nteam = HW >= 128 ? 128 : HW >= 64 ? 64 : 32;  // teams per block
+  dim3 grid(team ? cdiv(T, std::max(HW, nteam)) : cdiv(T, 256));
   float* tpart = nullptr;
   bool deferred = false;
   if (g_temp) {
     tpart = mg_fold_partials((size_t)grid.x * sizeof(float), st, &deferred);
     if (!tpart) return MG_ERR_LAUNCH;
   }
-#define L_(KN, EE) hipLaunchKernelGGL((KN<EE>), grid, dim3(256), 0, st, probs, zlog, topi, gate, g_gate, g_probs, g_logits, coef, T, k, lg, \
+#define L_(KN, TH) hipLaunchKernelGGL(KN, grid, dim3(TH), 0, st, probs, zlog, topi, gate, g_gate, g_probs, g_logits, coef, T, k, lg, \
                                       temperature, anneal, g_raw, gsum, tpart)
+#define LT_(EE) if (nteam == 32) L_((k_router_bwd_team<EE, 32>), 256); else if (nteam == 64) L_((k_router_bwd_team<EE, 64>), 512); \
+                else L_((k_router_bwd_team<EE, 128>), 1024)
   if (team) {
-    if (E == 8) L_(k_router_bwd_team, 8); else if (E == 16) L_(k_router_bwd_team, 16); else L_(k_router_bwd_team, 32);
+    if (E == 8) { LT_(8); } else if (E == 16) { LT_(16); } else { LT_(32); }
   } else {
-    if (E == 4) L_(k_router_bwd, 4); else if (E == 8) L_(k_router_bwd, 8); else if (E == 16) L_(k_router_bwd, 16); else L_(k_router_bwd, 32);
+    if (E == 4) L_(k_router_bwd<4>, 256); else if (E == 8) L_(k_router_bwd<8>, 256); else if (E == 16) L_(k_router_bwd<16>, 256); else L_(k_router_bwd<32>, 256);
   }
+#undef LT_
 #undef L_
   // the temperature partials (one per block) as a one-column rows fold
   if (g_temp) mg_fold_rows_submit(mg_fold_rows{tpart, 1, (int)grid.x, 1, 1, g_temp, nullptr}, deferred, st);
@@ -1812,9 +1814,10 @@ extern "C" int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const
                             int nt, const float* mu_c, const float* rho_c, int nc, float* out, void* stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int64_t n = (int64_t)nf + nt + nc;
-  int nparts = (int)std::min<int64_t>(64, std::max<int64_t>(1, cdiv(n, 2048)));
-  // 64 partials in this stream's workspace block (reuse is ordered by the stream)
-  float* s_part = reinterpret_cast<float*>(mg_workspace(64 * sizeof(float), st));
+  // up to 256 partials (~2 elements per thread: a longer grid-stride loop is one load round trip per element)
+  // in this stream's workspace block (reuse is ordered by the stream)
+  int nparts = (int)std::min<int64_t>(256, std::max<int64_t>(1, cdiv(n, 512)));
+  float* s_part = reinterpret_cast<float*>(mg_workspace(256 * sizeof(float), st));
   MG_REQUIRE(s_part, "no workspace");
   hipLaunchKernelGGL(k_router_kl_part, dim3(nparts), dim3(256), 0, st, mu_f, rho_f, nf, mu_t, rho_t, nt, mu_c, rho_c,
                      nc, s_part);
