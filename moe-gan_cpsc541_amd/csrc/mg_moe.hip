@@ -1109,6 +1109,8 @@ __global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict_
   for (int j = 0; j < CV; ++j)
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[j][e] = 0.f;
+  // four tokens' loads in flight per lane (the accumulation order per lane is unchanged)
+#pragma unroll 4
   for (int t = t0 + ty; t < t1; t += TY) {
     float x[CV];
     if constexpr (CV == 8) {
@@ -1139,7 +1141,7 @@ __global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict_
       for (int e = 0; e < E; ++e) acc[j][e] += __shfl_xor(acc[j][e], o, 64);
   const int R = TY / tyw;  // partial rows of this block (one per wave-row group)
   if (R > 1 && (int64_t)R * C * E <= 16384) {  // fold them in LDS (fixed order): one row per block
-    __shared__ float red[16384];
+    extern __shared__ float red[];  // R * C * E floats (dynamic: 16 KiB at C = 128, E = 8 keeps 8 blocks per CU)
     if (ty % tyw == 0) {
 #pragma unroll
       for (int j = 0; j < CV; ++j)
@@ -1739,8 +1741,9 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
     bool deferred = false;
     float* part = mg_fold_partials((size_t)nb * rows_per_block * C * E * sizeof(float), st, &deferred);
     MG_REQUIRE(part != nullptr, "mg_router_feat_grad: no workspace");
-#define LV_(TT, EE, CC) hipLaunchKernelGGL((k_router_feat_grad_v<TT, EE, CC>), dim3(nb), dim3(256), 0, st, (const TT*)tok, \
-                                           ld, T, C, g_raw, chunk, part)
+    const size_t smem = rows_per_block == 1 ? (size_t)R * C * E * sizeof(float) : 0;
+#define LV_(TT, EE, CC) hipLaunchKernelGGL((k_router_feat_grad_v<TT, EE, CC>), dim3(nb), dim3(256), smem, st, \
+                                           (const TT*)tok, ld, T, C, g_raw, chunk, part)
 #define LVE_(TT) if (E == 4) LV_(TT, 4, 8); else if (E == 8) LV_(TT, 8, 8); else if (E == 16) LV_(TT, 16, 4); \
                  else LV_(TT, 32, 2)
     if (dtype == MG_F32) { LVE_(float); } else { LVE_(bf16_t); }
