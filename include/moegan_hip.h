@@ -361,6 +361,14 @@ int mg_grouped_colsum(int dtype, const void* X, int64_t ld, const int32_t* idx, 
 
 /* BayesianRouter.kl_divergence (t2i_moe_gan.py:405-423): out[0] = clamped KL, out[1] = gradient-pass flag. */
 int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const float* mu_t, const float* rho_t, int nt, const float* mu_c, const float* rho_c, int nc, float* out, void* stream);
+/* The KL terms of up to 8 routers in two launches (the generator's per-block routers at the start of its forward;
+   replaces one mg_router_kl pair per block, t2i_moe_gan.py:405-423): out[2 j] = KL of record j, out[2 j + 1] = its
+   pass flag, bit-identical to mg_router_kl on the same record. */
+typedef struct {
+  const float* mu_f; const float* rho_f; const float* mu_t; const float* rho_t; const float* mu_c; const float* rho_c;
+  int32_t nf; int32_t nt; int32_t nc; int32_t pad;
+} mg_kl_rec;
+int mg_router_kl_batch(int n, const mg_kl_rec* recs, float* out, void* stream);
 
 /* Router parameter gradients: reparameterisation chain (gW, NULL = none) + KL term (coefficient *kl_coef).
    flags[0] & mask (optional): drop the gW chain -- a non-finite generator loss was replaced by 0 and only the

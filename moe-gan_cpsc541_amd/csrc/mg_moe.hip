@@ -1338,15 +1338,16 @@ __global__ __launch_bounds__(256) void k_grouped_colsum_fold(const float* __rest
 
 // KL of one router, two passes: per-block partial sums over the three (mu, rho) pairs, then one block
 // folds the partials and applies the reference's nan/inf/clamp rules.
-__global__ __launch_bounds__(256) void k_router_kl_part(const float* __restrict__ mf, const float* __restrict__ rf,
-                                                        int nf, const float* __restrict__ mt,
-                                                        const float* __restrict__ rt, int nt,
-                                                        const float* __restrict__ mc, const float* __restrict__ rc,
-                                                        int nc, float* __restrict__ part) {
+// 0.5 sum(sigma^2 + mu^2 - 1 - log sigma^2) over one router's three (mu, rho) pairs, one partial per block of a
+// grid-stride split into nparts blocks
+MG_DEV void router_kl_part_block(const float* __restrict__ mf, const float* __restrict__ rf, int nf,
+                                 const float* __restrict__ mt, const float* __restrict__ rt, int nt,
+                                 const float* __restrict__ mc, const float* __restrict__ rc, int nc, int part_i,
+                                 int nparts, float* __restrict__ part) {
   __shared__ float red[4];
   const int64_t n = (int64_t)nf + nt + nc;
   float ps = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = (int64_t)part_i * 256 + threadIdx.x; i < n; i += (int64_t)nparts * 256) {
     float m, r;
     if (i < nf) { m = mf[i]; r = rf[i]; }
     else if (i < nf + nt) { m = mt[i - nf]; r = rt[i - nf]; }
@@ -1358,10 +1359,32 @@ __global__ __launch_bounds__(256) void k_router_kl_part(const float* __restrict_
   ps = wave_sum(ps);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ps;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = 0.5f * (red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) part[part_i] = 0.5f * (red[0] + red[1] + red[2] + red[3]);
 }
 
-__global__ void k_router_kl_fin(const float* __restrict__ part, int nparts, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_router_kl_part(const float* __restrict__ mf, const float* __restrict__ rf,
+                                                        int nf, const float* __restrict__ mt,
+                                                        const float* __restrict__ rt, int nt,
+                                                        const float* __restrict__ mc, const float* __restrict__ rc,
+                                                        int nc, float* __restrict__ part) {
+  router_kl_part_block(mf, rf, nf, mt, rt, nt, mc, rc, nc, blockIdx.x, gridDim.x, part);
+}
+
+// several routers: blockIdx.y = record, each with its own number of partials (the single-router split, so the
+// terms are bit-identical to mg_router_kl's); partials of record j at part + 256 j
+constexpr int KL_MAX_RECS = 8;
+struct KlBatch {
+  mg_kl_rec r[KL_MAX_RECS];
+  int nparts[KL_MAX_RECS];
+};
+__global__ __launch_bounds__(256) void k_router_kl_part_batch(KlBatch b, float* __restrict__ part) {
+  const int j = blockIdx.y;
+  const mg_kl_rec& r = b.r[j];
+  if ((int)blockIdx.x >= b.nparts[j]) return;  // block-uniform
+  router_kl_part_block(r.mu_f, r.rho_f, r.nf, r.mu_t, r.rho_t, r.nt, r.mu_c, r.rho_c, r.nc, blockIdx.x, b.nparts[j],
+                       part + 256 * j);
+}
+MG_DEV void router_kl_fin_wave(const float* __restrict__ part, int nparts, float* __restrict__ out) {
   float s = 0.f;
   for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
   s = wave_sum(s);
@@ -1375,6 +1398,12 @@ __global__ void k_router_kl_fin(const float* __restrict__ part, int nparts, floa
     out[0] = v;
     out[1] = pass;
   }
+}
+__global__ void k_router_kl_fin(const float* __restrict__ part, int nparts, float* __restrict__ out) {
+  router_kl_fin_wave(part, nparts, out);
+}
+__global__ void k_router_kl_fin_batch(KlBatch b, const float* __restrict__ part, float* __restrict__ out) {
+  router_kl_fin_wave(part + 256 * blockIdx.x, b.nparts[blockIdx.x], out + 2 * blockIdx.x);
 }
 
 // KL of one router (t2i_moe_gan.py:405-423): out[0] = clamp(nan_to_num(sum), 0, 120), out[1] = grad-pass flag
@@ -1826,6 +1855,24 @@ extern "C" int mg_router_kl(const float* mu_f, const float* rho_f, int nf, const
                      nc, s_part);
   hipLaunchKernelGGL(k_router_kl_fin, dim3(1), dim3(64), 0, st, s_part, nparts, out);
   return mg_check_launch("mg_router_kl");
+}
+
+extern "C" int mg_router_kl_batch(int n, const mg_kl_rec* recs, float* out, void* stream) {
+  MG_REQUIRE(n >= 1 && n <= KL_MAX_RECS && recs && out, "mg_router_kl_batch: 1..8 records");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  KlBatch b{};
+  int maxp = 1;
+  for (int j = 0; j < n; ++j) {
+    b.r[j] = recs[j];
+    const int64_t m = (int64_t)recs[j].nf + recs[j].nt + recs[j].nc;
+    b.nparts[j] = (int)std::min<int64_t>(256, std::max<int64_t>(1, cdiv(m, 512)));  // as mg_router_kl
+    maxp = std::max(maxp, b.nparts[j]);
+  }
+  float* s_part = reinterpret_cast<float*>(mg_workspace((size_t)256 * n * sizeof(float), st));
+  MG_REQUIRE(s_part, "no workspace");
+  hipLaunchKernelGGL(k_router_kl_part_batch, dim3(maxp, n), dim3(256), 0, st, b, s_part);
+  hipLaunchKernelGGL(k_router_kl_fin_batch, dim3(n), dim3(64), 0, st, b, s_part, out);
+  return mg_check_launch("mg_router_kl_batch");
 }
 
 extern "C" int mg_router_param_bwd(const float* mu, const float* rho, const float* eps, const float* gW, int64_t n,

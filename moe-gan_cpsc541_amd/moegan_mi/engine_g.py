@@ -389,9 +389,12 @@ class GeneratorEngine:
         ops.moe_combine(Y, pos_of, gate, resid, out)  # x_spatial + moe_out (:571)
         kl2 = None
         if train and self._want_kl:
-            kl2 = kl_out if kl_out is not None else torch.empty(2, device=self.dev, dtype=torch.float32)
-            ops.router_kl(self.P(r + "feature_mu"), self.P(r + "feature_rho"), self.P(r + "text_mu"),
-                          self.P(r + "text_rho"), self.P(r + "combined_mu"), self.P(r + "combined_rho"), kl2)
+            if kl_out is not None:  # filled by the forward's batched KL launch (ops.router_kl_batch)
+                kl2 = kl_out
+            else:
+                kl2 = torch.empty(2, device=self.dev, dtype=torch.float32)
+                ops.router_kl(self.P(r + "feature_mu"), self.P(r + "feature_rho"), self.P(r + "text_mu"),
+                              self.P(r + "text_rho"), self.P(r + "combined_mu"), self.P(r + "combined_rho"), kl2)
         sv = None
         if save:
             sv = dict(tok=tok, w=w, HW=HW, eps=eps, anneal=anneal, Wf=Wf, Wt=Wt, Wc=Wc, Wfc=Wfc, u=u, probs=probs,
@@ -759,6 +762,10 @@ class GeneratorEngine:
         # every block's two KL terms in one [blocks, 2] buffer (no stack of per-block results afterwards)
         klbuf = (torch.empty(len(self.attn_blocks), 2, device=self.dev, dtype=torch.float32)
                  if train and self._want_kl else None)
+        if klbuf is not None:  # the KL terms depend on the router parameters only: all blocks in two launches
+            ops.router_kl_batch([tuple(self.P(f"{name}.attn_block.moe.router.{t}") for t in (
+                "feature_mu", "feature_rho", "text_mu", "text_rho", "combined_mu", "combined_rho"))
+                for (name, _, _, _, _, attn) in self.blocks if attn], klbuf)
         img8, rgb8sv = None, None
         x = None
         ai = 0

@@ -798,6 +798,25 @@ def router_kl(mf, rf, mt, rt, mc, rc, out):
     return out
 
 
+class _KlRec(ctypes.Structure):
+    """Mirror of ``mg_kl_rec``."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("mu_f", "rho_f", "mu_t", "rho_t", "mu_c", "rho_c")] + \
+               [(n, ctypes.c_int32) for n in ("nf", "nt", "nc", "pad")]
+
+
+def router_kl_batch(routers, out):
+    """KL terms of several routers in two launches: routers = [(mf, rf, mt, rt, mc, rc), ...], out [n, 2]
+    (row j as router_kl's out for router j, bit-identical)."""
+    for j0 in range(0, len(routers), 8):  # at most 8 records per call
+        group = routers[j0:j0 + 8]
+        recs = (_KlRec * len(group))()
+        for j, (mf, rf, mt, rt, mc, rc) in enumerate(group):
+            recs[j] = _KlRec(ptr(mf), ptr(rf), ptr(mt), ptr(rt), ptr(mc), ptr(rc), mf.numel(), mt.numel(), mc.numel(),
+                             0)
+        call("mg_router_kl_batch", len(group), ctypes.addressof(recs), ptr(out[j0:]), S())
+    return out
+
+
 def kl_coefs(kl2, R, eff_w, coef, total):
     call("mg_kl_coefs", ptr(kl2), R, eff_w, ptr(coef), ptr(total), S())
 

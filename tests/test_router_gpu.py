@@ -197,3 +197,20 @@ def test_warp_fwd_scaled_matches_warp_then_scale(dtype, H, C):
     out2, samp2, xs = ops.warp_fwd(x, o1, w2, b2, s=s)
     assert torch.equal(out, out2) and torch.equal(samp, samp2)
     assert torch.equal(xs, xs_ref)
+
+
+def test_router_kl_batch_bit_identical():
+    """mg_router_kl_batch (every router's KL terms in two launches) == mg_router_kl per router, bit for bit, for
+    routers of different sizes (each record keeps the single-router partial split), and > 8 routers (chunked)."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    routers = []
+    for C, E in ((512, 8), (256, 8), (128, 32), (64, 4), (512, 16), (128, 8), (256, 32), (128, 16), (64, 8)):
+        shapes = ((C, 128), (C, 128), (512, 128), (512, 128), (256, E), (256, E))
+        routers.append(tuple(torch.randn(*sh, device=DEV, generator=g) * (0.3 if i % 2 == 0 else 1.0) - (3.0 if i % 2 else 0.0)
+                             for i, sh in enumerate(shapes)))
+    out = torch.empty(len(routers), 2, device=DEV)
+    ops.router_kl_batch(routers, out)
+    for j, r in enumerate(routers):
+        one = torch.empty(2, device=DEV)
+        ops.router_kl(*r, one)
+        assert torch.equal(out[j], one), (j, out[j], one)
