@@ -206,7 +206,8 @@ def test_router_kl_batch_bit_identical():
     routers = []
     for C, E in ((512, 8), (256, 8), (128, 32), (64, 4), (512, 16), (128, 8), (256, 32), (128, 16), (64, 8)):
         shapes = ((C, 128), (C, 128), (512, 128), (512, 128), (256, E), (256, E))
-        routers.append(tuple(torch.randn(*sh, device=DEV, generator=g) * (0.3 if i % 2 == 0 else 1.0) - (3.0 if i % 2 else 0.0)
+        # mu ~ 0, rho ~ softplus^-1(1): sigma ~ 1, so the sums stay below the 120 clamp (KL ~ 1e-4 per element)
+        routers.append(tuple(torch.randn(*sh, device=DEV, generator=g) * 0.01 + (0.5413 if i % 2 else 0.0)
                              for i, sh in enumerate(shapes)))
     out = torch.empty(len(routers), 2, device=DEV)
     ops.router_kl_batch(routers, out)
@@ -214,3 +215,4 @@ def test_router_kl_batch_bit_identical():
         one = torch.empty(2, device=DEV)
         ops.router_kl(*r, one)
         assert torch.equal(out[j], one), (j, out[j], one)
+        assert one[1].item() == 1.0 and 0.0 < one[0].item() < 120.0  # a real (unclamped) sum
