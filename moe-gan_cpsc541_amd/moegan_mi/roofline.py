@@ -43,7 +43,8 @@ FAMILIES = {
                             "mg_prep_batch")),
     "layernorm": ("hbm", ("mg_layernorm_fwd", "mg_layernorm_bwd")),
     "router_aux": ("hbm", ("mg_router_bwd", "mg_moe_gate_grad", "mg_moe_token_grad", "mg_router_feat_grad",
-                           "mg_router_param_bwd", "mg_router_param_bwd_batch", "mg_moe_dispatch", "mg_router_kl")),
+                           "mg_router_param_bwd", "mg_router_param_bwd_batch", "mg_moe_dispatch", "mg_router_kl",
+                           "mg_router_kl_batch")),
     "im2col_col2im": ("hbm", ("mg_im2col_4x4s2", "mg_col2im_4x4s2")),
     # deferred second passes of the two-pass gradient reductions (mg_fold.hip), one batched launch per kind
     "grad_fold": ("hbm", ("mg_fold_flush", "mg_fold_rows_batch", "mg_fold_rows_queue", "mg_fold_defer")),
