@@ -14,7 +14,7 @@ import sys
 # (key, kernel-name substring, Grid_Size in threads, algorithmic bytes per launch, description)
 B = 256
 KERNELS = [
-    ("moe_ffn_bwd_16", "k_moe_ffn_bwd_w2<128>", 1032 * 512,
+    ("moe_ffn_bwd_16", "k_moe_ffn_bwd_w2<128, 128>", 1032 * 512,
      # gG in (n x C bf16), Pre in (n x 4C), gP out (n x 4C), gX out (n x C); n = 2 * B * 256 routed rows
      (2 * B * 256) * (128 * 2 + 512 * 2 + 512 * 2 + 128 * 2),
      "fused expert FFN backward, 16x16 block (mg_moe_ffn_bwd, C=128, Hd=512, 131072 routed rows)"),
