@@ -395,6 +395,20 @@ __global__ void k_adamw_dev(float* __restrict__ p, const float* __restrict__ g, 
 
 // AdamW + clip coefficient, 4 parameters per thread (16-B loads / stores), optionally also writing the
 // bf16 compute shadow of the updated parameters (the next step's per-step cast, fused away).
+template <bool NT>
+MG_DEV f32x4_t ld4s(const f32x4_t* q) {
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+template <bool NT, typename V>
+MG_DEV void st_s(V* q, V x) {
+  if constexpr (NT) __builtin_nontemporal_store(x, q);
+  else *q = x;
+}
+
+// NT: the optimizer state and gradients stream through non-temporal (cache-streaming) vector loads / stores:
+// every byte is touched once per step, so keeping them out of L2 / MALL leaves those to the parameters' next users
+template <bool NT>
 __global__ __launch_bounds__(256) void k_adamw_dev_v(float* __restrict__ p, const float* __restrict__ g,
                                                      float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                      float lr, float b1, float b2, float eps, float wd,
@@ -428,9 +442,9 @@ __global__ __launch_bounds__(256) void k_adamw_dev_v(float* __restrict__ p, cons
       mv[j] = mj;
       vv[j] = vj;
     }
-    reinterpret_cast<f32x4_t*>(p)[i] = pv;
-    reinterpret_cast<f32x4_t*>(m)[i] = mv;
-    reinterpret_cast<f32x4_t*>(v)[i] = vv;
+    st_s<NT>(reinterpret_cast<f32x4_t*>(p) + i, pv);
+    st_s<NT>(reinterpret_cast<f32x4_t*>(m) + i, mv);
+    st_s<NT>(reinterpret_cast<f32x4_t*>(v) + i, vv);
     if (shadow) {
       u16x4_t h;
 #pragma unroll
@@ -445,12 +459,12 @@ __global__ __launch_bounds__(256) void k_adamw_dev_v(float* __restrict__ p, cons
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   for (; i + stride < n4; i += 2 * stride) {
     const int64_t i2 = i + stride;
-    const f32x4_t pa = p4[i], ga = g4[i], ma = m4[i], va = v4[i];
-    const f32x4_t pb = p4[i2], gb = g4[i2], mb = m4[i2], vb = v4[i2];
+    const f32x4_t pa = ld4s<NT>(p4 + i), ga = ld4s<NT>(g4 + i), ma = ld4s<NT>(m4 + i), va = ld4s<NT>(v4 + i);
+    const f32x4_t pb = ld4s<NT>(p4 + i2), gb = ld4s<NT>(g4 + i2), mb = ld4s<NT>(m4 + i2), vb = ld4s<NT>(v4 + i2);
     upd4(i, pa, ga, ma, va);
     upd4(i2, pb, gb, mb, vb);
   }
-  if (i < n4) upd4(i, p4[i], g4[i], m4[i], v4[i]);
+  if (i < n4) upd4(i, ld4s<NT>(p4 + i), ld4s<NT>(g4 + i), ld4s<NT>(m4 + i), ld4s<NT>(v4 + i));
   for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float pi = p[i], mi = m[i], vi = v[i];
@@ -713,9 +727,15 @@ extern "C" int mg_adamw_dev_shadow(float* p, const float* g, float* m, float* v,
   if (n == 0) return MG_OK;
   MG_REQUIRE(mg_al16(p) && mg_al16(g) && mg_al16(m) && mg_al16(v) &&
              (!shadow_bf16 || (reinterpret_cast<uintptr_t>(shadow_bf16) & 7) == 0), "16-B aligned p/g/m/v, 8-B shadow");
-  hipLaunchKernelGGL(k_adamw_dev_v, dim3(std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4 + 1, 256), 4096))),
-                     dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, sumsq, max_norm,
-                     reinterpret_cast<bf16_t*>(shadow_bf16), flags, skip_mask, win, run_mask);
+  const dim3 grid(std::max<int64_t>(1, std::min<int64_t>(cdiv(n / 4 + 1, 256), 4096)));
+  if (g_mg_tune[MG_TUNE_ADAMW_CACHED] == 1)
+    hipLaunchKernelGGL(k_adamw_dev_v<false>, grid, dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps,
+                       weight_decay, step, sumsq, max_norm, reinterpret_cast<bf16_t*>(shadow_bf16), flags, skip_mask,
+                       win, run_mask);
+  else
+    hipLaunchKernelGGL(k_adamw_dev_v<true>, grid, dim3(256), 0, st, p, g, m, v, n, lr, beta1, beta2, eps,
+                       weight_decay, step, sumsq, max_norm, reinterpret_cast<bf16_t*>(shadow_bf16), flags, skip_mask,
+                       win, run_mask);
   return mg_check_launch("mg_adamw_dev_shadow");
 }
 
