@@ -346,6 +346,90 @@ class bf16_weights(dict):
         return v
 
 
+def mx_quant(x, dim, s=1.0):
+    """OCP MX-fp8 of ``x`` as the device's mg_quant_mx8 forms it (csrc/mg_mx8.hip): blocks of 32 consecutive
+    elements along ``dim`` share one power-of-two scale 2^e with e = ceil(log2(amax / 448)) (so nothing saturates),
+    each element rounded to nearest-even e4m3 at that scale; returned dequantized, in x's dtype.  ``s`` != 1 is the
+    rescaled-grid realization q(x * s) / s (Rounder's construction: the same error distribution, an independent
+    pattern of which values round which way)."""
+    xt = x.detach().movedim(dim, -1).double() * s
+    shp = xt.shape
+    assert shp[-1] % 32 == 0, shp
+    xb = xt.reshape(*shp[:-1], shp[-1] // 32, 32)
+    amax = xb.abs().amax(-1, keepdim=True)
+    m, ex = torch.frexp(amax / 448.0)  # amax / 448 = m * 2^ex, m in [0.5, 1)
+    e = torch.where(m == 0.5, ex - 1, ex)
+    scale = torch.where(amax > 0, torch.ldexp(torch.ones_like(amax), e), torch.ones_like(amax))
+    q = (xb / scale).float().to(torch.float8_e4m3fn).double() * scale
+    return (q.reshape(shp) / s).movedim(-1, dim).to(x.dtype)
+
+
+def _mx8_ok(c):
+    """engine_g.GeneratorEngine._mx8_ok: the MX-fp8 conv reduces over 128-channel steps inside one tap."""
+    return c >= 128 and c % 128 == 0 and (c & (c - 1)) == 0
+
+
+class _MXConv3(torch.autograd.Function):
+    """conv2d(xs, W, padding=1) with the operands the device's MX-fp8 path quantizes (engine_g.mc_fwd / mc_bwd):
+    forward x*s and the packed weight (blocks along Cin per output channel and tap) when Cin qualifies; the data
+    gradient's output gradient and the flipped weight (blocks along Cout per input channel and tap) when Cout
+    qualifies.  The weight gradient takes the unquantized operands (bf16 on the device)."""
+
+    @staticmethod
+    def forward(ctx, xs, W, s):
+        ctx.save_for_backward(xs, W)
+        ctx.s = s
+        Cout, Cin = W.shape[:2]
+        if _mx8_ok(Cin):
+            return torch.nn.functional.conv2d(mx_quant(xs, 1, s), mx_quant(W, 1, s), padding=1)
+        return torch.nn.functional.conv2d(xs, W, padding=1)
+
+    @staticmethod
+    def backward(ctx, g):
+        xs, W = ctx.saved_tensors
+        s = ctx.s
+        if _mx8_ok(W.shape[0]):
+            gx = torch.nn.grad.conv2d_input(xs.shape, mx_quant(W, 0, s), mx_quant(g, 1, s), padding=1)
+        else:
+            gx = torch.nn.grad.conv2d_input(xs.shape, W, g, padding=1)
+        gW = torch.nn.grad.conv2d_weight(xs, W.shape, g, padding=1)
+        return gx, gW, None
+
+
+class mx8_modconv_rounding:
+    """Context manager: oracle.modconv's 3x3 modulated convs evaluated as the MX-fp8 device path computes them --
+    y = d * conv(q(x * s), q(W)) (d the demodulation, s the style), data gradient conv(q(g), q(W_flip)) -- so an
+    oracle step run inside it (together with bf16_module_rounding / bf16_weights / d_round) gives the MX-fp8 step's
+    FLOOR: how far the precision the device stores and multiplies in moves each gradient, in otherwise exact fp32
+    arithmetic.  The factorisation (style on the activation, demodulation on the output) is the reference's math
+    (t2i_moe_gan.py:158-180) regrouped; only where the quantization sits depends on it.  ``rounder``: a Rounder whose
+    grid scale gives the realization (nearest-even grid for Rounder())."""
+
+    def __init__(self, rounder=None):
+        self.s = (rounder or Rounder()).s
+
+    def __enter__(self):
+        self.orig = O.modconv
+        orig, s = self.orig, self.s
+
+        def modconv(x, w, P, pre, padding=0, demod=True):
+            weight = P[pre + "weight"]
+            Cout, Cin, k, _ = weight.shape
+            if k != 3 or padding != 1 or not demod or not (_mx8_ok(Cin) or _mx8_ok(Cout)):
+                return orig(x, w, P, pre, padding, demod)
+            B = x.shape[0]
+            style = O.F.linear(w, P[pre + "modulation.weight"], P[pre + "modulation.bias"])  # :158
+            d = torch.rsqrt((weight.unsqueeze(0) * style.view(B, 1, Cin, 1, 1)).pow(2).sum(dim=(2, 3, 4)) + 1e-8)
+            y = _MXConv3.apply(x * style.view(B, Cin, 1, 1), weight, s)
+            return y * d.view(B, Cout, 1, 1)
+        O.modconv = modconv
+        return self
+
+    def __exit__(self, *exc):
+        O.modconv = self.orig
+        return False
+
+
 def whole(grads, names=None):
     """One vector of every gradient in ``grads`` (dict name -> tensor or None), in a fixed name order."""
     names = sorted(n for n, v in grads.items() if v is not None) if names is None else names
@@ -360,9 +444,10 @@ def whole(grads, names=None):
 BLOCK_OF_HW = {16: "gen_block_4", 64: "gen_block_8", 256: "gen_block_16"}
 
 
-def router_temp_terms(z, topi, g_gate, coef, te, anneal, k):
+def router_temp_terms(z, topi, g_gate, coef, te, anneal, k, parts=False):
     """fp64 restatement of k_router_bwd's temperature term per token from the kernel's own inputs (scaled logits
-    z [T,E], selection topi [T,k], gate gradient [T,k], balance coefficients [E] or None); returns [T]."""
+    z [T,E], selection topi [T,k], gate gradient [T,k], balance coefficients [E] or None); returns [T] (``parts``:
+    also the logit gradient dL/dz [T,E] the term contracts with z)."""
     z = z.double()
     T, E = z.shape
     s = torch.softmax(z.clamp(-20, 20), dim=1)
@@ -384,7 +469,8 @@ def router_temp_terms(z, topi, g_gate, coef, te, anneal, k):
     gs = torch.where((s >= 1e-6) & (s <= 1.0), (gp - d1) / Sq, torch.zeros_like(gp))
     gl = s * (gs - (gs * s).sum(1, keepdim=True))
     gl = torch.where((z >= -20) & (z <= 20), gl, torch.zeros_like(gl))
-    return -(gl * z).sum(1) / te * anneal
+    terms = -(gl * z).sum(1) / te * anneal
+    return (terms, gl) if parts else terms
 
 
 class DeviceTempTap:
@@ -422,10 +508,12 @@ class DeviceTempTap:
         for blk, r in self.rec.items():
             te = min(max(float(r["temperature"].detach().cpu()[0]) * r["anneal"], 0.5), 5.0)
             k = r["topi"].shape[1]
-            terms = router_temp_terms(r["zlog"].detach().cpu(), r["topi"].detach().cpu(),
-                                      r["g_gate"].detach().float().cpu(),
-                                      None if r["coef"] is None else r["coef"].detach().cpu(), te, r["anneal"], k)
-            out[blk] = dict(terms=terms, kernel=float(r["g_temp"].detach().cpu()[0]))
+            z = r["zlog"].detach().cpu()
+            terms, gl = router_temp_terms(z, r["topi"].detach().cpu(), r["g_gate"].detach().float().cpu(),
+                                          None if r["coef"] is None else r["coef"].detach().cpu(), te, r["anneal"], k,
+                                          parts=True)
+            out[blk] = dict(terms=terms, kernel=float(r["g_temp"].detach().cpu()[0]), z=z.double(), gl=gl,
+                            scale=-r["anneal"] / te)
         return out
 
 
@@ -463,6 +551,11 @@ class OracleTempTap:
         s = self.store[block]
         lg, gr = s["logits"].detach().double(), s["logits"].grad.double()
         return -(gr * lg).sum(1) / s["t_eff"] * s["anneal"]
+
+    def parts(self, block):
+        """(scaled logits z [T,E], their gradient dL/dz [T,E], -anneal / t_eff) of the block's G-phase router."""
+        s = self.store[block]
+        return s["logits"].detach().double(), s["logits"].grad.double(), -s["anneal"] / s["t_eff"]
 
 
 def training_router_matches(orig, tapped):

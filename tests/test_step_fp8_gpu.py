@@ -9,24 +9,37 @@ bounded.  Bars (stated per check; measured values printed with pytest -s):
   * generator outputs (images, routing probabilities, the generator loss): relative L2 <= REL8 (measured at
     E=32 top-4, B=4: images 2.3e-2, probabilities <= 2.3e-2, g_gan 3e-3);
   * the generator's whole-model clipped gradient: cosine >= COS8 with the oracle's (measured 0.981: the image
-    gradient passes six MX-fp8 data-gradient convs, each ~3.8 % relative RMS, test_fp8_gpu.py); every tensor
-    with >= 64 elements >= COS8_TENSOR (a wrong sign, transpose or missing term sits far below that), the experts'
-    weights >= COS8_EXPERT (their routed rows are a draw under MX-fp8, see the check; measured 0.816-0.927).  The MTM offset heads' biases (2 / 32 elements, gradients that are sums
-    over all pixels of cancelling warp terms: measured 0.73-0.90) are reported only.  The bf16 mode's bars (test_step_bf16_gpu.py) are the tighter reference.
+    gradient passes six MX-fp8 data-gradient convs, each ~3.8 % relative RMS, test_fp8_gpu.py);
+  * every generator tensor with >= 64 elements, the experts' included: cosine >= COS8_TENSOR, or a relative error
+    within FLOOR_X x the largest of its MX-fp8 FLOOR realizations, and never above RATIO_MAX x its RMS floor.  The
+    FLOOR is the same oracle step (device routes replayed) with everything the device stores in bf16 rounded
+    (test_step_bf16_gpu.py's floor: bf16_module_rounding, bf16_weights, d_round) AND the 3x3 modulated convs
+    evaluated as the device's MX-fp8 path computes them: x * s, the packed weights, the output gradient and the
+    flipped weights quantized to e4m3 with one power-of-two scale per 32 reduction elements (steputil
+    mx8_modconv_rounding / mx_quant, the quantizer of csrc/mg_mx8.hip restated).  FLOOR_RUNS realizations:
+    nearest-even grids, and the rescaled grids q(x * s) / s of steputil.Rounder (same error distribution,
+    independent pattern).  An expert holds ~32 routed rows at B = 4, so its floor is large and heavy-tailed; the
+    yardstick is measured on the oracle, never on a second device run.  The MTM offset heads' biases (2 / 32
+    elements, gradients that are sums over all pixels of cancelling warp terms) and tensors whose reference gradient
+    is < 1e-4 of the model's are reported only.  The bf16 mode's bars (test_step_bf16_gpu.py) are the tighter
+    reference.
 The kernel-level exactness of the MX-fp8 conv (vs the dequantized operands) is test_fp8_gpu.py's job.
 """
 import pytest
 import torch
 
 from oracle import aurora_cpu as O
-from steputil import cosine, gpu_step, make_inputs, nchw, oracle_models, rel_norm_diff
+from steputil import (Rounder, bf16_module_rounding, bf16_weights, cosine, gpu_step, make_inputs, mx8_modconv_rounding,
+                      nchw, oracle_clone, oracle_models, rel_norm_diff)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 REL8 = 0.12      # fp8-touched outputs, relative L2
 COS8 = 0.97      # generator whole-model gradient cosine
-COS8_TENSOR = 0.85
-COS8_EXPERT = 0.7  # per-expert tensors (B = 4: ~32 routed rows each, see the check)
+COS8_TENSOR = 0.85  # every >= 64-element generator tensor's direction ...
+FLOOR_X = 2.5      # ... or its relative error within FLOOR_X x the largest MX-fp8 floor realization
+RATIO_MAX = 5.0    # and never above RATIO_MAX x its RMS floor
+FLOOR_RUNS = 5     # floor realizations: nearest-even + 4 rescaled grids (steputil.Rounder)
 EFF_KL = 0.001 * 1e-5
 torch.set_num_threads(8)
 
@@ -50,6 +63,18 @@ def test_fp8_step_vs_oracle(E, topk, B):
         with torch.no_grad():
             for n, t in P.items():
                 t.copy_(d_after[n].view(t.shape))
+    # the MX-fp8 floor (before the reference run, which steps PG / PD in place)
+    floors = []
+    for fi in range(FLOOR_RUNS):
+        rounder = Rounder() if fi == 0 else Rounder(seed=fi)
+        PGw, PDw, optGw, optDw, wgrads = oracle_clone(PG, PD, optG, optD)
+        PGw_r = bf16_weights(PGw)
+        PGw_r.rounder = rounder
+        with mx8_modconv_rounding(rounder), bf16_module_rounding(rounder=rounder):
+            O.train_step(PGw_r, PDw, optGw, optDw, real, text, z, eps_d, eps_g, perm.long(), topk=topk,
+                         kl_weight_eff=EFF_KL, routes_d=routes_d, routes_g=routes_g, d_round=rounder.d_round(),
+                         after_d_step=use_device_d)
+        floors.append(wgrads)
     ref = O.train_step(PG, PD, optG, optD, real, text, z, eps_d, eps_g, perm.long(), topk=topk, kl_weight_eff=EFF_KL,
                        routes_d=routes_d, routes_g=routes_g, full=True, after_d_step=use_device_d)
     report, fails = [], []
@@ -90,32 +115,43 @@ def test_fp8_step_vs_oracle(E, topk, B):
             g = (gbuf[off:off + numel] * coef).cpu()
             a.append(g.reshape(-1))
             b.append(rg.reshape(-1))
-            worst.append((cosine(g, rg), n, float(rg.double().norm()) if rg.numel() >= 64 else 0.0))
+            rn = rel_norm_diff(g, rg)
+            fws = [rel_norm_diff(f[which][n], rg) for f in floors]
+            fw = (sum(e * e for e in fws) / len(fws)) ** 0.5  # RMS floor over the realizations
+            worst.append((cosine(g, rg), n, float(rg.double().norm()) if rg.numel() >= 64 else 0.0, rn, fw, max(fws)))
         cg = cosine(torch.cat(a), torch.cat(b))
         # tensors whose reference gradient is negligible (< 1e-4 of the whole model's, e.g. the scalar router
         # temperature under top-k renormalisation) or that have fewer than 64 elements (the MTM offset heads'
         # 2- / 32-element biases: sums over every pixel of warp-gradient terms that largely cancel) have no stable
         # direction at this precision: reported only, and still inside the whole-model cosine
         gnorm = float(torch.cat(b).double().norm())
-        tiny = [(c, n) for c, n, r in worst if r < 1e-4 * gnorm]
+        tiny = [(c, n) for c, n, r, *_ in worst if r < 1e-4 * gnorm]
         if tiny:
             report.append(f"{which}: small / negligible-gradient tensors (direction not asserted): " +
                           ", ".join(f"{n} {c:.3f}" for c, n in tiny))
-        worst = sorted((c, n) for c, n, r in worst if r >= 1e-4 * gnorm)
+        worst = sorted(w for w in worst if w[2] >= 1e-4 * gnorm)
         check(cg >= bar, f"{which}: whole-model gradient cosine {cg:.6f} (bar {bar}); worst tensors " +
-              ", ".join(f"{n} {c:.4f}" for c, n in worst[:3]))
-        tb = 0.9 if which == "D" else COS8_TENSOR
-        # expert weights are a draw at B = 4: an expert holds ~32 routed rows, and the MX-fp8 activations between the
-        # MoE layers turn any 1e-5 perturbation into %-level rounding flips, so which tokens reach an expert (and
-        # how noisy they are) changes with the summation order of any upstream kernel (tools/router_ab_probe.py:
-        # the router's MFMA and lane-FMA forms, equal to 1e-5, route 2 / 36 tokens of layers 1 / 2 differently and
-        # their per-expert gradients differ by up to 2.4x relative L2 from each other; against the oracle the worst
-        # expert measured 0.816 / 0.859 between the two forms).  Experts: COS8_EXPERT; everything else: tb
-        other = [(c, n) for c, n in worst if ".moe.experts." not in n]
-        experts = [(c, n) for c, n in worst if ".moe.experts." in n]
-        check(other[0][0] >= tb, f"{which}: every non-expert tensor cosine >= {tb} (min {other[0][0]:.4f} {other[0][1]})")
-        if experts:
-            check(experts[0][0] >= COS8_EXPERT,
-                  f"{which}: every expert tensor cosine >= {COS8_EXPERT} (min {experts[0][0]:.4f} {experts[0][1]})")
+              ", ".join(f"{n} {c:.4f}" for c, n, *_ in worst[:3]))
+        if which == "D":  # no fp8 operand: every tensor >= 0.9
+            check(worst[0][0] >= 0.9, f"D: every tensor cosine >= 0.9 (min {worst[0][0]:.4f} {worst[0][1]})")
+            continue
+        # every non-expert generator tensor: cosine >= COS8_TENSOR; every expert tensor (~32 routed rows at B = 4: a
+        # heavy-tailed floor): cosine >= COS8_TENSOR or within FLOOR_X x its largest MX-fp8 floor realization; and
+        # no tensor's error above RATIO_MAX x its RMS floor
+        other = [w for w in worst if ".moe.experts." not in w[1]]
+        check(other[0][0] >= COS8_TENSOR,
+              f"G: every non-expert tensor cosine >= {COS8_TENSOR} (min {other[0][0]:.4f} {other[0][1]})")
+        for c, n, _, rn, fw, fmax in worst:
+            if ".moe.experts." in n:
+                check(c >= COS8_TENSOR or rn <= FLOOR_X * fmax,
+                      f"G:{n} cosine {c:.4f} rel {rn:.3e} (MX-fp8 floor {fw:.3e}, largest realization {fmax:.3e})")
+        ratios = sorted((rn / max(fw, 1e-12), n) for c, n, _, rn, fw, fmax in worst)
+        ex = [x for x, n in ratios if ".moe.experts." in n]
+        check(ratios[-1][0] <= RATIO_MAX,
+              f"G: gradient error / MX-fp8 floor: median {ratios[len(ratios) // 2][0]:.2f}, max {ratios[-1][0]:.2f} "
+              f"over {len(ratios)} tensors (experts: median {ex[len(ex) // 2] if ex else 0:.2f}, max "
+              f"{ex[-1] if ex else 0:.2f}); largest " + ", ".join(f"{n} {x:.2f}" for x, n in ratios[-4:]))
+        report.append("G: worst cosines " + ", ".join(f"{n} {c:.4f} rel {rn:.2e} (floor {fw:.2e})"
+                                                   for c, n, _, rn, fw, _ in worst[:4]))
     print("\n".join(report))
     assert not fails, fails
