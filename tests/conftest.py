@@ -22,3 +22,16 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _library_tuning():
+    """MOEGAN_TUNE="slot=value,..." (the bench's A/B switch) applied to the HIP library for a whole test session,
+    so a parity test can be re-run on an alternative kernel form (e.g. slot 24: the router's lane-FMA forms)."""
+    spec = os.environ.get("MOEGAN_TUNE", "")
+    if spec:
+        from moegan_mi import _lib
+        for kv in filter(None, spec.split(",")):
+            k, v = kv.split("=")
+            _lib.call("mg_set_tuning", int(k), int(v))
+    yield
