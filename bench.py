@@ -268,6 +268,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
+    world_seen = 1
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -276,6 +277,8 @@ def main():
         else:
             dist.init_process_group(args.backend, rank=rank, world_size=world)
         pg = dist.group.WORLD
+        world_seen = dist.get_world_size(pg)
+        assert world_seen == world, (world_seen, world)
 
     from moegan_mi import ops
     from moegan_mi import _lib
@@ -519,6 +522,7 @@ def main():
                            else f"C2: 64x64, {E} experts top-{k}, batch {B}/GPU, {args.dtype}"
                                 + (" + MX-fp8 3x3 convs" if args.fp8 else "") + ", R1 on",
                            "global_batch": B * world, "experts": E, "topk": k, "parallelism": f"dp{world}",
+                           "world_seen": world_seen,
                            "launch": "eager" if args.eager else "hipGraph replay"},
                 "step_tflops_algorithmic": round(step_tflops, 2),
                 "step_mfma_frac": round(step_tflops / peak, 4), "finite": finite,

@@ -128,6 +128,66 @@ def test_two_rank_bf16_topk_accumulation_window(tmp_path):
         assert c >= 0.99, (key, c)
 
 
+def test_four_rank_skewed_topk_trainstep(tmp_path):
+    """C3's routing (E=8 top-2) over 4 ranks whose shards route unevenly (ddp_worker.skew_inputs: each rank's
+    captions share a rank-specific direction, so each rank loads its own experts): the [E] load all-reduce must
+    produce the single process's global balance loss on every rank, and the bucketed G all-reduce (expert ranges
+    handed over during the backward, complement at the end) the single process's gradients -- including experts
+    that only some ranks touched.  fp32, 4 gloo ranks x B = 2 on cuda:0 against one process stepping all 8
+    images with the block-diagonal permutation."""
+    import torch.multiprocessing as mp
+    from ddp_worker import run, skew_inputs
+    world, B, E, k = 4, 2, 8, 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=run, args=(r, world, port, str(tmp_path), B, E, 16, k, "fp32", 1, 6.0))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0, p.exitcode
+    res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    assert all(res[r]["world_seen"] == world for r in range(world))
+    real, text, z, eps_d, eps_g, _ = skew_inputs(make_inputs(B * world, E, seed=7), B, world, 6.0)
+    perm = torch.cat([res[r]["local_perm"] + r * B for r in range(world)])
+    ts = gpu_step(E, k, "fp32", "cuda")
+    cu = lambda t: t.to("cuda")  # noqa: E731
+    out = ts.step(cu(real), cu(text), cu(z), [tuple(map(cu, e)) for e in eps_d], [tuple(map(cu, e)) for e in eps_g],
+                  cu(perm.int()), anneal=3.0, eff_kl_weight=0.001 * 1e-5)
+    torch.cuda.synchronize()
+    # the shards really are skewed: per-rank expert loads of the last MoE layer differ, and the ranks' selections
+    # are the single process's rows (routing is per token)
+    loads = [torch.bincount(res[r]["topi"][-1].reshape(-1).long(), minlength=E) for r in range(world)]
+    print("per-rank last-layer expert loads:", [l.tolist() for l in loads])
+    assert len({tuple(l.tolist()) for l in loads}) > 1
+    spread = torch.stack(loads).float()
+    assert float((spread.max(0).values - spread.min(0).values).max()) >= 0.25 * float(spread.sum(1).mean())
+    for li in range(3):
+        ref_t = out["topi"][li].cpu().sort(1).values
+        n = ref_t.shape[0] // world
+        for r in range(world):
+            got = res[r]["topi"][li].sort(1).values
+            assert torch.equal(got, ref_t[r * n:(r + 1) * n]), (li, r)
+    for r in range(world):
+        assert abs(float(res[r]["balance"][0]) - float(out["balance"][0])) <= 1e-4 * float(out["balance"][0]) + 1e-7
+    for kk in ("d_losses", "r1", "g_gan"):
+        avg = sum(float(res[r][kk][0]) for r in range(world)) / world
+        assert abs(avg - float(out[kk][0])) <= 1e-4 * abs(float(out[kk][0])) + 1e-6, kk
+    for key, ref in (("d_grad", out["d_grad"]), ("g_grad", out["g_grad"])):
+        for r in range(world):
+            got = res[r][key]
+            assert cosine(got, ref) >= 0.99999 and rel_norm_diff(got, ref) <= 1e-3, (key, r)
+    # expert ranges one rank never touched still carry the other ranks' gradient after the bucketed all-reduce
+    for key, ref in (("d_data", ts.ds.data), ("g_data", ts.gs.data)):
+        for r in range(1, world):
+            assert torch.equal(res[0][key], res[r][key]), (key, r)
+        assert rel_norm_diff(res[0][key], ref) <= 1e-5, key
+
+
 def test_bench_two_rank_graph_replay():
     """bench.py's N>1 path (captured hipGraph segments + eager all-reduces) with 2 gloo ranks on one GPU."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
@@ -141,3 +201,4 @@ def test_bench_two_rank_graph_replay():
     line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
     rec = json.loads(line)
     assert rec["n_gpus"] == 2 and rec["finite"] and rec["value"] > 0
+    assert rec["config"]["world_seen"] == 2  # the rank count the process group reported
