@@ -533,10 +533,12 @@ class OracleTempTap:
             wt = O.reparam(P[pre + "text_mu"], P[pre + "text_rho"], eps[1])
             wc = O.reparam(P[pre + "combined_mu"], P[pre + "combined_rho"], eps[2])
             t_eff = (P[pre + "temperature"] * anneal).clamp(0.5, 5.0)  # :375
-            logits = ((torch.cat([feature @ wf, text @ wt], dim=1) @ wc) / t_eff).clamp(-20.0, 20.0)
+            raw = (torch.cat([feature @ wf, text @ wt], dim=1) @ wc) / t_eff
+            logits = raw.clamp(-20.0, 20.0)  # :378
             if logits.requires_grad:
                 logits.retain_grad()
-                store[pre.split(".")[0]] = dict(logits=logits, t_eff=float(t_eff.detach()), anneal=anneal)
+                store[pre.split(".")[0]] = dict(logits=logits, raw=raw.detach(), t_eff=float(t_eff.detach()),
+                                                anneal=anneal)
             probs = torch.softmax(logits, dim=1).clamp(1e-6, 1.0)
             return probs / probs.sum(dim=1, keepdim=True), logits
         assert training_router_matches(self.orig, router)
@@ -547,15 +549,19 @@ class OracleTempTap:
         O.router = self.orig
         return False
 
-    def terms(self, block):
-        s = self.store[block]
-        lg, gr = s["logits"].detach().double(), s["logits"].grad.double()
-        return -(gr * lg).sum(1) / s["t_eff"] * s["anneal"]
-
     def parts(self, block):
-        """(scaled logits z [T,E], their gradient dL/dz [T,E], -anneal / t_eff) of the block's G-phase router."""
+        """(scaled logits z [T,E] before the clamp -- the device's zlog --, the gradient dL/dz that reaches them
+        [T,E], -anneal / t_eff) of the block's G-phase router.  The clamp to [-20, 20] (:378) passes no gradient
+        where it is active, so there the temperature receives nothing: dL/dz is zeroed where |z| > 20 (the clamp
+        output's own gradient is not)."""
         s = self.store[block]
-        return s["logits"].detach().double(), s["logits"].grad.double(), -s["anneal"] / s["t_eff"]
+        z = s["raw"].double()
+        gl = torch.where((z >= -20.0) & (z <= 20.0), s["logits"].grad.double(), torch.zeros_like(z))
+        return z, gl, -s["anneal"] / s["t_eff"]
+
+    def terms(self, block):
+        z, gl, sc = self.parts(block)
+        return sc * (gl * z).sum(1)
 
 
 def training_router_matches(orig, tapped):
