@@ -102,7 +102,7 @@ def test_discriminator_module_bf16_direct_kernel_limits(res):
     """The bf16 discriminator at a size the direct conv_layers.0 / head kernels take (64: W/2 = 32, Hf = 16) and at
     one past their limits (256: W/2 = 128 > 64, Hf = 64 > 32), which falls back to im2col + GEMMs and the GEMM head
     (DiscriminatorEngine._d0_ok / _head_ok; the implicit convs of conv_layers.2 take power-of-two sizes): logits and
-    the image gradient against the fp32 oracle: relative L2 within 2e-2, or within 2.5x the bf16 floor of the same
+    the image gradient against the fp32 oracle: relative L2 within 2e-2, or within 1.5x the bf16 floor of the same
     oracle (steputil.Rounder.d_round: image, effective weights and the two conv activations rounded to bf16 in value
     and gradient; root-mean-square over 3 realizations) -- the image gradient sums many cancelling bf16 terms."""
     M = _M()
@@ -135,8 +135,10 @@ def test_discriminator_module_bf16_direct_kernel_limits(res):
     f_o, f_g = (sum(floors_o) / 3) ** 0.5, (sum(floors_g) / 3) ** 0.5
     e_o, e_g = rel(out, ref.detach()), rel(gimg.grad, ximg.grad)
     print(f"res {res}: logits rel {e_o:.3e} (bf16 floor {f_o:.3e}), image gradient rel {e_g:.3e} (floor {f_g:.3e})")
-    assert e_o <= max(2e-2, 2.5 * f_o), (e_o, f_o)
-    assert e_g <= max(2e-2, 2.5 * f_g), (e_g, f_g)
+    # the image gradient's bar is the step test's R1 input-gradient bar (test_step_bf16_gpu.py: 1.5x its bf16 floor);
+    # measured device / floor 0.98 at 64 and 1.00 at 256 (gpurun_out/s6a_tests.log), logits 0.5-0.6x
+    assert e_o <= max(2e-2, 1.5 * f_o), (e_o, f_o)
+    assert e_g <= max(2e-2, 1.5 * f_g), (e_g, f_g)
 
 
 def test_sample_and_checkpoint_roundtrip(tmp_path):
