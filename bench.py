@@ -49,13 +49,12 @@ def parse():
                     help="comma-separated configs measured after the headline one, each in a child bench.py process "
                          "(N=1 only), reported under 'secondary' in the same JSON line; '' to skip")
     ap.add_argument("--cpu-steps", type=int, default=12, help="timed CPU-oracle steps (B=8; ~10-20 s of CPU work)")
-    ap.add_argument("--time-kernel", default="d_conv1",
-                    help="kernel whose launches are timed with HIP events for the roofline field")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the captured hipGraphs")
     ap.add_argument("--backend", default="nccl", help="process-group backend for N>1 (nccl = RCCL)")
     ap.add_argument("--no-families", action="store_true",
-                    help="skip the per-family roofline attribution step (one extra eager step after the timed region)")
+                    help="skip the per-family roofline attribution step (one extra eager step before the capture, "
+                         "outside the timed region) and with it the live roofline kernel")
     ap.add_argument("--one-device", action="store_true",
                     help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box, with --backend gloo)")
     args = ap.parse_args()
@@ -222,6 +221,84 @@ def loop_bench(args, dev):
             "batches_timed": n - 1 - args.warmup}
 
 
+def _prof(args, B, E, name):
+    """A committed rocprofv3 record of this same workload (tools/gpu.sh prof / pmc): the config's own file
+    (family_time_C5.json ...) first, then the C2 one; None unless batch / dtype / experts / fp8 / res match."""
+    stem, ext = os.path.splitext(name)
+    for path in (os.path.join(REPO, "profiles", f"{stem}_{args.config}{ext}"), os.path.join(REPO, "profiles", name)):
+        if not os.path.exists(path):
+            continue
+        rec = json.load(open(path))
+        ok = (rec.get("batch") == B and rec.get("dtype") == args.dtype and rec.get("experts") == E and
+              bool(rec.get("fp8", False)) == args.fp8 and rec.get("max_res", 16) == args.max_res)
+        if ok:
+            return rec
+    return None
+
+
+def _fam_time(f):
+    """A family's time per step: the committed rocprof figure where there is one, else the live event time."""
+    return f.get("rocprof_ms_per_step", f.get("event_ms_per_step", f.get("ms_per_step", 0.0)))
+
+
+ROOFLINE_KERNEL_FILE = os.path.join(REPO, "profiles", "roofline_kernel.json")
+
+
+def roofline_record(args, B, E, k, families, roof_call, kms, step_ms):
+    """The ``roofline`` object: the dominant family (most time per step) and its largest call, timed live over the
+    timed region with fence-free HIP events (``kms``: ms per launch).  ``profiles/roofline_kernel.json``
+    (tools/roofline_kernel.py, from a rocprofv3 kernel trace and the PMC FETCH_SIZE / WRITE_SIZE passes of this
+    same bench command, the call's dispatches found between its mg_mark kernels) supplies the rocprof duration and
+    the HBM traffic of the same call where its signature and workload match."""
+    roof = {}
+    if families:
+        dom = max((f for f in families if f["bound"] is not None), key=_fam_time, default=None)
+        if dom is not None:
+            roof["dominant"] = {kk: dom.get(kk) for kk in ("family", "bound", "achieved", "peak", "unit", "frac",
+                                                          "launches_per_step", "gflop_per_step", "mb_per_step",
+                                                          "time_source")}
+            roof["dominant"].update({"ms_per_step": round(_fam_time(dom), 4),
+                                     "traffic_mb_per_step": dom.get("traffic_mb_per_step"),
+                                     "share_of_step": round(_fam_time(dom) / step_ms, 4)})
+    if roof_call is None:
+        roof.update({"bound": None, "kernel": None, "achieved": None, "peak": None, "unit": None, "frac": None,
+                     "traffic": None, "note": "no attribution step (--no-families): no roofline kernel"})
+        return roof
+    fam = roof_call["family"]
+    mfma = fam["bound"] == "mfma"
+    peak = fam["peak"]
+    work = roof_call["work_per_launch"] or 0.0
+    avg_ms = sum(kms) / len(kms) if kms else None
+
+    def rate(ms_):
+        if not ms_:
+            return None
+        return work / (ms_ * 1e-3) / (1e12 if mfma else 1e9)
+    ach = rate(avg_ms)
+    shape = ", ".join(f"{a}={v}" for a, v in roof_call["args"].items() if a not in ("dtype",))
+    roof.update({"bound": fam["bound"], "family": fam["family"],
+                 "kernel": f"{roof_call['entry']}({shape}): the largest call of the dominant family {fam['family']} "
+                           f"({roof_call['launches_per_step']:.0f} launches per step)",
+                 "achieved": round(ach, 2) if ach else None, "peak": peak, "unit": fam["unit"],
+                 "frac": round(ach / peak, 4) if ach else None,
+                 "algorithmic_per_launch": work, "algorithmic_unit": "FLOP" if mfma else "bytes",
+                 "algorithmic_bytes_per_launch": work if not mfma else roof_call.get("bytes_per_launch"),
+                 "launches_timed": len(kms), "avg_launch_ms": round(avg_ms, 4) if avg_ms else None,
+                 "time_source": "fence-free HIP events over the timed region (mg_timer_event_*)",
+                 "traffic": None, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"})
+    rec = None
+    if os.path.exists(ROOFLINE_KERNEL_FILE):
+        rec = json.load(open(ROOFLINE_KERNEL_FILE)).get(args.config)
+    sig = [roof_call["signature"][0], list(roof_call["signature"][1])]
+    roof["signature"] = sig
+    if rec and rec.get("signature") == sig and rec.get("batch") == B and rec.get("experts") == E:
+        r_ms = rec.get("rocprof_avg_ms")
+        roof.update({"avg_launch_ms_rocprof": r_ms, "frac_rocprof": round(rate(r_ms) / peak, 4) if r_ms else None,
+                     "traffic": rec.get("traffic_bytes_per_launch"), "rocprof_kernels": rec.get("kernels"),
+                     "profile": rec.get("source")})
+    return roof
+
+
 def reap_children():
     """End (and report) any process this bench started that is still alive: the driver counts leftovers."""
     try:
@@ -282,6 +359,7 @@ def main():
 
     from moegan_mi import ops
     from moegan_mi import _lib
+    from moegan_mi import roofline as roofline_mod
     from moegan_mi.graphs import SegmentedGraph
     for kv in filter(None, os.environ.get("MOEGAN_TUNE", "").split(",")):  # A/B switches: "key=value,..."
         k_, v_ = kv.split("=")
@@ -323,14 +401,12 @@ def main():
     def run_step():
         return ts.step(real, text, z, eps_d, eps_g, perm, anneal=3.0, lr_g=2e-4, lr_d=2e-4, eff_kl_weight=1e-8)
 
-    # live timing of the roofline kernel: the largest kernel of the step's dominant family (expert_gemm), the fused
-    # expert FFN backward of the 16x16 block (mg_moe_ffn_bwd: B*256*k routed rows, C = 128, Hd = 512); inactive until
-    # the timed region
-    want_dims = (B * 256 * k, 128, 512)
-    ops.TIMER = ops.KernelTimer(lambda kind, dims: kind == "moe_ffn_bwd" and dims == want_dims, active=False)
-
     graph = None
-    if not args.eager:
+    if args.eager:
+        refill()
+        run_step()  # first-use allocations and code-object loads, before the attributed step
+        torch.cuda.synchronize()
+    else:
         graph = SegmentedGraph()
         refill()
         t_w = time.perf_counter()
@@ -345,59 +421,13 @@ def main():
             print(f"[bench] first eager step {(t_h - t_w) * 1e3:.1f} ms (host enqueue {(t_f - t_w) * 1e3:.1f} ms: "
                   f"first-use allocations + code-object loads); second: host enqueue {(t_e - t_h) * 1e3:.1f} ms, "
                   f"with device {(time.perf_counter() - t_h) * 1e3:.1f} ms", file=sys.stderr, flush=True)
-        out = graph.capture(run_step)
-        torch.cuda.synchronize()
-        if rank == 0:
-            print(f"[bench] captured the step: {graph.n_graphs} graph segment(s), {len(graph.items)} items",
-                  file=sys.stderr, flush=True)
 
-    def one_step():
-        refill()
-        if graph is not None:
-            graph.replay()
-            return out
-        return run_step()
-
-    for i in range(args.warmup):
-        t_w = time.perf_counter()
-        one_step()
-        torch.cuda.synchronize()
-        if rank == 0:
-            print(f"[bench] warmup step {i}: {(time.perf_counter() - t_w) * 1e3:.1f} ms", file=sys.stderr, flush=True)
-
-    ops.TIMER.active = True
-    # per-step device time for the median (SURVEY §8(d)): an event between consecutive steps on the stream the
-    # steps are enqueued on (no host synchronisation inside the timed region)
-    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    if pg is not None:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    step_ev[0].record()
-    for i in range(args.steps):
-        out = one_step()
-        step_ev[i + 1].record()
-        if rank == 0 and (i + 1) % max(1, args.steps // 4) == 0:
-            print(f"[bench] enqueued {i + 1}/{args.steps} steps", file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
-    if pg is not None:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    ops.TIMER.active = False
-    kt = ops.TIMER.results()
-    if pg is not None:
-        t = torch.tensor([elapsed], device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t)
-    finite = bool(torch.isfinite(out["d_losses"]).all() and torch.isfinite(out["g_gan"]).all())
-    step_ms = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(args.steps))
-    median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * sum(step_ms[len(step_ms) // 2 - 1:
-                                                                                      len(step_ms) // 2 + 1])
-
-    families = fam_meta = None
-    if not args.no_families and rank == 0 and world == 1:
-        # per-family roofline: one more eager step (outside the timed region) with every C-ABI call bracketed
-        # by HIP events and its algorithmic work computed from its shape arguments (moegan_mi/roofline.py)
+    # per-family roofline attribution: one eager step (before capture, outside the timed region) with every C-ABI
+    # call bracketed by HIP events and its algorithmic work computed from its shape arguments (moegan_mi/roofline.py).
+    # It also names the roofline kernel: the largest call (signature with the most time per step) of the step's
+    # dominant family, which the timed region then times live (_lib.LiveTimer).
+    families = fam_meta = roof_call = None
+    if not args.no_families:
         from moegan_mi.roofline import Attribution
         refill()
         with Attribution() as at:
@@ -406,26 +436,10 @@ def main():
             else:
                 run_step()
         families = at.summary(steps=1, peak_tflops=MFMA_PEAK_TFLOPS[args.dtype], peak_gbs=HBM_PEAK_GBS)
-        fam_total = sum(f["ms_per_step"] for f in families)
         if rank == 0:
-            print(f"[bench] family attribution: {fam_total:.3f} ms of call time in the attributed step "
-                  f"(host_bound={at.host_bound})", file=sys.stderr, flush=True)
-
-        def _prof(name):  # committed rocprofv3 records of this same workload (tools/gpu_families.sh): the
-            # config's own file (family_time_C5.json ...) first, then the C2 one
-            stem, ext = os.path.splitext(name)
-            for path in (os.path.join(REPO, "profiles", f"{stem}_{args.config}{ext}"),
-                         os.path.join(REPO, "profiles", name)):
-                if not os.path.exists(path):
-                    continue
-                rec = json.load(open(path))
-                ok = (rec.get("batch") == B and rec.get("dtype") == args.dtype and rec.get("experts") == E and
-                      bool(rec.get("fp8", False)) == args.fp8 and rec.get("max_res", 16) == args.max_res)
-                if ok:
-                    return rec
-            return None
-
-        ftime, ftraf = _prof("family_time.json"), _prof("family_traffic.json")
+            print(f"[bench] family attribution: {sum(f['ms_per_step'] for f in families):.3f} ms of call time in the "
+                  f"attributed step (host_bound={at.host_bound})", file=sys.stderr, flush=True)
+        ftime, ftraf = _prof(args, B, E, "family_time.json"), _prof(args, B, E, "family_traffic.json")
         for f in families:
             f["event_ms_per_step"] = f.pop("ms_per_step")  # live, includes ~3 us of event overhead per call
             t = ftime["families"].get(f["family"]) if ftime else None
@@ -450,49 +464,87 @@ def main():
                     "time": ftime["source"] if ftime else "live HIP events per call",
                     "profile_busy_ms_per_step": ftime["busy_ms_per_step"] if ftime else None,
                     "traffic": ftraf["source"] if ftraf else None}
+        dom = max((f for f in families if f["bound"] is not None), key=_fam_time, default=None)
+        if dom is not None:
+            roof_call = at.largest_call(dom["family"])
+            if roof_call is not None:
+                roof_call["family"] = dom
+                _lib.LIVE = _lib.LiveTimer(roof_call["signature"], active=False)
+
+    if graph is not None:
+        out = graph.capture(run_step)
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] captured the step: {graph.n_graphs} graph segment(s), {len(graph.items)} items",
+                  file=sys.stderr, flush=True)
+
+    def one_step():
+        refill()
+        if graph is not None:
+            graph.replay()
+            return out
+        return run_step()
+
+    for i in range(args.warmup):
+        t_w = time.perf_counter()
+        one_step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup step {i}: {(time.perf_counter() - t_w) * 1e3:.1f} ms", file=sys.stderr, flush=True)
+
+    if _lib.LIVE is not None:
+        _lib.LIVE.active = True
+    # per-step device time for the median (SURVEY §8(d)): an event between consecutive steps on the stream the
+    # steps are enqueued on (no host synchronisation inside the timed region)
+    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step_ev[0].record()
+    for i in range(args.steps):
+        out = one_step()
+        step_ev[i + 1].record()
+        if rank == 0 and (i + 1) % max(1, args.steps // 4) == 0:
+            print(f"[bench] enqueued {i + 1}/{args.steps} steps", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    kms = []
+    if _lib.LIVE is not None:
+        _lib.LIVE.active = False
+        kms = _lib.LIVE.results()
+    if pg is not None:
+        t = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t)
+    finite = bool(torch.isfinite(out["d_losses"]).all() and torch.isfinite(out["g_gan"]).all())
+    step_ms = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * sum(step_ms[len(step_ms) // 2 - 1:
+                                                                                      len(step_ms) // 2 + 1])
 
     if rank == 0:
         imgs = B * world * args.steps
         value = imgs / elapsed
         ms = elapsed / args.steps * 1e3
-        kms = [ms_ for _, _, ms_ in kt]
-        avg_ms = sum(kms) / max(len(kms), 1)
-        rows, Cx, Hx = want_dims
-        flop = 4.0 * rows * Cx * Hx  # gH = gG W2 (2 rows C Hd) + gX = gP W1 (2 rows Hd C)
-        achieved = flop / (avg_ms * 1e-3) / 1e12 if kms else None
         peak = MFMA_PEAK_TFLOPS[args.dtype]
-        traffic = alg_bytes = None
-        pmc = os.path.join(REPO, "profiles", "pmc_roofline_kernel.json")
-        if os.path.exists(pmc):  # HBM bytes per launch from the committed rocprofv3 --pmc passes
-            rec = json.load(open(pmc)).get("kernels", {}).get("moe_ffn_bwd_16")
-            if rec and B == 256 and args.dtype == "bf16" and not args.fp8 and args.res == 64 and E == 8 and k == 2:
-                traffic, alg_bytes = rec["traffic_bytes_per_launch"], rec["algorithmic_bytes_per_launch"]
-        roof = {}
-        if families:  # the family that takes the most time in the step leads (rocprof time where committed)
-            def _t(f):
-                return f.get("rocprof_ms_per_step", f["event_ms_per_step"])
-            dom = max((f for f in families if f["bound"] is not None), key=_t, default=None)
-            if dom is not None:
-                roof["dominant"] = {k: dom.get(k) for k in ("family", "bound", "achieved", "peak", "unit", "frac",
-                                                            "launches_per_step", "gflop_per_step", "mb_per_step",
-                                                            "time_source")}
-                roof["dominant"].update({"ms_per_step": round(_t(dom), 4),
-                                         "traffic_mb_per_step": dom.get("traffic_mb_per_step"),
-                                         "share_of_step": round(_t(dom) / ms, 4)})
-        roof.update({"bound": "mfma", "kernel": f"mg_moe_ffn_bwd: fused expert FFN backward of the 16x16 block "
-                                                f"(largest kernel of the dominant family expert_gemm), {rows} routed "
-                                                f"rows, C={Cx}, Hd={Hx}",
-                     "achieved": round(achieved, 2) if achieved else None,
-                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-                     "traffic": traffic, "traffic_unit": "bytes per launch (HBM, PMC)",
-                     "algorithmic_bytes_per_launch": alg_bytes,
-                     "algorithmic_flop_per_launch": flop, "launches_timed": len(kms),
-                     "avg_launch_ms": round(avg_ms, 4)})
+        roof = roofline_record(args, B, E, k, families, roof_call, kms, ms)
         if args.config == "C4":  # extension: no reference FLOP formula; the executed MFMA work (roofline.py)
             gf_step = sum(f.get("gflop_per_step", 0.0) for f in (families or []) if f["bound"] == "mfma")
             step_tflops = gf_step * world / (ms * 1e-3) / 1e3 if gf_step else 0.0
         else:
             step_tflops = gflop_per_image(k) * B * world / (ms * 1e-3) / 1e3
+        step_frac = step_tflops / peak
+        peak_note = f"{args.dtype} dense MFMA peak"
+        fp8_gf = sum(f.get("gflop_per_step", 0.0) for f in (families or []) if f["family"] == "conv_fwd_mx8")
+        if args.fp8 and fp8_gf and args.config != "C4":
+            # the MX-fp8 share of the algorithmic work priced at the fp8 peak, the rest at the bf16 peak
+            all_gf = gflop_per_image(k) * B
+            t_peak = (all_gf - fp8_gf) / (peak * 1e3) + fp8_gf / (roofline_mod.MX8_PEAK_TFLOPS * 1e3)
+            step_frac = t_peak / (ms * 1e-3)
+            peak_note = (f"mixed: {fp8_gf:.0f} of {all_gf:.0f} GFLOP per step on the MX-fp8 peak "
+                         f"({roofline_mod.MX8_PEAK_TFLOPS:.0f} TF/s), the rest on the bf16 peak ({peak:.0f} TF/s)")
         cpu = None
         if not args.no_cpu_baseline and world == 1 and args.config != "C4":
             try:
@@ -525,7 +577,7 @@ def main():
                            "world_seen": world_seen,
                            "launch": "eager" if args.eager else "hipGraph replay"},
                 "step_tflops_algorithmic": round(step_tflops, 2),
-                "step_mfma_frac": round(step_tflops / peak, 4), "finite": finite,
+                "step_mfma_frac": round(step_frac, 4), "step_mfma_peak": peak_note, "finite": finite,
                 "roofline": roof, "cpu_baseline": cpu, "secondary": secondary or None}
         if families:  # the full per-family tables go to a file; the line names it
             _write_families(args.config, dict(line, roofline_families=families, roofline_families_sources=fam_meta,

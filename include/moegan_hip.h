@@ -111,6 +111,20 @@ int64_t mg_workspace_bytes(void* stream);
    order; value 0 = automatic). */
 int mg_set_tuning(int key, int value);
 
+/* Measurement of one call inside a training step (bench.py's roofline kernel; no reference
+   counterpart: the reference times nothing below the Python loop, t2i_moe_gan.py:1262-1421).
+   mg_timer_event_create: a timing event WITHOUT the system-scope release / acquire fence of a default HIP event
+   (hipEventDisableSystemFence): a default event's L2 writeback + invalidate was measured to add ~18 % to the
+   bracketed kernel's time; *event receives the handle.  mg_timer_event_record: record on `stream`.
+   mg_timer_event_elapsed: waits for `stop`, *ms = stop - start.  mg_mark: one empty single-wave kernel,
+   k_roofline_mark_begin (tag 0) or k_roofline_mark_end (tag 1), so a rocprofv3 kernel trace / PMC pass of the same
+   run can find the dispatches the bracketed call made (tools/roofline_kernel.py). */
+int mg_timer_event_create(void** event);
+int mg_timer_event_record(void* event, void* stream);
+int mg_timer_event_elapsed(void* start, void* stop, float* ms);
+int mg_timer_event_destroy(void* event);
+int mg_mark(int tag, void* stream);
+
 /* One problem of a batched GEMM launch (mg_gemm_batch): C[M,N] = epilogue(op(A) @ op(B)). */
 typedef struct mg_gemm_desc {
   int32_t M, N, K;

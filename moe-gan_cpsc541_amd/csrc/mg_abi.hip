@@ -157,3 +157,50 @@ extern "C" int mg_set_tuning(int key, int value) {
 extern "C" const char* mg_last_error(void) { return g_last_error.c_str(); }
 extern "C" int mg_version(void) { return 2; }
 extern "C" const char* mg_source_hash(void) { return MG_SRC_HASH; }
+
+// ---- measurement of one call inside a step (include/moegan_hip.h: mg_timer_event_* / mg_mark) ----
+__global__ void k_roofline_mark_begin() {}
+__global__ void k_roofline_mark_end() {}
+
+extern "C" int mg_timer_event_create(void** event) {
+  MG_REQUIRE(event != nullptr, "event must not be NULL");
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
+    mg_set_error("mg_timer_event_create: hipEventCreateWithFlags failed");
+    return MG_ERR_LAUNCH;
+  }
+  *event = reinterpret_cast<void*>(e);
+  return MG_OK;
+}
+
+extern "C" int mg_timer_event_record(void* event, void* stream) {
+  MG_REQUIRE(event != nullptr, "event must not be NULL");
+  if (hipEventRecord(reinterpret_cast<hipEvent_t>(event), reinterpret_cast<hipStream_t>(stream)) != hipSuccess) {
+    mg_set_error("mg_timer_event_record: hipEventRecord failed");
+    return MG_ERR_LAUNCH;
+  }
+  return MG_OK;
+}
+
+extern "C" int mg_timer_event_elapsed(void* start, void* stop, float* ms) {
+  MG_REQUIRE(start != nullptr && stop != nullptr && ms != nullptr, "events and ms must not be NULL");
+  hipEvent_t s = reinterpret_cast<hipEvent_t>(start), e = reinterpret_cast<hipEvent_t>(stop);
+  if (hipEventSynchronize(e) != hipSuccess || hipEventElapsedTime(ms, s, e) != hipSuccess) {
+    mg_set_error("mg_timer_event_elapsed: hipEventSynchronize / hipEventElapsedTime failed");
+    return MG_ERR_LAUNCH;
+  }
+  return MG_OK;
+}
+
+extern "C" int mg_timer_event_destroy(void* event) {
+  if (event) (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(event));
+  return MG_OK;
+}
+
+extern "C" int mg_mark(int tag, void* stream) {
+  MG_REQUIRE(tag == 0 || tag == 1, "tag must be 0 (begin) or 1 (end)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (tag == 0) hipLaunchKernelGGL(k_roofline_mark_begin, dim3(1), dim3(64), 0, st);
+  else hipLaunchKernelGGL(k_roofline_mark_end, dim3(1), dim3(64), 0, st);
+  return mg_check_launch("mg_mark");
+}

@@ -155,11 +155,86 @@ def exported_symbols():
 
 # Optional observer of every C-ABI call (moegan_mi/roofline.py): HOOK(name, args, run) must call run() once.
 HOOK = None
+# Optional live timer of one call signature (LiveTimer below; bench.py's roofline kernel)
+LIVE = None
+
+
+def scalar_signature(name, args):
+    """(name, the call's integer / float arguments in order): the shape of a call, without its pointers."""
+    types = _SIGS[name][1]
+    vals = []
+    for t, v in zip(types, args):
+        if t in (_i32, _i64, _f32):
+            vals.append(v.value if hasattr(v, "value") else v)
+    return (name, tuple(vals))
+
+
+class LiveTimer:
+    """Times every call whose scalar_signature equals ``signature`` while ``active``: the call becomes an eager
+    segment of a captured step (graphs.eager), bracketed by fence-free HIP events (mg_timer_event_*: a default
+    event's system-scope release writes back and invalidates L2, which inflated the bracketed kernel by ~18 %) and,
+    outside the events, by mg_mark begin / end kernels so a rocprofv3 trace of the same run finds the call's
+    dispatches (tools/roofline_kernel.py).  Marks and events run whether or not ``active``, so every replay has the
+    same dispatch sequence."""
+
+    def __init__(self, signature, active=False):
+        self.signature = signature
+        self.active = active
+        self.pairs = []
+
+    def want(self, name, args):
+        return name == self.signature[0] and scalar_signature(name, args) == self.signature
+
+    def _event(self):
+        h = ctypes.c_void_p()
+        if lib().mg_timer_event_create(ctypes.addressof(h)) != 0:
+            raise MGError(lib().mg_last_error().decode())
+        return h
+
+    def run(self, fn, args):
+        from . import graphs
+
+        # the call enqueues on the stream current when it runs: at a replay of a captured step that is the
+        # stream the graphs replay on, not the capture stream its arguments were built on (the last parameter
+        # of every entry point is the stream)
+        names = ARGNAMES.get(fn.__name__, [])
+        restream = bool(names) and names[-1] == "stream"
+
+        def timed():
+            st = stream()
+            call_args = args[:-1] + (st,) if restream else args
+            lib().mg_mark(0, st)
+            s, e = (self._event(), self._event()) if self.active else (None, None)
+            if s is not None:
+                lib().mg_timer_event_record(s, st)
+            rc = fn(*call_args)
+            if e is not None:
+                lib().mg_timer_event_record(e, st)
+                self.pairs.append((s, e))
+            lib().mg_mark(1, st)
+            return rc
+        return graphs.eager(timed)
+
+    def results(self):
+        """Per timed launch, its duration in ms (waits for the last event); releases the events."""
+        out = []
+        for s, e in self.pairs:
+            ms = ctypes.c_float()
+            if lib().mg_timer_event_elapsed(s, e, ctypes.addressof(ms)) != 0:
+                raise MGError(lib().mg_last_error().decode())
+            out.append(ms.value)
+            lib().mg_timer_event_destroy(s)
+            lib().mg_timer_event_destroy(e)
+        self.pairs = []
+        return out
 
 
 def call(name, *args):
     fn = getattr(lib(), name)
-    rc = fn(*args) if HOOK is None else HOOK(name, args, lambda: fn(*args))
+    if LIVE is not None and LIVE.want(name, args):
+        rc = LIVE.run(fn, args)
+    else:
+        rc = fn(*args) if HOOK is None else HOOK(name, args, lambda: fn(*args))
     if rc != 0:
         raise MGError(f"{name} failed ({rc}): {lib().mg_last_error().decode()}")
 

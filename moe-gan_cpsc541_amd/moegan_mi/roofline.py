@@ -128,6 +128,8 @@ def work(name, a):
         return 2.0 * a["M"] * a["N"] * a["total_rows"]
     if name == "mg_moe_ffn_fwd":  # two GEMMs per routed row
         return 4.0 * a["total_rows"] * a["C"] * a["Hd"]
+    if name == "mg_moe_ffn_bwd":  # gH = gG W2 and gX = gP W1 per routed row
+        return 4.0 * a["total_rows"] * a["C"] * a["Hd"]
     if name == "mg_attn_fwd":  # S = QK^T, O = PV
         return 4.0 * a["B"] * a["L"] * a["L"] * a["C"]
     if name == "mg_attn_bwd":  # dV, dP, dQ, dK (the S recompute is not algorithmic work)
@@ -319,6 +321,32 @@ def work(name, a):
     return None
 
 
+def alg_bytes(name, a):
+    """Compulsory HBM bytes of one MFMA-family call (each operand read once, each output written once); None where
+    not modelled.  Beside work(): an MFMA call's roofline is FLOPs, its traffic is judged against these bytes."""
+    if name == "mg_conv2d_fwd":
+        OH, OW = _conv_out(a["H"], a["W"], a["KH"], a["KW"], a["stride"], a["pad"])
+        e = ELT[a["dtype"]]
+        return (a["B"] * a["H"] * a["W"] * a["Cin"] * e + a["Cout"] * a["KH"] * a["KW"] * a["Cin"] * e +
+                a["B"] * OH * OW * a["Cout"] * ELT[a["y_dtype"]])
+    if name == "mg_conv2d_wgrad":
+        OH, OW = _conv_out(a["H"], a["W"], a["KH"], a["KW"], a["stride"], a["pad"])
+        e = ELT[a["dtype"]]
+        return (a["B"] * OH * OW * a["Cout"] * e + a["B"] * a["H"] * a["W"] * a["Cin"] * e +
+                a["Cout"] * a["Cin"] * a["KH"] * a["KW"] * 4)
+    if name == "mg_gemm":
+        e = ELT[a["dtype"]]
+        return (a["M"] * a["K"] + a["K"] * a["N"]) * e + a["M"] * a["N"] * ELT[a["c_dtype"]]
+    if name == "mg_gemm_grouped":
+        e = ELT[a["dtype"]]
+        return (a["total_rows"] * a["K"] + a["ngroups"] * a["N"] * a["K"]) * e + a["total_rows"] * a["N"] * ELT[a["c_dtype"]]
+    if name == "mg_moe_ffn_bwd":  # gG and gX (C), pre and gP (Hd) per routed row, bf16
+        return a["total_rows"] * (2 * a["C"] + 2 * a["Hd"]) * 2
+    if name == "mg_moe_ffn_fwd":
+        return a["total_rows"] * 2 * a["C"] * 2
+    return None
+
+
 class Attribution:
     """Install with ``with Attribution() as at: run_step()``; then ``at.summary(steps=1)``.
 
@@ -330,6 +358,7 @@ class Attribution:
 
     def __init__(self, lead_ms=150.0, keep_args=False):
         self.calls = []  # (entry point, family, work, start event, end event)
+        self.sigs = []  # _lib.scalar_signature of each call
         self.keep_args = keep_args
         self.args = []  # scalar arguments per call (keep_args)
         self.lead_ms = lead_ms
@@ -350,6 +379,7 @@ class Attribution:
         rc = run()
         e.record()
         self.calls.append((name, _FAMILY_OF.get(name, "other"), w, s, e))
+        self.sigs.append(L.scalar_signature(name, args))
         if self.keep_args:
             self.args.append({k: v for k, v in a.items() if isinstance(v, (int, float))})
         return rc
@@ -380,6 +410,33 @@ class Attribution:
                 ms = s.elapsed_time(e)
                 rows.append((ms, name, w, self.args[i] if self.keep_args else {}))
         return sorted(rows, key=lambda r: -r[0])[:n]
+
+    def largest_call(self, family, steps=1):
+        """The call signature of ``family`` with the most event time per launch (the family's largest kernel):
+        dict(signature, entry, launches_per_step, ms_per_launch, work_per_launch, args {name: value})."""
+        torch.cuda.synchronize()
+        groups = {}
+        for i, (name, f, w, s, e) in enumerate(self.calls):
+            if f != family:
+                continue
+            g = groups.setdefault(self.sigs[i], {"ms": 0.0, "n": 0, "work": w, "i": i})
+            g["ms"] += s.elapsed_time(e)
+            g["n"] += 1
+        if not groups:
+            return None
+        # the largest kernel: the most time per launch (its share per step is reported beside it); a per-step
+        # total would let a cheap call repeated many times win, and flip between near-equal totals run to run
+        sig, g = max(groups.items(), key=lambda kv: (kv[1]["ms"] / kv[1]["n"], kv[1]["ms"]))
+        name = sig[0]
+        types = L._SIGS[name][1]
+        scal = [n for n, t in zip(L.ARGNAMES[name], types) if t in (L._i32, L._i64, L._f32)]
+        args = dict(zip(scal, sig[1]))
+        try:
+            nbytes = alg_bytes(name, args)
+        except KeyError:
+            nbytes = None
+        return {"signature": sig, "entry": name, "launches_per_step": g["n"] / steps, "ms_per_launch": g["ms"] / g["n"],
+                "work_per_launch": g["work"], "bytes_per_launch": nbytes, "args": args}
 
     def summary(self, steps=1, peak_tflops=2500.0, peak_gbs=8000.0):
         torch.cuda.synchronize()

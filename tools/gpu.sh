@@ -58,17 +58,28 @@ for step in "$@"; do
     prof|c5prof)
       extra=""
       fargs=""
-      [ "$step" = c5prof ] && extra="--config C5" && fargs="256 32 bf16 fp8"
+      cfgname=C2
+      [ "$step" = c5prof ] && extra="--config C5" && fargs="256 32 bf16 fp8" && cfgname=C5
+      # with the attribution step (no --no-families): the roofline kernel is chosen, timed and mg_mark-bracketed
       run 400 ${O}_${step}.log rocprofv3 --kernel-trace --stats -d ${O}_${step} -o run --output-format csv -- \
-        python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-families --secondary "" $extra
+        python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --secondary "" $extra
+      grep '^{' ${O}_${step}.log > ${O}_${step}_line.json
       python3 tools/prof_summary.py ${O}_${step}/run_kernel_stats.csv > ${O}_${step}_stats.txt
       FAMILY_LAST=9 python3 tools/family_time.py ${O}_${step}/run_kernel_trace.csv ${O}_${step}_family.json $fargs > ${O}_${step}_family.txt
-      cat ${O}_${step}_family.txt ;;
+      python3 tools/roofline_kernel.py $cfgname ${O}_${step}_line.json ${O}_${step}/run_kernel_trace.csv --last 10 > ${O}_${step}_roofk.txt
+      cat ${O}_${step}_family.txt
+      head -12 ${O}_${step}_roofk.txt ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         run 300 ${O}_pmc_$c.log rocprofv3 --pmc $c -d ${O}_pmc_$c -o run --output-format csv -- \
-          python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-families --secondary "" --eager
+          python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --secondary "" --eager
       done
+      if [ -f ${O}_prof_line.json ]; then  # the roofline kernel's traffic, bracketed by its mg_mark kernels
+        python3 tools/roofline_kernel.py C2 ${O}_prof_line.json ${O}_prof/run_kernel_trace.csv --last 10 \
+          $(find ${O}_pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1) \
+          $(find ${O}_pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1) > ${O}_pmc_roofk.txt
+        cat ${O}_pmc_roofk.txt
+      fi
       echo "pmc ok" ;;
     issue)  # two SQ passes (at most 8 SQ counters per run) over 3 eager C2 steps
       P1="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS"

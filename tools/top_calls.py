@@ -38,10 +38,13 @@ def main():
     torch.cuda.synchronize()
     with Attribution(keep_args=True) as at:
         run()
-    fams = sys.argv[1:] or [None]
+    fams = sys.argv[1:] or os.environ.get("TOP_FAMILIES", "gemm,expert_gemm,conv_fwd,conv_wgrad+fold").split(",")
+    top_n = int(os.environ.get("TOP_N", "60"))
     for f in fams:
         print(f"== {f}")
-        for ms, name, w, a in at.top_calls(f, 40):
+        calls = at.top_calls(f, 10 ** 6)
+        print(f"   {len(calls)} calls, {sum(c[0] for c in calls) * 1e3:.1f} us")
+        for ms, name, w, a in calls[:top_n]:
             rate = ""
             if w:
                 rate = f"{w / (ms * 1e-3) / 1e12:7.1f} TF/s" if f in ("gemm", "conv_fwd", "conv_wgrad+fold",
