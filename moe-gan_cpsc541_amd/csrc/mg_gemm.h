@@ -56,6 +56,17 @@ constexpr int NTHREADS = 256;
 #ifndef MG_GLDS
 #define MG_GLDS 0  // measured: on par with register staging at C2 (gemm 4096^3 +9%, expert GEMMs -20%)
 #endif
+// LDS-DMA staging for the implicit-conv forward / data-gradient tiles of at most 64 x 64 outputs only (the latency-
+// bound 3x3 modulated convs on 4x4 / 8x8 / 16x16 maps: their per-step VGPR -> LDS stores are the register path's
+// cost; measured round 6 with MG_GLDS on everything: conv8 41.4 -> 35.7 us, conv4 47.7 -> 42.9 us, while the
+// expert GEMMs lost, so the switch is per loader)
+#ifndef MG_GLDS_CONV
+#define MG_GLDS_CONV 1
+#endif
+// LDS stages of the LDS-DMA pipeline: the loads of step t + STAGES - 1 are in flight while step t is multiplied
+#ifndef MG_GLDS_STAGES
+#define MG_GLDS_STAGES 2
+#endif
 
 template <typename T> struct Frag;
 template <> struct Frag<bf16_t> { static constexpr int PAD = 8; };
@@ -170,6 +181,7 @@ struct LdKC {
     return s;
   }
   static constexpr bool kGlds = !XF;  // no transform: may stage by LDS-DMA
+  static constexpr bool kConv = false;  // implicit-convolution A loader (LdKCConv)
   template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
     off = s.off;
     if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
@@ -216,6 +228,7 @@ struct LdKCConv {
     return s;
   }
   static constexpr bool kGlds = !XF;
+  static constexpr bool kConv = true;
   template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
     const int k = k0 + s.kofs;
     const int kk = SC ? k : k0;  // SC = false: k0 is a multiple of TBK <= Cin, the step stays inside tap k0 / Cin
@@ -382,6 +395,7 @@ struct LdKCConvT {
     return s;
   }
   static constexpr bool kGlds = !XF;
+  static constexpr bool kConv = false;
   template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
     const int k = k0 + s.kofs;
     const int kk = SC ? k : k0;  // SC = false: the step stays inside tap k0 / Cg (wave-uniform)
@@ -409,6 +423,7 @@ struct LdKCGroupW {
     return Slot{(ok && r < rows) ? (uint32_t)(((int64_t)r * ld + kofs) * (int64_t)sizeof(T)) : MG_OOB, kofs};
   }
   static constexpr bool kGlds = !XF;
+  static constexpr bool kConv = false;
   template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
     off = s.off;
     if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
@@ -653,8 +668,14 @@ template <> struct Tile<float> { static constexpr int BK = 32, PADK = 4, PADM = 
 #ifndef MG_BK_SMALL
 #define MG_BK_SMALL 64
 #endif
+// MG_X3_BK: the K step of the split-bf16 fp32 tiles (64 x 64 only; the small-M prefix / demodulation GEMMs are
+// serial chains of K steps on few tiles, so a deeper step halves their chain; 64 = the bf16 step)
+#ifndef MG_X3_BK
+#define MG_X3_BK 64
+#endif
 template <typename T, bool X3, int BM = 128, int BN = 128> constexpr int tile_bk() {
-  return X3 ? Tile<bf16_t>::BK : (sizeof(T) == 2 && BM * BN <= 64 * 64) ? MG_BK_SMALL : Tile<T>::BK;
+  return X3 ? (BM * BN <= 64 * 64 ? MG_X3_BK : Tile<bf16_t>::BK)
+            : (sizeof(T) == 2 && BM * BN <= 64 * 64) ? MG_BK_SMALL : Tile<T>::BK;
 }
 // the largest K step any bf16 tile uses (the implicit-conv loaders' "one tap per K step" test needs Cin >= it)
 template <typename T> constexpr int max_tile_bk() { return tile_bk<T, false, 64, 64>() > Tile<T>::BK ? tile_bk<T, false, 64, 64>() : Tile<T>::BK; }
@@ -805,9 +826,17 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   // X3: (A_hi, A_lo, B_hi, B_lo) images in one stage
   constexpr int STAGE = (X3 ? 2 : 1) * (A_ELEMS + B_ELEMS);
   // LDS-DMA staging (bf16, both operands k-contiguous without transforms): two LDS stages, no registers
-  constexpr bool GLDS = MG_GLDS && !X3 && sizeof(T) == 2 && A_KC && B_KC && AL::kGlds && BL::kGlds &&
-                        2 * STAGE * (int)sizeof(T) <= 65536;
-  constexpr int NBUF = (GLDS || (!X3 && 2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE)) ? 2 : 1;
+  constexpr bool GLDS_SEL = [] {
+    if constexpr (A_KC && B_KC) return MG_GLDS || (MG_GLDS_CONV && AL::kConv && BM * BN <= 64 * 64);
+    else return false;
+  }();
+  constexpr int GSTAGES = MG_GLDS ? 2 : MG_GLDS_STAGES;
+  constexpr bool GLDS = [] {
+    if constexpr (A_KC && B_KC)
+      return GLDS_SEL && !X3 && sizeof(T) == 2 && AL::kGlds && BL::kGlds && GSTAGES * STAGE * (int)sizeof(T) <= 65536;
+    else return false;
+  }();
+  constexpr int NBUF = GLDS ? GSTAGES : ((!X3 && 2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE) ? 2 : 1);
   constexpr bool SB2 = NBUF == 1 && !X3 && BM * BN <= MG_SB2_MAX_TILE;
   constexpr int NS = NBUF == 2 ? MG_NSTAGE : (SB2 ? 2 : 1);
   __shared__ __attribute__((aligned(16))) LT smem[NBUF * STAGE];
@@ -995,7 +1024,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     // LDS-DMA, two stages: step t+1's loads are issued before step t is multiplied; a counted vmcnt
     // retires only step t's (issued earlier), a raw barrier publishes them, and a second barrier keeps
     // step t+2's DMA from overwriting the buffer while another wave still reads it.
-    static_assert(A_VPT + B_VPT < 64, "vmcnt range");
+    static_assert((NBUF - 1) * (A_VPT + B_VPT) < 64, "vmcnt range");
+    static_assert(NBUF == 2 || NBUF == 3, "LDS-DMA pipeline: 2 or 3 stages");
     auto issue = [&](int k0, LT* buf) {
       if (k0 + TBK <= kend) {
 #pragma unroll
@@ -1011,13 +1041,20 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
           B.template glds<true, TBK>(rB, bs_[i], k0, kend, buf + A_ELEMS + (i * 4 + wid) * 8 * LDK);
       }
     };
+    // NBUF stages: steps t + 1 .. t + NBUF - 1 are in flight while step t is multiplied
     const int nsteps = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
-    if (nsteps > 0) issue(kbeg, smem);
+    constexpr int PER = A_VPT + B_VPT;  // DMA instructions per step
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; ++p)
+      if (p < nsteps) issue(kbeg + p * TBK, smem + p * STAGE);
     for (int t = 0; t < nsteps; ++t) {
-      LT* cur = smem + (t & 1) * STAGE;
-      if (t + 1 < nsteps) {
-        issue(kbeg + (t + 1) * TBK, smem + ((t + 1) & 1) * STAGE);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_VPT + B_VPT) : "memory");
+      LT* cur = smem + (t % NBUF) * STAGE;
+      const int ahead = t + NBUF - 1;
+      if (ahead < nsteps) {
+        issue(kbeg + ahead * TBK, smem + (ahead % NBUF) * STAGE);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 1) * PER) : "memory");
+      } else if (NBUF > 2 && nsteps - 1 - t == 1) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }

@@ -195,7 +195,10 @@ extern "C" int mg_gemm(int dtype, int M, int N, int K, const void* A, int64_t ld
       int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
       const int target = g_mg_tune[MG_TUNE_ATOMIC_BLOCKS] > 0 ? (int)g_mg_tune[MG_TUNE_ATOMIC_BLOCKS] : 512;
       int64_t want = std::max<int64_t>(1, target / std::max<int64_t>(tiles, 1));
-      splits = (int)std::max<int64_t>(1, std::min<int64_t>(want, K / 256));
+      // the least K per split: 256 (one bf16 128-deep step pair), or the tuned value (A/B: a few-tile fp32 weight
+      // gradient at K = B = 256 rows otherwise walks its 4 K steps serially on 64 blocks)
+      const int mink = g_mg_tune[MG_TUNE_ATOMIC_MINK] > 0 ? (int)g_mg_tune[MG_TUNE_ATOMIC_MINK] : 256;
+      splits = (int)std::max<int64_t>(1, std::min<int64_t>(want, K / mink));
     } else {
       splits = 1;
     }
