@@ -520,6 +520,11 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t)
     finite = bool(torch.isfinite(out["d_losses"]).all() and torch.isfinite(out["g_gan"]).all())
+    if rank == 0:
+        arena = ops.fold_arena_bytes(graph.stream if graph is not None else None)
+        print(f"[bench] gradient-fold arena: {arena / 2 ** 20:.0f} MiB on the step's stream; torch allocated "
+              f"{torch.cuda.memory_allocated(dev) / 2 ** 30:.2f} GiB (peak {torch.cuda.max_memory_allocated(dev) / 2 ** 30:.2f})",
+              file=sys.stderr, flush=True)
     step_ms = sorted(step_ev[i].elapsed_time(step_ev[i + 1]) for i in range(args.steps))
     median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * sum(step_ms[len(step_ms) // 2 - 1:
                                                                                       len(step_ms) // 2 + 1])

@@ -354,6 +354,10 @@ int mg_moe_dispatch(const int32_t* topi, const float* gate, int T, int k, int E,
 
 /* out[t] = resid[t] + sum_j gate[t,j] Y[pos_of[t*k+j]]  (SparseMoE combine + AttentionBlock residual, t2i_moe_gan.py:465-470, :571). */
 int mg_moe_combine(int dtype, const void* Y, int64_t ldy, const int32_t* pos_of, const float* gate, int T, int k, int C, const void* resid, int64_t ldr, void* out, int64_t ldo, void* stream);
+/* mg_moe_combine plus the AttentionBlock's proj_out modulated-conv input (t2i_moe_gan.py:158-161, :574): also
+   xs[t] = bf16(out[t]) * s[t / HW] (s: [T / HW, C] fp32, one style row per image; HW a power of two), the bytes
+   mg_scale_bc would form from the stored out. */
+int mg_moe_combine_scaled(int dtype, const void* Y, int64_t ldy, const int32_t* pos_of, const float* gate, int T, int k, int C, const void* resid, int64_t ldr, void* out, int64_t ldo, const float* s, int64_t lds, int HW, void* xs, int64_t ldxs, void* stream);
 
 /* g_gate[t*k+j] = <gout[t], Y[pos_of[t*k+j]]>. */
 int mg_moe_gate_grad(int dtype, int gout_dtype, const void* gout, int64_t ldg, const void* Y, int64_t ldy, const int32_t* pos_of, int T, int k, int C, float* g_gate, void* stream);
@@ -425,6 +429,9 @@ int mg_offset_head_bwd(int dtype, const float* goff, const void* o1, const float
 
 /* nn.Upsample(scale_factor=2, bilinear, align_corners=False), NHWC (t2i_moe_gan.py:633). */
 int mg_upsample2x_fwd(int dtype, const void* x, int B, int H, int W, int C, void* out, void* stream);
+/* mg_upsample2x_fwd plus the ConvolutionBlock's skip_proj modulated-conv input (:615-616, :158-161): also
+   xs = bf16(out) * s[b] (s: [B, C] fp32 style rows, pitch lds), what mg_scale_bc would form from out. */
+int mg_upsample2x_fwd_scaled(int dtype, const void* x, int B, int H, int W, int C, void* out, const float* s, int64_t lds, void* xs, void* stream);
 
 /* bilinear x2 backward (gather form, deterministic). */
 int mg_upsample2x_bwd(int gout_dtype, const void* gout, int B, int H, int W, int C, int gx_dtype, void* gx, int accumulate, void* stream);
@@ -494,6 +501,10 @@ typedef struct mg_fold_wgrad {
 } mg_fold_wgrad;
 int mg_fold_defer(int on, void* stream);
 int mg_fold_flush(void* stream);
+/* The arena: capped at 2 GiB per stream (a producer that finds no room folds immediately).  mg_fold_release frees a
+   stream's arena (after a stream synchronize; the stream must not be deferring); mg_fold_arena_bytes: bytes held. */
+int mg_fold_release(void* stream);
+int64_t mg_fold_arena_bytes(void* stream);
 /* the rows-fold kernel on caller records (tests / tools) */
 int mg_fold_rows_batch(int n, const mg_fold_rows* recs, void* stream);
 /* caller records as folds of the stream: queued behind its pending folds when it defers them (they run after

@@ -299,6 +299,8 @@ struct Defer {
 };
 std::mutex g_fold_mu;
 std::vector<Defer> g_defer;
+// device bytes one stream's partials arena may hold (C2 step: ~0.3 GB on the capture stream)
+constexpr size_t kFoldArenaCap = (size_t)2 << 30;
 
 Defer* defer_entry(hipStream_t st, bool create) {
   int dev = 0;
@@ -326,7 +328,12 @@ void* mg_fold_alloc(size_t bytes, hipStream_t st) {
     // capture then replays the same allocation sequence); under capture the caller folds immediately instead
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    Chunk c{nullptr, std::max(bytes, (size_t)64 << 20)};
+    // capped per stream: past the cap the producer folds immediately (same kernels, bit-identical gradients)
+    size_t held = 0;
+    for (const Chunk& c : d->chunks) held += c.bytes;
+    const size_t chunk = std::max(bytes, (size_t)64 << 20);
+    if (held + chunk > kFoldArenaCap) return nullptr;
+    Chunk c{nullptr, chunk};
     if (hipMalloc(reinterpret_cast<void**>(&c.p), c.bytes) != hipSuccess) return nullptr;
     d->chunks.push_back(c);
     d->used = 0;
@@ -395,6 +402,43 @@ extern "C" int mg_fold_defer(int on, void* stream) {
   MG_REQUIRE(d->rows.empty() && d->wgrad.empty(), "mg_fold_defer: folds pending (flush first)");
   d->on = true;
   return MG_OK;
+}
+
+extern "C" int mg_fold_release(void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  std::vector<Chunk> chunks;
+  {
+    std::lock_guard<std::mutex> lk(g_fold_mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return MG_OK;
+    for (size_t i = 0; i < g_defer.size(); ++i) {
+      Defer& d = g_defer[i];
+      if (d.device != dev || d.stream != st) continue;
+      MG_REQUIRE(!d.on && d.rows.empty() && d.wgrad.empty(), "mg_fold_release: the stream still defers folds");
+      chunks.swap(d.chunks);
+      g_defer.erase(g_defer.begin() + i);
+      break;
+    }
+  }
+  if (!chunks.empty()) {
+    // the partials may still be read by folds enqueued on the stream
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      mg_set_error("mg_fold_release: hipStreamSynchronize failed");
+      return MG_ERR_LAUNCH;
+    }
+    for (const Chunk& c : chunks) (void)hipFree(c.p);
+  }
+  return MG_OK;
+}
+
+extern "C" int64_t mg_fold_arena_bytes(void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lk(g_fold_mu);
+  Defer* d = defer_entry(st, false);
+  if (!d) return 0;
+  int64_t held = 0;
+  for (const Chunk& c : d->chunks) held += (int64_t)c.bytes;
+  return held;
 }
 
 extern "C" int mg_fold_rows_batch(int n, const mg_fold_rows* recs, void* stream) {

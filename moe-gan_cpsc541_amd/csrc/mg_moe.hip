@@ -544,12 +544,16 @@ __global__ void k_combine(const T* __restrict__ Y, int64_t ldy, const int* __res
   }
 }
 
-// 8-channel vector form of k_combine (same arithmetic order)
-template <typename T>
+// 8-channel vector form of k_combine (same arithmetic order).  XS: also the next modulated conv's input x * s
+// (t2i_moe_gan.py:158-161, AttentionBlock.proj_out), s [B, C] one style row per image of HW tokens, from the
+// stored (rounded) out -- the bytes k_scale_bc would write, without re-reading out
+template <typename T, bool XS = false>
 __global__ __launch_bounds__(256) void k_combine_v(const T* __restrict__ Y, int64_t ldy, const int* __restrict__ pos_of,
                                                    const float* __restrict__ gate, int Tn, int k, int C,
                                                    const T* __restrict__ resid, int64_t ldr, T* __restrict__ out,
-                                                   int64_t ldo) {
+                                                   int64_t ldo, const float* __restrict__ sty = nullptr,
+                                                   int64_t ld_sty = 0, int lg_hw = 0, T* __restrict__ xs = nullptr,
+                                                   int64_t ldxs = 0) {
   const int cv = C >> 3;
   const int n = Tn * cv;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
@@ -570,6 +574,20 @@ __global__ __launch_bounds__(256) void k_combine_v(const T* __restrict__ Y, int6
       for (int q = 0; q < 8; ++q) s[q] = y[q] + s[q];
     }
     st8(out + (int64_t)t * ldo + c, s);
+    if constexpr (XS) {
+      float r[8];
+      if constexpr (sizeof(T) == 2) {  // the product of the stored bf16 value, as k_scale_bc forms it
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r[q] = bf2f(f2bf(s[q]));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r[q] = s[q];
+      }
+      ld8(sty + (int64_t)(t >> lg_hw) * ld_sty + c, y);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) r[q] *= y[q];
+      st8(xs + (int64_t)t * ldxs + c, r);
+    }
   }
 }
 
@@ -1655,6 +1673,30 @@ extern "C" int mg_moe_combine(int dtype, const void* Y, int64_t ldy, const int32
     hipLaunchKernelGGL(k_combine<bf16_t>, dim3(nblk(n)), dim3(256), 0, st, (const bf16_t*)Y, ldy, pos_of, gate, T, k,
                        C, (const bf16_t*)resid, ldr, (bf16_t*)out, ldo);
   return mg_check_launch("mg_moe_combine");
+}
+
+extern "C" int mg_moe_combine_scaled(int dtype, const void* Y, int64_t ldy, const int32_t* pos_of, const float* gate,
+                                     int T, int k, int C, const void* resid, int64_t ldr, void* out, int64_t ldo,
+                                     const float* s, int64_t lds, int HW, void* xs, int64_t ldxs, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t n = (int64_t)T * C;
+  MG_REQUIRE(C % 8 == 0 && ldy % 8 == 0 && ldo % 8 == 0 && ldxs % 8 == 0 && lds % 4 == 0 && (!resid || ldr % 8 == 0),
+             "mg_moe_combine_scaled: C and pitches multiples of 8 (style pitch of 4)");
+  MG_REQUIRE(mg_al16(Y) && mg_al16(out) && mg_al16(xs) && mg_al16(s) && (!resid || mg_al16(resid)),
+             "mg_moe_combine_scaled: 16-byte aligned operands");
+  MG_REQUIRE(HW > 0 && (HW & (HW - 1)) == 0 && T % HW == 0, "mg_moe_combine_scaled: HW a power of two dividing T");
+  MG_REQUIRE(n / 8 < (1LL << 31), "mg_moe_combine_scaled: too many elements");
+  if (n == 0) return MG_OK;
+  int lg = 0;
+  while ((1 << lg) < HW) ++lg;
+  const int blocks = nblk(n / 8);
+  if (dtype == MG_F32)
+    hipLaunchKernelGGL((k_combine_v<float, true>), dim3(blocks), dim3(256), 0, st, (const float*)Y, ldy, pos_of, gate, T,
+                       k, C, (const float*)resid, ldr, (float*)out, ldo, s, lds, lg, (float*)xs, ldxs);
+  else
+    hipLaunchKernelGGL((k_combine_v<bf16_t, true>), dim3(blocks), dim3(256), 0, st, (const bf16_t*)Y, ldy, pos_of, gate,
+                       T, k, C, (const bf16_t*)resid, ldr, (bf16_t*)out, ldo, s, lds, lg, (bf16_t*)xs, ldxs);
+  return mg_check_launch("mg_moe_combine_scaled");
 }
 
 extern "C" int mg_moe_gate_grad(int dtype, int gout_dtype, const void* gout, int64_t ldg, const void* Y, int64_t ldy,

@@ -469,9 +469,12 @@ __global__ void k_up2_fwd(const T* __restrict__ x, int B, int H, int W, int C, T
 }
 
 // 8-channel vector forms (C % 8 == 0); same arithmetic order as the scalar kernels
-template <typename T>
+// XS: also x * s for the block's 1x1 skip modulated conv (t2i_moe_gan.py:158-161, :615-616), s [B, C], formed from the
+// stored (rounded) upsampled value as k_scale_bc would
+template <typename T, bool XS = false>
 __global__ __launch_bounds__(256) void k_up2_fwd_v(const T* __restrict__ x, int B, int H, int W, int C,
-                                                   T* __restrict__ out) {
+                                                   T* __restrict__ out, const float* __restrict__ sty = nullptr,
+                                                   int64_t ld_sty = 0, T* __restrict__ xs = nullptr) {
   const int OH = 2 * H, OW = 2 * W, cv = C >> 3;
   const int n = B * OH * OW * cv;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
@@ -492,6 +495,16 @@ __global__ __launch_bounds__(256) void k_up2_fwd_v(const T* __restrict__ x, int 
     for (int j = 0; j < 8; ++j)
       v[j] = (1.f - ly) * ((1.f - lx) * a[j] + lx * bb[j]) + ly * ((1.f - lx) * cc[j] + lx * dd[j]);
     st8(out + (int64_t)pix * C + c, v);
+    if constexpr (XS) {
+      float sc[8];
+      ld8(sty + (int64_t)b * ld_sty + c, sc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (sizeof(T) == 2) v[j] = bf2f(f2bf(v[j]));
+        v[j] *= sc[j];
+      }
+      st8(xs + (int64_t)pix * C + c, v);
+    }
   }
 }
 
@@ -925,6 +938,24 @@ extern "C" int mg_offset_head_bwd(int dtype, const float* goff, const void* o1, 
   else
     hipLaunchKernelGGL(k_offset_head_bwd<bf16_t>, grid, dim3(256), 0, st, goff, (const bf16_t*)o1, w2, B, H, W, ppb, (bf16_t*)ga1, gw2, gb2);
   return mg_check_launch("mg_offset_head_bwd");
+}
+
+extern "C" int mg_upsample2x_fwd_scaled(int dtype, const void* x, int B, int H, int W, int C, void* out,
+                                        const float* s, int64_t lds, void* xs, void* stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t n = 4LL * B * H * W * C;
+  MG_REQUIRE(C % 8 == 0 && lds % 4 == 0 && mg_al16(x) && mg_al16(out) && mg_al16(xs) && mg_al16(s),
+             "mg_upsample2x_fwd_scaled: C a multiple of 8, 16-byte aligned operands");
+  MG_REQUIRE(n / 8 < (1LL << 31), "mg_upsample2x_fwd_scaled: too many elements");
+  if (n == 0) return MG_OK;
+  const int blocks = nblk(n / 8);
+  if (dtype == MG_F32)
+    hipLaunchKernelGGL((k_up2_fwd_v<float, true>), dim3(blocks), dim3(256), 0, st, (const float*)x, B, H, W, C,
+                       (float*)out, s, lds, (float*)xs);
+  else
+    hipLaunchKernelGGL((k_up2_fwd_v<bf16_t, true>), dim3(blocks), dim3(256), 0, st, (const bf16_t*)x, B, H, W, C,
+                       (bf16_t*)out, s, lds, (bf16_t*)xs);
+  return mg_check_launch("mg_upsample2x_fwd_scaled");
 }
 
 extern "C" int mg_upsample2x_fwd(int dtype, const void* x, int B, int H, int W, int C, void* out, void* stream) {

@@ -117,7 +117,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise MGError(f"libmoegan_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
         h = ctypes.CDLL(LIB_PATH)
+        variant = bool(os.environ.get("MOEGAN_HIP_LIB"))  # an A/B build (tools/build_variants.sh) of older sources
         for name, (res, args) in _SIGS.items():
+            if variant and not hasattr(h, name):
+                continue  # an entry point newer than the variant: left unbound there
             fn = getattr(h, name)
             fn.argtypes = list(args)
             fn.restype = res

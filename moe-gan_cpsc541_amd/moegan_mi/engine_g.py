@@ -171,6 +171,14 @@ class GeneratorEngine:
         s = ops.linear(w, self.P(pre + "modulation.weight"), bias=self.P(pre + "modulation.bias"))  # :158
         return s, ops.cast(s, square=1)
 
+    def _batched_style(self, pre, Cin):
+        """The style rows s [B, Cin] of a modulated conv from the step's batched style GEMM (a column slice of S),
+        or None when there is none (then mc_fwd forms x * s itself)."""
+        if self._S is not None and pre in self.style_cols and Cin % 8 == 0:
+            c = self.style_cols[pre]
+            return self._S[:, c:c + Cin]
+        return None
+
     def mc_fwd(self, pre, x, w, act=0, resid=None, save=True, xs=None):
         B, H, W, Cin = x.shape
         HW = H * W
@@ -311,11 +319,12 @@ class GeneratorEngine:
     # ------------------------------------------------------------------
     # ConvolutionBlock  (t2i_moe_gan.py:579-621)
     # ------------------------------------------------------------------
-    def cb_fwd(self, pre, x, w, save=True):
+    def cb_fwd(self, pre, x, w, save=True, skip_xs=None):
+        """``skip_xs``: the skip conv's input x * s when the producer of x already formed it (upsample2x)."""
         h1, sv1 = self.mtm_fwd(pre + "mtm1.", x, w, save=save)
         svs = None
         if (pre + "skip_proj.weight") in self.st.offsets:
-            sk, svs = self.mc_fwd(pre + "skip_proj.", x, w, save=save)
+            sk, svs = self.mc_fwd(pre + "skip_proj.", x, w, save=save, xs=skip_xs)
         else:
             sk = x
         out, sv2 = self.mtm_fwd(pre + "mtm2.", h1, w, resid=sk, save=save)
@@ -335,7 +344,9 @@ class GeneratorEngine:
     # ------------------------------------------------------------------
     # SparseMoE + BayesianRouter  (t2i_moe_gan.py:265-491)
     # ------------------------------------------------------------------
-    def moe_fwd(self, pre, tok, resid, w, HW, eps, anneal, train=True, save=True, kl_out=None):
+    def moe_fwd(self, pre, tok, resid, w, HW, eps, anneal, train=True, save=True, kl_out=None, out_style=None):
+        """``out_style`` [B, C] (the next modulated conv's style rows): the combine also writes that conv's input
+        x * s, returned as the sixth value (else None)."""
         r = pre + "router."
         T, C = tok.shape
         B = w.shape[0]
@@ -386,7 +397,11 @@ class GeneratorEngine:
             ops.gemm_grouped(Hid, W2, row_off, tile_off, max_tiles, C, Hd, b_gstride=C * Hd, out=Y, ldb=Hd,
                              ep=E_(bias=b2))
         out = torch.empty(T, C, device=self.dev, dtype=self.cdt)
-        ops.moe_combine(Y, pos_of, gate, resid, out)  # x_spatial + moe_out (:571)
+        xs_next = None
+        if out_style is not None:  # x_spatial + moe_out (:571), and proj_out's x * s from the same pass
+            out, xs_next = ops.moe_combine(Y, pos_of, gate, resid, out, style=out_style, HW=HW)
+        else:
+            ops.moe_combine(Y, pos_of, gate, resid, out)  # x_spatial + moe_out (:571)
         kl2 = None
         if train and self._want_kl:
             if kl_out is not None:  # filled by the forward's batched KL launch (ops.router_kl_batch)
@@ -400,6 +415,8 @@ class GeneratorEngine:
             sv = dict(tok=tok, w=w, HW=HW, eps=eps, anneal=anneal, Wf=Wf, Wt=Wt, Wc=Wc, Wfc=Wfc, u=u, probs=probs,
                       zlog=zlog, topi=topi, gate=gate, row_off=row_off, tile_off=tile_off, perm=perm, pos_of=pos_of,
                       gate_pos=gate_pos, Pre=Pre, Hid=Hid, Xg=Xg, Y=Y, W1=W1, W2=W2, max_tiles=max_tiles)
+        if out_style is not None:
+            return out, probs, kl2, topi, sv, xs_next
         return out, probs, kl2, topi, sv
 
     def _router_weights(self, r, eps, train, pb=None):
@@ -624,9 +641,16 @@ class GeneratorEngine:
         xf1 = ops.linear(att, self.Pc(pre + "self_attn.out_proj.weight"), bias=self.P(pre + "self_attn.out_proj.bias"),
                          resid=xf0, ld_res=C, addvec=ca, add_shift=ops.ilog2(L_), add_ld=C)
         n3, mu3, rs3 = ops.layernorm_fwd(xf1, self.P(pre + "norm3.weight"), self.P(pre + "norm3.bias"))
-        xpre, probs, kl2, topi, sv_moe = self.moe_fwd(pre + "moe.", n3, xf1, w, L_, eps, anneal, train, save,
-                                                      kl_out=kl_out)
-        out, sv_out = self.mc_fwd(pre + "proj_out.", xpre.view(B, H, W, C), w, save=save)
+        s_out = self._batched_style(pre + "proj_out.", C)
+        if s_out is not None and (L_ & (L_ - 1)) == 0:  # proj_out's x * s written by the combine itself
+            xpre, probs, kl2, topi, sv_moe, xs_out = self.moe_fwd(pre + "moe.", n3, xf1, w, L_, eps, anneal, train,
+                                                                  save, kl_out=kl_out, out_style=s_out)
+            xs_out = xs_out.view(B, H, W, C)
+        else:
+            xpre, probs, kl2, topi, sv_moe = self.moe_fwd(pre + "moe.", n3, xf1, w, L_, eps, anneal, train, save,
+                                                          kl_out=kl_out)
+            xs_out = None
+        out, sv_out = self.mc_fwd(pre + "proj_out.", xpre.view(B, H, W, C), w, save=save, xs=xs_out)
         sv = None
         if save:
             sv = dict(sv_in=sv_in, xf0=xf0, n1=n1, mu1=mu1, rs1=rs1, qkv=qkv, att=att, lse=lse, tp=tp, vv=vv,
@@ -773,9 +797,15 @@ class GeneratorEngine:
             if i == 0:
                 x, cbsv = prefix["x0"], (prefix["cbsv0"] if save else None)
             else:
+                skip_xs = None
                 if up:
-                    x = ops.upsample2x(x)
-                x, cbsv = self.cb_fwd(name + ".conv_block.", x, w, save=save)
+                    s_skip = (self._batched_style(name + ".conv_block.skip_proj.", x.shape[-1])
+                              if (name + ".conv_block.skip_proj.weight") in self.st.offsets else None)
+                    if s_skip is not None:  # the skip conv's x * s from the upsample pass itself
+                        x, skip_xs = ops.upsample2x(x, style=s_skip)
+                    else:
+                        x = ops.upsample2x(x)
+                x, cbsv = self.cb_fwd(name + ".conv_block.", x, w, save=save, skip_xs=skip_xs)
             asv = None
             if attn:
                 x, p, kl2, topi, asv = self.attn_fwd(name + ".attn_block.", x, w, text_seq,

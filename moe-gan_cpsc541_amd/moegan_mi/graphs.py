@@ -94,6 +94,13 @@ class SegmentedGraph:
         self._begin()
         return r
 
+    def release(self):
+        """Drop the captured graphs and free the library's gradient-fold arena of the capture stream (the arena
+        persists across replays; ops.fold_release)."""
+        from . import ops
+        self.items = []
+        ops.fold_release(self.stream)
+
     @property
     def n_graphs(self):
         return sum(1 for k, _ in self.items if k == "graph")

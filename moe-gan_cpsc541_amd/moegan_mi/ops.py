@@ -142,6 +142,20 @@ def fold_add(pairs):
     call("mg_fold_rows_queue", len(pairs), ctypes.addressof(recs), S())
 
 
+def fold_release(stream=None):
+    """Free the gradient-fold partials arena of ``stream`` (default: the current stream) -- mg_fold_release.  The
+    arena is kept across steps on purpose (a captured step replays its allocations); release it when the stream's
+    training ends (TrainStep.release)."""
+    st = L.ctypes.c_void_p(stream.cuda_stream) if stream is not None else S()
+    call("mg_fold_release", st)
+
+
+def fold_arena_bytes(stream=None):
+    """Device bytes held by the gradient-fold arena of ``stream`` (memory accounting; mg_fold_arena_bytes)."""
+    st = L.ctypes.c_void_p(stream.cuda_stream) if stream is not None else S()
+    return int(L.lib().mg_fold_arena_bytes(st))
+
+
 def fold_flush():
     """Run every deferred gradient fold of the current stream (one launch per fold kind; mg_fold_flush)."""
     call("mg_fold_flush", S())
@@ -747,12 +761,22 @@ def moe_dispatch(topi, gate, E_, bm=128):
     return row_off, tile_off, perm, pos_of, gate_pos
 
 
-def moe_combine(Y, pos_of, gate, resid, out):
+def moe_combine(Y, pos_of, gate, resid, out, style=None, HW=None):
+    """out = resid + the gated expert rows (mg_moe_combine).  ``style`` [B, C] fp32 (a row view with unit column
+    stride) and ``HW`` (tokens per image): also return xs = out * style[image] for the modulated conv that reads out
+    (mg_moe_combine_scaled; replaces an mg_scale_bc pass)."""
     T, k = gate.shape
     C = out.shape[-1]
-    call("mg_moe_combine", dt(Y), ptr(Y), Y.shape[-1], ptr(pos_of), ptr(gate), T, k, C, ptr(resid),
-         resid.shape[-1] if resid is not None else 0, ptr(out), out.shape[-1], S())
-    return out
+    if style is None:
+        call("mg_moe_combine", dt(Y), ptr(Y), Y.shape[-1], ptr(pos_of), ptr(gate), T, k, C, ptr(resid),
+             resid.shape[-1] if resid is not None else 0, ptr(out), out.shape[-1], S())
+        return out
+    assert style.stride(1) == 1 and style.dtype == torch.float32
+    xs = torch.empty_like(out)
+    call("mg_moe_combine_scaled", dt(Y), ptr(Y), Y.shape[-1], ptr(pos_of), ptr(gate), T, k, C, ptr(resid),
+         resid.shape[-1] if resid is not None else 0, ptr(out), out.shape[-1], ptr(style), style.stride(0), HW,
+         ptr(xs), xs.shape[-1], S())
+    return out, xs
 
 
 def moe_gate_grad(gout, Y, pos_of, T, k):
@@ -884,11 +908,18 @@ def offset_head_bwd(goff, o1, w2, ga1, gw2, gb2):
     call("mg_offset_head_bwd", dt(o1), ptr(goff), ptr(o1), ptr(w2), B, H, W, ptr(ga1), ptr(gw2), ptr(gb2), S())
 
 
-def upsample2x(x):
+def upsample2x(x, style=None):
+    """nn.Upsample(2, bilinear) NHWC (mg_upsample2x_fwd).  ``style`` [B, C] fp32 (unit column stride): also return
+    xs = out * style[b] for the 1x1 skip modulated conv that reads out (mg_upsample2x_fwd_scaled)."""
     B, H, W, C = x.shape
     out = torch.empty(B, 2 * H, 2 * W, C, device=x.device, dtype=x.dtype)
-    call("mg_upsample2x_fwd", dt(x), ptr(x), B, H, W, C, ptr(out), S())
-    return out
+    if style is None:
+        call("mg_upsample2x_fwd", dt(x), ptr(x), B, H, W, C, ptr(out), S())
+        return out
+    assert style.stride(1) == 1 and style.dtype == torch.float32
+    xs = torch.empty_like(out)
+    call("mg_upsample2x_fwd_scaled", dt(x), ptr(x), B, H, W, C, ptr(out), ptr(style), style.stride(0), ptr(xs), S())
+    return out, xs
 
 
 def upsample2x_bwd(gout, gx, accumulate=0):

@@ -158,3 +158,26 @@ def test_splitk_in_launch_reduction_conv():
                                                                      bias.double(), padding=1), 0.2)
     err = ((one.double().permute(0, 3, 1, 2) - ref).norm() / ref.norm()).item()
     assert err < 2e-2, err
+
+
+def test_fold_arena_release_and_size():
+    """The deferred-fold arena is reported (mg_fold_arena_bytes) and freed by mg_fold_release once the stream no
+    longer defers; releasing a deferring stream is refused."""
+    import torch
+    from moegan_mi import _lib as L
+    from moegan_mi import ops
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        ops.fold_defer(True)
+        x = torch.randn(64, 4, 4, 128, device="cuda", dtype=torch.bfloat16)
+        gy = torch.randn(64, 4, 4, 256, device="cuda", dtype=torch.bfloat16)
+        gw = torch.zeros(256, 128, 3, 3, device="cuda")
+        ops.conv2d_wgrad(gy.view(-1, 256), x, 256, 3, 3, 1, 1, gw)
+        held = ops.fold_arena_bytes()
+        with pytest.raises(L.MGError):
+            ops.fold_release()
+        ops.fold_defer(False)
+        ops.fold_release()
+        assert ops.fold_arena_bytes() == 0
+    torch.cuda.synchronize()
+    assert held >= 0
