@@ -137,7 +137,7 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_S1_OFF = 12,  // 1: weight gradients of stride-1 convs through the generic LdMCConv (A/B)
        MG_TUNE_D0_STORE = 13,  // mg_d0_fwd output path: 0 automatic, 1 straight from the accumulators, 2 LDS-staged rows
        MG_TUNE_FFN_BWD_OCC = 14,  // mg_moe_ffn_bwd: 0 automatic (one block per CU, 256 VGPRs, 128-unit chunks), 2 two blocks (128 VGPRs), 3 64-unit chunks
-       MG_TUNE_WIDE_WGRAD = 15,   // 1: linear-layer weight gradients through the generic split-K GEMM (A/B), 2: wide kernel on every eligible shape
+       MG_TUNE_WIDE_WGRAD = 15,   // 1: long-reduction weight gradients through the generic split-K GEMM (A/B), 2: mg_wgrad_wide.hip on every eligible shape, 3: the same (128^2 tiles), 4: 256^2 tiles where M, N >= 256
        MG_TUNE_NARROW = 16,  // the 32-channel 3x3 convs (offset heads) through the implicit GEMM: 1 all, 2 fwd, 3 dgrad, 4 wgrad
        MG_TUNE_NARROW_BLOCKS = 17,  // mg_narrow.hip grid target (blocks): 0 automatic
        MG_TUNE_DISPATCH3 = 18,  // 1: mg_moe_dispatch as count / scan / scatter (A/B; default count + scatter-scan)
@@ -150,7 +150,8 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
                                      // logits, 2 router backward (thread per token), 4 token gradient
        MG_TUNE_ADAMW_CACHED = 25,    // 1: AdamW streams through the caches (A/B; default non-temporal loads / stores)
        MG_TUNE_ATOMIC_MINK = 26,     // atomic split-K GEMMs: the least K per split (0: automatic)
-       MG_TUNE_COUNT = 27 };
+       MG_TUNE_WIDE_BLOCKS = 27,     // mg_wgrad_wide.hip grid target (blocks): 0 automatic (256)
+       MG_TUNE_COUNT = 28 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 // Deterministic mode (mg_set_tuning(MG_TUNE_DETERMINISTIC, 1)): every reduction that crosses workgroups runs in
 // a fixed order -- per-block partial rows in the stream's workspace folded by one pass, or one writer per

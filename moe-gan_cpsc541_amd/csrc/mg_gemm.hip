@@ -622,6 +622,11 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
                                                                                       : P / 2048));
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // 1x1 / stride-1 convolutions: gw[Cout][Cin] += gy^T x over the B*H*W pixels, the long-reduction kernel of the
+  // linear-layer weight gradients (mg_wgrad_wide.hip; it declines shapes it does not win on)
+  if (dtype == MG_BF16 && !in_scale && KH == 1 && KW == 1 && stride == 1 && pad == 0 &&
+      mg_wgrad_wide(Cout, Cin, (int)P, gy, ldg, x, Cin, gw, Cin, 1.f, st))
+    return mg_check_launch("mg_conv2d_wgrad (1x1, long reduction)");
   if (dtype == MG_BF16 && !in_scale && Cout == 32 && Cin >= 32 && mg_conv3_direct_ok(H, W, Cin, Cout, KH, KW, stride, pad, true)) {
     float* ws = nullptr;
     int ng = 0;

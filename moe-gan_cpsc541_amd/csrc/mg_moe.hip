@@ -1805,6 +1805,9 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
     // ~1024 blocks with at most 4 M floats of partial rows (at 32 experts the old 256-block / 1 M-float budget
     // left 64 blocks walking 1024 tokens each: 175 us for the 16x16 block's 65536 tokens at C5)
     int chunk = std::max(TY, (T / 1024 + TY - 1) / TY * TY);
+    // and >= 4E tokens per block, so the partial rows (C x E fp32 per block) stay within half the token bytes read
+    // (C x 2 per token): at the 4x4 block (T = 4096, C = 512) 4-token chunks wrote 16 MB of partials for 4 MB of tokens
+    chunk = std::max(chunk, (4 * E + TY - 1) / TY * TY);
     const int64_t row = (int64_t)rows_per_block * C * E;
     const int64_t min_chunk = ((int64_t)T * row / (4 << 20) + TY - 1) / TY * TY;
     if (min_chunk > chunk) chunk = (int)min_chunk;

@@ -1,180 +1,255 @@
-// Weight gradients of the step's linear layers as "wide" split-K GEMMs: C[M][N] += alpha * sum_k A[k][m] B[k][n]
-// with A = the output gradient [K tokens x M] and B = the layer input [K x N], both bf16 and row-major (M / N
-// contiguous), K = tokens (4096 .. 65536) and M x N small (the self-attention in/out projections and 1x1 skips,
-// t2i_moe_gan.py:545-556 backward: 128 x 128 .. 1536 x 512).
+// Long-reduction weight gradients: C[M][N] += alpha * sum_k A[k][m] B[k][n] with A = the output gradient [K x M] and
+// B = the layer input [K x N], both bf16 and row-major (M / N contiguous), K = tokens / pixels (16384 .. 65536) and
+// M x N small: the self-attention in / out projections (t2i_moe_gan.py:545-556 backward, 128 x 128 .. 768 x 256)
+// and the 1x1 convolutions (ConvolutionBlock.skip_proj / AttentionBlock.proj_in / proj_out, :574, :615-616: Cout x Cin
+// over B*H*W pixels).
 //
-// The generic GEMM runs these as 64 x 64 tiles split over K into ~512 blocks with fp32 atomics: every A column strip
-// is re-read N / 64 times and every B strip M / 64 times (4-8x the operand bytes), and the 2-8 M atomic adds run at
-// the chip's ~1.3 TB/s atomic rate (MI355X_MICROARCH.md) -- 20-40 us per call for 8-67 MB of operands.  Here a block
-// owns a 128 x 128 or 256 x 256 output tile (all of M x N for most shapes) for one K chunk: the operands are read
-// once or twice, K is split so that ~256 blocks stream them, and the per-block fp32 partial tiles are folded in a
-// fixed order by two passes (deterministic in both library modes).
+// The generic GEMM runs these as 64 x 64 tiles split over K with fp32 atomics: every A strip is re-read N / 64 times
+// and every B strip M / 64 times, and each block walks its K chunk with one step of loads in flight, so a step costs a
+// full HBM round trip (~1-2 us) against ~50 ns of MFMA work -- 20-40 us per call for 8-67 MB of operands.  Here a
+// block owns a 128 x 128 or 256 x 256 output tile (all of M x N for most shapes) for one K chunk, so the operands are
+// read once or twice, and streams its chunk through a 4-stage LDS-DMA ring (buffer_load ... lds) with two K steps
+// (64 KiB) in flight while one is multiplied.  The per-block fp32 partial tiles are folded in a fixed order by two
+// passes (deterministic in both library modes).
 //
-// Block: 512 threads = 8 waves as 2 (M) x 4 (N), wave tile (BM/2) x (BN/4) of 16x16 fragments; k-steps of 32 rows
-// staged as MC images (rows stored as they arrive, 16-B coalesced) in a double-buffered LDS ring, one barrier per
-// k-step, the next step's global loads in registers while the current one multiplies; fragments by the hardware
-// transpose read (ds_read_b64_tr_b16).
+// Block: 512 threads = 8 waves as 2 (M) x 4 (N), wave tile (BM/2) x (BN/4) of 16x16 fragments, read from the
+// row-major ("MC") LDS images by the hardware transpose read (ds_read_b64_tr_b16).  Rows past the split's chunk and
+// columns past M / N take an out-of-range offset (the hardware writes zeros): no branches in the loop.
 #include <algorithm>
 
-#include "mg_common.h"
+#include "mg_gemm.h"
 
 namespace {
+using mg::MG_OOB;
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 constexpr int WT = 512;  // threads
-constexpr int WBK = 32;  // k rows per step
 
-MG_DEV int swz(int k) { return ((k >> 3) & 1) << 4; }
+// LDS image of one K step: [BK rows][BM cols] bf16 per operand, unpadded (each LDS-DMA wave-instruction fills 1 KiB
+// = 1024 / (2 BM) consecutive rows in lane order), 16-B chunk c of row k stored at chunk c ^ swz(k): the eight rows
+// k = 8g + q (g = 0, 1; q < 4) that one 32-lane half of a ds_read_b64_tr_b16 touches land on distinct 32-B bank pairs.
+MG_DEV int swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
 
-MG_DEV bf16x8_t mc_frag(const bf16_t* img, int ld, int kr0, int c0, int lane) {
+// One LDS-DMA (buffer_load_dwordx4 ... lds) as an asm statement: the compiler's wait-count pass treats the
+// ds_read_b64_tr_b16 intrinsic as possibly aliasing an in-flight LDS-DMA and would drain every DMA (vmcnt(0)) before
+// each step's fragment reads; hidden from it, the DMAs are waited for by the kernel's own counted vmcnt.  M0 (the
+// wave's LDS destination) is saved and restored inside the statement; s_nop 4 covers a descriptor / soffset SGPR just
+// written by v_readfirstlane, s_nop 0 the M0 write before the DMA (cdna_hip_programming.md §5.7).
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+MG_DEV i32x4_t dma_desc(const void* p) {  // raw buffer descriptor: base, stride 0, 2^31 - 1 bytes (as make_rsrc)
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  return i32x4_t{(int)__builtin_amdgcn_readfirstlane((uint32_t)a), (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)),
+                 0x7fffffff, 0x00020000};
+}
+MG_DEV void dma16(const i32x4_t& d, uint32_t voff, uint32_t soff, const bf16_t* lds) {
+  const uint32_t m = __builtin_amdgcn_readfirstlane(
+      (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const bf16_t*)lds));
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(d), "s"(m), "s"(__builtin_amdgcn_readfirstlane(soff))
+      : "memory");
+}
+
+MG_DEV bf16x8_t mc_frag(const bf16_t* img, int cols, int kbase, int c0, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int k = kr0 + 8 * g + q;
+  const int k = kbase + 8 * g + q;
   auto base = (__attribute__((address_space(3))) char*)(img);
-  const int col = (c0 ^ swz(k)) + 4 * p;
-  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + (k * ld + col) * 2));
-  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + ((k + 4) * ld + col) * 2));
+  const int ch = (c0 >> 3) + (p >> 1), sub = (p & 1) * 8;  // 16-B chunk of column c0 + 4p, byte offset in it
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4_t*)(base + k * cols * 2 + ((ch ^ swz(k)) << 4) + sub));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4_t*)(base + (k + 4) * cols * 2 + ((ch ^ swz(k + 4)) << 4) + sub));
   u16x8_t r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
-template <int BM, int BN>
+// NB LDS stages, NB - 2 K steps of LDS-DMA in flight while one is multiplied: step t + NB - 2 is issued into the stage
+// step t - 2 read (every wave finished reading it before the barrier of step t - 1), a counted vmcnt retires this
+// wave's DMA of step t, and one raw barrier per step publishes it (the pipeline rules of cdna_hip_programming.md
+// "Pipelining across barriers": all LDS in one array, no __syncthreads while a DMA is in flight).  Steps past the
+// split's rows read zeros (out-of-range offsets), so every step issues the same DMA count.
+template <int BM, int BN, int BK, int NB>
 __global__ __launch_bounds__(WT) void k_wgrad_wide(const bf16_t* __restrict__ A, int64_t lda,
                                                    const bf16_t* __restrict__ B, int64_t ldb, int M, int N, int K,
                                                    int kchunk, float* __restrict__ part) {
-  constexpr int LDA = BM + 32, LDB = BN + 32;  // pitches: odd multiples of 16 dwords
-  constexpr int AV = WBK * BM / 8 / WT, BV = WBK * BN / 8 / WT;  // 16-B loads per thread per k-step
+  extern __shared__ __attribute__((aligned(16))) bf16_t dsm[];
+  constexpr int AE = BK * BM, STAGE = BK * (BM + BN);
+  constexpr int ARI = 512 / BM, BRI = 512 / BN;  // rows per 1-KiB DMA instruction
+  constexpr int AI = BK / ARI / 8, BI = BK / BRI / 8;  // DMA instructions per wave per step
+  constexpr int PER = AI + BI;
   constexpr int WM = BM / 2, WN = BN / 4, FM = WM / 16, FN = WN / 16;
-  static_assert(AV >= 1 && BV >= 1, "tile too small for the block");
-  __shared__ bf16_t As[2][WBK * LDA];
-  __shared__ bf16_t Bs[2][WBK * LDB];
+  static_assert(AI >= 1 && BI >= 1 && NB >= 3, "tile / stage shape");
+  static_assert((NB - 2) * PER < 64, "vmcnt range");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int k_lo = blockIdx.z * kchunk, k_hi = std::min(K, k_lo + kchunk);
-  u16x8_t ar[AV], br[BV];
-  auto load = [&](int k0) {
+  const i32x4_t ra = dma_desc(A), rb = dma_desc(B);
+  // instruction i of wave w fills rows (8i + w) * RI ..; lane L: row + L / (cols / 8), physical chunk L % (cols / 8)
+  int a_r[AI], b_r[BI];
+  uint32_t a_off[AI], b_off[BI];
 #pragma unroll
-    for (int j = 0; j < AV; ++j) {
-      const int i = tid + j * WT, r = i / (BM / 8), c = (i % (BM / 8)) * 8;
-      ar[j] = (k0 + r < k_hi && m0 + c < M) ? *reinterpret_cast<const u16x8_t*>(A + (int64_t)(k0 + r) * lda + m0 + c)
-                                            : u16x8_t(0);
-    }
+  for (int i = 0; i < AI; ++i) {
+    const int r = (8 * i + wid) * ARI + lane / (BM / 8), c = m0 + 8 * ((lane % (BM / 8)) ^ swz(r));
+    a_r[i] = r;
+    a_off[i] = c < M ? (uint32_t)(((int64_t)(k_lo + r) * lda + c) * 2) : MG_OOB;
+  }
 #pragma unroll
-    for (int j = 0; j < BV; ++j) {
-      const int i = tid + j * WT, r = i / (BN / 8), c = (i % (BN / 8)) * 8;
-      br[j] = (k0 + r < k_hi && n0 + c < N) ? *reinterpret_cast<const u16x8_t*>(B + (int64_t)(k0 + r) * ldb + n0 + c)
-                                            : u16x8_t(0);
-    }
+  for (int i = 0; i < BI; ++i) {
+    const int r = (8 * i + wid) * BRI + lane / (BN / 8), c = n0 + 8 * ((lane % (BN / 8)) ^ swz(r));
+    b_r[i] = r;
+    b_off[i] = c < N ? (uint32_t)(((int64_t)(k_lo + r) * ldb + c) * 2) : MG_OOB;
+  }
+  auto issue = [&](int t) {
+    const int k0 = t * BK;
+    bf16_t* st = dsm + (t % NB) * STAGE;
+    const uint32_t sa = (uint32_t)((int64_t)k0 * lda * 2), sb = (uint32_t)((int64_t)k0 * ldb * 2);
+#pragma unroll
+    for (int i = 0; i < AI; ++i)
+      dma16(ra, k_lo + k0 + a_r[i] < k_hi ? a_off[i] : MG_OOB, sa, st + (8 * i + wid) * 512);
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      dma16(rb, k_lo + k0 + b_r[i] < k_hi ? b_off[i] : MG_OOB, sb, st + AE + (8 * i + wid) * 512);
   };
   f32x4_t acc[FM][FN];
 #pragma unroll
   for (int a = 0; a < FM; ++a)
 #pragma unroll
     for (int b = 0; b < FN; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  load(k_lo);
-  int buf = 0;
-  for (int k0 = k_lo; k0 < k_hi; k0 += WBK) {
+  const int nsteps = std::max(0, (k_hi - k_lo + BK - 1) / BK);
 #pragma unroll
-    for (int j = 0; j < AV; ++j) {
-      const int i = tid + j * WT, r = i / (BM / 8), c = (i % (BM / 8)) * 8;
-      *reinterpret_cast<u16x8_t*>(&As[buf][r * LDA + (c ^ swz(r))]) = ar[j];
+  for (int p = 0; p < NB - 2; ++p) issue(p);
+  for (int t = 0; t < nsteps; ++t) {
+    issue(t + NB - 2);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * PER) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bf16_t* as = dsm + (t % NB) * STAGE;
+    const bf16_t* bs = as + AE;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8_t b[FN];
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) b[fn] = mc_frag(bs, BN, kk, wn * WN + 16 * fn, lane);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const bf16x8_t a = mc_frag(as, BM, kk, wm * WM + 16 * fm, lane);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[fn], acc[fm][fn], 0, 0, 0);
+      }
     }
-#pragma unroll
-    for (int j = 0; j < BV; ++j) {
-      const int i = tid + j * WT, r = i / (BN / 8), c = (i % (BN / 8)) * 8;
-      *reinterpret_cast<u16x8_t*>(&Bs[buf][r * LDB + (c ^ swz(r))]) = br[j];
-    }
-    __syncthreads();  // (the other buffer was last read before the previous barrier)
-    if (k0 + WBK < k_hi) load(k0 + WBK);
-    bf16x8_t b[FN];
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) b[fn] = mc_frag(Bs[buf], LDB, 0, wn * WN + 16 * fn, lane);
-#pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
-      const bf16x8_t a = mc_frag(As[buf], LDA, 0, wm * WM + 16 * fm, lane);
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[fn], acc[fm][fn], 0, 0, 0);
-    }
-    buf ^= 1;
   }
-  // this block's partial tile: acc[fm][fn][j] = C[m0 + wm*WM + 16fm + 4(lane>>4) + j][n0 + wn*WN + 16fn + (lane&15)]
-  float* pb = part + (int64_t)blockIdx.z * M * N;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-row DMAs past the last step land before the block ends
+  // this block's partial tile in fragment order (one 1-KiB coalesced store per fragment and wave; k_wide_final maps it
+  // back to (m, n)): part[split][tile][(fm * FN + fn) * 8 + wave][lane][4]
+  float* pb = part + ((int64_t)blockIdx.z * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x) * (BM * BN);
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = m0 + wm * WM + 16 * fm + 4 * (lane >> 4) + j, n = n0 + wn * WN + 16 * fn + (lane & 15);
-        if (m < M && n < N) pb[(int64_t)m * N + n] = acc[fm][fn][j];
-      }
+      *reinterpret_cast<f32x4_t*>(pb + (((fm * FN + fn) * 8 + wid) * 64 + lane) * 4) = acc[fm][fn];
 }
 
-// fold level 1: tmp[grp][i] = sum of part[s][i] for s in the group's split range (ascending); level 2 (final):
-// C[m][n] += alpha * sum of tmp[grp][i] (ascending)
-__global__ __launch_bounds__(256) void k_wide_fold(const float* __restrict__ part, int nsplit, int64_t MN, int per,
+// fold level 1: tmp[grp][i] = sum of part[s][i] for s in the group's split range (ascending), 4 elements per thread;
+// level 2 (final): C[m][n] += alpha * sum of tmp[grp][i] (ascending), the fragment-order index i mapped to (m, n)
+__global__ __launch_bounds__(256) void k_wide_fold(const float* __restrict__ part, int nsplit, int64_t TT, int per,
                                                    float* __restrict__ tmp) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= MN) return;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= TT) return;
   const int s0 = blockIdx.y * per, s1 = std::min(nsplit, s0 + per);
-  float s = 0.f;
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
   int r = s0;
   for (; r + 8 <= s1; r += 8) {
-    float v[8];
+    f32x4_t v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = part[(int64_t)(r + q) * MN + i];
+    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const f32x4_t*>(part + (int64_t)(r + q) * TT + i);
 #pragma unroll
     for (int q = 0; q < 8; ++q) s += v[q];
   }
-  for (; r < s1; ++r) s += part[(int64_t)r * MN + i];
-  tmp[(int64_t)blockIdx.y * MN + i] = s;
+  for (; r < s1; ++r) s += *reinterpret_cast<const f32x4_t*>(part + (int64_t)r * TT + i);
+  *reinterpret_cast<f32x4_t*>(tmp + (int64_t)blockIdx.y * TT + i) = s;
 }
-__global__ __launch_bounds__(256) void k_wide_final(const float* __restrict__ tmp, int ngrp, int M, int N, float alpha,
-                                                    float* __restrict__ C, int64_t ldc) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, MN = (int64_t)M * N;
-  if (i >= MN) return;
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_wide_final(const float* __restrict__ tmp, int ngrp, int64_t TT, int tiles_m,
+                                                    int M, int N, float alpha, float* __restrict__ C, int64_t ldc) {
+  constexpr int WM = BM / 2, WN = BN / 4, FN = WN / 16;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= TT) return;
+  const int tile = (int)(i / (BM * BN)), r = (int)(i % (BM * BN));
+  const int q = r >> 8, lane = (r >> 2) & 63, j = r & 3;
+  const int w = q & 7, fmn = q >> 3, fm = fmn / FN, fn = fmn % FN;
+  const int m = (tile % tiles_m) * BM + (w >> 2) * WM + 16 * fm + 4 * (lane >> 4) + j;
+  const int n = (tile / tiles_m) * BN + (w & 3) * WN + 16 * fn + (lane & 15);
+  if (m >= M || n >= N) return;
   float s = 0.f;
-  for (int g = 0; g < ngrp; ++g) s += tmp[(int64_t)g * MN + i];
-  const int64_t m = i / N, n = i - m * N;
+  for (int g = 0; g < ngrp; ++g) s += tmp[(int64_t)g * TT + i];
   // an atomic add keeps mg_gemm's atomic-epilogue contract (concurrent writers into one gradient buffer, e.g. from
   // the main and the side stream, accumulate); with one writer it is the same single fp32 addition as C += alpha s
-  atomicAdd(C + m * ldc + n, alpha * s);
+  atomicAdd(C + (int64_t)m * ldc + n, alpha * s);
+}
+
+template <int BM, int BN, int BK, int NB>
+void launch_wide(dim3 grid, hipStream_t st, const bf16_t* a, int64_t lda, const bf16_t* b, int64_t ldb, int M, int N,
+                 int K, int kchunk, float* part) {
+  constexpr int bytes = NB * BK * (BM + BN) * 2;
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad_wide<BM, BN, BK, NB>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((k_wgrad_wide<BM, BN, BK, NB>), grid, dim3(WT), bytes, st, a, lda, b, ldb, M, N, K, kchunk, part);
 }
 
 }  // namespace
 
 // Called by mg_gemm for bf16, a_kc = b_kc = 0 (both operands [K][*] row-major), an fp32 C accumulated through a
-// plain atomic epilogue (alpha only), large K and small M x N.  Returns true when it handled the call.
+// plain atomic epilogue (alpha only), and by mg_conv2d_wgrad for 1x1 / stride-1 convolutions.  Returns true when it
+// handled the call.
 bool mg_wgrad_wide(int M, int N, int K, const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
                    float alpha, hipStream_t st) {
-  if (g_mg_tune[MG_TUNE_WIDE_WGRAD] == 1) return false;  // A/B: the generic split-K GEMM
+  const int mode = g_mg_tune[MG_TUNE_WIDE_WGRAD];
+  if (mode == 1) return false;  // A/B: the generic split-K GEMM
   if (K < 2048 || M % 8 || N % 8 || (int64_t)M * N > 1024 * 1024) return false;
-  // measured (profiles/round4_wgrad_wide_probe.txt): a win only when K is long against the tile edges -- the
-  // (384|128) x 128 x 65536 projections, 1.2-1.3x; at K = 4096-16384 the partial-tile folds cost more than the
-  // generic GEMM's re-reads save, and a 16-wide N leaves the MFMA tile mostly empty (2: every eligible shape, tests)
-  if (g_mg_tune[MG_TUNE_WIDE_WGRAD] != 2 && ((int64_t)K < 64 * (int64_t)(M + N) || M < 64 || N < 64)) return false;
-  const bool big = M >= 256 && N >= 256;
-  const int BM = big ? 256 : 128, BN = big ? 256 : 128;
-  const int64_t tiles = (int64_t)cdiv(M, BM) * cdiv(N, BN), MN = (int64_t)M * N;
-  // ~256 blocks, >= 512 rows of K each
-  int splits = (int)std::max<int64_t>(1, std::min<int64_t>(256 / tiles, K / 512));
-  int kchunk = (K + splits - 1) / splits;
-  kchunk = (kchunk + WBK - 1) / WBK * WBK;
-  splits = (K + kchunk - 1) / kchunk;
+  // a win when K is long against the tile edges (profiles/round6_wgrad_wide_probe.txt); a 16-wide N leaves the MFMA
+  // tile mostly empty (2: every eligible shape, tests)
+  if (mode < 2 && ((int64_t)K < 32 * (int64_t)(M + N) || M < 64 || N < 64)) return false;
+  // 128^2 tiles, K steps of 32 rows in 8 LDS stages of 16 KiB (six steps = 96 KiB in flight per block: the HBM
+  // latency under load is ~2 us against ~0.1 us of MFMA work per step); 256^2 tiles (operands read once, only two
+  // 32 KiB steps in flight within the LDS) on request (mode 4)
+  const bool big = M >= 256 && N >= 256 && mode == 4;
+  const int BM = big ? 256 : 128, BN = BM, BK = 32;
+  const int64_t tiles = (int64_t)cdiv(M, BM) * cdiv(N, BN);
+  // ~target blocks (tuning slot MG_TUNE_WIDE_BLOCKS, default 256), >= 8 K steps each, <= 128 splits: the folds read
+  // every split's partial tile (measured, profiles/round6_wgrad_wide_probe.txt: 128 x 128 x 65536 in 128 splits
+  // 18.8 us with its folds, in 256 splits 23.6 us)
+  const int target = g_mg_tune[MG_TUNE_WIDE_BLOCKS] > 0 ? (int)g_mg_tune[MG_TUNE_WIDE_BLOCKS] : 256;
+  int splits = (int)std::max<int64_t>(
+      1, std::min<int64_t>({std::max<int64_t>(1, target / tiles), (int64_t)K / (8 * BK), (int64_t)128}));
+  const int kchunk = cdiv(cdiv(K, splits), BK) * BK;
+  splits = cdiv(K, kchunk);
   const int per = 16, ngrp = (splits + per - 1) / per;
-  float* part = reinterpret_cast<float*>(mg_workspace((size_t)(splits + ngrp) * MN * sizeof(float), st));
+  const int64_t TT = tiles * BM * BN;  // partial elements per split (fragment order, whole tiles)
+  float* part = reinterpret_cast<float*>(mg_workspace((size_t)(splits + ngrp) * TT * sizeof(float), st));
   if (!part) return false;
-  float* tmp = part + (size_t)splits * MN;
+  float* tmp = part + (size_t)splits * TT;
   const dim3 grid(cdiv(M, BM), cdiv(N, BN), splits);
   const bf16_t* a = reinterpret_cast<const bf16_t*>(A);
   const bf16_t* b = reinterpret_cast<const bf16_t*>(B);
-  if (big) hipLaunchKernelGGL((k_wgrad_wide<256, 256>), grid, dim3(WT), 0, st, a, lda, b, ldb, M, N, K, kchunk, part);
-  else hipLaunchKernelGGL((k_wgrad_wide<128, 128>), grid, dim3(WT), 0, st, a, lda, b, ldb, M, N, K, kchunk, part);
-  hipLaunchKernelGGL(k_wide_fold, dim3(cdiv(MN, 256), ngrp), dim3(256), 0, st, part, splits, MN, per, tmp);
-  hipLaunchKernelGGL(k_wide_final, dim3(cdiv(MN, 256)), dim3(256), 0, st, tmp, ngrp, M, N, alpha, C, ldc);
+  if (big) launch_wide<256, 256, 32, 4>(grid, st, a, lda, b, ldb, M, N, K, kchunk, part);
+  else launch_wide<128, 128, 32, 8>(grid, st, a, lda, b, ldb, M, N, K, kchunk, part);
+  hipLaunchKernelGGL(k_wide_fold, dim3(cdiv(TT, 1024), ngrp), dim3(256), 0, st, part, splits, TT, per, tmp);
+  if (big)
+    hipLaunchKernelGGL((k_wide_final<256, 256>), dim3(cdiv(TT, 256)), dim3(256), 0, st, tmp, ngrp, TT, (int)grid.x, M,
+                       N, alpha, C, ldc);
+  else
+    hipLaunchKernelGGL((k_wide_final<128, 128>), dim3(cdiv(TT, 256)), dim3(256), 0, st, tmp, ngrp, TT, (int)grid.x, M,
+                       N, alpha, C, ldc);
   return true;
 }

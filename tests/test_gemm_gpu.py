@@ -377,10 +377,12 @@ def test_conv_wgrad_stride1_loader(dtype, B, H, Cin, Cout, k):
 
 
 @pytest.mark.parametrize("M,N,K,alpha", [(384, 128, 65536, 1.0), (128, 128, 65536, 1.0), (256, 256, 16384, 0.5),
-                                         (1536, 512, 4096, 1.0), (256, 16, 65536, 1.0), (136, 200, 5000, 1.0)])
+                                         (1536, 512, 4096, 1.0), (256, 16, 65536, 1.0), (136, 200, 5000, 1.0),
+                                         (128, 256, 65536, 1.0), (512, 512, 2048, 1.0), (8, 128, 3000, 2.0)])
 def test_wide_weight_gradient(M, N, K, alpha):
     """Linear-layer weight gradients C += alpha * A^T B (bf16 [K][M] x [K][N], fp32 C through an atomic epilogue):
-    the wide split-K kernel (csrc/mg_wgrad_wide.hip, forced onto every eligible shape: tuning slot 15 = 2) against
+    the long-reduction kernel (csrc/mg_wgrad_wide.hip, forced onto every eligible shape: tuning slot 15 = 2, and on
+    256^2 tiles: 4) against
     fp64 on the same bf16 operands and against the generic split-K GEMM (slot 15 = 1); fixed-order fold: two calls
     give the same bits.  The automatic routing (slot 15 = 0) is held to the same fp64 bound."""
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
@@ -396,6 +398,8 @@ def test_wide_weight_gradient(M, N, K, alpha):
     L.call("mg_set_tuning", 15, 2)
     try:
         C1, C2 = run(), run()
+        L.call("mg_set_tuning", 15, 4)  # 256^2 tiles where M, N >= 256
+        C5 = run()
         L.call("mg_set_tuning", 15, 1)
         C3 = run()
     finally:
@@ -405,4 +409,35 @@ def test_wide_weight_gradient(M, N, K, alpha):
     assert float((C1.double() - ref).abs().max()) <= 2e-6 * scale * (K / 4096) ** 0.5 + 1e-6
     assert float((C1 - C3).abs().max()) <= 4e-6 * scale * (K / 4096) ** 0.5 + 1e-6
     assert torch.equal(C1, C2)
+    assert float((C5.double() - ref).abs().max()) <= 2e-6 * scale * (K / 4096) ** 0.5 + 1e-6
     assert float((C4.double() - ref).abs().max()) <= 2e-6 * scale * (K / 4096) ** 0.5 + 1e-6
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout", [(64, 16, 256, 128), (256, 8, 256, 256), (16, 8, 512, 512), (8, 16, 128, 8)])
+def test_conv1x1_weight_gradient_long_reduction(B, H, Cin, Cout):
+    """1x1 / stride-1 conv weight gradients (ConvolutionBlock.skip_proj, AttentionBlock.proj_in / proj_out,
+    t2i_moe_gan.py:574, :615-616) go through the long-reduction kernel (mg_wgrad_wide.hip) when it takes the shape:
+    gw += gy^T x over the B*H*W pixels, against fp64 on the same bf16 operands and against the generic conv weight
+    gradient (tuning slot 15 = 1), accumulating into a non-zero gradient."""
+    g = torch.Generator(device=DEV).manual_seed(B * H + Cin)
+    x = torch.randn(B, H, H, Cin, device=DEV, generator=g).bfloat16()
+    gy = torch.randn(B, H, H, Cout, device=DEV, generator=g).bfloat16()
+    base = torch.randn(Cout, Cin, 1, 1, device=DEV, generator=g)
+    ref = base.double() + (gy.reshape(-1, Cout).double().T @ x.reshape(-1, Cin).double()).view(Cout, Cin, 1, 1)
+
+    def run():
+        gw = base.clone()
+        ops.conv2d_wgrad(gy, x, Cout, 1, 1, 1, 0, gw)
+        return gw
+    gw_auto = run()
+    L.call("mg_set_tuning", 15, 1)
+    try:
+        gw_gen = run()
+    finally:
+        L.call("mg_set_tuning", 15, 0)
+    torch.cuda.synchronize()
+    scale = float((ref - base.double()).abs().max())
+    P = B * H * H
+    bound = 2e-6 * scale * (P / 4096) ** 0.5 + 1e-5
+    assert float((gw_auto.double() - ref).abs().max()) <= bound
+    assert float((gw_gen.double() - ref).abs().max()) <= bound

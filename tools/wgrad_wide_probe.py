@@ -1,5 +1,7 @@
-"""Isolated timing of the step's linear-layer weight gradients (C += A^T B, bf16 [K][M] x [K][N], fp32 C through an
-atomic epilogue) at their C2 shapes: the wide split-K kernel (mg_wgrad_wide.hip) vs the generic split-K GEMM."""
+"""Isolated timing of the step's long-reduction weight gradients (C += A^T B, bf16 [K][M] x [K][N], fp32 C through
+an atomic epilogue) at their C2 shapes -- the linear layers' (attention in / out projections, router features) and
+the 1x1 convolutions' (Cout x Cin over B*H*W pixels) -- through the long-reduction kernel (mg_wgrad_wide.hip) at
+several grid targets vs the generic split-K GEMM, and a parity check of the kernel against the generic result."""
 import os
 import sys
 
@@ -11,28 +13,51 @@ from moegan_mi import _lib as L  # noqa: E402
 from moegan_mi import ops  # noqa: E402
 
 DEV = "cuda"
-SHAPES = [(384, 128, 65536), (128, 128, 65536), (768, 256, 16384), (256, 256, 16384), (1536, 512, 4096),
-          (512, 512, 4096), (256, 16, 65536)]
+SHAPES = [(384, 128, 65536), (128, 128, 65536), (128, 256, 65536), (768, 256, 16384), (256, 256, 16384),
+          (256, 512, 16384), (1536, 512, 4096), (512, 512, 4096), (256, 16, 65536)]
+MODES = (2, 4)
+
+
+def timeit(fn, n=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e3
+
+
 for M, N, K in SHAPES:
     g = torch.Generator(device=DEV).manual_seed(0)
     A = torch.randn(K, M, device=DEV, generator=g).bfloat16()
     B = torch.randn(K, N, device=DEV, generator=g).bfloat16()
     C = torch.zeros(M, N, device=DEV)
-    res = []
-    for mode in (1, 2, 0):  # generic, wide (forced), automatic routing
+    fn = lambda: ops.gemm(A, B, M, N, K, a_kc=False, b_kc=False, out=C, ep=ops.E(atomic=1), splits=0)  # noqa
+    res = {}
+    L.call("mg_set_tuning", 15, 1)
+    res["generic"] = timeit(fn)
+    C.zero_()
+    fn()
+    ref = C.clone()
+    errs = []
+    for mode in MODES:
         L.call("mg_set_tuning", 15, mode)
-        fn = lambda: ops.gemm(A, B, M, N, K, a_kc=False, b_kc=False, out=C, ep=ops.E(atomic=1), splits=0)  # noqa
-        for _ in range(3):
-            fn()
+        for tb in (128, 256, 512):
+            L.call("mg_set_tuning", 27, tb)
+            res[f"{'w' if mode == 2 else 'w256'}/{tb}"] = timeit(fn)
+        L.call("mg_set_tuning", 27, 0)
+        C.zero_()
+        fn()
         torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(20):
-            fn()
-        e.record()
-        torch.cuda.synchronize()
-        res.append(s.elapsed_time(e) / 20 * 1e3)
+        errs.append(((C - ref).norm() / ref.norm()).item())
+    err = max(errs)
     L.call("mg_set_tuning", 15, 0)
+    res["auto"] = timeit(fn)
     mb = K * (M + N) * 2 / 1e6
-    print(f"({M:5d},{N:4d},{K:6d}) generic {res[0]:7.1f} us  wide {res[1]:7.1f} us  auto {res[2]:7.1f} us  "
-          f"({mb:.0f} MB operands: {mb / res[1]:.2f} TB/s wide)", flush=True)
+    best = min(v for k_, v in res.items() if k_.startswith("w"))
+    print(f"({M:5d},{N:4d},{K:6d}) " + "  ".join(f"{k_} {v:6.1f}" for k_, v in res.items()) +
+          f"  us | {mb:.0f} MB operands, best wide {mb / best:.2f} TB/s, rel diff vs generic {err:.1e}", flush=True)
