@@ -297,7 +297,8 @@ __global__ __launch_bounds__(256) void k_ln_fwd_v(const T* __restrict__ x, int64
 }
 
 // backward: each wave walks ROWS_PER_WAVE rows (RPW at a time); gamma/beta gradients are accumulated per lane
-// (fixed channels), folded over the wave's row slots and the block's waves in LDS, one atomic per channel/block.
+// (fixed channels), folded over the wave's row slots and the block's waves in LDS into one partial row per block
+// (part; the host folds the rows), or one atomic per channel and block when part is null.
 template <typename T, typename TG, int LPR>
 __global__ __launch_bounds__(256) void k_ln_bwd_v(const TG* __restrict__ gy, int64_t ldg, const T* __restrict__ x,
                                                   int64_t ldx, int R, const float* __restrict__ mean,
@@ -424,16 +425,18 @@ extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t
   if (R == 0) return MG_OK;
   if (ldg % 8 == 0 && ldx % 8 == 0 && (!gx || ldgx % 8 == 0) && mg_al16(gy) && mg_al16(x) && (!gx || mg_al16(gx)) &&
       mg_al16(gamma)) {
-    // ~1024 waves; each walks a multiple of the rows it covers at once
+    // two iterations of two row slots per wave (16 rows at C = 128, 4 at C = 512): 1024 - 4096 waves, ~4 per SIMD
+    // to hide the row loads.  Round 5 ran ~1024 waves (one per SIMD, 8 - 64 serial rows each: 16 - 28 us per call)
+    // because every block added its gamma / beta sums into the same 2C addresses with atomics; now each block
+    // writes one partial row [2C] and a fixed-order rows fold (mg_fold.hip, deferred to the backward's flush inside
+    // a step) adds them, in both library modes
     const int lpr = C / 8, rw = 64 / lpr;
-    // ~1024 waves (more blocks measured slower at C = 256 / 512: each adds 2C same-address atomics for
-    // ggamma / gbeta), two row slots per iteration
-    int rows = std::max(2 * rw, cdiv(R, 1024));
-    rows = cdiv(rows, 2 * rw) * 2 * rw;
+    const int rows = 4 * rw;
     dim3 g2(cdiv(cdiv(R, rows), 4)), b2(256);
     float* part = nullptr;
-    if (ggamma && mg_det()) {
-      part = reinterpret_cast<float*>(mg_workspace((size_t)g2.x * 2 * C * sizeof(float), st));
+    bool deferred = false;
+    if (ggamma) {
+      part = mg_fold_partials((size_t)g2.x * 2 * C * sizeof(float), st, &deferred);
       if (!part) return MG_ERR_LAUNCH;
     }
 #define LV_(T, TG, P) hipLaunchKernelGGL((k_ln_bwd_v<T, TG, P>), g2, b2, 0, st, (const TG*)gy, ldg, (const T*)x, ldx, R, \
@@ -446,7 +449,7 @@ extern "C" int mg_layernorm_bwd(int dtype, int gy_dtype, const void* gy, int64_t
     }
 #undef LVC_
 #undef LV_
-    if (part) mg_det_fold_rows(part, (int)g2.x, 2 * C, C, ggamma, gbeta, st);
+    if (part) mg_fold_rows_submit(mg_fold_rows{part, 2 * C, (int32_t)g2.x, 2 * C, C, ggamma, gbeta}, deferred, st);
     return mg_check_launch("mg_layernorm_bwd");
   }
   int rpw = std::max(1, std::min(64, R / 1024));

@@ -395,7 +395,7 @@ struct LdKCConvT {
     return s;
   }
   static constexpr bool kGlds = !XF;
-  static constexpr bool kConv = false;
+  static constexpr bool kConv = true;  // (64^2 tiles stage it by LDS-DMA)
   template <bool TAIL, int TBK> MG_DEV void offs(const Slot& s, int k0, int kend, uint32_t& off, uint32_t& soff) const {
     const int k = k0 + s.kofs;
     const int kk = SC ? k : k0;  // SC = false: the step stays inside tap k0 / Cg (wave-uniform)

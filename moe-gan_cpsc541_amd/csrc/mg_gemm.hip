@@ -848,7 +848,9 @@ void run_dgrad_s2(const void* g, int B, int OH, int OW, int Cg, const void* wcls
   ep.rm_lgOW = ilog2(OW);
   ep.rm_lgOHW = ilog2(OH * OW);
   Grouping grp{3, 4, nullptr, nullptr, Mc};
-  if (Cin >= 128 && !SC)
+  // 128^2 tiles when they fill the chip; the 8x8 -> 4x4 discriminator conv (4 x 4096 rows x 128) had 128 of them,
+  // 16 serial K steps each on half the CUs: 64^2 tiles (512, LDS-DMA staged: LdKCConvT::kConv)
+  if (Cin >= 128 && !SC && (int64_t)cdiv(4 * Mc, 128) * cdiv(Cin, 128) >= 256)
     launch_gemm<T, 128, 128, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);
   else if (sizeof(T) == 2 && Cin <= 32 && !SC)  // image gradient (Cin = 3): 128 x 32 tiles waste 8x, not 16x, MFMA work
     launch_gemm<T, 128, 32, true, true>(la, lb, ep, 4 * Mc, Cin, 4 * Cg, 1, grp, 0, st);

@@ -58,3 +58,36 @@ def test_attention_ragged_tokens_forward(L):
     assert rel(out[:B * L], ref) < 2e-2
     assert (lse[:B * heads * L].view(B, heads, L) - torch.logsumexp(s, -1)).abs().max().item() < 2e-2
     assert bool((out[B * L:].float() == 7.0).all()) and bool((lse[B * heads * L:] == 7.0).all())
+
+
+@pytest.mark.parametrize("R,C", [(65536, 128), (16384, 256), (4096, 512), (1000, 128), (7, 512)])
+@pytest.mark.parametrize("accumulate", [0, 1])
+def test_layernorm_bwd_vs_autograd(R, C, accumulate):
+    """LayerNorm backward (AttentionBlock.norm1 / norm2, t2i_moe_gan.py:545-560) at the step's row counts and ragged
+    ones: input gradient (optionally accumulated) and the gamma / beta gradients (per-block partial rows + the
+    fixed-order rows fold) against fp32 autograd on the same bf16 operands; two calls give the same bits."""
+    g = torch.Generator(device=DEV).manual_seed(R + C)
+    x = (torch.randn(R, C, device=DEV, generator=g) * 2 + 0.5).bfloat16()
+    gy = torch.randn(R, C, device=DEV, generator=g).bfloat16()
+    gamma = torch.rand(C, device=DEV, generator=g) + 0.5
+    beta = torch.randn(C, device=DEV, generator=g)
+    base = torch.randn(R, C, device=DEV, generator=g).bfloat16()
+    _, mean, rstd = ops.layernorm_fwd(x, gamma, beta)
+    xr = x.float().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (C,), gr, br, 1e-5).backward(gy.float())
+
+    def run():
+        gx = base.clone()
+        gg = torch.full((C,), 0.25, device=DEV)
+        gb = torch.full((C,), -0.5, device=DEV)
+        ops.layernorm_bwd(gy, x, mean, rstd, gamma, gx, gg, gb, accumulate=accumulate)
+        return gx, gg, gb
+    gx, gg, gb = run()
+    gx2, gg2, gb2 = run()
+    torch.cuda.synchronize()
+    want_gx = xr.grad + (base.float() if accumulate else 0)
+    assert float((gx.float() - want_gx).abs().max()) <= 2e-2 * float(want_gx.abs().max()) + 1e-2
+    assert torch.allclose(gg, gr.grad + 0.25, rtol=1e-4, atol=1e-3 * (R / 1000) ** 0.5)
+    assert torch.allclose(gb, br.grad - 0.5, rtol=1e-4, atol=1e-3 * (R / 1000) ** 0.5)
+    assert torch.equal(gx, gx2) and torch.equal(gg, gg2) and torch.equal(gb, gb2)
