@@ -231,8 +231,9 @@ int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngroups, const 
    one block per CU, gfx950), Hd % 128 == 0; gb2 (fp32 [ngroups, C], accumulated; NULL skips it) += the column
    sums of gG over the group's rows (the layer-2 bias gradient, from the gG tile the pass holds in LDS, per-tile
    partial rows folded in tile order); W1 [G, Hd, C],
-   W2 [G, C, Hd]; grid = max_tiles blocks of 128 rows. */
-int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1, const void* W2, void* gP, void* gX, float* gb1, float* gb2, void* stream);
+   W2 [G, C, Hd]; grid = max_tiles blocks of 128 rows.  hid (optional, bf16 [total_rows, Hd]): GELU(pre) as the
+   weight gradient of W2 reads it, from the same erf evaluation as GELU'(pre). */
+int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off, const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1, const void* W2, void* gP, void* gX, void* hid, float* gb1, float* gb2, void* stream);
 
 /* ---- op-level entry points ---- */
 

@@ -253,11 +253,23 @@ MG_DEV bf16x8_t mc_frag(const bf16_t* img, int ld, int kr0, int c0, int lane) {
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// GELU'(x) and GELU(x) from one erf evaluation: the operation sequences of gelu_fast_grad2 and gelu_fast2
+// (mg_common.h), so both results are bit-identical to those functions -- the GELU output is what the weight gradient
+// of W2 otherwise forms on load from the pre-activation (mg_gemm.h vgelu)
+MG_DEV f32x2_t gelu_fast_both2(f32x2_t x, f32x2_t& y) {
+  f32x2_t g;
+  const f32x2_t e = gelu_erf_core(x, g);
+  const f32x2_t hx = x * gsplat<f32x2_t>(0.5f);
+  y = gfma(hx, e, hx);
+  return gfma(x * gsplat<f32x2_t>(0.3989422804014327f), g, gfma(gsplat<f32x2_t>(0.5f), e, gsplat<f32x2_t>(0.5f)));
+}
+
 template <int C, int FH>
 __device__ __forceinline__ void ffn_bwd_body(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
-    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2,
+    bf16_t* __restrict__ hid) {
   __shared__ FfnBwdSmem<C, FH> sm;
   const int t = blockIdx.x;
   int g = -1;
@@ -276,6 +288,7 @@ __device__ __forceinline__ void ffn_bwd_body(
   const bf16_t* W2g = W2 + (int64_t)g * C * Hd;
   const bf16_t* preb = Pre + (int64_t)r0 * Hd;
   bf16_t* gpb = gP + (int64_t)r0 * Hd;
+  bf16_t* hidb = hid ? hid + (int64_t)r0 * Hd : nullptr;
   float* partb = part + (int64_t)t * Hd;
 
   // ---- gG tile -> LDS (rows past the group read as zeros) ----
@@ -361,14 +374,20 @@ __device__ __forceinline__ void ffn_bwd_body(
         const int row = wm * 32 + fm * 16 + fr;
         const int col = wn * (FH / 2) + fn * 16 + 4 * (lane >> 4);
         const u16x4_t pv = pre_r[fm][fn];
-        u16x4_t gv;
+        u16x4_t gv, hv;
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {  // element pairs on packed fp32 (mg_common.h gelu_fast_grad2)
-          const f32x2_t d = gelu_fast_grad2(f32x2_t{bf2f(pv[j]), bf2f(pv[j + 1])});
+          f32x2_t y;
+          const f32x2_t d = gelu_fast_both2(f32x2_t{bf2f(pv[j]), bf2f(pv[j + 1])}, y);
           gv[j] = __builtin_bit_cast(unsigned short, f2bf(acc1[fm][fn][j] * d.x));
           gv[j + 1] = __builtin_bit_cast(unsigned short, f2bf(acc1[fm][fn][j + 1] * d.y));
+          hv[j] = __builtin_bit_cast(unsigned short, f2bf(y.x));
+          hv[j + 1] = __builtin_bit_cast(unsigned short, f2bf(y.y));
         }
-        if (row < nrows) *reinterpret_cast<u16x4_t*>(gpb + (int64_t)row * Hd + h0 + col) = gv;
+        if (row < nrows) {
+          *reinterpret_cast<u16x4_t*>(gpb + (int64_t)row * Hd + h0 + col) = gv;
+          if (hidb) *reinterpret_cast<u16x4_t*>(hidb + (int64_t)row * Hd + h0 + col) = hv;
+        }
         *reinterpret_cast<u16x4_t*>(sm.hs + kci<FBM>(row, col)) = gv;  // rows past the group: gG = 0, so gP = 0
       }
     if (h0 + FH < Hd) load_pre(h0 + FH);
@@ -450,15 +469,17 @@ template <int C>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_moe_ffn_bwd(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
-    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
-  ffn_bwd_body<C, 64>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2);
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2,
+    bf16_t* __restrict__ hid) {
+  ffn_bwd_body<C, 64>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2, hid);
 }
 template <int C, int FH>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_moe_ffn_bwd_w2(
     const bf16_t* __restrict__ gG, const bf16_t* __restrict__ Pre, int ngroups, const int* __restrict__ row_off,
     const int* __restrict__ tile_off, int Hd, const bf16_t* __restrict__ W1, const bf16_t* __restrict__ W2,
-    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2) {
-  ffn_bwd_body<C, FH>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2);
+    bf16_t* __restrict__ gP, bf16_t* __restrict__ gX, float* __restrict__ part, float* __restrict__ part2,
+    bf16_t* __restrict__ hid) {
+  ffn_bwd_body<C, FH>(gG, Pre, ngroups, row_off, tile_off, Hd, W1, W2, gP, gX, part, part2, hid);
 }
 
 // gb1[g][h] += sum over the tiles of group g (tile order) of part[tile][h]: 64 columns x 4 tile lanes per block,
@@ -515,10 +536,11 @@ extern "C" int mg_moe_ffn_fwd(int dtype, int total_rows, int C, int Hd, int ngro
 
 extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngroups, const int32_t* row_off,
                               const int32_t* tile_off, int max_tiles, const void* gG, const void* pre, const void* W1,
-                              const void* W2, void* gP, void* gX, float* gb1, float* gb2, void* stream) {
+                              const void* W2, void* gP, void* gX, void* hid, float* gb1, float* gb2, void* stream) {
   MG_REQUIRE(dtype == MG_BF16, "bf16 only");
   MG_REQUIRE(C == 128 || C == 256, "C must be 128 or 256");
   MG_REQUIRE(Hd > 0 && Hd % 128 == 0, "Hd must be a multiple of 128");
+  MG_REQUIRE(!hid || mg_al16(hid), "hid must be 16-byte aligned");
   MG_REQUIRE(ngroups >= 1 && ngroups <= 64, "1 <= ngroups <= 64");
   MG_REQUIRE(mg_al16(gG) && mg_al16(pre) && mg_al16(W1) && mg_al16(W2) && mg_al16(gP) && mg_al16(gX),
              "operands must be 16-byte aligned");
@@ -534,7 +556,8 @@ extern "C" int mg_moe_ffn_bwd(int dtype, int total_rows, int C, int Hd, int ngro
   hipLaunchKernelGGL((K<__VA_ARGS__>), dim3(max_tiles), dim3(FT), 0, st, reinterpret_cast<const bf16_t*>(gG),       \
                      reinterpret_cast<const bf16_t*>(pre), ngroups, row_off, tile_off, Hd,                            \
                      reinterpret_cast<const bf16_t*>(W1), reinterpret_cast<const bf16_t*>(W2),                        \
-                     reinterpret_cast<bf16_t*>(gP), reinterpret_cast<bf16_t*>(gX), part, part2)
+                     reinterpret_cast<bf16_t*>(gP), reinterpret_cast<bf16_t*>(gX), part, part2,                  \
+                     reinterpret_cast<bf16_t*>(hid))
   // C = 128: 128-unit hidden chunks by default (half the chunk barriers, twice the MFMA work between them; 144 KiB of
   // LDS); tuning slot MG_TUNE_FFN_BWD_OCC = 3 keeps the 64-unit chunks of rounds 4-5 (A/B)
   if (C == 256) L_(k_moe_ffn_bwd_w2, 256, 64);

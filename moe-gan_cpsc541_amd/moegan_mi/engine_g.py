@@ -579,16 +579,21 @@ class GeneratorEngine:
         gP = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
         gX = torch.empty(n, C, device=self.dev, dtype=self.cdt)
         fused = ops.ffn_bwd_fusable(self.cdt, C)
+        Hid = sv["Hid"]
         if fused:
-            # one pass per 128-row tile: gP = (gG W2_e) * GELU'(pre), gX = gP W1_e, gb1 column sums (mg_moe_ffn_bwd)
+            # one pass per 128-row tile: gP = (gG W2_e) * GELU'(pre), gX = gP W1_e, gb1 column sums, and GELU(pre)
+            # from the same erf evaluation for the W2 weight gradient (mg_moe_ffn_bwd): an 8-B store per 4 hidden
+            # units instead of the GELU formed on load in that GEMM's K loop
+            if Hid is None:
+                Hid = torch.empty(n, Hd, device=self.dev, dtype=self.cdt)
             ops.moe_ffn_bwd(gG, Pre, sv["W1"].view(E, Hd, C), sv["W2"].view(E, C, Hd), row_off, tile_off,
-                            sv["max_tiles"], gP, gX, gb1.view(E, Hd), gb2.view(E, C))
+                            sv["max_tiles"], gP, gX, gb1.view(E, Hd), gb2.view(E, C), hid=Hid)
         else:
             # expert layer 2: dH = gG @ W2_e, times GELU'(pre)
             ops.gemm_grouped(gG, sv["W2"], row_off, tile_off, sv["max_tiles"], Hd, C, b_kc=False, b_gstride=C * Hd,
                              out=gP, ldb=Hd, ep=E_(act=MUL_GELU_GRAD, aux=Pre, ld_aux=Hd))
-        if sv["Hid"] is not None:
-            gw2 = lambda: ops.gemm_grouped_wgrad(gG, sv["Hid"], row_off, n, C, Hd, gW2)  # noqa: E731
+        if Hid is not None:
+            gw2 = lambda: ops.gemm_grouped_wgrad(gG, Hid, row_off, n, C, Hd, gW2)  # noqa: E731
         else:  # GELU(Pre) formed by the B loader (the forward kept only the pre-activation)
             gw2 = lambda: ops.gemm_grouped_wgrad(gG, Pre, row_off, n, C, Hd, gW2, b_gelu=1)  # noqa: E731
         self.side.run(lambda: (gw2(), None if fused else ops.grouped_colsum(gG, row_off, C, n, gb2)), gG)

@@ -349,13 +349,13 @@ def moe_ffn_fwd(X, W1, b1, W2, b2, row_off, tile_off, max_tiles, Y, *, pre=None,
     return Y
 
 
-def moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1=None, gb2=None):
+def moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1=None, gb2=None, hid=None):
     """Fused expert FFN backward (mg_moe_ffn_bwd): gP = (gG W2_g) * GELU'(Pre), gX = gP W1_g, gb1 += colsum(gP),
-    gb2 += colsum(gG) (per group)."""
+    gb2 += colsum(gG) (per group); optionally hid = GELU(Pre) (bf16, what the W2 weight gradient reads)."""
     G, Hd, C = W1.shape
     _timed("moe_ffn_bwd", (gG.shape[0], C, Hd),
            lambda: call("mg_moe_ffn_bwd", L.MG_BF16, gG.shape[0], C, Hd, G, ptr(row_off), ptr(tile_off), max_tiles,
-                        ptr(gG), ptr(Pre), ptr(W1), ptr(W2), ptr(gP), ptr(gX), ptr(gb1), ptr(gb2), S()))
+                        ptr(gG), ptr(Pre), ptr(W1), ptr(W2), ptr(gP), ptr(gX), ptr(hid), ptr(gb1), ptr(gb2), S()))
     return gP, gX
 
 

@@ -3,6 +3,7 @@ bias + GELU (pre-activation saved) and bias epilogues): bit-identical Y, pre-act
 dispatch gather inside the kernel or from pre-gathered rows; skewed and empty experts, ragged last tiles."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
@@ -99,13 +100,25 @@ def test_fused_ffn_backward_matches_grouped_gemms(T, E, k, skew, C, occ):
     gX = torch.empty(n, C, device=DEV, dtype=bf)
     gb1 = torch.full((E, Hd), 0.25, device=DEV)
     gb2 = torch.full((E, C), -0.5, device=DEV)
-    ops.moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1, gb2)
+    Hid = torch.empty(n, Hd, device=DEV, dtype=bf)
+    ops.moe_ffn_bwd(gG, Pre, W1, W2, row_off, tile_off, max_tiles, gP, gX, gb1, gb2, hid=Hid)
+    # GELU(Pre) out of the backward = the GELU the W2 weight gradient forms on load: the two weight gradients are
+    # bit-identical (deterministic mode: one writer per element, same MFMA inputs and order)
+    L.call("mg_set_tuning", 11, 1)
+    try:
+        gw_load = ops.gemm_grouped_wgrad(gG, Pre, row_off, n, C, Hd, torch.zeros(E, C, Hd, device=DEV), b_gelu=1)
+        gw_hid = ops.gemm_grouped_wgrad(gG, Hid, row_off, n, C, Hd, torch.zeros(E, C, Hd, device=DEV))
+    finally:
+        L.call("mg_set_tuning", 11, 0)
     gb2_r = torch.full((E * C,), -0.5, device=DEV)
     ops.grouped_colsum(gG, row_off, C, n, gb2_r)
     torch.cuda.synchronize()
     L.call("mg_set_tuning", 14, 0)
     assert torch.equal(gP, gP_r)
     assert torch.equal(gX, gX_r)
+    assert torch.equal(gw_hid, gw_load)
+    hid_ref = F.gelu(Pre.float()).to(bf)  # (exact erf vs the fast form: at most one bf16 ulp apart)
+    assert float((Hid.float() - hid_ref.float()).abs().max()) <= float(hid_ref.float().abs().max()) * 2 ** -7
     scale = float((gb1_r - 0.25).abs().max())
     assert float((gb1.view(-1) - gb1_r).abs().max()) <= 1e-5 * scale + 1e-7
     # float64 column sums of the bf16 gP (layer-1 bias) and of gG (layer-2 bias), per expert
