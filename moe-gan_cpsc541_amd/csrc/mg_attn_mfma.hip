@@ -118,6 +118,18 @@ MG_DEV void stage(bf16_t* img, const bf16_t* src, int64_t ld, int L, int Lp, int
   }
 }
 
+// Block -> (image, head) unit.  A head's q / k / v / out columns are D * 2 bytes of each token row (32 B at the 16x16
+// block's D = 16), so the heads of one image share every 128-B line.  Blocks are dispatched round-robin over the 8
+// XCDs (blockIdx % 8), each with its own L2: with unit = blockIdx every XCD held one head of every image and fetched
+// each line for its 32 B (4x the algorithmic bytes; profiles/family_traffic.json round 6: 1.15 GB per step for the
+// attention family).  With one unit per block and B % 8 == 0, XCD x runs all heads of images x, x + 8, ...
+template <int U>
+MG_DEV int attn_block_unit(int bid, int B, int heads) {
+  if (U != 1 || (B & 7)) return bid;
+  const int x = bid & 7, s = bid >> 3;
+  return ((s / heads) * 8 + x) * heads + s % heads;
+}
+
 // ---------------------------------------------------------------------------
 // forward: O = softmax(Q K^T / sqrt(D)) V, lse per query
 // ---------------------------------------------------------------------------
@@ -136,7 +148,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd_mfma(const bf16_t* __restrict_
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, fr = lane & 15;
   const int ul = wave / WPU, wu = wave % WPU;
-  const int unit = blockIdx.x * U + ul;
+  const int unit = attn_block_unit<U>(blockIdx.x, B, heads) * U + ul;
   const bool live = unit < B * heads;
   const int b = live ? unit / heads : 0, h = live ? unit - (unit / heads) * heads : 0;
   bf16_t* Ks = smem + ul * 2 * Lp * P;
@@ -227,7 +239,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_mfma(const bf16_t* __restrict_
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, fr = lane & 15;
   const int ul = wave / WPU, wu = wave % WPU;
-  const int unit = blockIdx.x * U + ul;
+  const int unit = attn_block_unit<U>(blockIdx.x, B, heads) * U + ul;
   const bool live = unit < B * heads;
   const int b = live ? unit / heads : 0, h = live ? unit - (unit / heads) * heads : 0;
   bf16_t* Qs = smem + ul * (4 * Lp * P + 4 * Lp);  // 4 images + 2 float vectors (as 4*Lp bf16 slots)

@@ -151,7 +151,8 @@ enum { MG_TUNE_WGRAD_TILE = 0, MG_TUNE_GWGRAD_TILE = 1, MG_TUNE_CONV_TILE = 2, M
        MG_TUNE_ADAMW_CACHED = 25,    // 1: AdamW streams through the caches (A/B; default non-temporal loads / stores)
        MG_TUNE_ATOMIC_MINK = 26,     // atomic split-K GEMMs: the least K per split (0: automatic)
        MG_TUNE_WIDE_BLOCKS = 27,     // mg_wgrad_wide.hip grid target (blocks): 0 automatic (256)
-       MG_TUNE_COUNT = 28 };
+       MG_TUNE_WGRAD_SLAB_BLOCKS = 28,  // conv weight-gradient slab split target (blocks): 0 automatic (1024)
+       MG_TUNE_COUNT = 29 };
 extern std::atomic<int> g_mg_tune[MG_TUNE_COUNT];
 // Deterministic mode (mg_set_tuning(MG_TUNE_DETERMINISTIC, 1)): every reduction that crosses workgroups runs in
 // a fixed order -- per-block partial rows in the stream's workspace folded by one pass, or one writer per

@@ -63,6 +63,12 @@ constexpr int NTHREADS = 256;
 #ifndef MG_GLDS_CONV
 #define MG_GLDS_CONV 1
 #endif
+// LDS-DMA staging for 64 x 64 tiles whose operands are both k-major ("MC": weight gradients, C = A^T B over pixels
+// / tokens): unpadded LDS images swizzled on the source side, the DMAs as asm statements (hipcc treats the
+// ds_read_b64_tr_b16 intrinsic as aliasing any in-flight LDS-DMA and would wait vmcnt(0) before every fragment read)
+#ifndef MG_GLDS_MC
+#define MG_GLDS_MC 1
+#endif
 // LDS stages of the LDS-DMA pipeline: the loads of step t + STAGES - 1 are in flight while step t is multiplied
 #ifndef MG_GLDS_STAGES
 #define MG_GLDS_STAGES 2
@@ -143,6 +149,29 @@ template <typename V> MG_DEV V bload(rsrc_t r, uint32_t voff, uint32_t soff) {
 MG_DEV void bload_lds(rsrc_t r, uint32_t voff, uint32_t soff, void* lds) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
+// The same DMA as an asm statement, for the MC images (see MG_GLDS_MC): raw descriptor words (as make_rsrc), M0 saved
+// and restored inside the statement; s_nop 4 covers a descriptor / soffset SGPR just written by v_readfirstlane,
+// s_nop 0 the M0 write before the DMA (cdna_hip_programming.md §5.7).  Waited for by the kernel's counted vmcnt.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+MG_DEV i32x4_t dma_desc(const void* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  return i32x4_t{(int)__builtin_amdgcn_readfirstlane((uint32_t)a), (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)),
+                 0x7fffffff, 0x00020000};
+}
+MG_DEV void dma16(const i32x4_t& d, uint32_t voff, uint32_t soff, const void* lds) {
+  const uint32_t m = __builtin_amdgcn_readfirstlane(
+      (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)lds));
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(d), "s"(m), "s"(__builtin_amdgcn_readfirstlane(soff))
+      : "memory");
+}
+template <class L, class = void> struct has_gldsmc : std::false_type {};
+template <class L> struct has_gldsmc<L, std::void_t<decltype(L::kGldsMC)>> : std::integral_constant<bool, L::kGldsMC> {};
+
 // KC loaders define offs<TAIL, TBK>(slot, k0, kend, voff, soff); load / glds derive from it.
 #define MG_KC_LOADS                                                                                           \
   template <bool TAIL, int TBK> MG_DEV vec_t load(rsrc_t r, const Slot& s, int k0, int kend) const {          \
@@ -283,6 +312,13 @@ struct LdMC {
       if (rs) v = vscale1(v, rs[k]);
     }
   }
+  static constexpr bool kGldsMC = !XF;
+  MG_DEV i32x4_t desc() const { return dma_desc(p); }
+  template <bool TAIL, int TBK> MG_DEV void gldsmc(const i32x4_t& d, const Slot& s, int k0, int kend, void* lds) const {
+    uint32_t off = s.off;
+    if constexpr (TAIL) off = (k0 + s.kofs < kend) ? off : MG_OOB;
+    dma16(d, off, (uint32_t)((int64_t)k0 * ld * (int64_t)sizeof(T)), lds);
+  }
 };
 
 // MC, implicit conv columns for weight gradients: element (k = output pixel, c = tap*Cin + ci).
@@ -363,6 +399,14 @@ struct LdMCConvS1 {
     return bload<vec_t>(r, off, 0);
   }
   MG_DEV void fix(const Slot&, int, vec_t&) const {}
+  static constexpr bool kGldsMC = true;
+  MG_DEV i32x4_t desc() const { return dma_desc(x); }
+  template <bool TAIL, int TBK> MG_DEV void gldsmc(const i32x4_t& d, const Slot& s, int k0, int kend, void* lds) const {
+    const int oh = ((k0 >> lgOW) + s.kr) & (OH - 1);
+    bool bad = (s.bad_rows >> oh) & 1u;
+    if constexpr (TAIL) bad = bad || (k0 + s.kofs >= kend);
+    dma16(d, bad ? MG_OOB : (uint32_t)(s.voff + (k0 << lgCin) * (int)sizeof(T)), 0u, lds);
+  }
 };
 
 // KC, data gradient of a 4x4 / stride-2 / pad-1 convolution ("transposed conv"),
@@ -706,6 +750,24 @@ MG_DEV bf16x8_t mc_frag_bf16(const bf16_t* img, int ld, int kr0, int c0, int lan
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// MG_GLDS_MC images (64 columns = 128-B rows, unpadded): 16-B chunk c of k-row k stored at chunk c ^ swz64(k).  Rows
+// alternate 32-bank halves; the four same-parity rows of one 32-lane half of a transposed read (k = 8g + q) get
+// distinct chunk pairs.
+MG_DEV constexpr int swz64(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }
+MG_DEV bf16x8_t mc_frag_glds64(const bf16_t* img, int kr0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int k = kr0 + 8 * g + q;
+  const int ch = (c0 >> 3) + (p >> 1), sub = (p & 1) * 8;
+  auto base = (__attribute__((address_space(3))) char*)(img);
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + k * 128 + ((ch ^ swz64(k)) << 4) + sub));
+  s16x4_t hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + (k + 4) * 128 + ((ch ^ swz64(k + 4)) << 4) + sub));
+  u16x8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
 // Epilogue of one output tile: stage one 16-row band of each wave's accumulators through LDS (`smem`, at
 // least 4 * 16 * (BN/2 + 4) floats), then a plain (non-unrolled) loop applies the fused epilogue with
 // consecutive lanes on consecutive columns.  Static indexing keeps acc in registers; the loop keeps the
@@ -812,8 +874,16 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   typedef typename std::conditional<X3, bf16_t, T>::type LT;
   constexpr int TBK = tile_bk<T, X3, BM, BN>();
   constexpr int LDK = TBK + Tile<LT>::PADK;
-  constexpr int LDA = A_KC ? LDK : BM + Tile<LT>::PADM;
-  constexpr int LDB = B_KC ? LDK : BN + Tile<LT>::PADM;
+  // LDS-DMA staging of two MC operands (MG_GLDS_MC): unpadded, source-swizzled images
+  constexpr bool GMC = [] {
+    if constexpr (!A_KC && !B_KC)
+      return MG_GLDS_MC && !X3 && sizeof(T) == 2 && BM == 64 && BN == 64 && TBK == 64 && has_gldsmc<AL>::value &&
+             has_gldsmc<BL>::value;
+    else return false;
+  }();
+  constexpr int PADMC = GMC ? 0 : Tile<LT>::PADM;
+  constexpr int LDA = A_KC ? LDK : BM + PADMC;
+  constexpr int LDB = B_KC ? LDK : BN + PADMC;
   constexpr int A_ELEMS = A_KC ? BM * LDK : TBK * LDA;
   constexpr int B_ELEMS = B_KC ? BN * LDK : TBK * LDB;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
@@ -834,7 +904,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   constexpr bool GLDS = [] {
     if constexpr (A_KC && B_KC)
       return GLDS_SEL && !X3 && sizeof(T) == 2 && AL::kGlds && BL::kGlds && GSTAGES * STAGE * (int)sizeof(T) <= 65536;
-    else return false;
+    else return GMC;
   }();
   constexpr int NBUF = GLDS ? GSTAGES : ((!X3 && 2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE) ? 2 : 1);
   constexpr bool SB2 = NBUF == 1 && !X3 && BM * BN <= MG_SB2_MAX_TILE;
@@ -858,7 +928,10 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 #pragma unroll
   for (int i = 0; i < A_VPT; ++i) {
     int v = tid + i * NTHREADS;
-    if constexpr (GLDS) { a_r[i] = (i * 4 + wid) * 8 + (lane >> 3); a_k[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7)); }
+    // GMC: wave-instruction i of wave w fills k-rows (4i + w) * 8 .. +8 of the [TBK][64] image; lane L takes k-row
+    // + (L >> 3), physical chunk L & 7, so it loads column chunk (L & 7) ^ swz64(k-row)
+    if constexpr (GMC) { a_k[i] = (i * 4 + wid) * 8 + (lane >> 3); a_r[i] = 8 * ((lane & 7) ^ swz64(a_k[i])); }
+    else if constexpr (GLDS) { a_r[i] = (i * 4 + wid) * 8 + (lane >> 3); a_k[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7)); }
     else if constexpr (A_KC) { a_r[i] = v / (TBK / VEC); a_k[i] = (v % (TBK / VEC)) * VEC; }
     else { a_k[i] = v / (BM / VEC); a_r[i] = (v % (BM / VEC)) * VEC; }
     const int r = mrow_base + m0 + a_r[i];
@@ -867,12 +940,18 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 #pragma unroll
   for (int i = 0; i < B_VPT; ++i) {
     int v = tid + i * NTHREADS;
-    if constexpr (GLDS) { b_r[i] = (i * 4 + wid) * 8 + (lane >> 3); b_k[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7)); }
+    if constexpr (GMC) { b_k[i] = (i * 4 + wid) * 8 + (lane >> 3); b_r[i] = 8 * ((lane & 7) ^ swz64(b_k[i])); }
+    else if constexpr (GLDS) { b_r[i] = (i * 4 + wid) * 8 + (lane >> 3); b_k[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7)); }
     else if constexpr (B_KC) { b_r[i] = v / (TBK / VEC); b_k[i] = (v % (TBK / VEC)) * VEC; }
     else { b_k[i] = v / (BN / VEC); b_r[i] = (v % (BN / VEC)) * VEC; }
     bs_[i] = B.slot(n0 + b_r[i], b_k[i], true);
   }
   const rsrc_t rA = A.rsrc(), rB = B.rsrc();
+  i32x4_t dA{}, dB{};  // (GMC: raw descriptors for the asm DMAs)
+  if constexpr (GMC) {
+    dA = A.desc();
+    dB = B.desc();
+  }
 
   // NS register stages: the loads of K step t + NS are issued while step t is multiplied
   vec_t ra[NS][A_VPT], rb[NS][B_VPT];
@@ -985,6 +1064,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
         for (int i = 0; i < FM; ++i) {
           if constexpr (A_KC)
             af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&As[kc_off<T>(wm * WM + i * 16 + fr, kk * 32 + fq * 8, LDK)]));
+          else if constexpr (GMC)
+            af[i] = mc_frag_glds64(As, kk * 32, wm * WM + i * 16, lane);
           else
             af[i] = mc_frag_bf16(As, LDA, kk * 32, wm * WM + i * 16, lane);
         }
@@ -992,6 +1073,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
         for (int j = 0; j < FN; ++j) {
           if constexpr (B_KC)
             bfv[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&Bs[kc_off<T>(wn * WN + j * 16 + fr, kk * 32 + fq * 8, LDK)]));
+          else if constexpr (GMC)
+            bfv[j] = mc_frag_glds64(Bs, kk * 32, wn * WN + j * 16, lane);
           else
             bfv[j] = mc_frag_bf16(Bs, LDB, kk * 32, wn * WN + j * 16, lane);
         }
@@ -1027,7 +1110,22 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
     static_assert((NBUF - 1) * (A_VPT + B_VPT) < 64, "vmcnt range");
     static_assert(NBUF == 2 || NBUF == 3, "LDS-DMA pipeline: 2 or 3 stages");
     auto issue = [&](int k0, LT* buf) {
-      if (k0 + TBK <= kend) {
+      if constexpr (GMC) {
+        if (k0 + TBK <= kend) {
+#pragma unroll
+          for (int i = 0; i < A_VPT; ++i) A.template gldsmc<false, TBK>(dA, as_[i], k0, kend, buf + (i * 4 + wid) * 512);
+#pragma unroll
+          for (int i = 0; i < B_VPT; ++i)
+            B.template gldsmc<false, TBK>(dB, bs_[i], k0, kend, buf + A_ELEMS + (i * 4 + wid) * 512);
+        } else {
+#pragma unroll
+          for (int i = 0; i < A_VPT; ++i) A.template gldsmc<true, TBK>(dA, as_[i], k0, kend, buf + (i * 4 + wid) * 512);
+#pragma unroll
+          for (int i = 0; i < B_VPT; ++i)
+            B.template gldsmc<true, TBK>(dB, bs_[i], k0, kend, buf + A_ELEMS + (i * 4 + wid) * 512);
+        }
+        return;
+      } else if (k0 + TBK <= kend) {
 #pragma unroll
         for (int i = 0; i < A_VPT; ++i) A.template glds<false, TBK>(rA, as_[i], k0, kend, buf + (i * 4 + wid) * 8 * LDK);
 #pragma unroll

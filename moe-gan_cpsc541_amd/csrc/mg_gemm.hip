@@ -613,7 +613,10 @@ extern "C" int mg_conv2d_wgrad(int dtype, const void* gy, int64_t ldg, const voi
     // atomics: measured sweet spot ~576 blocks, >= 2048 pixels per split (the remapped fp32 atomics are
     // scattered, so few splits); slabs: ~2048 blocks, >= 1024 pixels and <= 16 slabs (measured at B=256:
     // D conv1 / modconv 8x8 / modconv 16x16 weight gradients 1.36x / 1.2x / 1.6x over ~512 blocks)
-    const int64_t want = slabs ? (big ? 1024 : 2048) : (big ? 288 : 576);
+    const int sb = g_mg_tune[MG_TUNE_WGRAD_SLAB_BLOCKS];
+    // (slabs, 64^2 tiles: 1024 blocks since round 6 -- same step time as 2048, half the slab bytes the deferred fold
+    // reads: same box 8.056 / 8.047 ms at 2048 / 1024, 8.161 at 512; tuning slot MG_TUNE_WGRAD_SLAB_BLOCKS)
+    const int64_t want = slabs ? (sb > 0 ? sb : 1024) : (big ? 288 : 576);
     int64_t t = std::max<int64_t>(tiles, 1);
     // few 64^2 tiles: up to 32 slabs (modconv 16x16 wgrad 65 -> 58 us); a handful (to_rgb, Cout 3 -> 8 rows):
     // up to 128, so the reduction over B*H*W pixels still spreads over >= 128 blocks

@@ -20,6 +20,9 @@
 #include "mg_gemm.h"
 
 namespace {
+using mg::dma16;
+using mg::dma_desc;
+using mg::i32x4_t;
 using mg::MG_OOB;
 
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
@@ -32,28 +35,8 @@ constexpr int WT = 512;  // threads
 // k = 8g + q (g = 0, 1; q < 4) that one 32-lane half of a ds_read_b64_tr_b16 touches land on distinct 32-B bank pairs.
 MG_DEV int swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
 
-// One LDS-DMA (buffer_load_dwordx4 ... lds) as an asm statement: the compiler's wait-count pass treats the
-// ds_read_b64_tr_b16 intrinsic as possibly aliasing an in-flight LDS-DMA and would drain every DMA (vmcnt(0)) before
-// each step's fragment reads; hidden from it, the DMAs are waited for by the kernel's own counted vmcnt.  M0 (the
-// wave's LDS destination) is saved and restored inside the statement; s_nop 4 covers a descriptor / soffset SGPR just
-// written by v_readfirstlane, s_nop 0 the M0 write before the DMA (cdna_hip_programming.md §5.7).
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-MG_DEV i32x4_t dma_desc(const void* p) {  // raw buffer descriptor: base, stride 0, 2^31 - 1 bytes (as make_rsrc)
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  return i32x4_t{(int)__builtin_amdgcn_readfirstlane((uint32_t)a), (int)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)),
-                 0x7fffffff, 0x00020000};
-}
-MG_DEV void dma16(const i32x4_t& d, uint32_t voff, uint32_t soff, const bf16_t* lds) {
-  const uint32_t m = __builtin_amdgcn_readfirstlane(
-      (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const bf16_t*)lds));
-  unsigned keep;
-  asm volatile(
-      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(d), "s"(m), "s"(__builtin_amdgcn_readfirstlane(soff))
-      : "memory");
-}
-
+// the LDS-DMAs are asm statements (mg_gemm.h dma16): hipcc treats the ds_read_b64_tr_b16 intrinsic as aliasing any
+// in-flight LDS-DMA and would drain every DMA (vmcnt(0)) before each step's fragment reads
 MG_DEV bf16x8_t mc_frag(const bf16_t* img, int cols, int kbase, int c0, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int k = kbase + 8 * g + q;
