@@ -753,15 +753,21 @@ MG_DEV bf16x8_t mc_frag_bf16(const bf16_t* img, int ld, int kr0, int c0, int lan
 // MG_GLDS_MC images (64 columns = 128-B rows, unpadded): 16-B chunk c of k-row k stored at chunk c ^ swz64(k).  Rows
 // alternate 32-bank halves; the four same-parity rows of one 32-lane half of a transposed read (k = 8g + q) get
 // distinct chunk pairs.
+// 128 columns (256-B rows, every row on the same banks): the eight rows of a 32-lane half get distinct chunk pairs
+// of the 16.
 MG_DEV constexpr int swz64(int k) { return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1; }
-MG_DEV bf16x8_t mc_frag_glds64(const bf16_t* img, int kr0, int c0, int lane) {
+MG_DEV constexpr int swz128(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+template <int COLS> MG_DEV constexpr int swzmc(int k) { return COLS == 64 ? swz64(k) : swz128(k); }
+template <int COLS>
+MG_DEV bf16x8_t mc_frag_glds(const bf16_t* img, int kr0, int c0, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int k = kr0 + 8 * g + q;
   const int ch = (c0 >> 3) + (p >> 1), sub = (p & 1) * 8;
   auto base = (__attribute__((address_space(3))) char*)(img);
-  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + k * 128 + ((ch ^ swz64(k)) << 4) + sub));
-  s16x4_t hi =
-      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + (k + 4) * 128 + ((ch ^ swz64(k + 4)) << 4) + sub));
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4_t*)(base + k * (COLS * 2) + ((ch ^ swzmc<COLS>(k)) << 4) + sub));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4_t*)(base + (k + 4) * (COLS * 2) + ((ch ^ swzmc<COLS>(k + 4)) << 4) + sub));
   u16x8_t r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
@@ -877,8 +883,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
   // LDS-DMA staging of two MC operands (MG_GLDS_MC): unpadded, source-swizzled images
   constexpr bool GMC = [] {
     if constexpr (!A_KC && !B_KC)
-      return MG_GLDS_MC && !X3 && sizeof(T) == 2 && BM == 64 && BN == 64 && TBK == 64 && has_gldsmc<AL>::value &&
-             has_gldsmc<BL>::value;
+      return MG_GLDS_MC && !X3 && sizeof(T) == 2 && BM == BN && (BM == 64 || BM == 128) && TBK == 64 &&
+             has_gldsmc<AL>::value && has_gldsmc<BL>::value;
     else return false;
   }();
   constexpr int PADMC = GMC ? 0 : Tile<LT>::PADM;
@@ -928,9 +934,13 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 #pragma unroll
   for (int i = 0; i < A_VPT; ++i) {
     int v = tid + i * NTHREADS;
-    // GMC: wave-instruction i of wave w fills k-rows (4i + w) * 8 .. +8 of the [TBK][64] image; lane L takes k-row
-    // + (L >> 3), physical chunk L & 7, so it loads column chunk (L & 7) ^ swz64(k-row)
-    if constexpr (GMC) { a_k[i] = (i * 4 + wid) * 8 + (lane >> 3); a_r[i] = 8 * ((lane & 7) ^ swz64(a_k[i])); }
+    // GMC: wave-instruction i of wave w fills the 1 KiB of k-rows (4i + w) * R .. + R of the [TBK][BM] image (R = 8 /
+    // 4 rows of 64 / 128 columns); lane L takes k-row + L / (BM / 8), physical 16-B chunk L % (BM / 8), so it loads
+    // column chunk (L % (BM / 8)) ^ swzmc(k-row)
+    if constexpr (GMC) {
+      a_k[i] = (i * 4 + wid) * (64 / (BM / 8)) + lane / (BM / 8);
+      a_r[i] = 8 * ((lane % (BM / 8)) ^ swzmc<BM>(a_k[i]));
+    }
     else if constexpr (GLDS) { a_r[i] = (i * 4 + wid) * 8 + (lane >> 3); a_k[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7)); }
     else if constexpr (A_KC) { a_r[i] = v / (TBK / VEC); a_k[i] = (v % (TBK / VEC)) * VEC; }
     else { a_k[i] = v / (BM / VEC); a_r[i] = (v % (BM / VEC)) * VEC; }
@@ -940,7 +950,10 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
 #pragma unroll
   for (int i = 0; i < B_VPT; ++i) {
     int v = tid + i * NTHREADS;
-    if constexpr (GMC) { b_k[i] = (i * 4 + wid) * 8 + (lane >> 3); b_r[i] = 8 * ((lane & 7) ^ swz64(b_k[i])); }
+    if constexpr (GMC) {
+      b_k[i] = (i * 4 + wid) * (64 / (BN / 8)) + lane / (BN / 8);
+      b_r[i] = 8 * ((lane % (BN / 8)) ^ swzmc<BN>(b_k[i]));
+    }
     else if constexpr (GLDS) { b_r[i] = (i * 4 + wid) * 8 + (lane >> 3); b_k[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7)); }
     else if constexpr (B_KC) { b_r[i] = v / (TBK / VEC); b_k[i] = (v % (TBK / VEC)) * VEC; }
     else { b_k[i] = v / (BN / VEC); b_r[i] = (v % (BN / VEC)) * VEC; }
@@ -1065,7 +1078,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
           if constexpr (A_KC)
             af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&As[kc_off<T>(wm * WM + i * 16 + fr, kk * 32 + fq * 8, LDK)]));
           else if constexpr (GMC)
-            af[i] = mc_frag_glds64(As, kk * 32, wm * WM + i * 16, lane);
+            af[i] = mc_frag_glds<BM>(As, kk * 32, wm * WM + i * 16, lane);
           else
             af[i] = mc_frag_bf16(As, LDA, kk * 32, wm * WM + i * 16, lane);
         }
@@ -1074,7 +1087,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
           if constexpr (B_KC)
             bfv[j] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8_t*>(&Bs[kc_off<T>(wn * WN + j * 16 + fr, kk * 32 + fq * 8, LDK)]));
           else if constexpr (GMC)
-            bfv[j] = mc_frag_glds64(Bs, kk * 32, wn * WN + j * 16, lane);
+            bfv[j] = mc_frag_glds<BN>(Bs, kk * 32, wn * WN + j * 16, lane);
           else
             bfv[j] = mc_frag_bf16(Bs, LDB, kk * 32, wn * WN + j * 16, lane);
         }
