@@ -178,6 +178,19 @@ int mg_conv2d_fwd_mx8(const void* x, const void* xscale, int B, int H, int W, in
  * scale [rows][K/32] E8M0 bytes; per 32-element block e = ceil(log2(amax / 448)) + 127 (nothing saturates),
  * round-to-nearest-even.  K % 32 == 0.  Used per optimizer step for the fp8 conv weights. */
 int mg_quant_mx8(const void* x, int64_t ldx, int64_t rows, int K, void* q, void* scale, void* stream);
+/* Several mg_quant_mx8 quantizations in one launch (the per-step MX-fp8 copies of the packed 3x3 weights and their
+   flipped data-gradient forms); each descriptor as mg_quant_mx8's arguments, at most MG_QUANT_BATCH_MAX per launch
+   (more are split into launches). */
+#define MG_QUANT_BATCH_MAX 32
+typedef struct mg_quant_desc {
+  const void* x;
+  int64_t ldx;
+  int64_t rows;
+  int32_t K;
+  void* q;
+  void* scale;
+} mg_quant_desc;
+int mg_quant_mx8_batch(int n, const mg_quant_desc* d, void* stream);
 
 /* Weight gradient of the convolution above, accumulated (fp32 atomics) into
  * gw in the reference layout [Cout][Cin][KH][KW]:

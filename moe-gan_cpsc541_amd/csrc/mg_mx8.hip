@@ -213,6 +213,34 @@ __global__ __launch_bounds__(256) void k_quant_mx8(const bf16_t* __restrict__ x,
   }
 }
 
+// several weight quantizations in one launch (the per-step MX-fp8 copies of every packed 3x3 weight and its flipped
+// data-gradient form): blockIdx.y = descriptor, the same per-vector arithmetic as k_quant_mx8
+struct QuantBatch {
+  const bf16_t* x[MG_QUANT_BATCH_MAX];
+  int64_t ldx[MG_QUANT_BATCH_MAX];
+  int64_t rows[MG_QUANT_BATCH_MAX];
+  int K[MG_QUANT_BATCH_MAX];
+  uint8_t* q[MG_QUANT_BATCH_MAX];
+  uint8_t* sc[MG_QUANT_BATCH_MAX];
+};
+__global__ __launch_bounds__(256) void k_quant_mx8_batch(QuantBatch b) {
+  const int d = blockIdx.y, K = b.K[d], kv = K >> 3;
+  const int64_t nvec = b.rows[d] * kv;
+  const bf16_t* x = b.x[d];
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t - (threadIdx.x & 3) < nvec; t += (int64_t)gridDim.x * 256) {
+    const bool ok = t < nvec;
+    const int64_t r = ok ? t / kv : 0;
+    const int c = ok ? (int)(t - r * kv) : 0;
+    const u16x8_t v = ok ? *reinterpret_cast<const u16x8_t*>(x + r * b.ldx[d] + c * 8) : u16x8_t(0);
+    const int e = mx_exp(quad_max(amax8(v)));
+    const u32x2_t p = mx_pack8(v, mx_inv(e));
+    if (ok) {
+      *reinterpret_cast<u32x2_t*>(b.q[d] + r * K + c * 8) = p;
+      if ((c & 3) == 0) b.sc[d][r * (K >> 5) + (c >> 2)] = (uint8_t)e;
+    }
+  }
+}
+
 template <int BM, int BN, typename TO>
 void run_mx8(const void* x, const void* xsc, int B, int H, int W, int Cin, const void* wq, const void* wsc, int Cout,
              int KH, int KW, int stride, int pad, void* y, int64_t ldy, const mg_epilogue* e, hipStream_t st) {
@@ -255,6 +283,32 @@ extern "C" int mg_quant_mx8(const void* x, int64_t ldx, int64_t rows, int K, voi
                      reinterpret_cast<const bf16_t*>(x), ldx, rows, K, reinterpret_cast<uint8_t*>(q),
                      reinterpret_cast<uint8_t*>(scale));
   return mg_check_launch("mg_quant_mx8");
+}
+
+extern "C" int mg_quant_mx8_batch(int n, const mg_quant_desc* d, void* stream) {
+  MG_REQUIRE(n >= 0, "n must be >= 0");
+  for (int i0 = 0; i0 < n; i0 += MG_QUANT_BATCH_MAX) {
+    const int cnt = std::min(MG_QUANT_BATCH_MAX, n - i0);
+    QuantBatch b{};
+    int64_t most = 0;
+    for (int j = 0; j < cnt; ++j) {
+      const mg_quant_desc& q = d[i0 + j];
+      MG_REQUIRE(q.K > 0 && q.K % 32 == 0 && q.ldx >= q.K && q.ldx % 8 == 0 && q.rows >= 0,
+                 "mg_quant_mx8_batch: K a positive multiple of 32, ldx >= K and a multiple of 8");
+      MG_REQUIRE(mg_al16(q.x) && (reinterpret_cast<uintptr_t>(q.q) & 7) == 0, "x must be 16-B and q 8-B aligned");
+      b.x[j] = reinterpret_cast<const bf16_t*>(q.x);
+      b.ldx[j] = q.ldx;
+      b.rows[j] = q.rows;
+      b.K[j] = q.K;
+      b.q[j] = reinterpret_cast<uint8_t*>(q.q);
+      b.sc[j] = reinterpret_cast<uint8_t*>(q.scale);
+      most = std::max<int64_t>(most, q.rows * (q.K / 8));
+    }
+    if (most == 0) continue;
+    const int blocks = (int)std::min<int64_t>(cdiv(most, 256), 2048);
+    hipLaunchKernelGGL(k_quant_mx8_batch, dim3(blocks, cnt), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), b);
+  }
+  return mg_check_launch("mg_quant_mx8_batch");
 }
 
 extern "C" int mg_conv2d_fwd_mx8(const void* x, const void* xscale, int B, int H, int W, int Cin, const void* wq, const void* wscale,

@@ -58,6 +58,11 @@ class RouterParamDesc(ctypes.Structure):
                 ("gmu", _c_void_p), ("grho", _c_void_p), ("n", _i64)]
 
 
+class QuantDesc(ctypes.Structure):
+    """Mirror of ``mg_quant_desc``."""
+    _fields_ = [("x", _c_void_p), ("ldx", _i64), ("rows", _i64), ("K", _i32), ("q", _c_void_p), ("scale", _c_void_p)]
+
+
 class GuardDesc(ctypes.Structure):
     """Mirror of ``mg_guard_desc``."""
     _fields_ = [("x", _c_void_p * 4), ("n", _i32 * 4), ("bit", _i32 * 4), ("nwin", _i32), ("reset_bits", _i32 * 2),
@@ -72,7 +77,7 @@ _CTYPE = {"int": _i32, "int32_t": _i32, "int64_t": _i64, "uint64_t": ctypes.c_ui
           "void": _c_void_p, "mg_epilogue": ctypes.POINTER(Epilogue), "mg_gemm_desc": ctypes.POINTER(GemmDesc),
           "mg_prep_desc": ctypes.POINTER(PrepDesc), "mg_colsum_desc": ctypes.POINTER(ColsumDesc),
           "mg_wn_desc": ctypes.POINTER(WnDesc), "mg_router_param_desc": ctypes.POINTER(RouterParamDesc),
-          "mg_guard_desc": ctypes.POINTER(GuardDesc)}
+          "mg_guard_desc": ctypes.POINTER(GuardDesc), "mg_quant_desc": ctypes.POINTER(QuantDesc)}
 _RESTYPE = {"int": ctypes.c_int32, "int64_t": ctypes.c_int64, "const char*": ctypes.c_char_p}
 SIG_RE = r"\b(int|int64_t|const char\*)\s+(mg_\w+)\(([^)]*)\);"
 

@@ -146,13 +146,16 @@ class GeneratorEngine:
             W = self.P(pre + "weight")
             pk[pre] = {"w": pb.pack(W), "wflip": pb.pack(W, flip=True)}
         pb.run()
-        if self.fp8:  # per-step MX-fp8 copies of the packed 3x3 weights (forward and flipped data-gradient form)
+        if self.fp8:  # per-step MX-fp8 copies of the packed 3x3 weights (forward and flipped data-gradient form),
+            jobs = []  # all in one launch
             for pre, k in self.mc_list:
                 ent = pk[pre]
                 if k == 3 and self._mx8_ok(self.P(pre + "weight").shape[1]):
-                    ent["wq"] = ops.quant_mx8(ent["w"])
+                    jobs.append((ent, "wq", ent["w"]))
                 if k == 3 and self._mx8_ok(ent["rows"]):
-                    ent["wflipq"] = ops.quant_mx8(ent["wflip"])
+                    jobs.append((ent, "wflipq", ent["wflip"]))
+            for (ent, key, _), r in zip(jobs, ops.quant_mx8_batch([w.reshape(-1, w.shape[-1]) for _, _, w in jobs])):
+                ent[key] = r
         self.packs = pk
 
     @staticmethod

@@ -276,6 +276,21 @@ def quant_mx8(x, K=None):
     return q, sc
 
 
+def quant_mx8_batch(xs):
+    """quant_mx8 of several bf16 [rows, K] matrices in one launch (mg_quant_mx8_batch): [(q, scale)] per input."""
+    out = []
+    arr = (L.QuantDesc * max(1, len(xs)))()
+    for i, x in enumerate(xs):
+        rows, K = x.shape
+        q = torch.empty(rows, K, device=x.device, dtype=torch.uint8)
+        sc = torch.empty(rows, K // 32, device=x.device, dtype=torch.uint8)
+        arr[i] = L.QuantDesc(ptr(x), x.stride(0), rows, K, ptr(q), ptr(sc))
+        out.append((q, sc))
+    if xs:
+        call("mg_quant_mx8_batch", len(xs), arr, S())
+    return out
+
+
 def conv2d_mx8(xq, xsc, wq, wsc, Cout, KH, KW, stride=1, pad=0, out=None, out_dtype=torch.bfloat16, ep=None,
                ldy=None, tag=None):
     """MX-fp8 NHWC implicit-GEMM conv (mg_conv2d_fwd_mx8): xq [B,H,W,Cin] e4m3 / xsc [B*H*W, Cin/32] and

@@ -118,3 +118,19 @@ def test_conv_mx8_rejects_bad_shapes():
     sc = torch.zeros(64, 18, device=DEV, dtype=torch.uint8)
     with pytest.raises(RuntimeError, match="Cin"):
         ops.conv2d_mx8(x, xs, wq, sc, 64, 3, 3, 1, 1)
+
+
+def test_quant_mx8_batch_equals_single():
+    """mg_quant_mx8_batch (the per-step MX-fp8 weight copies in one launch) gives, descriptor by descriptor, the bytes
+    of separate mg_quant_mx8 calls: ragged row counts and K, a strided source, more descriptors than one launch holds."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    xs = []
+    for i in range(37):
+        rows, K = 1 + (i * 53) % 700, 32 * (1 + (i * 7) % 40)
+        base = (torch.randn(rows, K + 32 * (i % 3), device="cuda", generator=g) * (10.0 ** (i % 5 - 2))).bfloat16()
+        xs.append(base[:, :K])
+    got = ops.quant_mx8_batch(xs)
+    torch.cuda.synchronize()
+    for x, (q, sc) in zip(xs, got):
+        q1, sc1 = ops.quant_mx8(x)
+        assert torch.equal(q, q1) and torch.equal(sc, sc1)
