@@ -69,7 +69,10 @@ constexpr int NTHREADS = 256;
 #ifndef MG_GLDS_MC
 #define MG_GLDS_MC 1
 #endif
-// LDS stages of the LDS-DMA pipeline: the loads of step t + STAGES - 1 are in flight while step t is multiplied
+// LDS stages of the LDS-DMA pipeline: the loads of step t + STAGES - 1 are in flight while step t is multiplied.
+// 3 runs one barrier per step (step t + 2 issued after step t's barrier); measured slower on every 64^2 conv tile
+// (conv 3x3 at 8^2 35.7 -> 43.4 us, the 16^2 weight gradient 46.9 -> 61.6 us, step 8.10 -> 8.29 ms, same box): the
+// third 16 KiB stage costs more resident blocks than the deeper prefetch and the saved barrier give back
 #ifndef MG_GLDS_STAGES
 #define MG_GLDS_STAGES 2
 #endif
@@ -912,7 +915,8 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
       return GLDS_SEL && !X3 && sizeof(T) == 2 && AL::kGlds && BL::kGlds && GSTAGES * STAGE * (int)sizeof(T) <= 65536;
     else return GMC;
   }();
-  constexpr int NBUF = GLDS ? GSTAGES : ((!X3 && 2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE) ? 2 : 1);
+  constexpr int NBUF = GLDS ? (GSTAGES * STAGE * (int)sizeof(LT) <= 65536 ? GSTAGES : 2)
+                            : ((!X3 && 2 * STAGE * (int)sizeof(T) <= 65536 && BM * BN <= MG_DB_MAX_TILE) ? 2 : 1);
   constexpr bool SB2 = NBUF == 1 && !X3 && BM * BN <= MG_SB2_MAX_TILE;
   constexpr int NS = NBUF == 2 ? MG_NSTAGE : (SB2 ? 2 : 1);
   __shared__ __attribute__((aligned(16))) LT smem[NBUF * STAGE];
@@ -1152,9 +1156,25 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
           B.template glds<true, TBK>(rB, bs_[i], k0, kend, buf + A_ELEMS + (i * 4 + wid) * 8 * LDK);
       }
     };
-    // NBUF stages: steps t + 1 .. t + NBUF - 1 are in flight while step t is multiplied
     const int nsteps = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
     constexpr int PER = A_VPT + B_VPT;  // DMA instructions per step
+    if constexpr (NBUF == 3) {
+      // three stages, ONE barrier per step: step t + 2 is issued after the barrier of step t, into the stage step
+      // t - 1 read (every wave finished step t - 1 before arriving at that barrier); before it, a counted vmcnt
+      // retires this wave's DMA of step t (step t + 1's may stay in flight)
+      if (nsteps > 0) issue(kbeg, smem);
+      if (nsteps > 1) issue(kbeg + TBK, smem + STAGE);
+      for (int t = 0; t < nsteps; ++t) {
+        LT* cur = smem + (t % 3) * STAGE;
+        if (t + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of step t - 1 have landed (WAR)
+        __builtin_amdgcn_s_barrier();
+        if (t + 2 < nsteps) issue(kbeg + (t + 2) * TBK, smem + ((t + 2) % 3) * STAGE);
+        compute(cur, cur + A_ELEMS);
+      }
+    } else {
+    // two stages: step t + 1 is in flight while step t is multiplied
 #pragma unroll
     for (int p = 0; p < NBUF - 1; ++p)
       if (p < nsteps) issue(kbeg + p * TBK, smem + p * STAGE);
@@ -1173,6 +1193,7 @@ MG_DEV void gemm_tile(const AL& A, const BL& B, const EP& ep, int m0, int n0, in
       compute(cur, cur + A_ELEMS);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of cur have landed (WAR)
       __builtin_amdgcn_s_barrier();
+    }
     }
   } else if constexpr (NBUF == 2) {
     // Two LDS buffers, one barrier per K step.  Step t multiplies LDS[t & 1], then writes the register
