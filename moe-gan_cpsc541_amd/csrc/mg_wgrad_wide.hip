@@ -8,9 +8,10 @@
 // and every B strip M / 64 times, and each block walks its K chunk with one step of loads in flight, so a step costs a
 // full HBM round trip (~1-2 us) against ~50 ns of MFMA work -- 20-40 us per call for 8-67 MB of operands.  Here a
 // block owns a 128 x 128 or 256 x 256 output tile (all of M x N for most shapes) for one K chunk, so the operands are
-// read once or twice, and streams its chunk through a 4-stage LDS-DMA ring (buffer_load ... lds) with two K steps
-// (64 KiB) in flight while one is multiplied.  The per-block fp32 partial tiles are folded in a fixed order by two
-// passes (deterministic in both library modes).
+// read once or twice, and streams its chunk through an 8-stage LDS-DMA ring (buffer_load ... lds) with six 16 KiB K
+// steps in flight while one is multiplied.  The per-block fp32 partial tiles are folded in a fixed order
+// (deterministic in both library modes) by the gradient-fold rows pass (mg_fold.hip, deferred to the backward's flush
+// inside a step), or by two passes of their own for a scaled / strided C.
 //
 // Block: 512 threads = 8 waves as 2 (M) x 4 (N), wave tile (BM/2) x (BN/4) of 16x16 fragments, read from the
 // row-major ("MC") LDS images by the hardware transpose read (ds_read_b64_tr_b16).  Rows past the split's chunk and
@@ -130,52 +131,68 @@ __global__ __launch_bounds__(WT) void k_wgrad_wide(const bf16_t* __restrict__ A,
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-row DMAs past the last step land before the block ends
-  // this block's partial tile in fragment order (one 1-KiB coalesced store per fragment and wave; k_wide_final maps it
-  // back to (m, n)): part[split][tile][(fm * FN + fn) * 8 + wave][lane][4]
-  float* pb = part + ((int64_t)blockIdx.z * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x) * (BM * BN);
+  // this block's partial tile, staged through the (now idle) LDS as [BM][BN] fp32 and stored in natural order as
+  // 16-B row runs: part[split][m][n] (row pitch N), what the gradient-fold rows pass reads
+  float* pb = part + (int64_t)blockIdx.z * M * N;
+  if constexpr (BM * BN * 4 <= NB * STAGE * 2) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* tile = reinterpret_cast<float*>(dsm);
 #pragma unroll
-  for (int fm = 0; fm < FM; ++fm)
+    for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-    for (int fn = 0; fn < FN; ++fn)
-      *reinterpret_cast<f32x4_t*>(pb + (((fm * FN + fn) * 8 + wid) * 64 + lane) * 4) = acc[fm][fn];
+      for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          tile[(wm * WM + 16 * fm + 4 * (lane >> 4) + j) * BN + wn * WN + 16 * fn + (lane & 15)] = acc[fm][fn][j];
+    __syncthreads();
+    for (int v = tid; v < BM * BN / 4; v += WT) {
+      const int r = v / (BN / 4), c = (v % (BN / 4)) * 4, m = m0 + r, n = n0 + c;
+      if (m < M && n < N)
+        *reinterpret_cast<f32x4_t*>(pb + (int64_t)m * N + n) = *reinterpret_cast<const f32x4_t*>(tile + r * BN + c);
+    }
+  } else {  // (256^2 tiles: 256 KiB of partial tile, more than the LDS ring -- straight from the accumulators)
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = m0 + wm * WM + 16 * fm + 4 * (lane >> 4) + j, n = n0 + wn * WN + 16 * fn + (lane & 15);
+          if (m < M && n < N) pb[(int64_t)m * N + n] = acc[fm][fn][j];
+        }
+  }
 }
 
-// fold level 1: tmp[grp][i] = sum of part[s][i] for s in the group's split range (ascending), 4 elements per thread;
-// level 2 (final): C[m][n] += alpha * sum of tmp[grp][i] (ascending), the fragment-order index i mapped to (m, n)
-__global__ __launch_bounds__(256) void k_wide_fold(const float* __restrict__ part, int nsplit, int64_t TT, int per,
+// immediate fold (a scaled or strided C): level 1 tmp[grp][i] = sum of part[s][i] over the group's splits
+// (ascending), level 2 C[m][n] += alpha * sum of tmp[grp][i] (ascending); i = m * N + n
+__global__ __launch_bounds__(256) void k_wide_fold(const float* __restrict__ part, int nsplit, int64_t MN, int per,
                                                    float* __restrict__ tmp) {
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= TT) return;
+  if (i >= MN) return;
   const int s0 = blockIdx.y * per, s1 = std::min(nsplit, s0 + per);
   f32x4_t s = {0.f, 0.f, 0.f, 0.f};
   int r = s0;
   for (; r + 8 <= s1; r += 8) {
     f32x4_t v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const f32x4_t*>(part + (int64_t)(r + q) * TT + i);
+    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const f32x4_t*>(part + (int64_t)(r + q) * MN + i);
 #pragma unroll
     for (int q = 0; q < 8; ++q) s += v[q];
   }
-  for (; r < s1; ++r) s += *reinterpret_cast<const f32x4_t*>(part + (int64_t)r * TT + i);
-  *reinterpret_cast<f32x4_t*>(tmp + (int64_t)blockIdx.y * TT + i) = s;
+  for (; r < s1; ++r) s += *reinterpret_cast<const f32x4_t*>(part + (int64_t)r * MN + i);
+  *reinterpret_cast<f32x4_t*>(tmp + (int64_t)blockIdx.y * MN + i) = s;
 }
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void k_wide_final(const float* __restrict__ tmp, int ngrp, int64_t TT, int tiles_m,
-                                                    int M, int N, float alpha, float* __restrict__ C, int64_t ldc) {
-  constexpr int WM = BM / 2, WN = BN / 4, FN = WN / 16;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= TT) return;
-  const int tile = (int)(i / (BM * BN)), r = (int)(i % (BM * BN));
-  const int q = r >> 8, lane = (r >> 2) & 63, j = r & 3;
-  const int w = q & 7, fmn = q >> 3, fm = fmn / FN, fn = fmn % FN;
-  const int m = (tile % tiles_m) * BM + (w >> 2) * WM + 16 * fm + 4 * (lane >> 4) + j;
-  const int n = (tile / tiles_m) * BN + (w & 3) * WN + 16 * fn + (lane & 15);
-  if (m >= M || n >= N) return;
+__global__ __launch_bounds__(256) void k_wide_final(const float* __restrict__ tmp, int ngrp, int M, int N, float alpha,
+                                                    float* __restrict__ C, int64_t ldc) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, MN = (int64_t)M * N;
+  if (i >= MN) return;
   float s = 0.f;
-  for (int g = 0; g < ngrp; ++g) s += tmp[(int64_t)g * TT + i];
+  for (int g = 0; g < ngrp; ++g) s += tmp[(int64_t)g * MN + i];
+  const int64_t m = i / N, n = i - m * N;
   // an atomic add keeps mg_gemm's atomic-epilogue contract (concurrent writers into one gradient buffer, e.g. from
   // the main and the side stream, accumulate); with one writer it is the same single fp32 addition as C += alpha s
-  atomicAdd(C + (int64_t)m * ldc + n, alpha * s);
+  atomicAdd(C + m * ldc + n, alpha * s);
 }
 
 template <int BM, int BN, int BK, int NB>
@@ -217,22 +234,29 @@ bool mg_wgrad_wide(int M, int N, int K, const void* A, int64_t lda, const void* 
       1, std::min<int64_t>({std::max<int64_t>(1, target / tiles), (int64_t)K / (8 * BK), (int64_t)128}));
   const int kchunk = cdiv(cdiv(K, splits), BK) * BK;
   splits = cdiv(K, kchunk);
-  const int per = 16, ngrp = (splits + per - 1) / per;
-  const int64_t TT = tiles * BM * BN;  // partial elements per split (fragment order, whole tiles)
-  float* part = reinterpret_cast<float*>(mg_workspace((size_t)(splits + ngrp) * TT * sizeof(float), st));
-  if (!part) return false;
-  float* tmp = part + (size_t)splits * TT;
-  const dim3 grid(cdiv(M, BM), cdiv(N, BN), splits);
+  const int64_t MN = (int64_t)M * N;
   const bf16_t* a = reinterpret_cast<const bf16_t*>(A);
   const bf16_t* b = reinterpret_cast<const bf16_t*>(B);
+  const dim3 grid(cdiv(M, BM), cdiv(N, BN), splits);
+  // an unscaled, dense C (every weight gradient of the step): the partial tiles go through the gradient-fold rows
+  // pass -- deferred to the backward's flush inside a step (one launch for every fold of the phase), immediate
+  // otherwise; same fixed split order either way
+  if (alpha == 1.f && ldc == N) {
+    bool deferred = false;
+    float* part = mg_fold_partials((size_t)splits * MN * sizeof(float), st, &deferred);
+    if (!part) return false;
+    if (big) launch_wide<256, 256, 32, 4>(grid, st, a, lda, b, ldb, M, N, K, kchunk, part);
+    else launch_wide<128, 128, 32, 8>(grid, st, a, lda, b, ldb, M, N, K, kchunk, part);
+    mg_fold_rows_submit(mg_fold_rows{part, MN, (int32_t)splits, (int32_t)MN, (int32_t)MN, C, nullptr}, deferred, st);
+    return true;
+  }
+  const int per = 16, ngrp = (splits + per - 1) / per;
+  float* part = reinterpret_cast<float*>(mg_workspace((size_t)(splits + ngrp) * MN * sizeof(float), st));
+  if (!part) return false;
+  float* tmp = part + (size_t)splits * MN;
   if (big) launch_wide<256, 256, 32, 4>(grid, st, a, lda, b, ldb, M, N, K, kchunk, part);
   else launch_wide<128, 128, 32, 8>(grid, st, a, lda, b, ldb, M, N, K, kchunk, part);
-  hipLaunchKernelGGL(k_wide_fold, dim3(cdiv(TT, 1024), ngrp), dim3(256), 0, st, part, splits, TT, per, tmp);
-  if (big)
-    hipLaunchKernelGGL((k_wide_final<256, 256>), dim3(cdiv(TT, 256)), dim3(256), 0, st, tmp, ngrp, TT, (int)grid.x, M,
-                       N, alpha, C, ldc);
-  else
-    hipLaunchKernelGGL((k_wide_final<128, 128>), dim3(cdiv(TT, 256)), dim3(256), 0, st, tmp, ngrp, TT, (int)grid.x, M,
-                       N, alpha, C, ldc);
+  hipLaunchKernelGGL(k_wide_fold, dim3(cdiv(MN, 1024), ngrp), dim3(256), 0, st, part, splits, MN, per, tmp);
+  hipLaunchKernelGGL(k_wide_final, dim3(cdiv(MN, 256)), dim3(256), 0, st, tmp, ngrp, M, N, alpha, C, ldc);
   return true;
 }
