@@ -1,4 +1,5 @@
-"""The slowest C-ABI calls of one eager C2 step, per family, with shapes (event-timed; ~3 us event overhead each).
+"""The slowest C-ABI calls of one eager C2 (or TOP_CONFIG=C5) step, per family, with shapes (event-timed; ~3 us
+event overhead each).
 
   python tools/top_calls.py [family ...]
 """
@@ -18,8 +19,10 @@ def main():
     from moegan_mi.roofline import Attribution
     from moegan_mi.step import StepConfig, TrainStep
     dev = torch.device("cuda", 0)
-    E, k, B = 8, 2, 256
-    ts = TrainStep(StepConfig(E=E, topk=k, dtype="bf16"), dev)
+    # TOP_CONFIG=C5: 32 experts top-4 with the MX-fp8 3x3 convs (bench.py --config C5)
+    c5 = os.environ.get("TOP_CONFIG", "C2") == "C5"
+    E, k, B = (32, 4, 256) if c5 else (8, 2, 256)
+    ts = TrainStep(StepConfig(E=E, topk=k, dtype="bf16", fp8=c5), dev)
     init_generator(ts.gs, seed=0)
     init_discriminator(ts.ds, seed=1)
     g = torch.Generator(device=dev).manual_seed(1)
