@@ -1118,9 +1118,11 @@ template <typename T, int E, int CV>
 __global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict__ tok, int64_t ld, int Tn, int C,
                                                             const float* __restrict__ g_raw, int chunk,
                                                             float* __restrict__ part) {
-  const int TX = C / CV, TY = 256 / TX;
+  // channel group blockIdx.y of gridDim.y: channels [cb, cb + Cb)
+  const int Cb = C / gridDim.y, cb = blockIdx.y * Cb;
+  const int TX = Cb / CV, TY = 256 / TX;
   const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
-  const int c = tx * CV;
+  const int c = cb + tx * CV;
   const int t0 = blockIdx.x * chunk, t1 = min(Tn, t0 + chunk);
   float acc[CV][E];
 #pragma unroll
@@ -1158,19 +1160,19 @@ __global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict_
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[j][e] += __shfl_xor(acc[j][e], o, 64);
   const int R = TY / tyw;  // partial rows of this block (one per wave-row group)
-  if (R > 1 && (int64_t)R * C * E <= 16384) {  // fold them in LDS (fixed order): one row per block
-    extern __shared__ float red[];  // R * C * E floats (dynamic: 16 KiB at C = 128, E = 8 keeps 8 blocks per CU)
+  if (R > 1 && (int64_t)R * Cb * E <= 16384) {  // fold them in LDS (fixed order): one row per block
+    extern __shared__ float red[];  // R * Cb * E floats (dynamic: 16 KiB at C = 128, E = 8 keeps 8 blocks per CU)
     if (ty % tyw == 0) {
 #pragma unroll
       for (int j = 0; j < CV; ++j)
 #pragma unroll
-        for (int e = 0; e < E; ++e) red[(ty / tyw) * C * E + (c + j) * E + e] = acc[j][e];
+        for (int e = 0; e < E; ++e) red[(ty / tyw) * Cb * E + (c - cb + j) * E + e] = acc[j][e];
     }
     __syncthreads();
-    float* pr = part + (int64_t)blockIdx.x * C * E;
-    for (int i = threadIdx.x; i < C * E; i += 256) {
+    float* pr = part + (int64_t)blockIdx.x * C * E + (int64_t)cb * E;  // (this group's channel slice of the row)
+    for (int i = threadIdx.x; i < Cb * E; i += 256) {
       float v = 0.f;
-      for (int r = 0; r < R; ++r) v += red[r * C * E + i];
+      for (int r = 0; r < R; ++r) v += red[r * Cb * E + i];
       pr[i] = v;
     }
     return;
@@ -1800,14 +1802,17 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
   const int CV = E <= 8 ? 8 : (E == 16 ? 4 : 2);
   if (C % CV == 0 && C / CV <= 256 && (256 % (C / CV)) == 0 && ld % 8 == 0 && mg_al16(tok) && mg_al16(g_raw) &&
       T > 0) {
-    const int TX = C / CV, TY = 256 / TX, R = TY / (TX < 64 ? 64 / TX : 1);
-    const int rows_per_block = (R > 1 && (int64_t)R * C * E <= 16384) ? 1 : R;  // in-block LDS fold (kernel)
+    // channel groups (grid y) of at most 64 lanes x CV channels: at 32 experts (CV = 2) a 512-channel block was 256
+    // channel lanes x ONE token lane walking its whole chunk serially (120 us for the 4x4 block's 4096 tokens at C5)
+    const int Cb = std::min(C, 64 * CV), CG = C / Cb;
+    const int TX = Cb / CV, TY = 256 / TX, R = TY / (TX < 64 ? 64 / TX : 1);
+    const int rows_per_block = (R > 1 && (int64_t)R * Cb * E <= 16384) ? 1 : R;  // in-block LDS fold (kernel)
     // ~1024 blocks with at most 4 M floats of partial rows (at 32 experts the old 256-block / 1 M-float budget
     // left 64 blocks walking 1024 tokens each: 175 us for the 16x16 block's 65536 tokens at C5)
     int chunk = std::max(TY, (T / 1024 + TY - 1) / TY * TY);
-    // and >= 4E tokens per block, so the partial rows (C x E fp32 per block) stay within half the token bytes read
+    // and >= 2E tokens per block, so the partial rows (C x E fp32 per block) stay within the token bytes read
     // (C x 2 per token): at the 4x4 block (T = 4096, C = 512) 4-token chunks wrote 16 MB of partials for 4 MB of tokens
-    chunk = std::max(chunk, (4 * E + TY - 1) / TY * TY);
+    chunk = std::max(chunk, (2 * E + TY - 1) / TY * TY);
     const int64_t row = (int64_t)rows_per_block * C * E;
     const int64_t min_chunk = ((int64_t)T * row / (4 << 20) + TY - 1) / TY * TY;
     if (min_chunk > chunk) chunk = (int)min_chunk;
@@ -1815,8 +1820,8 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
     bool deferred = false;
     float* part = mg_fold_partials((size_t)nb * rows_per_block * C * E * sizeof(float), st, &deferred);
     MG_REQUIRE(part != nullptr, "mg_router_feat_grad: no workspace");
-    const size_t smem = rows_per_block == 1 ? (size_t)R * C * E * sizeof(float) : 0;
-#define LV_(TT, EE, CC) hipLaunchKernelGGL((k_router_feat_grad_v<TT, EE, CC>), dim3(nb), dim3(256), smem, st, \
+    const size_t smem = rows_per_block == 1 ? (size_t)R * Cb * E * sizeof(float) : 0;
+#define LV_(TT, EE, CC) hipLaunchKernelGGL((k_router_feat_grad_v<TT, EE, CC>), dim3(nb, CG), dim3(256), smem, st, \
                                            (const TT*)tok, ld, T, C, g_raw, chunk, part)
 #define LVE_(TT) if (E == 4) LV_(TT, 4, 8); else if (E == 8) LV_(TT, 8, 8); else if (E == 16) LV_(TT, 16, 4); \
                  else LV_(TT, 32, 2)
