@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void k_bwd_out_v(const TG* __restrict__ gz, in
                                                    int64_t ld_z, const T* __restrict__ zsub, int64_t ld_zsub,
                                                    const float* __restrict__ d, int HW, int Cout, int act,
                                                    T* __restrict__ gyt, int64_t ld_gyt, float* __restrict__ gdd) {
-  __shared__ float red[256 * 8];
+  __shared__ __attribute__((aligned(16))) float red[256 * 8];
   const int b = blockIdx.x, tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int o = (blockIdx.y * TX + tx) * 8;
   const bool live = o < Cout;
@@ -152,12 +152,19 @@ __global__ __launch_bounds__(256) void k_bwd_out_v(const TG* __restrict__ gz, in
   }
   const int tid = ty * TX + tx;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = acc[j];
+  for (int j = 0; j < 8; j += 4)  // (16-B LDS writes: the 4-B ones at a 32-B lane stride were 8-way bank conflicts)
+    *reinterpret_cast<f32x4_t*>(&red[tid * 8 + j]) = f32x4_t{acc[j], acc[j + 1], acc[j + 2], acc[j + 3]};
   __syncthreads();
   if (ty == 0 && live) {
     for (int y = 1; y < TY; ++y)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += red[(y * TX + tx) * 8 + j];
+      for (int j = 0; j < 8; j += 4) {
+        const f32x4_t v = *reinterpret_cast<const f32x4_t*>(&red[(y * TX + tx) * 8 + j]);
+        acc[j] += v[0];
+        acc[j + 1] += v[1];
+        acc[j + 2] += v[2];
+        acc[j + 3] += v[3];
+      }
 #pragma unroll
     for (int j = 0; j < 8; ++j) gdd[(int64_t)b * Cout + o + j] = -0.5f * dd[j] * dd[j] * acc[j];
   }
@@ -168,7 +175,7 @@ __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, in
                                                   int64_t ld_x, const float* __restrict__ s, int64_t ld_s, int HW, int Cin,
                                                   TO* __restrict__ gx, int64_t ld_gx, int accumulate,
                                                   float* __restrict__ gs) {
-  __shared__ float red[256 * 8];
+  __shared__ __attribute__((aligned(16))) float red[256 * 8];
   const int b = blockIdx.x, tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int c = (blockIdx.y * TX + tx) * 8;
   const bool live = c < Cin;
@@ -221,12 +228,19 @@ __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, in
   }
   const int tid = ty * TX + tx;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = acc[j];
+  for (int j = 0; j < 8; j += 4)  // (16-B LDS writes: the 4-B ones at a 32-B lane stride were 8-way bank conflicts)
+    *reinterpret_cast<f32x4_t*>(&red[tid * 8 + j]) = f32x4_t{acc[j], acc[j + 1], acc[j + 2], acc[j + 3]};
   __syncthreads();
   if (ty == 0 && live) {
     for (int y = 1; y < TY; ++y)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += red[(y * TX + tx) * 8 + j];
+      for (int j = 0; j < 8; j += 4) {
+        const f32x4_t v = *reinterpret_cast<const f32x4_t*>(&red[(y * TX + tx) * 8 + j]);
+        acc[j] += v[0];
+        acc[j + 1] += v[1];
+        acc[j + 2] += v[2];
+        acc[j + 3] += v[3];
+      }
     if (gridDim.z > 1) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) atomicAdd(&gs[(int64_t)b * ld_s + c + j], acc[j]);
@@ -240,7 +254,7 @@ __global__ __launch_bounds__(256) void k_bwd_in_v(const TG* __restrict__ gxt, in
 template <typename T>
 __global__ __launch_bounds__(256) void k_segsum_v(const T* __restrict__ X, int64_t ld, int HW, int C,
                                                   float* __restrict__ out) {
-  __shared__ float red[256 * 8];
+  __shared__ __attribute__((aligned(16))) float red[256 * 8];
   const int b = blockIdx.x, tx = threadIdx.x, ty = threadIdx.y, TX = blockDim.x, TY = blockDim.y;
   const int c = (blockIdx.y * TX + tx) * 8;
   const bool live = c < C;
@@ -254,12 +268,19 @@ __global__ __launch_bounds__(256) void k_segsum_v(const T* __restrict__ X, int64
   }
   const int tid = ty * TX + tx;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = acc[j];
+  for (int j = 0; j < 8; j += 4)  // (16-B LDS writes: the 4-B ones at a 32-B lane stride were 8-way bank conflicts)
+    *reinterpret_cast<f32x4_t*>(&red[tid * 8 + j]) = f32x4_t{acc[j], acc[j + 1], acc[j + 2], acc[j + 3]};
   __syncthreads();
   if (ty == 0 && live) {
     for (int y = 1; y < TY; ++y)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += red[(y * TX + tx) * 8 + j];
+      for (int j = 0; j < 8; j += 4) {
+        const f32x4_t v = *reinterpret_cast<const f32x4_t*>(&red[(y * TX + tx) * 8 + j]);
+        acc[j] += v[0];
+        acc[j + 1] += v[1];
+        acc[j + 2] += v[2];
+        acc[j + 3] += v[3];
+      }
 #pragma unroll
     for (int j = 0; j < 8; ++j) out[(int64_t)b * C + c + j] += acc[j];
   }
