@@ -579,6 +579,24 @@ __global__ void k_up2_bwd(const TG* __restrict__ gout, int B, int H, int W, int 
   }
 }
 
+// 8 consecutive elements held in their storage format until used (bf16: 4 VGPRs rather than 8 floats)
+template <typename T> struct Raw8;
+template <> struct Raw8<float> {
+  f32x4_t a, b;
+  MG_DEV void load(const float* p) {
+    a = *reinterpret_cast<const f32x4_t*>(p);
+    b = *reinterpret_cast<const f32x4_t*>(p + 4);
+  }
+  MG_DEV void zero() { a = b = f32x4_t{0.f, 0.f, 0.f, 0.f}; }
+  MG_DEV float operator[](int j) const { return j < 4 ? a[j] : b[j - 4]; }
+};
+template <> struct Raw8<bf16_t> {
+  u16x8_t a;
+  MG_DEV void load(const bf16_t* p) { a = *reinterpret_cast<const u16x8_t*>(p); }
+  MG_DEV void zero() { a = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
+  MG_DEV float operator[](int j) const { return bf2f(a[j]); }
+};
+
 inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
 
 
@@ -677,48 +695,75 @@ __global__ __launch_bounds__(1024) void k_mtm_bwd_img(const TG* __restrict__ gou
     const int p = live ? it >> lgV : 0, c = (it & (V - 1)) * 8;
     float gix = 0.f, giy = 0.f, mx = 0.f, my = 0.f;
     if (live) {
-      // gather: q = p
-      float acc[8], g[8];
+      // Every global load of the item is issued before any is consumed (the first GQ list entries, p's own gout
+      // row and its four corners): the list walk used to wait one load latency per entry, the kernel's bound
+      // at one 1024-thread block per CU.  Entries past GQ (rare: > GQ samples landing on one pixel) follow.
+      constexpr int GQ = 4;
+      const int e0 = cnt[p], e1 = cnt[p + 1];
+      Raw8<TG> gl[GQ];
+      float wl[GQ];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-      for (int e = cnt[p], e1 = cnt[p + 1]; e < e1; ++e) {
-        const int en = ent[e], pe = en >> 2, k = en & 3;
-        const f32x4_t sp = sinf[pe];
-        const float fx0 = floorf(sp[0]), fy0 = floorf(sp[1]);
-        const float ax = (k & 1) ? sp[0] - fx0 : (fx0 + 1.f) - sp[0];
-        const float ay = (k >> 1) ? sp[1] - fy0 : (fy0 + 1.f) - sp[1];
-        const float wgt = ax * ay;
-        ld8(gb + (int64_t)pe * C + c, g);
+      for (int i = 0; i < GQ; ++i) {
+        if (e0 + i < e1) {
+          const int en = ent[e0 + i], pe = en >> 2, k = en & 3;
+          const f32x4_t sp = sinf[pe];
+          const float fx0 = floorf(sp[0]), fy0 = floorf(sp[1]);
+          const float ax = (k & 1) ? sp[0] - fx0 : (fx0 + 1.f) - sp[0];
+          const float ay = (k >> 1) ? sp[1] - fy0 : (fy0 + 1.f) - sp[1];
+          wl[i] = ax * ay;
+          gl[i].load(gb + (int64_t)pe * C + c);
+        }
+      }
+      const f32x4_t sp = sinf[p];
+      mx = sp[2];
+      my = sp[3];
+      const int x0 = (int)floorf(sp[0]), y0 = (int)floorf(sp[1]);
+      Raw8<TG> g;
+      Raw8<T> xv[4];
+      g.load(gb + (int64_t)p * C + c);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += wgt * g[j];
+      for (int k = 0; k < 4; ++k) {
+        const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
+        if (xx >= 0 && xx < W && yy >= 0 && yy < H) {
+          xv[k].load(xb + (int64_t)(yy * W + xx) * C + c);
+        } else {
+          xv[k].zero();
+        }
       }
       TX* gq = gx + (row0 + p) * C + c;
+      Raw8<TX> o;
+      if (accumulate) o.load(gq);
+      // gather: q = p, summed in list order
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < GQ; ++i) {
+        if (e0 + i < e1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += wl[i] * gl[i][j];
+        }
+      }
+      for (int e = e0 + GQ; e < e1; ++e) {
+        const int en = ent[e], pe = en >> 2, k = en & 3;
+        const f32x4_t se = sinf[pe];
+        const float fx0 = floorf(se[0]), fy0 = floorf(se[1]);
+        const float ax = (k & 1) ? se[0] - fx0 : (fx0 + 1.f) - se[0];
+        const float ay = (k >> 1) ? se[1] - fy0 : (fy0 + 1.f) - se[1];
+        const float wgt = ax * ay;
+        float ge[8];
+        ld8(gb + (int64_t)pe * C + c, ge);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += wgt * ge[j];
+      }
       if (accumulate) {
-        float o[8];
-        ld8(gq, o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += o[j];
       }
       st8(gq, acc);
       // dL/dgrid of p
-      const f32x4_t sp = sinf[p];
-      mx = sp[2];
-      my = sp[3];
-      const int x0 = (int)floorf(sp[0]), y0 = (int)floorf(sp[1]);
       const float ax1 = (float)(x0 + 1) - sp[0], ax0 = sp[0] - (float)x0;
       const float ay1 = (float)(y0 + 1) - sp[1], ay0 = sp[1] - (float)y0;
-      ld8(gb + (int64_t)p * C + c, g);
-      float xv[4][8];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
-        if (xx >= 0 && xx < W && yy >= 0 && yy < H) {
-          ld8(xb + (int64_t)(yy * W + xx) * C + c, xv[k]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) xv[k][j] = 0.f;
-        }
-      }
       // dL/dgrid = sum_c g_c * (bilinear weight derivative . corner values): the corner values are differenced
       // per channel BEFORE the channel sum (as torch's grid_sampler backward does).  Summing each corner's dot
       // product first and differencing afterwards cancels two nearly equal sums -- neighbouring feature-map values
