@@ -43,6 +43,24 @@ MG_DEV void ld8(const bf16_t* p, float* t) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) t[j] = bf2f(a[j]);
 }
+// 8 consecutive elements held in their storage format until used (bf16: 4 VGPRs rather than 8 floats)
+template <typename T> struct Raw8;
+template <> struct Raw8<float> {
+  f32x4_t a, b;
+  MG_DEV void load(const float* p) {
+    a = *reinterpret_cast<const f32x4_t*>(p);
+    b = *reinterpret_cast<const f32x4_t*>(p + 4);
+  }
+  MG_DEV void zero() { a = b = f32x4_t{0.f, 0.f, 0.f, 0.f}; }
+  MG_DEV float operator[](int j) const { return j < 4 ? a[j] : b[j - 4]; }
+};
+template <> struct Raw8<bf16_t> {
+  u16x8_t a;
+  MG_DEV void load(const bf16_t* p) { a = *reinterpret_cast<const u16x8_t*>(p); }
+  MG_DEV void zero() { a = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
+  MG_DEV float operator[](int j) const { return bf2f(a[j]); }
+};
+
 MG_DEV void st8(float* p, const float* v) {
   *reinterpret_cast<f32x4_t*>(p) = f32x4_t{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<f32x4_t*>(p + 4) = f32x4_t{v[4], v[5], v[6], v[7]};

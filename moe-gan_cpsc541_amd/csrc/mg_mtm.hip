@@ -579,24 +579,6 @@ __global__ void k_up2_bwd(const TG* __restrict__ gout, int B, int H, int W, int 
   }
 }
 
-// 8 consecutive elements held in their storage format until used (bf16: 4 VGPRs rather than 8 floats)
-template <typename T> struct Raw8;
-template <> struct Raw8<float> {
-  f32x4_t a, b;
-  MG_DEV void load(const float* p) {
-    a = *reinterpret_cast<const f32x4_t*>(p);
-    b = *reinterpret_cast<const f32x4_t*>(p + 4);
-  }
-  MG_DEV void zero() { a = b = f32x4_t{0.f, 0.f, 0.f, 0.f}; }
-  MG_DEV float operator[](int j) const { return j < 4 ? a[j] : b[j - 4]; }
-};
-template <> struct Raw8<bf16_t> {
-  u16x8_t a;
-  MG_DEV void load(const bf16_t* p) { a = *reinterpret_cast<const u16x8_t*>(p); }
-  MG_DEV void zero() { a = u16x8_t{0, 0, 0, 0, 0, 0, 0, 0}; }
-  MG_DEV float operator[](int j) const { return bf2f(a[j]); }
-};
-
 inline int nblk(int64_t n, int t = 256) { return (int)std::min<int64_t>((n + t - 1) / t, 65536); }
 
 
