@@ -1110,6 +1110,12 @@ __global__ void k_router_feat_grad(const T* __restrict__ tok, int64_t ld, int Tn
   }
 }
 
+// LDS floats of k_router_feat_grad_v's in-block fold of R partial rows (CV * E values per channel lane, TX lanes
+// padded to TX + 1), and the most it may use (65 KiB: the C = 512 / 32-expert blocks; the launch raises the
+// dynamic-LDS limit past 64 KiB)
+__host__ __device__ inline int64_t rfg_fold_floats(int R, int cve, int TX) { return (int64_t)R * cve * (TX + 1); }
+constexpr int64_t kRfgFoldMax = 16640;
+
 // Vector form: a block is TX = C / CV channel lanes (CV channels each, 16-B loads for CV = 8 bf16) x TY = 256 / TX
 // token lanes walking its token chunk; the token lanes of a wave fold with shuffles and each wave-row group
 // writes one partial row [C * E] (folded by a rows fold, mg_fold.hip).  The thread-per-channel form issued 2-byte loads
@@ -1160,19 +1166,24 @@ __global__ __launch_bounds__(256) void k_router_feat_grad_v(const T* __restrict_
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[j][e] += __shfl_xor(acc[j][e], o, 64);
   const int R = TY / tyw;  // partial rows of this block (one per wave-row group)
-  if (R > 1 && (int64_t)R * Cb * E <= 16384) {  // fold them in LDS (fixed order): one row per block
-    extern __shared__ float red[];  // R * Cb * E floats (dynamic: 16 KiB at C = 128, E = 8 keeps 8 blocks per CU)
+  if (R > 1 && rfg_fold_floats(R, CV * E, TX) <= kRfgFoldMax) {  // fold them in LDS (fixed order): one row per block
+    // red[r][j * E + e][tx], rows of TX + 1 words: a lane's CV * E values used to be consecutive words (lanes CV * E
+    // words apart: every lane on one bank, 77 % bank-conflict cycles); now the lanes of one store are consecutive
+    // words and the fold's reads (consecutive (j, e) of one channel lane) are TX + 1 (odd) words apart
+    extern __shared__ float red[];  // R * CV * E * (TX + 1) floats (dynamic; host: rfg_fold_floats)
+    const int TXP = TX + 1;
     if (ty % tyw == 0) {
 #pragma unroll
       for (int j = 0; j < CV; ++j)
 #pragma unroll
-        for (int e = 0; e < E; ++e) red[(ty / tyw) * Cb * E + (c - cb + j) * E + e] = acc[j][e];
+        for (int e = 0; e < E; ++e) red[((ty / tyw) * CV * E + j * E + e) * TXP + tx] = acc[j][e];
     }
     __syncthreads();
     float* pr = part + (int64_t)blockIdx.x * C * E + (int64_t)cb * E;  // (this group's channel slice of the row)
     for (int i = threadIdx.x; i < Cb * E; i += 256) {
+      const int li = i / (CV * E), je = i - li * (CV * E);  // element (c - cb) * E + e = (li * CV + j) * E + e
       float v = 0.f;
-      for (int r = 0; r < R; ++r) v += red[r * Cb * E + i];
+      for (int r = 0; r < R; ++r) v += red[(r * CV * E + je) * TXP + li];
       pr[i] = v;
     }
     return;
@@ -1806,7 +1817,7 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
     // channel lanes x ONE token lane walking its whole chunk serially (120 us for the 4x4 block's 4096 tokens at C5)
     const int Cb = std::min(C, 64 * CV), CG = C / Cb;
     const int TX = Cb / CV, TY = 256 / TX, R = TY / (TX < 64 ? 64 / TX : 1);
-    const int rows_per_block = (R > 1 && (int64_t)R * Cb * E <= 16384) ? 1 : R;  // in-block LDS fold (kernel)
+    const int rows_per_block = (R > 1 && rfg_fold_floats(R, CV * E, TX) <= kRfgFoldMax) ? 1 : R;  // in-block LDS fold
     // ~1024 blocks with at most 4 M floats of partial rows (at 32 experts the old 256-block / 1 M-float budget
     // left 64 blocks walking 1024 tokens each: 175 us for the 16x16 block's 65536 tokens at C5)
     int chunk = std::max(TY, (T / 1024 + TY - 1) / TY * TY);
@@ -1820,9 +1831,16 @@ extern "C" int mg_router_feat_grad(int dtype, const void* tok, int64_t ld, int T
     bool deferred = false;
     float* part = mg_fold_partials((size_t)nb * rows_per_block * C * E * sizeof(float), st, &deferred);
     MG_REQUIRE(part != nullptr, "mg_router_feat_grad: no workspace");
-    const size_t smem = rows_per_block == 1 ? (size_t)R * Cb * E * sizeof(float) : 0;
-#define LV_(TT, EE, CC) hipLaunchKernelGGL((k_router_feat_grad_v<TT, EE, CC>), dim3(nb, CG), dim3(256), smem, st, \
-                                           (const TT*)tok, ld, T, C, g_raw, chunk, part)
+    const size_t smem = rows_per_block == 1 ? (size_t)rfg_fold_floats(R, CV * E, TX) * sizeof(float) : 0;
+#define LV_(TT, EE, CC)                                                                                              \
+  do {                                                                                                              \
+    if (smem > 65536)                                                                                               \
+      MG_REQUIRE(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_router_feat_grad_v<TT, EE, CC>),              \
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) == hipSuccess,          \
+                 "mg_router_feat_grad: dynamic LDS limit");                                                         \
+    hipLaunchKernelGGL((k_router_feat_grad_v<TT, EE, CC>), dim3(nb, CG), dim3(256), smem, st, (const TT*)tok, ld, T, \
+                       C, g_raw, chunk, part);                                                                      \
+  } while (0)
 #define LVE_(TT) if (E == 4) LV_(TT, 4, 8); else if (E == 8) LV_(TT, 8, 8); else if (E == 16) LV_(TT, 16, 4); \
                  else LV_(TT, 32, 2)
     if (dtype == MG_F32) { LVE_(float); } else { LVE_(bf16_t); }
